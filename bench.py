@@ -1,0 +1,146 @@
+#!/usr/bin/env python3
+"""Headline benchmark: all-reduce bus bandwidth on MI355X (RCCL over xGMI), one rank per GPU.
+
+Metric (BASELINE.json): "all-reduce bus BW (GB/s) + p50 latency vs msg size at 1/2/4/8 MI355X".
+Headline config: the reference's best 3D all-reduce data point — a bf16 activation tensor
+``[8, 2048, 2048]`` (64 MiB per rank), reference busBW 5.46 GB/s at P=8
+(``collectives/3d/stats/mpiccl/benchmark_statistics_3d_mpiccl_standard.csv:10``).
+
+One "step" = one in-place SUM all-reduce of that tensor on every rank. W untimed warmup steps,
+then EXACTLY K steps timed between [barrier + synchronize] and [synchronize]; the elapsed time is
+the MAX over ranks. busBW follows nccl-tests: ``bytes / t * 2(P-1)/P`` — identically 0 at P=1
+(no inter-GPU traffic), where ``vs_baseline`` is null (the reference has no P=1 data).
+Per-GPU message size is fixed as N grows: weak scaling.
+
+Side measurements (also in the JSON line): p50 latency of a 512 B all-reduce (reference best
+22.9 µs at P=2, 32.0 µs at P=8) and busBW at 8 MiB (reference best 7.53 GB/s).
+
+Usage: ``python bench.py [--gpus N] [--steps K] [--warmup W]``; for N>1 launch with
+``python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py``.
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REF_BUSBW_GBPS = 5.46          # best 3D all-reduce busBW (P=8, 64 MiB bf16)
+REF_LAT_512B_US = {2: 22.9, 8: 32.0}
+REF_BUSBW_8MIB = 7.53
+
+
+def parse(argv=None):
+    ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--shape", default="8,2048,2048", help="B,S,H of the bf16 message")
+    ap.add_argument("--impl", default="rccl", choices=["rccl", "custom", "auto"])
+    ap.add_argument("--no-side", action="store_true", help="skip the 512 B / 8 MiB side runs")
+    return ap.parse_args(argv)
+
+
+def _timed_steps(comm, op, steps: int) -> float:
+    import torch  # noqa: F401
+
+    comm.barrier()
+    comm.sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        op.run()
+    comm.sync()
+    dt = time.perf_counter() - t0
+    return comm.allreduce_max(dt)
+
+
+def main(argv=None) -> int:
+    args = parse(argv)
+    import torch
+
+    from distributed_llm_backend_benchmark_amd.bench.timing import time_per_iteration
+    from distributed_llm_backend_benchmark_amd.parallel.collectives import make_data, make_op
+    from distributed_llm_backend_benchmark_amd.parallel.comm import init_distributed
+    from distributed_llm_backend_benchmark_amd.stats.bandwidth import algbw_gbps, busbw_gbps
+
+    backend = "rccl" if torch.cuda.is_available() else "gloo"
+    comm = init_distributed(backend, timeout_s=900)
+    P = comm.world_size
+    if args.gpus != P and comm.rank == 0:
+        print(f"note: --gpus {args.gpus} but world size is {P}; using {P}", file=sys.stderr)
+
+    B, S, H = (int(x) for x in args.shape.split(","))
+    data = make_data((B, S, H), torch.bfloat16, comm.rank, comm.device)
+    op = make_op("allreduce", comm, data, impl=args.impl)
+    nbytes = op.message_bytes
+
+    for _ in range(args.warmup):
+        op.run()
+    comm.sync()
+    total = _timed_steps(comm, op, args.steps)
+    per_step = total / args.steps
+    bus = busbw_gbps("allreduce", nbytes, per_step, P)
+    alg = algbw_gbps("allreduce", nbytes, per_step, P)
+
+    side = {}
+    if not args.no_side:
+        small = make_op("allreduce", comm, make_data((256,), torch.bfloat16, comm.rank,
+                                                     comm.device), impl="auto")
+        tr = time_per_iteration(comm, small, iters=100, warmup=10)
+        allt = comm.gather_floats(tr.timings)
+        mid = make_op("allreduce", comm, make_data((4 * 1024 * 1024,), torch.bfloat16,
+                                                   comm.rank, comm.device), impl=args.impl)
+        for _ in range(5):
+            mid.run()
+        mid_t = _timed_steps(comm, mid, 20) / 20
+        if comm.rank == 0:
+            import numpy as np
+
+            lat = float(np.median(np.asarray(allt, dtype=np.float64))) * 1e6
+            side = {
+                "p50_latency_us_512B": lat,
+                "p50_latency_512B_impl": getattr(small, "impl", "rccl"),
+                "ref_p50_latency_us_512B": REF_LAT_512B_US.get(P),
+                "busbw_GBps_8MiB": busbw_gbps("allreduce", 8 << 20, mid_t, P),
+                "ref_busbw_GBps_8MiB": REF_BUSBW_8MIB,
+            }
+
+    if comm.rank == 0:
+        rec = {
+            "metric": "all-reduce bus BW (GB/s)",
+            "value": round(bus, 4),
+            "unit": "GB/s",
+            "n_gpus": P,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": per_step * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": (round(bus / REF_BUSBW_GBPS, 3) if P > 1 else None),
+            "dtype": "bf16",
+            "data": "synthetic (rank-seeded randn, on device)",
+            "config": {
+                "model": f"allreduce_3d_b{B}_s{S}_h{H}",
+                "global_batch": B,
+                "seq_len": S,
+                "hidden": H,
+                "message_bytes_per_rank": nbytes,
+                "parallelism": f"{'rccl' if comm.backend == 'nccl' else comm.backend}_world{P}",
+                "impl": getattr(op, "impl", args.impl),
+            },
+            "algbw_GBps": alg,
+            "baseline_busbw_GBps": REF_BUSBW_GBPS,
+            "note": ("busBW = bytes/t*2(P-1)/P (nccl-tests); identically 0 at P=1, where "
+                     "vs_baseline is null (reference has no single-rank data)"),
+            **side,
+        }
+        print(json.dumps(rec), flush=True)
+    comm.barrier()
+    comm.destroy()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,195 @@
+"""Tensor-parallel transformer forward benchmark — ``run_mpi.py`` parity.
+
+Reference: ``run_mpi.py:52-248`` (argparse ``--config``/``--backend``; world-size check;
+init timing; warmup loop; timed loop with a barrier before and after each forward; per-rank
+forward means gathered to rank 0 with variance / CV; JSON ``{output_dir}/{backend}_{name}.json``
+with keys ``experiment, backend, config, system_info, rank_0_summary, rank_statistics,
+raw_metrics_rank_0`` (``run_mpi.py:217-225``)).
+
+Launch (one process per GPU)::
+
+    torchrun --nproc-per-node 4 --master-addr 127.0.0.1 -m \
+        distributed_llm_backend_benchmark_amd.cli.run_tp --config config/baseline_config.yaml \
+        --backend rccl
+
+Differences by design: the forward is device-timed (barrier, then synchronised wall clock and
+HIP events); ``--backend`` picks the process-group backend (``rccl`` | ``gloo``) and names the
+output file; extra result keys: ``tokens_per_s``, ``tflops_per_rank``, ``allreduce_bytes``.
+"""
+
+from __future__ import annotations
+
+import argparse
+import os
+import sys
+import time
+
+
+def parse_args(argv=None):
+    ap = argparse.ArgumentParser(description="TP transformer forward benchmark (run_mpi.py parity)")
+    ap.add_argument("--config", required=True, help="YAML config (reference schema)")
+    ap.add_argument("--backend", default="rccl", choices=["rccl", "gloo", "nccl"],
+                    help="process-group backend; also names the output file")
+    ap.add_argument("--allreduce", choices=["auto", "rccl", "custom"], default=None,
+                    help="override execution.allreduce")
+    ap.add_argument("--allreduce-dtype", choices=["bf16", "fp32"], default=None)
+    ap.add_argument("--attention", choices=["slice", "sdpa"], default=None)
+    ap.add_argument("--kernels", choices=["hip", "torch"], default=None)
+    ap.add_argument("--model-size", default=None, help="override with a MODEL_CONFIGS size")
+    ap.add_argument("--num-layers", type=int, default=None)
+    ap.add_argument("--warmup", type=int, default=None)
+    ap.add_argument("--iters", type=int, default=None)
+    ap.add_argument("--output-dir", default=None)
+    ap.add_argument("--ignore-world-size", action="store_true",
+                    help="accept any world size (reference exits on mismatch, run_mpi.py:73-77)")
+    return ap.parse_args(argv)
+
+
+def main(argv=None) -> int:
+    args = parse_args(argv)
+    # config + thread env BEFORE importing torch (reference sets it after: SURVEY §2.8 item 8)
+    from ..utils.config import load_config, setup_environment
+
+    config = load_config(args.config)
+    setup_environment(config)
+
+    import numpy as np
+    import torch
+
+    from ..data import create_dataset_from_config
+    from ..models.tp_transformer import MODEL_CONFIGS, create_model_from_config
+    from ..parallel.comm import init_distributed
+    from ..utils.io import save_results
+    from ..utils.metrics import MetricsCollector, print_summary, rank_statistics
+    from ..utils.sysinfo import collect_system_info
+
+    ex = config["execution"]
+    if args.allreduce:
+        ex["allreduce"] = args.allreduce
+    if args.allreduce_dtype:
+        ex["allreduce_dtype"] = args.allreduce_dtype
+    if args.attention:
+        ex["attention"] = args.attention
+    if args.kernels:
+        ex["kernels"] = args.kernels
+    if args.model_size:
+        config["model"].update(MODEL_CONFIGS[args.model_size])
+        config["model"]["size"] = args.model_size
+    if args.num_layers:
+        config["model"]["num_layers"] = args.num_layers
+    if args.warmup is not None:
+        ex["warmup_iterations"] = args.warmup
+    if args.iters is not None:
+        ex["benchmark_iterations"] = args.iters
+    if args.output_dir:
+        config["experiment"]["output_dir"] = args.output_dir
+
+    t0 = time.perf_counter()
+    comm = init_distributed(args.backend)
+    comm.barrier()
+    init_elapsed = time.perf_counter() - t0
+    rank, world = comm.rank, comm.world_size
+
+    expected = config["parallelism"]["world_size"]
+    if expected != "auto" and int(expected) != world and not args.ignore_world_size:
+        if rank == 0:
+            print(f"ERROR: World size mismatch. Expected {expected}, got {world}")
+        comm.destroy()
+        return 1
+
+    if rank == 0:
+        si = collect_system_info()
+        print(f"\n{'=' * 60}\nExperiment: {config['experiment']['name']}\n"
+              f"Backend: {args.backend.upper()} ({comm.backend})\n{'=' * 60}")
+        print(f"World size: {world}\nInitialization time: {init_elapsed:.4f}s")
+        print(f"Device: {si.get('gpu_name', 'cpu')} arch={si.get('gpu_arch')} "
+              f"HIP={si.get('hip_version')} RCCL={si.get('rccl_version')}")
+        m = config["model"]
+        print(f"Model: {m.get('size')} H={m['hidden_size']} L={m['num_layers']} "
+              f"heads={m['num_heads']} F={m['ffn_intermediate']}")
+        print(f"Input: B={config['input']['batch_size']} S={config['input']['sequence_length']}")
+        print(f"Execution: {ex}")
+
+    model = create_model_from_config(config, comm)
+    dataset = create_dataset_from_config(config, comm.device)
+    if rank == 0:
+        print(f"[Rank 0] Model created: total params {model.get_num_parameters() / 1e9:.2f}B "
+              f"(reference formula), {model.num_parameters_exact() / 1e9:.2f}B exact; "
+              f"{model.get_memory_footprint() / 1e9:.2f} GB per rank")
+    comm.barrier()
+
+    metrics = MetricsCollector(rank, world)
+    metrics.record_init_time(init_elapsed)
+    gpu = comm.is_gpu
+
+    for _ in range(int(ex["warmup_iterations"])):
+        batch = dataset.get_batch()
+        t = time.perf_counter()
+        model(batch)
+        comm.sync()
+        metrics.record_warmup_time(time.perf_counter() - t)
+    comm.barrier()
+
+    base_bytes = model.comm_bytes()
+    ev = []
+    for _ in range(int(ex["benchmark_iterations"])):
+        batch = dataset.get_batch()
+        comm.barrier()                          # reference run_mpi.py:177
+        if gpu:
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+        t = time.perf_counter()
+        model(batch)
+        if gpu:
+            e.record()
+        comm.sync()
+        comm.barrier()                          # reference run_mpi.py:183
+        metrics.record_forward_time(time.perf_counter() - t)
+        if gpu:
+            ev.append(s.elapsed_time(e) * 1e-3)
+    iters = int(ex["benchmark_iterations"])
+    ar_bytes = (model.comm_bytes() - base_bytes) // max(1, iters)
+    if ev:
+        metrics.metrics["forward_device_times"] = ev
+
+    summary = metrics.get_summary()
+    means = comm.all_gather_object(summary["forward_mean"])
+    if rank == 0:
+        rs = rank_statistics(means)
+        B, S = int(config["input"]["batch_size"]), int(config["input"]["sequence_length"])
+        fwd = summary["forward_mean"]
+        extra = {
+            "tokens_per_s": B * S / fwd,
+            "tflops_per_rank": model.flops_per_forward(B, S) / fwd / 1e12,
+            "allreduce_bytes_per_forward_per_rank": ar_bytes,
+            "allreduces_per_forward": 2 * int(config["model"]["num_layers"]),
+            "forward_device_mean": float(np.mean(ev)) if ev else None,
+            "kernels": ex.get("kernels"),
+            "gemm_fallbacks": __import__(
+                "distributed_llm_backend_benchmark_amd.ops.gemm", fromlist=["x"]).FALLBACKS["count"],
+        }
+        results = {
+            "experiment": config["experiment"]["name"],
+            "backend": args.backend,
+            "config": config,
+            "system_info": collect_system_info(),
+            "rank_0_summary": summary,
+            "rank_statistics": rs,
+            "raw_metrics_rank_0": metrics.get_raw_metrics(),
+            "throughput": extra,
+        }
+        print_summary(summary, args.backend.upper(), rank)
+        print(f"\nRank Statistics:\n  Variance across ranks: {rs['variance_across_ranks']:.6g}"
+              f"\n  Coefficient of variation: {rs['coefficient_of_variation']:.4f}"
+              f"\n  tokens/s: {extra['tokens_per_s']:.1f}  TFLOP/s/rank: "
+              f"{extra['tflops_per_rank']:.1f}")
+        out = os.path.join(config["experiment"]["output_dir"],
+                           f"{args.backend}_{config['experiment']['name']}.json")
+        save_results(results, out, rank)
+    comm.barrier()
+    comm.destroy()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

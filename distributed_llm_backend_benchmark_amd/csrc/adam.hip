@@ -1,0 +1,85 @@
+// Fused AdamW over flat buffers (one launch for the whole model).
+//
+// The reference's only optimizer step is DeepSpeed's Adam inside `model_engine.step()`
+// (test/ccl.py:114-115). The DDP microbenchmark keeps parameters, gradients and optimizer state
+// as single flat device buffers (gradient buckets are views of the flat gradient buffer), so the
+// optimizer is one HBM-streaming pass:
+//   reads  fp32 master p, m, v, and the bf16|fp32 reduced gradient g (scaled by grad_scale,
+//          e.g. 1/world for averaging — fused here instead of a separate pass)
+//   writes fp32 p, m, v and the bf16 working copy used by the next forward.
+#include "common.h"
+
+namespace dlbb {
+
+struct AdamArgs {
+  float* p;
+  float* m;
+  float* v;
+  const void* g;
+  uint16_t* p_bf16;   // optional bf16 shadow of p
+  int64_t n;
+  float lr, beta1, beta2, eps, weight_decay;
+  float bc1, bc2;     // 1 - beta^t
+  float grad_scale;
+};
+
+template <int GDT>
+__global__ void __launch_bounds__(256) adamw_kernel(AdamArgs a) {
+  const int64_t nvec = a.n / 8;
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
+  const float step = a.lr / a.bc1;
+  const float inv_bc2 = 1.0f / a.bc2;
+  auto body = [&](float& p, float& m, float& v, float g) {
+    g *= a.grad_scale;
+    m = a.beta1 * m + (1.f - a.beta1) * g;
+    v = a.beta2 * v + (1.f - a.beta2) * g * g;
+    const float denom = sqrtf(v * inv_bc2) + a.eps;
+    p = p * (1.f - a.lr * a.weight_decay) - step * m / denom;
+  };
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < nvec;
+       i += stride) {
+    float p[8], m[8], v[8], g[8];
+    load8<DT_F32>(a.p, i, p);
+    load8<DT_F32>(a.m, i, m);
+    load8<DT_F32>(a.v, i, v);
+    load8<GDT>(a.g, i, g);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) body(p[j], m[j], v[j], g[j]);
+    store8<DT_F32>(a.p, i, p);
+    store8<DT_F32>(a.m, i, m);
+    store8<DT_F32>(a.v, i, v);
+    if (a.p_bf16) store8<DT_BF16>(a.p_bf16, i, p);
+  }
+  if (blockIdx.x == 0) {
+    const int64_t t = nvec * 8 + threadIdx.x;
+    if (t < a.n) {
+      float p = a.p[t], m = a.m[t], v = a.v[t];
+      const float g = Elem<GDT>::ld(static_cast<const typename Elem<GDT>::T*>(a.g), t);
+      body(p, m, v, g);
+      a.p[t] = p; a.m[t] = m; a.v[t] = v;
+      if (a.p_bf16) a.p_bf16[t] = f32_to_bf16(p);
+    }
+  }
+}
+
+}  // namespace dlbb
+
+using namespace dlbb;
+
+DLBB_API int dlbb_adamw(float* p, float* m, float* v, const void* g, int grad_dtype,
+                        void* p_bf16, int64_t n, float lr, float beta1, float beta2, float eps,
+                        float weight_decay, int step, float grad_scale, hipStream_t stream) {
+  if (n <= 0) return hipSuccess;
+  if (step < 1) return hipErrorInvalidValue;
+  AdamArgs a{p, m, v, g, static_cast<uint16_t*>(p_bf16), n, lr, beta1, beta2, eps,
+             weight_decay, 1.f - powf(beta1, static_cast<float>(step)),
+             1.f - powf(beta2, static_cast<float>(step)), grad_scale};
+  const int grid = stream_grid((n + 7) / 8, 256);
+  if (grad_dtype == DT_BF16)
+    hipLaunchKernelGGL(adamw_kernel<DT_BF16>, dim3(grid), dim3(256), 0, stream, a);
+  else if (grad_dtype == DT_F32)
+    hipLaunchKernelGGL(adamw_kernel<DT_F32>, dim3(grid), dim3(256), 0, stream, a);
+  else
+    return hipErrorInvalidValue;
+  return hipGetLastError();
+}

@@ -1,0 +1,128 @@
+// Shared helpers for the gfx950 (MI355X, CDNA4) kernels of this package.
+//
+// Conventions used by every kernel file:
+//   * wave = 64 lanes; block sizes are multiples of 64.
+//   * bf16/fp16 move as 16-byte vectors (8 elements / lane) — hipcc does not vectorise
+//     scalar 16-bit loads (CDNA guide, Guideline 13).
+//   * accumulation is fp32; bf16 rounding uses the native v_cvt_pk_bf16_f32 (RNE, NaN-safe),
+//     which hipcc emits for a plain (__bf16) cast on gfx950.
+//   * every launcher is a plain C ABI function taking raw device pointers and a hipStream_t,
+//     returns hipError_t as int, allocates nothing and never synchronises (graph-capturable).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define DLBB_API extern "C" __attribute__((visibility("default")))
+
+namespace dlbb {
+
+enum DType : int { DT_F32 = 0, DT_BF16 = 1, DT_F16 = 2 };
+
+constexpr int kWave = 64;
+
+typedef uint16_t u16x8 __attribute__((ext_vector_type(8)));
+typedef uint16_t u16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef short bf16x8 __attribute__((ext_vector_type(8)));   // MFMA operand fragment
+
+__device__ __forceinline__ float bf16_to_f32(uint16_t v) {
+  return __uint_as_float(static_cast<uint32_t>(v) << 16);
+}
+__device__ __forceinline__ uint16_t f32_to_bf16(float f) {
+  return __builtin_bit_cast(uint16_t, static_cast<__bf16>(f));
+}
+__device__ __forceinline__ float f16_to_f32(uint16_t v) {
+  return static_cast<float>(__builtin_bit_cast(_Float16, v));
+}
+__device__ __forceinline__ uint16_t f32_to_f16(float f) {
+  return __builtin_bit_cast(uint16_t, static_cast<_Float16>(f));
+}
+
+// Element traits: load/store one element as fp32.
+template <int DT> struct Elem;
+template <> struct Elem<DT_F32> {
+  using T = float;
+  static constexpr int kBytes = 4;
+  __device__ __forceinline__ static float ld(const T* p, int64_t i) { return p[i]; }
+  __device__ __forceinline__ static void st(T* p, int64_t i, float v) { p[i] = v; }
+};
+template <> struct Elem<DT_BF16> {
+  using T = uint16_t;
+  static constexpr int kBytes = 2;
+  __device__ __forceinline__ static float ld(const T* p, int64_t i) { return bf16_to_f32(p[i]); }
+  __device__ __forceinline__ static void st(T* p, int64_t i, float v) { p[i] = f32_to_bf16(v); }
+};
+template <> struct Elem<DT_F16> {
+  using T = uint16_t;
+  static constexpr int kBytes = 2;
+  __device__ __forceinline__ static float ld(const T* p, int64_t i) { return f16_to_f32(p[i]); }
+  __device__ __forceinline__ static void st(T* p, int64_t i, float v) { p[i] = f32_to_f16(v); }
+};
+
+// 8 consecutive elements <-> 8 floats (one 16 B load for 16-bit types, two for fp32).
+template <int DT>
+__device__ __forceinline__ void load8(const void* base, int64_t i8, float (&v)[8]) {
+  if constexpr (DT == DT_F32) {
+    const float4* p = reinterpret_cast<const float4*>(base) + 2 * i8;
+    float4 a = p[0], b = p[1];
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+    v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+  } else {
+    u16x8 r = reinterpret_cast<const u16x8*>(base)[i8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      v[j] = (DT == DT_BF16) ? bf16_to_f32(r[j]) : f16_to_f32(r[j]);
+  }
+}
+
+template <int DT>
+__device__ __forceinline__ void store8(void* base, int64_t i8, const float (&v)[8]) {
+  if constexpr (DT == DT_F32) {
+    float4* p = reinterpret_cast<float4*>(base) + 2 * i8;
+    p[0] = make_float4(v[0], v[1], v[2], v[3]);
+    p[1] = make_float4(v[4], v[5], v[6], v[7]);
+  } else {
+    u16x8 r;
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      r[j] = (DT == DT_BF16) ? f32_to_bf16(v[j]) : f32_to_f16(v[j]);
+    reinterpret_cast<u16x8*>(base)[i8] = r;
+  }
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__device__ __forceinline__ float gelu_erf(float x) {
+  return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f));
+}
+__device__ __forceinline__ float gelu_erf_grad(float x) {
+  const float cdf = 0.5f * (1.0f + erff(x * 0.70710678118654752f));
+  const float pdf = 0.3989422804014327f * __expf(-0.5f * x * x);
+  return cdf + x * pdf;
+}
+__device__ __forceinline__ float gelu_tanh(float x) {
+  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+  return 0.5f * x * (1.0f + tanhf(k0 * (x + k1 * x * x * x)));
+}
+__device__ __forceinline__ float gelu_tanh_grad(float x) {
+  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+  const float x2 = x * x;
+  const float t = tanhf(k0 * (x + k1 * x2 * x));
+  return 0.5f * (1.0f + t) + 0.5f * x * (1.0f - t * t) * k0 * (1.0f + 3.0f * k1 * x2);
+}
+
+// Grid size for memory-bound grid-stride kernels: enough blocks to fill 256 CUs several
+// times over, capped (CDNA guide, Guideline 11).
+inline int stream_grid(int64_t work_items, int block) {
+  int64_t g = (work_items + block - 1) / block;
+  if (g < 1) g = 1;
+  if (g > 2048) g = 2048;
+  return static_cast<int>(g);
+}
+
+}  // namespace dlbb

@@ -1,0 +1,371 @@
+// IPC one-shot / two-shot all-reduce over xGMI (single node, up to 8 GPUs).
+//
+// What it replaces: the reference's all-reduce paths are host collectives — mpi4py
+// `comm.allreduce` / `comm.Allreduce` (collectives/1d/openmpi.py:63, models.py:95) and
+// oneCCL/Gloo `dist.all_reduce` (collectives/1d/dsccl.py:65) with oneCCL's algorithm menu
+// (direct / ring / 2d / ... selected by CCL_ALLREDUCE, collectives/3d/launch_dsccl.sh:46-47).
+// On MI355X every GPU has a dedicated xGMI link to each of its 7 peers (fully connected), so a
+// "direct" algorithm that reads all peers at once uses all 7 links concurrently, where a ring
+// uses one. RCCL stays the default; this kernel is the low-latency / all-links path.
+//
+// Protocol (per call, per workgroup b; `e` = per-workgroup epoch counter kept in device memory,
+// so the kernel is HIP-graph replayable):
+//   one-shot : copy my input range b -> my IPC buffer[e&1] ; signal(phase 0, e) to all peers ;
+//              wait all peers' phase-0 flag >= e ; out[b] = sum_p peer_buf[p][e&1][b]
+//   two-shot : copy sub-range b of every shard -> buffer[e&1] ; signal/wait phase 0 ;
+//              reduce sub-range b of MY shard from all peers -> my tmp[e&1] and out ;
+//              signal/wait phase 1 ; gather sub-range b of every peer shard from peer tmp -> out
+// Double buffering by epoch parity + the ">= e" wait makes one barrier per phase sufficient:
+// a rank reaches epoch e+2 (and overwrites buffer[e&1]) only after every peer signalled e+1,
+// i.e. finished reading epoch e.
+// Memory ordering (CDNA guide §6 G16, system scope because readers are other GPUs): payload
+// plain stores -> each wave `s_waitcnt vmcnt(0)` -> barrier -> one lane per peer:
+// release fence (buffer_wbl2 sc0 sc1) -> `s_waitcnt vmcnt(0)` (ROCm 7.2 pitfall 12) -> relaxed
+// system-scope flag store into the peer's uncached signal page. Consumer: relaxed system-scope
+// poll (sc0 sc1, bypasses caches) with s_sleep, ONE acquire fence (buffer_inv sc0 sc1), barrier,
+// then plain loads of peer memory. Every spin is bounded: on timeout the kernel records an error
+// code and exits, so a broken peer cannot hang the GPU.
+#include "common.h"
+
+#include <string.h>
+
+#include <new>
+
+namespace dlbb {
+
+constexpr int kMaxRanks = 8;
+constexpr int kMaxBlocks = 128;
+constexpr int kCarThreads = 512;
+constexpr unsigned kSpinLimit = 1u << 26;   // ~ seconds of polling, then give up
+
+struct Signal {
+  uint32_t flags[2][kMaxBlocks][kMaxRanks];   // written by peers (remote stores)
+  uint32_t epoch[kMaxBlocks];                 // local per-workgroup call counter
+  uint32_t error;                             // nonzero: a wait timed out
+  uint32_t pad[3];
+};
+
+struct CarKernelArgs {
+  char* data[kMaxRanks];        // each rank's IPC data region: 2 x cap bytes
+  char* tmp[kMaxRanks];         // each rank's IPC tmp region (two-shot): 2 x cap bytes
+  Signal* sig[kMaxRanks];
+  const void* inp;
+  void* out;
+  int64_t nbytes;               // message bytes, multiple of 16 * world (two-shot) / 16
+  int64_t cap;                  // capacity per buffer half
+  int rank;
+  int world;
+};
+
+__device__ __forceinline__ void signal_peers(const CarKernelArgs& a, int phase, uint32_t e) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x < static_cast<unsigned>(a.world)) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_store(&a.sig[threadIdx.x]->flags[phase][blockIdx.x][a.rank], e,
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+__device__ __forceinline__ bool wait_peers(const CarKernelArgs& a, int phase, uint32_t e) {
+  __shared__ int timed_out;
+  if (threadIdx.x == 0) timed_out = 0;
+  __syncthreads();
+  if (threadIdx.x < static_cast<unsigned>(a.world)) {
+    uint32_t* f = &a.sig[a.rank]->flags[phase][blockIdx.x][threadIdx.x];
+    unsigned spins = 0;
+    while (static_cast<int32_t>(
+               __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - e) < 0) {
+      __builtin_amdgcn_s_sleep(1);
+      if (++spins > kSpinLimit) {
+        timed_out = 1;
+        __hip_atomic_store(&a.sig[a.rank]->error, 1u, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+        break;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+  }
+  __syncthreads();
+  return timed_out == 0;
+}
+
+template <int DT>
+__device__ __forceinline__ void sum_vec(const CarKernelArgs& a, char* const* bufs, int64_t off,
+                                        float (&acc)[8]) {
+  // rotate the peer order per rank so ranks do not all hammer the same link first
+  load8<DT>(bufs[a.rank] + off, 0, acc);
+  for (int k = 1; k < a.world; ++k) {
+    const int p = (a.rank + k) % a.world;
+    float v[8];
+    load8<DT>(bufs[p] + off, 0, v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] += v[j];
+  }
+}
+
+template <int DT>
+__global__ void __launch_bounds__(kCarThreads) car_oneshot_kernel(CarKernelArgs a) {
+  constexpr int64_t kVecBytes = 8 * Elem<DT>::kBytes;
+  __shared__ uint32_t s_epoch;
+  if (threadIdx.x == 0) s_epoch = ++a.sig[a.rank]->epoch[blockIdx.x];
+  __syncthreads();
+  const uint32_t e = s_epoch;
+  const int64_t half = (e & 1) * a.cap;
+  const int64_t nvec = a.nbytes / kVecBytes;
+  const int64_t per = (nvec + gridDim.x - 1) / gridDim.x;
+  const int64_t v0 = blockIdx.x * per;
+  const int64_t v1 = v0 + per < nvec ? v0 + per : nvec;
+  char* mine = a.data[a.rank] + half;
+  for (int64_t v = v0 + threadIdx.x; v < v1; v += blockDim.x) {
+#pragma unroll
+    for (int q = 0; q < kVecBytes / 16; ++q)
+      reinterpret_cast<u16x8*>(mine + v * kVecBytes)[q] =
+          reinterpret_cast<const u16x8*>(static_cast<const char*>(a.inp) + v * kVecBytes)[q];
+  }
+  signal_peers(a, 0, e);
+  if (!wait_peers(a, 0, e)) return;
+  char* bufs[kMaxRanks];
+  for (int p = 0; p < a.world; ++p) bufs[p] = a.data[p] + half;
+  for (int64_t v = v0 + threadIdx.x; v < v1; v += blockDim.x) {
+    float acc[8];
+    sum_vec<DT>(a, bufs, v * kVecBytes, acc);
+    store8<DT>(a.out, v, acc);
+  }
+}
+
+template <int DT>
+__global__ void __launch_bounds__(kCarThreads) car_twoshot_kernel(CarKernelArgs a) {
+  constexpr int64_t kVecBytes = 8 * Elem<DT>::kBytes;
+  __shared__ uint32_t s_epoch;
+  if (threadIdx.x == 0) s_epoch = ++a.sig[a.rank]->epoch[blockIdx.x];
+  __syncthreads();
+  const uint32_t e = s_epoch;
+  const int64_t half = (e & 1) * a.cap;
+  const int64_t shard_vec = a.nbytes / kVecBytes / a.world;      // vectors per shard
+  const int64_t per = (shard_vec + gridDim.x - 1) / gridDim.x;
+  const int64_t s0 = blockIdx.x * per;
+  const int64_t s1 = s0 + per < shard_vec ? s0 + per : shard_vec;
+  char* mine = a.data[a.rank] + half;
+  // publish sub-range [s0, s1) of every shard
+  for (int p = 0; p < a.world; ++p) {
+    const int64_t base = p * shard_vec;
+    for (int64_t v = s0 + threadIdx.x; v < s1; v += blockDim.x) {
+      const int64_t off = (base + v) * kVecBytes;
+#pragma unroll
+      for (int q = 0; q < kVecBytes / 16; ++q)
+        reinterpret_cast<u16x8*>(mine + off)[q] =
+            reinterpret_cast<const u16x8*>(static_cast<const char*>(a.inp) + off)[q];
+    }
+  }
+  signal_peers(a, 0, e);
+  if (!wait_peers(a, 0, e)) return;
+  // reduce-scatter: my shard, sub-range b
+  char* bufs[kMaxRanks];
+  for (int p = 0; p < a.world; ++p) bufs[p] = a.data[p] + half;
+  char* my_tmp = a.tmp[a.rank] + half;
+  const int64_t mybase = a.rank * shard_vec;
+  for (int64_t v = s0 + threadIdx.x; v < s1; v += blockDim.x) {
+    float acc[8];
+    sum_vec<DT>(a, bufs, (mybase + v) * kVecBytes, acc);
+    store8<DT>(my_tmp, mybase + v, acc);
+    store8<DT>(a.out, mybase + v, acc);
+  }
+  signal_peers(a, 1, e);
+  if (!wait_peers(a, 1, e)) return;
+  // all-gather: every other shard's sub-range b from its owner's tmp
+  for (int k = 1; k < a.world; ++k) {
+    const int p = (a.rank + k) % a.world;
+    const char* src = a.tmp[p] + half;
+    const int64_t base = p * shard_vec;
+    for (int64_t v = s0 + threadIdx.x; v < s1; v += blockDim.x) {
+      const int64_t off = (base + v) * kVecBytes;
+#pragma unroll
+      for (int q = 0; q < kVecBytes / 16; ++q)
+        reinterpret_cast<u16x8*>(static_cast<char*>(a.out) + off)[q] =
+            reinterpret_cast<const u16x8*>(src + off)[q];
+    }
+  }
+}
+
+struct CarState {
+  int rank = 0, world = 1, device = 0;
+  int64_t cap = 0;
+  char* data = nullptr;       // 2 * cap (coarse-grained, IPC)
+  char* tmp = nullptr;        // 2 * cap
+  Signal* sig = nullptr;      // uncached, IPC
+  bool opened = false;
+  CarKernelArgs args{};
+  char* peer_data[kMaxRanks] = {};
+  char* peer_tmp[kMaxRanks] = {};
+  Signal* peer_sig[kMaxRanks] = {};
+};
+
+}  // namespace dlbb
+
+using namespace dlbb;
+
+#define CAR_CHECK(x)                         \
+  do {                                       \
+    hipError_t _e = (x);                     \
+    if (_e != hipSuccess) return (int)_e;    \
+  } while (0)
+
+DLBB_API int dlbb_car_create(int rank, int world, int64_t cap_bytes, void** out) {
+  if (world < 1 || world > kMaxRanks || rank < 0 || rank >= world || cap_bytes <= 0)
+    return hipErrorInvalidValue;
+  cap_bytes = (cap_bytes + 255) / 256 * 256;
+  CarState* s = new (std::nothrow) CarState();
+  if (!s) return hipErrorOutOfMemory;
+  s->rank = rank;
+  s->world = world;
+  s->cap = cap_bytes;
+  CAR_CHECK(hipGetDevice(&s->device));
+  hipError_t e = hipMalloc(reinterpret_cast<void**>(&s->data), 2 * cap_bytes);
+  if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&s->tmp), 2 * cap_bytes);
+  if (e == hipSuccess)
+    e = hipExtMallocWithFlags(reinterpret_cast<void**>(&s->sig), sizeof(Signal),
+                              hipDeviceMallocUncached);
+  if (e == hipSuccess) e = hipMemset(s->sig, 0, sizeof(Signal));
+  if (e == hipSuccess) e = hipDeviceSynchronize();
+  if (e != hipSuccess) {
+    if (s->data) (void)hipFree(s->data);
+    if (s->tmp) (void)hipFree(s->tmp);
+    if (s->sig) (void)hipFree(s->sig);
+    delete s;
+    return (int)e;
+  }
+  *out = s;
+  return hipSuccess;
+}
+
+// Writes 3 x 64-byte IPC handles (data, tmp, signal) into out_handles (192 bytes).
+DLBB_API int dlbb_car_ipc_handles(void* h, void* out_handles) {
+  CarState* s = static_cast<CarState*>(h);
+  hipIpcMemHandle_t hd, ht, hs;
+  CAR_CHECK(hipIpcGetMemHandle(&hd, s->data));
+  CAR_CHECK(hipIpcGetMemHandle(&ht, s->tmp));
+  CAR_CHECK(hipIpcGetMemHandle(&hs, s->sig));
+  char* o = static_cast<char*>(out_handles);
+  memcpy(o, &hd, 64);
+  memcpy(o + 64, &ht, 64);
+  memcpy(o + 128, &hs, 64);
+  return hipSuccess;
+}
+
+DLBB_API int dlbb_car_handle_bytes() { return 3 * 64; }
+
+// all_handles: world x 192 bytes in rank order; peer_devices: each rank's device ordinal
+// (used to decide whether peer access must be enabled; same device -> plain IPC mapping).
+DLBB_API int dlbb_car_open(void* h, const void* all_handles, const int* peer_devices) {
+  CarState* s = static_cast<CarState*>(h);
+  if (s->opened) return hipSuccess;
+  const char* hs = static_cast<const char*>(all_handles);
+  for (int p = 0; p < s->world; ++p) {
+    if (p == s->rank) {
+      s->peer_data[p] = s->data;
+      s->peer_tmp[p] = s->tmp;
+      s->peer_sig[p] = s->sig;
+      continue;
+    }
+    if (peer_devices && peer_devices[p] != s->device) {
+      int can = 0;
+      CAR_CHECK(hipDeviceCanAccessPeer(&can, s->device, peer_devices[p]));
+      if (!can) return hipErrorPeerAccessUnsupported;
+      hipError_t e = hipDeviceEnablePeerAccess(peer_devices[p], 0);
+      if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) return (int)e;
+      (void)hipGetLastError();
+    }
+    hipIpcMemHandle_t hd, ht, hsg;
+    memcpy(&hd, hs + p * 192, 64);
+    memcpy(&ht, hs + p * 192 + 64, 64);
+    memcpy(&hsg, hs + p * 192 + 128, 64);
+    void *pd = nullptr, *pt = nullptr, *ps = nullptr;
+    CAR_CHECK(hipIpcOpenMemHandle(&pd, hd, hipIpcMemLazyEnablePeerAccess));
+    CAR_CHECK(hipIpcOpenMemHandle(&pt, ht, hipIpcMemLazyEnablePeerAccess));
+    CAR_CHECK(hipIpcOpenMemHandle(&ps, hsg, hipIpcMemLazyEnablePeerAccess));
+    s->peer_data[p] = static_cast<char*>(pd);
+    s->peer_tmp[p] = static_cast<char*>(pt);
+    s->peer_sig[p] = static_cast<Signal*>(ps);
+  }
+  for (int p = 0; p < kMaxRanks; ++p) {
+    s->args.data[p] = s->peer_data[p];
+    s->args.tmp[p] = s->peer_tmp[p];
+    s->args.sig[p] = s->peer_sig[p];
+  }
+  s->args.rank = s->rank;
+  s->args.world = s->world;
+  s->args.cap = s->cap;
+  s->opened = true;
+  return hipSuccess;
+}
+
+DLBB_API int64_t dlbb_car_capacity(void* h) { return static_cast<CarState*>(h)->cap; }
+
+// algo: 1 = one-shot, 2 = two-shot. nblocks <= 128. dtype: bf16 | f16 | f32.
+// Requirements (checked): nbytes <= cap; nbytes % 16 == 0 (one-shot) or
+// nbytes % (vec_bytes * world) == 0 (two-shot).
+DLBB_API int dlbb_car_allreduce(void* h, const void* inp, void* out, int64_t n, int dtype,
+                                int algo, int nblocks, hipStream_t stream) {
+  CarState* s = static_cast<CarState*>(h);
+  if (!s->opened) return hipErrorNotInitialized;
+  const int64_t esz = dtype == DT_F32 ? 4 : 2;
+  const int64_t vec = 8 * esz;
+  const int64_t nbytes = n * esz;
+  if (nbytes <= 0) return hipSuccess;
+  if (nbytes > s->cap || nbytes % vec != 0) return hipErrorInvalidValue;
+  if (algo == 2 && nbytes % (vec * s->world) != 0) return hipErrorInvalidValue;
+  if (nblocks < 1) nblocks = 1;
+  if (nblocks > kMaxBlocks) nblocks = kMaxBlocks;
+  if (s->world == 1) {
+    if (out != inp) CAR_CHECK(hipMemcpyAsync(out, inp, nbytes, hipMemcpyDeviceToDevice, stream));
+    return hipSuccess;
+  }
+  CarKernelArgs a = s->args;
+  a.inp = inp;
+  a.out = out;
+  a.nbytes = nbytes;
+  const dim3 g(nblocks), b(kCarThreads);
+#define CAR_L(KERN, D) hipLaunchKernelGGL((KERN<D>), g, b, 0, stream, a)
+  if (algo == 2) {
+    if (dtype == DT_BF16) CAR_L(car_twoshot_kernel, DT_BF16);
+    else if (dtype == DT_F16) CAR_L(car_twoshot_kernel, DT_F16);
+    else CAR_L(car_twoshot_kernel, DT_F32);
+  } else {
+    if (dtype == DT_BF16) CAR_L(car_oneshot_kernel, DT_BF16);
+    else if (dtype == DT_F16) CAR_L(car_oneshot_kernel, DT_F16);
+    else CAR_L(car_oneshot_kernel, DT_F32);
+  }
+#undef CAR_L
+  return hipGetLastError();
+}
+
+// Reads (and clears) the device-side timeout flag. Synchronous: call outside timed regions.
+DLBB_API int dlbb_car_error(void* h) {
+  CarState* s = static_cast<CarState*>(h);
+  uint32_t err = 0;
+  CAR_CHECK(hipMemcpy(&err, &s->sig->error, sizeof(err), hipMemcpyDeviceToHost));
+  if (err) {
+    const uint32_t z = 0;
+    CAR_CHECK(hipMemcpy(&s->sig->error, &z, sizeof(z), hipMemcpyHostToDevice));
+  }
+  return static_cast<int>(err);
+}
+
+DLBB_API int dlbb_car_destroy(void* h) {
+  CarState* s = static_cast<CarState*>(h);
+  if (!s) return hipSuccess;
+  (void)hipDeviceSynchronize();
+  for (int p = 0; p < s->world; ++p) {
+    if (p == s->rank || !s->opened) continue;
+    if (s->peer_data[p]) (void)hipIpcCloseMemHandle(s->peer_data[p]);
+    if (s->peer_tmp[p]) (void)hipIpcCloseMemHandle(s->peer_tmp[p]);
+    if (s->peer_sig[p]) (void)hipIpcCloseMemHandle(s->peer_sig[p]);
+  }
+  (void)hipFree(s->data);
+  (void)hipFree(s->tmp);
+  (void)hipFree(s->sig);
+  delete s;
+  return hipSuccess;
+}

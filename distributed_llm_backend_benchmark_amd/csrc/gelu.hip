@@ -1,0 +1,121 @@
+// Bias + GELU, forward and backward.
+//
+// Reference: `torch.nn.functional.gelu(x)` after the column-parallel FFN-up GEMM
+// (models.py:181-182; erf form). GPT-2 uses the tanh form. Forward: y = gelu(x + b) in one
+// 16-byte-vector pass (the same epilogue is also fused into the MFMA GEMM, gemm.hip).
+// Backward: dx = dy * gelu'(x + b), with db = colsum(dx) accumulated in fp32 registers per
+// thread over a row strip and flushed with one float atomic per (column, strip) into an fp32
+// workspace (few atomics: rows / strip per column; CDNA guide Guideline 12), then cast.
+#include "common.h"
+
+namespace dlbb {
+
+template <int APPROX>
+__device__ __forceinline__ float act(float x) { return APPROX ? gelu_tanh(x) : gelu_erf(x); }
+template <int APPROX>
+__device__ __forceinline__ float act_grad(float x) {
+  return APPROX ? gelu_tanh_grad(x) : gelu_erf_grad(x);
+}
+
+// cols % 8 == 0. grid-stride over 8-element vectors.
+template <int APPROX>
+__global__ void __launch_bounds__(256) bias_gelu_fwd_kernel(const uint16_t* __restrict__ x,
+                                                            const uint16_t* __restrict__ b,
+                                                            uint16_t* __restrict__ y,
+                                                            int64_t rows, int cols) {
+  const int64_t cv = cols / 8;
+  const int64_t total = rows * cv;
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < total;
+       i += stride) {
+    float v[8];
+    load8<DT_BF16>(x, i, v);
+    if (b) {
+      float bb[8];
+      load8<DT_BF16>(b, i % cv, bb);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] += bb[j];
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = act<APPROX>(v[j]);
+    store8<DT_BF16>(y, i, v);
+  }
+}
+
+constexpr int kStripRows = 64;
+
+// grid: (ceil(cv / 256), ceil(rows / kStripRows)); thread owns one 8-column vector.
+template <int APPROX>
+__global__ void __launch_bounds__(256) bias_gelu_bwd_kernel(const uint16_t* __restrict__ dy,
+                                                            const uint16_t* __restrict__ x,
+                                                            const uint16_t* __restrict__ b,
+                                                            uint16_t* __restrict__ dx,
+                                                            float* __restrict__ db_ws,
+                                                            int64_t rows, int cols) {
+  const int64_t cv = cols / 8;
+  const int64_t c = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (c >= cv) return;
+  float bb[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (b) load8<DT_BF16>(b, c, bb);
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const int64_t r0 = static_cast<int64_t>(blockIdx.y) * kStripRows;
+  const int64_t r1 = r0 + kStripRows < rows ? r0 + kStripRows : rows;
+  for (int64_t r = r0; r < r1; ++r) {
+    float v[8], g[8];
+    load8<DT_BF16>(x, r * cv + c, v);
+    load8<DT_BF16>(dy, r * cv + c, g);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      g[j] *= act_grad<APPROX>(v[j] + bb[j]);
+      acc[j] += g[j];
+    }
+    store8<DT_BF16>(dx, r * cv + c, g);
+  }
+  if (db_ws) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) atomicAdd(db_ws + c * 8 + j, acc[j]);
+  }
+}
+
+}  // namespace dlbb
+
+using namespace dlbb;
+
+// approx: 0 = erf (torch default, reference models.py:182), 1 = tanh (GPT-2).
+DLBB_API int dlbb_bias_gelu_fwd(const void* x, const void* bias, void* y, int64_t rows, int cols,
+                                int approx, hipStream_t stream) {
+  if (rows <= 0) return hipSuccess;
+  if (cols % 8 != 0) return hipErrorInvalidValue;
+  const int grid = stream_grid(rows * (cols / 8), 256);
+  const uint16_t* xp = static_cast<const uint16_t*>(x);
+  const uint16_t* bp = static_cast<const uint16_t*>(bias);
+  uint16_t* yp = static_cast<uint16_t*>(y);
+  if (approx)
+    hipLaunchKernelGGL(bias_gelu_fwd_kernel<1>, dim3(grid), dim3(256), 0, stream, xp, bp, yp,
+                       rows, cols);
+  else
+    hipLaunchKernelGGL(bias_gelu_fwd_kernel<0>, dim3(grid), dim3(256), 0, stream, xp, bp, yp,
+                       rows, cols);
+  return hipGetLastError();
+}
+
+// db_ws: fp32 [cols] workspace, ZEROED by the caller on the same stream (or null: no dbias).
+DLBB_API int dlbb_bias_gelu_bwd(const void* dy, const void* x, const void* bias, void* dx,
+                                float* db_ws, int64_t rows, int cols, int approx,
+                                hipStream_t stream) {
+  if (rows <= 0) return hipSuccess;
+  if (cols % 8 != 0) return hipErrorInvalidValue;
+  const int64_t cv = cols / 8;
+  const dim3 grid((cv + 255) / 256, (rows + kStripRows - 1) / kStripRows);
+  auto* g = static_cast<const uint16_t*>(dy);
+  auto* xp = static_cast<const uint16_t*>(x);
+  auto* bp = static_cast<const uint16_t*>(bias);
+  auto* o = static_cast<uint16_t*>(dx);
+  if (approx)
+    hipLaunchKernelGGL(bias_gelu_bwd_kernel<1>, grid, dim3(256), 0, stream, g, xp, bp, o, db_ws,
+                       rows, cols);
+  else
+    hipLaunchKernelGGL(bias_gelu_bwd_kernel<0>, grid, dim3(256), 0, stream, g, xp, bp, o, db_ws,
+                       rows, cols);
+  return hipGetLastError();
+}

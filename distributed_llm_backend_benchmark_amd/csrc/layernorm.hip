@@ -1,0 +1,326 @@
+// Fused residual-add + LayerNorm, forward and backward.
+//
+// Reference: nn.LayerNorm(hidden, dtype=bf16) at models.py:122,135,222 applied at
+// models.py:156,177,236, with the residual adds at models.py:173,188. Per transformer block the
+// reference reads/writes the [B,S,H] activation once for the add and twice more for the LN;
+// here h = x + r, y = LN(h) is ONE pass: one wave owns a row, keeps it in registers
+// (NV x 4 elements per lane, 8-byte vector I/O), computes two-pass fp32 statistics with wave
+// shuffles, and writes both y and the new residual stream h.
+//
+// Backward recomputes x_hat from (h, mean, rstd), adds the incoming residual-stream gradient
+// (fusing the residual branch), and produces dgamma/dbeta through per-workgroup fp32 partials
+// + a column reduction (no float atomics, bitwise reproducible).
+#include "common.h"
+
+namespace dlbb {
+
+struct LnFwdArgs {
+  const uint16_t* x;      // [rows, cols] bf16
+  const uint16_t* r;      // optional residual [rows, cols] bf16
+  const void* gamma;      // [cols] bf16 or fp32 (param dtype)
+  const void* beta;       // optional [cols]
+  uint16_t* y;            // [rows, cols] bf16
+  uint16_t* h_out;        // optional: x + r (bf16)
+  float* mean;            // optional [rows]
+  float* rstd;            // optional [rows]
+  int64_t rows;
+  int cols;
+  float eps;
+};
+
+template <int PDT>
+__device__ __forceinline__ float ldp(const void* p, int i) {
+  return PDT == DT_F32 ? static_cast<const float*>(p)[i]
+                       : bf16_to_f32(static_cast<const uint16_t*>(p)[i]);
+}
+
+__device__ __forceinline__ void ld4(const uint16_t* p, int64_t i4, float (&v)[4]) {
+  u16x4 r = reinterpret_cast<const u16x4*>(p)[i4];
+  v[0] = bf16_to_f32(r[0]); v[1] = bf16_to_f32(r[1]);
+  v[2] = bf16_to_f32(r[2]); v[3] = bf16_to_f32(r[3]);
+}
+__device__ __forceinline__ void st4(uint16_t* p, int64_t i4, const float (&v)[4]) {
+  u16x4 r;
+  r[0] = f32_to_bf16(v[0]); r[1] = f32_to_bf16(v[1]);
+  r[2] = f32_to_bf16(v[2]); r[3] = f32_to_bf16(v[3]);
+  reinterpret_cast<u16x4*>(p)[i4] = r;
+}
+__device__ __forceinline__ float round_bf16(float f) { return bf16_to_f32(f32_to_bf16(f)); }
+
+// NV = number of 4-element vectors per lane; cols == NV * 256.
+template <int NV, int PDT>
+__global__ void __launch_bounds__(256) ln_fwd_kernel(LnFwdArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6);
+  if (row >= a.rows) return;
+  const int64_t base4 = row * (a.cols / 4);
+  float v[NV][4];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int64_t c4 = i * 64 + lane;
+    ld4(a.x, base4 + c4, v[i]);
+    if (a.r) {
+      float rr[4];
+      ld4(a.r, base4 + c4, rr);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[i][j] = round_bf16(v[i][j] + rr[j]);
+      if (a.h_out) st4(a.h_out, base4 + c4, v[i]);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) s += v[i][j];
+  }
+  const float inv_c = 1.0f / static_cast<float>(a.cols);
+  const float mean = wave_sum(s) * inv_c;
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float d = v[i][j] - mean;
+      ss += d * d;
+    }
+  const float rstd = rsqrtf(wave_sum(ss) * inv_c + a.eps);
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = (i * 64 + lane) * 4;
+    float o[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float g = ldp<PDT>(a.gamma, c + j);
+      const float b = a.beta ? ldp<PDT>(a.beta, c + j) : 0.f;
+      o[j] = (v[i][j] - mean) * rstd * g + b;
+    }
+    st4(a.y, base4 + i * 64 + lane, o);
+  }
+  if (lane == 0) {
+    if (a.mean) a.mean[row] = mean;
+    if (a.rstd) a.rstd[row] = rstd;
+  }
+}
+
+// Generic fallback for any cols (two passes over global memory, scalar).
+template <int PDT>
+__global__ void __launch_bounds__(256) ln_fwd_generic(LnFwdArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6);
+  if (row >= a.rows) return;
+  const int64_t base = row * a.cols;
+  float s = 0.f;
+  for (int c = lane; c < a.cols; c += 64) {
+    float v = bf16_to_f32(a.x[base + c]);
+    if (a.r) {
+      v = round_bf16(v + bf16_to_f32(a.r[base + c]));
+      if (a.h_out) a.h_out[base + c] = f32_to_bf16(v);
+    }
+    s += v;
+  }
+  const float inv_c = 1.0f / static_cast<float>(a.cols);
+  const float mean = wave_sum(s) * inv_c;
+  float ss = 0.f;
+  for (int c = lane; c < a.cols; c += 64) {
+    float v = bf16_to_f32(a.x[base + c]);
+    if (a.r) v = round_bf16(v + bf16_to_f32(a.r[base + c]));
+    ss += (v - mean) * (v - mean);
+  }
+  const float rstd = rsqrtf(wave_sum(ss) * inv_c + a.eps);
+  for (int c = lane; c < a.cols; c += 64) {
+    float v = bf16_to_f32(a.x[base + c]);
+    if (a.r) v = round_bf16(v + bf16_to_f32(a.r[base + c]));
+    const float b = a.beta ? ldp<PDT>(a.beta, c) : 0.f;
+    a.y[base + c] = f32_to_bf16((v - mean) * rstd * ldp<PDT>(a.gamma, c) + b);
+  }
+  if (lane == 0) {
+    if (a.mean) a.mean[row] = mean;
+    if (a.rstd) a.rstd[row] = rstd;
+  }
+}
+
+struct LnBwdArgs {
+  const uint16_t* dy;     // [rows, cols]
+  const uint16_t* h;      // LN input (x, or x + r) [rows, cols]
+  const void* gamma;
+  const float* mean;
+  const float* rstd;
+  const uint16_t* dres;   // optional gradient already flowing into h (residual stream)
+  uint16_t* dx;           // [rows, cols]: d(LN input) (+ dres)
+  float* dgamma_part;     // [gridDim.x, cols]
+  float* dbeta_part;      // [gridDim.x, cols] (may be null)
+  int64_t rows;
+  int cols;
+};
+
+template <int NV, int PDT>
+__global__ void __launch_bounds__(256) ln_bwd_kernel(LnBwdArgs a) {
+  __shared__ float red[2][4][NV * 256];
+  const int lane = threadIdx.x & 63;
+  const int w = threadIdx.x >> 6;
+  float dg[NV][4], db[NV][4];
+#pragma unroll
+  for (int i = 0; i < NV; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) dg[i][j] = db[i][j] = 0.f;
+  float gam[NV][4];
+#pragma unroll
+  for (int i = 0; i < NV; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) gam[i][j] = ldp<PDT>(a.gamma, (i * 64 + lane) * 4 + j);
+  const float inv_c = 1.0f / static_cast<float>(a.cols);
+  const int64_t nwaves = static_cast<int64_t>(gridDim.x) * 4;
+  for (int64_t row = static_cast<int64_t>(blockIdx.x) * 4 + w; row < a.rows; row += nwaves) {
+    const int64_t base4 = row * (a.cols / 4);
+    const float mu = a.mean[row], rs = a.rstd[row];
+    float xh[NV][4], g[NV][4];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      float hv[4], dyv[4];
+      ld4(a.h, base4 + i * 64 + lane, hv);
+      ld4(a.dy, base4 + i * 64 + lane, dyv);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        xh[i][j] = (hv[j] - mu) * rs;
+        g[i][j] = dyv[j] * gam[i][j];
+        s1 += g[i][j] * xh[i][j];
+        s2 += g[i][j];
+        dg[i][j] += dyv[j] * xh[i][j];
+        db[i][j] += dyv[j];
+      }
+    }
+    const float c1 = wave_sum(s1) * inv_c, c2 = wave_sum(s2) * inv_c;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      float o[4];
+      float dr[4] = {0.f, 0.f, 0.f, 0.f};
+      if (a.dres) ld4(a.dres, base4 + i * 64 + lane, dr);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o[j] = rs * (g[i][j] - xh[i][j] * c1 - c2) + dr[j];
+      st4(a.dx, base4 + i * 64 + lane, o);
+    }
+  }
+  // cross-wave reduction of the dgamma/dbeta partials through LDS
+#pragma unroll
+  for (int i = 0; i < NV; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      red[0][w][(i * 64 + lane) * 4 + j] = dg[i][j];
+      red[1][w][(i * 64 + lane) * 4 + j] = db[i][j];
+    }
+  __syncthreads();
+  for (int c = threadIdx.x; c < a.cols; c += 256) {
+    const float sg = red[0][0][c] + red[0][1][c] + red[0][2][c] + red[0][3][c];
+    const float sb = red[1][0][c] + red[1][1][c] + red[1][2][c] + red[1][3][c];
+    a.dgamma_part[static_cast<int64_t>(blockIdx.x) * a.cols + c] = sg;
+    if (a.dbeta_part) a.dbeta_part[static_cast<int64_t>(blockIdx.x) * a.cols + c] = sb;
+  }
+}
+
+// out[c] = sum_b part[b, c]  (fp32 accumulate, out in bf16 or fp32)
+template <int DTO>
+__global__ void __launch_bounds__(256) col_reduce_kernel(const float* __restrict__ part,
+                                                         int nparts, int cols, void* out) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= cols) return;
+  float s = 0.f;
+  for (int b = 0; b < nparts; ++b) s += part[static_cast<int64_t>(b) * cols + c];
+  Elem<DTO>::st(static_cast<typename Elem<DTO>::T*>(out), c, s);
+}
+
+template <int NV, int PDT>
+static hipError_t fwd_nv(const LnFwdArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL((ln_fwd_kernel<NV, PDT>), dim3((a.rows + 3) / 4), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+template <int PDT>
+static hipError_t fwd_dispatch(const LnFwdArgs& a, hipStream_t s) {
+  if (a.cols % 256 == 0) {
+    switch (a.cols / 256) {
+      case 1: return fwd_nv<1, PDT>(a, s);
+      case 2: return fwd_nv<2, PDT>(a, s);
+      case 3: return fwd_nv<3, PDT>(a, s);
+      case 4: return fwd_nv<4, PDT>(a, s);
+      case 5: return fwd_nv<5, PDT>(a, s);
+      case 6: return fwd_nv<6, PDT>(a, s);
+      case 8: return fwd_nv<8, PDT>(a, s);
+      case 10: return fwd_nv<10, PDT>(a, s);
+      case 12: return fwd_nv<12, PDT>(a, s);
+      case 16: return fwd_nv<16, PDT>(a, s);
+      case 20: return fwd_nv<20, PDT>(a, s);
+      case 24: return fwd_nv<24, PDT>(a, s);
+      case 32: return fwd_nv<32, PDT>(a, s);
+      default: break;
+    }
+  }
+  hipLaunchKernelGGL((ln_fwd_generic<PDT>), dim3((a.rows + 3) / 4), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+template <int NV, int PDT>
+static hipError_t bwd_nv(const LnBwdArgs& a, int grid, hipStream_t s) {
+  hipLaunchKernelGGL((ln_bwd_kernel<NV, PDT>), dim3(grid), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+}  // namespace dlbb
+
+using namespace dlbb;
+
+DLBB_API int dlbb_layernorm_fwd(const void* x, const void* residual, const void* gamma,
+                                const void* beta, int param_dtype, void* y, void* h_out,
+                                float* mean, float* rstd, int64_t rows, int cols, float eps,
+                                hipStream_t stream) {
+  if (rows <= 0) return hipSuccess;
+  if (cols <= 0 || cols % 4 != 0) return hipErrorInvalidValue;
+  LnFwdArgs a{static_cast<const uint16_t*>(x), static_cast<const uint16_t*>(residual), gamma,
+              beta, static_cast<uint16_t*>(y), static_cast<uint16_t*>(h_out), mean, rstd,
+              rows, cols, eps};
+  return param_dtype == DT_F32 ? fwd_dispatch<DT_F32>(a, stream)
+                               : fwd_dispatch<DT_BF16>(a, stream);
+}
+
+// Supported widths for the backward: cols in {256,512,768,1024,1536,2048,3072,4096}
+// (LDS: 2 x 4 x cols floats <= 128 KiB). Returns the number of partial rows the caller
+// must provide via `max_parts` query: call with dx == nullptr to get the grid size.
+DLBB_API int dlbb_layernorm_bwd_grid(int64_t rows) {
+  int64_t g = (rows + 3) / 4;
+  if (g > 512) g = 512;
+  return static_cast<int>(g < 1 ? 1 : g);
+}
+
+DLBB_API int dlbb_layernorm_bwd(const void* dy, const void* h, const void* gamma, int param_dtype,
+                                const float* mean, const float* rstd, const void* dres, void* dx,
+                                float* part_ws, void* dgamma, void* dbeta, int64_t rows,
+                                int cols, hipStream_t stream) {
+  if (rows <= 0) return hipSuccess;
+  if (cols % 256 != 0) return hipErrorInvalidValue;
+  const int grid = dlbb_layernorm_bwd_grid(rows);
+  float* pg = part_ws;
+  float* pb = dbeta ? part_ws + static_cast<int64_t>(grid) * cols : nullptr;
+  LnBwdArgs a{static_cast<const uint16_t*>(dy), static_cast<const uint16_t*>(h), gamma, mean,
+              rstd, static_cast<const uint16_t*>(dres), static_cast<uint16_t*>(dx), pg, pb,
+              rows, cols};
+  hipError_t e = hipErrorInvalidValue;
+#define LB(NV)                                                                   \
+  case NV:                                                                       \
+    e = param_dtype == DT_F32 ? bwd_nv<NV, DT_F32>(a, grid, stream)              \
+                              : bwd_nv<NV, DT_BF16>(a, grid, stream);            \
+    break;
+  switch (cols / 256) {
+    LB(1) LB(2) LB(3) LB(4) LB(6) LB(8) LB(12) LB(16)
+    default: return hipErrorInvalidValue;
+  }
+#undef LB
+  if (e != hipSuccess) return e;
+  const dim3 cg((cols + 255) / 256), cb(256);
+  if (param_dtype == DT_F32) {
+    hipLaunchKernelGGL((col_reduce_kernel<DT_F32>), cg, cb, 0, stream, pg, grid, cols, dgamma);
+    if (dbeta)
+      hipLaunchKernelGGL((col_reduce_kernel<DT_F32>), cg, cb, 0, stream, pb, grid, cols, dbeta);
+  } else {
+    hipLaunchKernelGGL((col_reduce_kernel<DT_BF16>), cg, cb, 0, stream, pg, grid, cols, dgamma);
+    if (dbeta)
+      hipLaunchKernelGGL((col_reduce_kernel<DT_BF16>), cg, cb, 0, stream, pb, grid, cols, dbeta);
+  }
+  return hipGetLastError();
+}

@@ -1,0 +1,118 @@
+"""GPT-2 (small by default) for the DDP training microbenchmark (BASELINE config 5: "GPT-2-small
+DDP training microbench (models.py path), grad-bucket all-reduce overlapped with backward").
+
+The reference's only training step is a 10→20→5 MLP under DeepSpeed ZeRO-2 (``test/ccl.py:59-117``)
+and its transformer is forward-only (``models.py``); this model is the training-side family the
+north star asks for, built from the same gfx950 kernels as the TP model:
+
+* residual adds fused into the following LayerNorm (``ops.layernorm(x, residual=h)``),
+* QKV / attention-out / MLP / LM-head GEMMs on the MFMA kernel with fused bias and, for c_fc,
+  fused tanh-GELU (pre-activation kept for backward),
+* causal attention via ``F.scaled_dot_product_attention`` (ROCm flash/efficient backends).
+
+All parameters are bf16 working copies (the trainer keeps fp32 masters); vocab is padded to a
+multiple of 128 (50257 → 50304) so the tied LM-head GEMM fits the MFMA tiling.
+Weights: N(0, 0.02), residual projections scaled by 1/sqrt(2*n_layer) (GPT-2 init).
+"""
+
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .. import ops
+from ..ops.linear_fn import linear_train
+
+
+@dataclass
+class GPT2Config:
+    vocab_size: int = 50304
+    block_size: int = 1024
+    n_layer: int = 12
+    n_head: int = 12
+    n_embd: int = 768
+
+
+def _param(shape, std, device, gen, dtype=torch.bfloat16):
+    t = torch.zeros(*shape, device=device, dtype=torch.float32)
+    if std > 0:
+        t.normal_(0.0, std, generator=gen)
+    return nn.Parameter(t.to(dtype))
+
+
+class LN(nn.Module):
+    def __init__(self, d, device):
+        super().__init__()
+        self.weight = nn.Parameter(torch.ones(d, device=device, dtype=torch.bfloat16))
+        self.bias = nn.Parameter(torch.zeros(d, device=device, dtype=torch.bfloat16))
+
+    def forward(self, x, residual=None):
+        y, h = ops.layernorm(x, self.weight, self.bias, 1e-5, residual=residual)
+        return y, (h if h is not None else x)
+
+
+class Block(nn.Module):
+    def __init__(self, cfg: GPT2Config, device, gen):
+        super().__init__()
+        d = cfg.n_embd
+        proj_std = 0.02 / math.sqrt(2 * cfg.n_layer)
+        self.n_head = cfg.n_head
+        self.ln_1 = LN(d, device)
+        self.attn_w = _param((3 * d, d), 0.02, device, gen)
+        self.attn_b = _param((3 * d,), 0.0, device, gen)
+        self.attn_proj_w = _param((d, d), proj_std, device, gen)
+        self.attn_proj_b = _param((d,), 0.0, device, gen)
+        self.ln_2 = LN(d, device)
+        self.fc_w = _param((4 * d, d), 0.02, device, gen)
+        self.fc_b = _param((4 * d,), 0.0, device, gen)
+        self.mlp_proj_w = _param((d, 4 * d), proj_std, device, gen)
+        self.mlp_proj_b = _param((d,), 0.0, device, gen)
+
+    def forward(self, y1, h):
+        B, T, C = y1.shape
+        qkv = linear_train(y1, self.attn_w, self.attn_b)
+        q, k, v = qkv.view(B, T, 3, self.n_head, C // self.n_head).permute(2, 0, 3, 1, 4).unbind(0)
+        att = F.scaled_dot_product_attention(q, k, v, is_causal=True)
+        att = att.transpose(1, 2).reshape(B, T, C)
+        a = linear_train(att, self.attn_proj_w, self.attn_proj_b)
+        y2, h = self.ln_2(a, residual=h)
+        g = linear_train(y2, self.fc_w, self.fc_b, act="gelu_tanh")
+        d = linear_train(g, self.mlp_proj_w, self.mlp_proj_b)
+        return d, h
+
+
+class GPT2(nn.Module):
+    def __init__(self, cfg: GPT2Config, device=torch.device("cpu"), seed: int = 1234):
+        super().__init__()
+        self.cfg = cfg
+        gen = torch.Generator(device=device)
+        gen.manual_seed(seed)
+        self.wte = _param((cfg.vocab_size, cfg.n_embd), 0.02, device, gen)
+        self.wpe = _param((cfg.block_size, cfg.n_embd), 0.01, device, gen)
+        self.blocks = nn.ModuleList([Block(cfg, device, gen) for _ in range(cfg.n_layer)])
+        self.ln_f = LN(cfg.n_embd, device)
+
+    def forward(self, idx, targets=None):
+        B, T = idx.shape
+        x = F.embedding(idx, self.wte) + self.wpe[:T]
+        y, h = self.blocks[0].ln_1(x)
+        for i, blk in enumerate(self.blocks):
+            d, h = blk(y, h)
+            nxt = self.blocks[i + 1].ln_1 if i + 1 < len(self.blocks) else self.ln_f
+            y, h = nxt(d, residual=h)
+        logits = linear_train(y, self.wte)
+        if targets is None:
+            return logits
+        return F.cross_entropy(logits.float().view(-1, logits.shape[-1]), targets.reshape(-1))
+
+    def num_parameters(self) -> int:
+        return sum(p.numel() for p in self.parameters())
+
+    def flops_per_token(self, T: int) -> float:
+        """6N + attention (12 * L * T * d) per token, the standard transformer estimate."""
+        n = self.num_parameters() - self.wpe.numel()
+        return 6.0 * n + 12.0 * self.cfg.n_layer * T * self.cfg.n_embd

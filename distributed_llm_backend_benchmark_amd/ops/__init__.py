@@ -1,0 +1,20 @@
+"""Python entry points of the gfx950 HIP kernel library (``csrc/`` -> ``_dlbb_hip.so``).
+
+* :mod:`.elementwise` — n-way sum-reduce, cast, strided pack, multi-tensor chunk copy
+  (flatten/unflatten/all-to-all packing).
+* :mod:`.gemm` — MFMA bf16 GEMM with fused bias / GELU / residual epilogues.
+* :mod:`.norm_act` — fused residual+LayerNorm and bias+GELU (fwd + bwd, autograd).
+* :mod:`.optim` — flat fused AdamW.
+* :mod:`._lib` — loader; ``available()``, ``loaded_path()``.
+"""
+
+from . import _lib
+from ._lib import available, loaded_path, KernelError
+from .elementwise import reduce_sum, cast, pack_rows, ChunkTable, ScaleTable, flatten_into
+from .gemm import linear
+from .norm_act import layernorm, bias_gelu
+from .optim import FlatAdamW
+
+__all__ = ["available", "loaded_path", "KernelError", "reduce_sum", "cast", "pack_rows",
+           "ChunkTable", "ScaleTable", "flatten_into", "linear", "layernorm", "bias_gelu",
+           "FlatAdamW"]

@@ -1,0 +1,82 @@
+"""Trainable linear: MFMA forward with fused bias/GELU epilogue, library GEMMs for backward.
+
+Forward: ``y = act(x @ W^T + b)`` through the hand-written MFMA kernel (``csrc/gemm.hip``);
+with an activation the epilogue also stores the pre-activation ``u`` (needed by the GELU
+backward). Backward: ``dU = dY * act'(u)`` and ``db = colsum(dU)`` in one pass of the bias-GELU
+backward kernel (``csrc/gelu.hip``); ``dX = dU @ W`` and ``dW = dU^T @ X`` are plain library
+GEMMs (hipBLASLt through ``torch.matmul``), as allowed for unfused GEMMs.
+"""
+
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+import torch.nn.functional as F
+
+from . import _lib
+from ._lib import check, use_hip
+from .gemm import hip_supported, linear as _linear
+
+_APPROX = {"gelu": 0, "gelu_erf": 0, "gelu_tanh": 1}
+
+
+class _LinearFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b, act):
+        K = x.shape[-1]
+        x2 = x.reshape(-1, K)
+        if x2.stride(-1) != 1 or x2.stride(0) % 8:
+            x2 = x2.contiguous()
+        M, N = x2.shape[0], w.shape[0]
+        u = None
+        if act is not None:
+            u = torch.empty(M, N, dtype=x.dtype, device=x.device)
+        y = _linear(x2, w, bias=b, act=act, preact=u)
+        ctx.save_for_backward(x2, w, u)
+        ctx.has_bias = b is not None
+        ctx.act = act
+        ctx.lead = x.shape[:-1]
+        return y.view(*x.shape[:-1], N)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, w, u = ctx.saved_tensors
+        M, K = x2.shape
+        N = w.shape[0]
+        dy2 = dy.reshape(M, N)
+        if not dy2.is_contiguous():
+            dy2 = dy2.contiguous()
+        db = None
+        if ctx.act is not None:
+            du = torch.empty_like(u)
+            ws = torch.zeros(N, dtype=torch.float32, device=u.device) if ctx.has_bias else None
+            check(_lib.lib().dlbb_bias_gelu_bwd(dy2.data_ptr(), u.data_ptr(), None, du.data_ptr(),
+                                                _lib.ptr(ws), M, N, _APPROX[ctx.act],
+                                                _lib.stream(u.device)), "bias_gelu_bwd")
+            if ctx.has_bias:
+                db = ws.to(w.dtype)
+        else:
+            du = dy2
+            if ctx.has_bias:
+                db = du.sum(0, dtype=torch.float32).to(w.dtype)
+        dx = torch.matmul(du, w) if ctx.needs_input_grad[0] else None
+        dw = torch.matmul(du.t(), x2) if ctx.needs_input_grad[1] else None
+        if dx is not None:
+            dx = dx.view(*ctx.lead, K)
+        return dx, dw, db, None
+
+
+def linear_train(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor] = None,
+                 act: Optional[str] = None) -> torch.Tensor:
+    """Autograd-aware ``act(x @ w.T + b)``; HIP MFMA forward on GPU tensors."""
+    if use_hip(x, w) and hip_supported(x.reshape(-1, x.shape[-1]), w):
+        if act is not None and w.shape[0] % 8:
+            raise _lib.KernelError("linear_train with activation needs N % 8 == 0")
+        return _LinearFn.apply(x, w, b, act)
+    y = F.linear(x, w, b)
+    if act in ("gelu", "gelu_erf"):
+        y = F.gelu(y)
+    elif act == "gelu_tanh":
+        y = F.gelu(y, approximate="tanh")
+    return y

@@ -1,0 +1,178 @@
+"""Process-group layer: ONE ``torch.distributed`` group per job.
+
+Replaces the reference's four CPU launch/backends (mpi4py ``COMM_WORLD``
+``run_mpi.py:29-43``, ``deepspeed.init_distributed(dist_backend=...)``
+``collectives/1d/dsccl.py:47-57``) with:
+
+* ``rccl`` — ``torch.distributed`` backend ``"nccl"``, which on ROCm is RCCL over xGMI.
+  One process per GPU; ``LOCAL_RANK`` selects the device.
+* ``gloo`` — CPU plumbing backend (BASELINE config 1, tests).
+
+Rendezvous comes from the launcher env (``torchrun``: RANK/WORLD_SIZE/LOCAL_RANK/MASTER_ADDR/
+MASTER_PORT). Without it a single-process world is created on 127.0.0.1. A process-group
+timeout makes a hung collective fail fast instead of eating the job's time limit
+(SURVEY §5.3).
+"""
+
+from __future__ import annotations
+
+import datetime
+import os
+import socket
+from dataclasses import dataclass, field
+from typing import Any, List, Optional, Sequence
+
+import torch
+import torch.distributed as dist
+
+BACKEND_ALIASES = {"rccl": "nccl", "nccl": "nccl", "gloo": "gloo", "cpu": "gloo"}
+
+
+def _free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def resolve_backend(name: str = "auto") -> str:
+    name = (name or "auto").lower()
+    if name == "auto":
+        return "nccl" if torch.cuda.is_available() else "gloo"
+    if name not in BACKEND_ALIASES:
+        raise ValueError(f"unknown backend {name!r}; expected rccl|gloo|auto")
+    return BACKEND_ALIASES[name]
+
+
+@dataclass
+class Comm:
+    """Thin handle over the default process group plus the rank's device."""
+
+    rank: int
+    world_size: int
+    local_rank: int
+    backend: str               # torch backend string: "nccl" (RCCL) or "gloo"
+    device: torch.device
+    owns_pg: bool = False
+    _extra: dict = field(default_factory=dict)
+
+    @property
+    def is_gpu(self) -> bool:
+        return self.device.type == "cuda"
+
+    @property
+    def backend_label(self) -> str:
+        return "rccl" if self.backend == "nccl" else self.backend
+
+    # ---------------------------------------------------------------- sync helpers
+    def barrier(self) -> None:
+        if self.world_size == 1:
+            if self.is_gpu:
+                torch.cuda.synchronize(self.device)
+            return
+        if self.backend == "nccl":
+            dist.barrier(device_ids=[self.device.index])
+        else:
+            dist.barrier()
+
+    def sync(self) -> None:
+        if self.is_gpu:
+            torch.cuda.synchronize(self.device)
+
+    # ---------------------------------------------------------------- side channel
+    def gather_floats(self, values: Sequence[float], dst: int = 0) -> Optional[List[List[float]]]:
+        """Gather a per-rank list of floats to ``dst`` as ``[rank][i]``.
+
+        Reference: ``comm.gather(timings)`` (``collectives/1d/openmpi.py:270``) and
+        ``dist.gather(float64 tensor)`` (``collectives/1d/dsccl.py:225-232``). Lists may differ
+        in length across ranks, so lengths travel first.
+        """
+        if self.world_size == 1:
+            return [list(map(float, values))]
+        dev = self.device if self.backend == "nccl" else torch.device("cpu")
+        n = torch.tensor([len(values)], dtype=torch.int64, device=dev)
+        ns = [torch.zeros_like(n) for _ in range(self.world_size)]
+        dist.all_gather(ns, n)
+        nmax = int(max(int(x.item()) for x in ns))
+        buf = torch.zeros(nmax, dtype=torch.float64, device=dev)
+        if len(values):
+            buf[: len(values)] = torch.tensor(list(values), dtype=torch.float64, device=dev)
+        outs = [torch.zeros_like(buf) for _ in range(self.world_size)]
+        dist.all_gather(outs, buf)
+        if self.rank != dst:
+            return None
+        return [outs[r][: int(ns[r].item())].cpu().tolist() for r in range(self.world_size)]
+
+    def all_gather_object(self, obj: Any) -> List[Any]:
+        if self.world_size == 1:
+            return [obj]
+        out: List[Any] = [None] * self.world_size
+        dist.all_gather_object(out, obj)
+        return out
+
+    def broadcast_object(self, obj: Any, src: int = 0) -> Any:
+        if self.world_size == 1:
+            return obj
+        lst = [obj]
+        dist.broadcast_object_list(lst, src=src)
+        return lst[0]
+
+    def allreduce_max(self, x: float) -> float:
+        if self.world_size == 1:
+            return float(x)
+        dev = self.device if self.backend == "nccl" else torch.device("cpu")
+        t = torch.tensor([float(x)], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def destroy(self) -> None:
+        if self.owns_pg and dist.is_initialized():
+            try:
+                dist.destroy_process_group()
+            except Exception:
+                pass
+
+
+def init_distributed(backend: str = "auto", timeout_s: float = 600.0,
+                     device: Optional[str] = None) -> Comm:
+    """Initialise (or attach to) the default process group.
+
+    ``backend``: ``rccl`` | ``nccl`` | ``gloo`` | ``auto``. ``device`` overrides the device
+    choice (``"cpu"`` forces CPU tensors even on a GPU box, e.g. gloo plumbing runs).
+    """
+    be = resolve_backend(backend)
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", str(rank)))
+
+    if be == "nccl":
+        if not torch.cuda.is_available():
+            raise RuntimeError("backend rccl requested but no HIP device is visible")
+        ndev = torch.cuda.device_count()
+        dev_index = local_rank % ndev
+        torch.cuda.set_device(dev_index)
+        dev = torch.device("cuda", dev_index)
+    else:
+        dev = torch.device(device or "cpu")
+        if dev.type == "cuda":
+            torch.cuda.set_device(local_rank % torch.cuda.device_count())
+            dev = torch.device("cuda", torch.cuda.current_device())
+
+    owns = False
+    if not dist.is_initialized():
+        kwargs = dict(backend=be, rank=rank, world_size=world,
+                      timeout=datetime.timedelta(seconds=timeout_s))
+        if "WORLD_SIZE" not in os.environ:
+            # standalone single process: private rendezvous on a fresh loopback port
+            kwargs["init_method"] = f"tcp://127.0.0.1:{_free_port()}"
+        else:
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            if "MASTER_PORT" not in os.environ:
+                raise RuntimeError("MASTER_PORT must be set when WORLD_SIZE is set")
+        if be == "nccl":
+            kwargs["device_id"] = dev  # eager RCCL communicator init, fixed device binding
+        dist.init_process_group(**kwargs)
+        owns = True
+    else:
+        rank, world = dist.get_rank(), dist.get_world_size()
+    return Comm(rank=rank, world_size=world, local_rank=local_rank, backend=be,
+                device=dev, owns_pg=owns)

@@ -1,0 +1,192 @@
+"""Data-parallel training with bucketed gradient all-reduce overlapped with backward.
+
+The reference's data parallelism is DeepSpeed's engine in smoke tests only
+(``test/ccl.py:74-115`` ZeRO-2, ``test/ds_mpi_test.py:13-47``, ``test/test.py:16-41``); the
+gradient reduction happens inside ``model_engine.backward`` and is never timed. This module is
+the MI355X-native replacement used by the GPT-2 DDP microbenchmark:
+
+* **Flat buffers, sized for 288 GB HBM.** All trainable parameters live in ONE flat bf16 buffer
+  (params become views), with ONE fp32 master copy and ONE flat bf16 gradient buffer whose
+  slices are the parameters' ``.grad`` — autograd accumulates straight into the buckets, so no
+  flatten/copy pass exists at all (``mode="view"``). ``mode="flatten"`` instead lets autograd
+  allocate grads and copies each ready bucket with the one-launch multi-tensor chunk-copy kernel.
+* **Buckets in backward order** (parameters laid out in reverse registration order), capped at
+  ``bucket_mb`` (default 64 MiB: on xGMI the ring all-reduce is link-bound, so few large
+  buckets amortise RCCL launch/protocol cost; still several buckets so the first all-reduce
+  starts early in backward).
+* **Overlap**: a post-accumulate-grad hook counts ready params; a full bucket is all-reduced
+  asynchronously (RCCL runs on ProcessGroupNCCL's own high-priority stream, ordered after the
+  producing kernels by an event), strictly in bucket order on every rank (identical collective
+  order — RCCL would hang otherwise). ``finish()`` waits the works; the optimizer consumes the
+  reduced flat gradient with the 1/world average fused into the AdamW kernel.
+* ``allreduce="custom"`` routes buckets that fit through the IPC xGMI kernel on a dedicated
+  comm stream instead.
+"""
+
+from __future__ import annotations
+
+from typing import List, Optional
+
+import torch
+import torch.distributed as dist
+
+from ..ops import FlatAdamW
+from ..ops.elementwise import ChunkTable
+from .comm import Comm
+
+_ALIGN = 64  # elements: keeps every param view 128-B aligned (16-B MFMA/glds rows)
+
+
+class _Bucket:
+    def __init__(self, idx: int, start: int, end: int, params: List[torch.nn.Parameter]):
+        self.idx, self.start, self.end = idx, start, end
+        self.params = params
+        self.ready = 0
+        self.launched = False
+        self.work = None
+        self.table: Optional[ChunkTable] = None
+
+
+class FlatParamTrainer:
+    def __init__(self, model: torch.nn.Module, comm: Optional[Comm], lr: float = 3e-4,
+                 betas=(0.9, 0.95), weight_decay: float = 0.0, bucket_mb: float = 64.0,
+                 overlap: bool = True, mode: str = "view", allreduce: str = "rccl",
+                 grad_dtype: torch.dtype = torch.bfloat16):
+        self.model = model
+        self.comm = comm
+        self.world = comm.world_size if comm is not None else 1
+        self.overlap = overlap
+        self.mode = mode
+        self.allreduce = allreduce
+        params = []
+        seen = set()
+        for p in model.parameters():
+            if p.requires_grad and id(p) not in seen:
+                seen.add(id(p))
+                params.append(p)
+        order = list(reversed(params))          # backward produces grads roughly in reverse
+        dev = params[0].device
+        offs, total = [], 0
+        for p in order:
+            offs.append(total)
+            total += (p.numel() + _ALIGN - 1) // _ALIGN * _ALIGN
+        self.numel = total
+        self.flat_param = torch.zeros(total, dtype=torch.bfloat16, device=dev)
+        self.flat_grad = torch.zeros(total, dtype=grad_dtype, device=dev)
+        with torch.no_grad():
+            for p, o in zip(order, offs):
+                view = self.flat_param[o:o + p.numel()].view_as(p)
+                view.copy_(p.data)
+                p.data = view
+        self.master = self.flat_param.float()
+        self.opt = FlatAdamW(self.master, lr=lr, betas=betas, weight_decay=weight_decay)
+        # buckets
+        cap = int(bucket_mb * (1 << 20) / self.flat_grad.element_size())
+        self.buckets: List[_Bucket] = []
+        self._bucket_of = {}
+        cur: List[torch.nn.Parameter] = []
+        start = 0
+        for p, o in zip(order, offs):
+            end = o + (p.numel() + _ALIGN - 1) // _ALIGN * _ALIGN
+            cur.append(p)
+            if end - start >= cap:
+                self._add_bucket(start, end, cur)
+                cur, start = [], end
+        if cur:
+            self._add_bucket(start, total, cur)
+        self._offsets = {id(p): o for p, o in zip(order, offs)}
+        self._params = order
+        if mode == "view":
+            for p, o in zip(order, offs):
+                p.grad = self.flat_grad[o:o + p.numel()].view_as(p)
+        self._hooks = [p.register_post_accumulate_grad_hook(self._on_grad) for p in order]
+        self._next = 0
+        self._comm_stream = None
+        self._car = None
+        if allreduce == "custom" and comm is not None and comm.is_gpu and self.world > 1:
+            from .custom_allreduce import get_custom_allreduce
+
+            self._car = get_custom_allreduce(comm)
+            self._comm_stream = torch.cuda.Stream(dev, priority=-1)
+        self.step_count = 0
+
+    # ------------------------------------------------------------------ buckets
+    def _add_bucket(self, start: int, end: int, params) -> None:
+        b = _Bucket(len(self.buckets), start, end, list(params))
+        for p in params:
+            self._bucket_of[id(p)] = b
+        self.buckets.append(b)
+
+    def _reset(self) -> None:
+        for b in self.buckets:
+            b.ready, b.launched, b.work = 0, False, None
+        self._next = 0
+
+    def _on_grad(self, p: torch.nn.Parameter) -> None:
+        b = self._bucket_of[id(p)]
+        b.ready += 1
+        if self.overlap and b.ready == len(b.params):
+            self._launch_ready()
+
+    def _launch_ready(self) -> None:
+        while self._next < len(self.buckets):
+            b = self.buckets[self._next]
+            if b.ready < len(b.params):
+                return
+            self._launch(b)
+            self._next += 1
+
+    def _launch(self, b: _Bucket) -> None:
+        b.launched = True
+        if self.mode == "flatten":
+            if b.table is None:
+                pairs = [(p.grad.reshape(-1), self.flat_grad[self._offsets[id(p)]:
+                                                              self._offsets[id(p)] + p.numel()])
+                         for p in b.params]
+                b.table = ChunkTable(pairs)
+            b.table.run()
+        if self.world == 1:
+            return
+        buf = self.flat_grad[b.start:b.end]
+        if self._car is not None and self._car.healthy and self._car.supports(buf):
+            cs = self._comm_stream
+            cs.wait_stream(torch.cuda.current_stream(buf.device))
+            with torch.cuda.stream(cs):
+                self._car.all_reduce_(buf)
+            b.work = "custom"
+        else:
+            b.work = dist.all_reduce(buf, async_op=True)
+
+    def finish(self) -> None:
+        """Launch what backward did not (e.g. overlap off), then wait every bucket."""
+        while self._next < len(self.buckets):
+            self._launch(self.buckets[self._next])
+            self._next += 1
+        for b in self.buckets:
+            if b.work == "custom":
+                torch.cuda.current_stream(self.flat_grad.device).wait_stream(self._comm_stream)
+            elif b.work is not None:
+                b.work.wait()
+
+    # ------------------------------------------------------------------ step
+    def zero_grad(self) -> None:
+        if self.mode == "view":
+            self.flat_grad.zero_()
+        else:
+            for p in self._params:
+                p.grad = None
+
+    def step(self, idx: torch.Tensor, targets: torch.Tensor, sync_loss: bool = True):
+        """One full training step: forward, backward (+ overlapped all-reduce), AdamW."""
+        self.zero_grad()
+        self._reset()
+        loss = self.model(idx, targets)
+        loss.backward()
+        self.finish()
+        self.step_count += 1
+        self.opt.step(self.flat_grad, working_bf16=self.flat_param, grad_scale=1.0 / self.world)
+        return float(loss.item()) if sync_loss else loss.detach()
+
+    def close(self) -> None:
+        for h in self._hooks:
+            h.remove()

@@ -1,0 +1,107 @@
+"""Megatron-1D tensor-parallel linears.
+
+Reference: ``ColumnParallelLinear`` (``models.py:19-47``; out-features sharded, ``:33``) and
+``RowParallelLinear`` (``models.py:50-100``; in-features sharded, ``:66``; partial outputs
+summed by ``comm.Allreduce`` on fp32 host numpy buffers, ``:84-98``).
+
+MI355X design:
+* weights are stored ``[out, in]`` (K-contiguous, MFMA-native) bf16 on the device;
+* the GEMM is the hand-written MFMA kernel (``ops.linear``) with GELU fused into the
+  column-parallel FFN-up epilogue;
+* the row-parallel partial sum is all-reduced ON DEVICE: bf16 over RCCL by default, or the
+  reference's fp32 wire format (GEMM epilogue writes fp32 directly — no cast pass), or the IPC
+  one-shot/two-shot xGMI kernel; the residual add is NOT done here but fused into the next
+  LayerNorm (``ops.layernorm(x, residual=...)``).
+"""
+
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+import torch.nn as nn
+
+from .. import ops
+from .comm import Comm
+
+
+def _randn_weight(out_f: int, in_f: int, device, dtype, generator, std: float) -> nn.Parameter:
+    w = torch.empty(out_f, in_f, device=device, dtype=torch.float32)
+    w.normal_(0.0, std, generator=generator)
+    return nn.Parameter(w.to(dtype), requires_grad=False)
+
+
+class ColumnParallelLinear(nn.Module):
+    """y_local = act(x @ W_local^T); W_local = rows [rank*out/P, (rank+1)*out/P) of W."""
+
+    def __init__(self, in_features: int, out_features: int, comm: Comm,
+                 dtype=torch.bfloat16, generator=None, std: float = 1.0,
+                 kernels: str = "hip"):
+        super().__init__()
+        P = comm.world_size
+        if out_features % P:
+            raise ValueError(f"out_features {out_features} not divisible by world {P}")
+        self.in_features, self.out_features = in_features, out_features
+        self.out_per_rank = out_features // P
+        self.kernels = kernels
+        self.weight = _randn_weight(self.out_per_rank, in_features, comm.device, dtype,
+                                    generator, std)
+
+    def forward(self, x: torch.Tensor, act: Optional[str] = None) -> torch.Tensor:
+        if self.kernels == "torch":
+            y = x @ self.weight.t()
+            return torch.nn.functional.gelu(y) if act else y
+        return ops.linear(x, self.weight, act=act)
+
+
+class RowParallelLinear(nn.Module):
+    """y = allreduce_sum(x_local @ W_local^T); W_local = columns of W for this rank's shard."""
+
+    def __init__(self, in_features: int, out_features: int, comm: Comm,
+                 dtype=torch.bfloat16, generator=None, std: float = 1.0,
+                 allreduce: str = "rccl", allreduce_dtype: str = "bf16",
+                 kernels: str = "hip"):
+        super().__init__()
+        P = comm.world_size
+        if in_features % P:
+            raise ValueError(f"in_features {in_features} not divisible by world {P}")
+        self.comm = comm
+        self.in_features, self.out_features = in_features, out_features
+        self.in_per_rank = in_features // P
+        self.allreduce = allreduce
+        self.allreduce_dtype = allreduce_dtype
+        self.kernels = kernels
+        self.weight = _randn_weight(out_features, self.in_per_rank, comm.device, dtype,
+                                    generator, std)
+        self._car = None
+        if allreduce in ("custom", "auto") and comm.is_gpu and comm.world_size > 1:
+            from .custom_allreduce import get_custom_allreduce
+
+            self._car = get_custom_allreduce(comm)
+        self.comm_bytes = 0   # bytes all-reduced by this layer (accounting)
+
+    def _all_reduce(self, t: torch.Tensor) -> None:
+        self.comm_bytes += t.numel() * t.element_size()
+        if self.comm.world_size == 1:
+            return
+        car = self._car
+        if car is not None and (self.allreduce == "custom" or car.should_use(t)) \
+                and car.supports(t):
+            car.all_reduce_(t)
+        else:
+            dist.all_reduce(t)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        fp32_wire = self.allreduce_dtype == "fp32"
+        if self.kernels == "torch":
+            y = x @ self.weight.t()
+            if fp32_wire:
+                y = y.float()
+            self._all_reduce(y)
+            return y.to(x.dtype)
+        y = ops.linear(x, self.weight, out_dtype=torch.float32 if fp32_wire else x.dtype)
+        self._all_reduce(y)
+        if fp32_wire:
+            return ops.cast(y, x.dtype)   # HIP cast kernel (reference models.py:98)
+        return y

@@ -1,0 +1,81 @@
+"""Bandwidth conventions.
+
+Two conventions are reported side by side:
+
+* ``legacy_bandwidth_gbps`` — the reference's own column, ``N·2·P / max_time / 2^30`` for
+  EVERY op with the element size hard-wired to 2 bytes (reference ``collectives/1d/stats.py:77-129``).
+  Kept bit-compatible so our CSVs line up with the committed reference CSVs.
+* ``algbw`` / ``busbw`` (GB/s, 1e9) — nccl-tests conventions, from the true byte count.
+  ``bytes`` is the per-rank *message* size as the sweep defines it (the input tensor of one rank):
+
+  ============== ====================================== ===========================
+  op             algbw                                  busbw factor
+  ============== ====================================== ===========================
+  allreduce      bytes / t                              2(P-1)/P
+  allgather      P*bytes / t  (output size)             (P-1)/P
+  reduce_scatter bytes / t    (input size)              (P-1)/P
+  alltoall       bytes / t    (send buffer)             (P-1)/P
+  alltoall_moe   bytes / t    (send buffer, uneven)     (P-1)/P
+  gather         P*bytes / t  (root receive buffer)     (P-1)/P
+  scatter        P*bytes / t  (root send buffer)        (P-1)/P
+  broadcast      bytes / t                              1
+  reduce         bytes / t                              1
+  sendrecv       bytes / t                              1
+  ============== ====================================== ===========================
+
+At P = 1 every factor with (P-1) is 0: there is no inter-GPU traffic, busBW is 0 by definition.
+"""
+
+from __future__ import annotations
+
+from typing import Optional
+
+GB = 1e9
+GIB = float(1024 ** 3)
+
+_OUTPUT_SCALED = {"allgather", "gather", "scatter"}
+_FACTOR = {
+    "allreduce": lambda p: 2.0 * (p - 1) / p,
+    "allgather": lambda p: (p - 1) / p,
+    "reduce_scatter": lambda p: (p - 1) / p,
+    "alltoall": lambda p: (p - 1) / p,
+    "alltoall_moe": lambda p: (p - 1) / p,
+    "gather": lambda p: (p - 1) / p,
+    "scatter": lambda p: (p - 1) / p,
+    "broadcast": lambda p: 1.0,
+    "reduce": lambda p: 1.0,
+    "sendrecv": lambda p: 1.0,
+}
+
+KNOWN_OPS = tuple(_FACTOR.keys())
+
+
+def bus_factor(op: str, num_ranks: int) -> float:
+    if op not in _FACTOR:
+        raise KeyError(f"unknown op {op!r}")
+    return _FACTOR[op](int(num_ranks))
+
+
+def algbw_gbps(op: str, nbytes: float, seconds: float, num_ranks: int) -> Optional[float]:
+    if seconds is None or seconds <= 0:
+        return None
+    scale = num_ranks if op in _OUTPUT_SCALED else 1
+    return (nbytes * scale / seconds) / GB
+
+
+def busbw_gbps(op: str, nbytes: float, seconds: float, num_ranks: int) -> Optional[float]:
+    a = algbw_gbps(op, nbytes, seconds, num_ranks)
+    if a is None:
+        return None
+    return a * bus_factor(op, num_ranks)
+
+
+def legacy_bandwidth_gbps(num_elements: int, seconds: float, num_ranks: int,
+                          op: str = "allreduce") -> Optional[float]:
+    """Reference ``collectives/1d/stats.py:77-129``: identical volume for every op,
+    element size fixed at 2 B, GiB/s."""
+    if op not in _FACTOR:
+        return None
+    if seconds is None or seconds <= 0:
+        return None
+    return (num_elements * 2 * num_ranks / seconds) / GIB

@@ -1,0 +1,41 @@
+"""Multi-process helpers for CPU (gloo) and single-GPU multi-rank tests."""
+
+import os
+import traceback
+
+import torch.multiprocessing as mp
+
+
+def _entry(rank, world, port, fn, args, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK="0")
+    try:
+        res = fn(rank, world, *args)
+        q.put((rank, "ok", res))
+    except BaseException as e:  # report to parent
+        q.put((rank, "err", f"{type(e).__name__}: {e}\n{traceback.format_exc()}"))
+
+
+def run_multiprocess(fn, world, args=(), timeout=240):
+    """Run ``fn(rank, world, *args)`` in ``world`` spawned processes; returns results by rank."""
+    from conftest import free_port
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=_entry, args=(r, world, port, fn, args, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = {}
+    try:
+        for _ in range(world):
+            rank, status, res = q.get(timeout=timeout)
+            if status != "ok":
+                raise AssertionError(f"rank {rank} failed:\n{res}")
+            out[rank] = res
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()
+    return [out[r] for r in range(world)]

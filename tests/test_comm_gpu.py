@@ -1,0 +1,121 @@
+"""Single-GPU RCCL paths (world 1), the collective sweep engine and the IPC all-reduce protocol
+exercised by 2 processes sharing one GPU."""
+
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+import torch
+
+from mp_utils import run_multiprocess
+
+pytestmark = pytest.mark.gpu
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_rccl_world1_sweep(tmp_path):
+    from distributed_llm_backend_benchmark_amd.bench.sweep import run_1d_sweep, run_3d_sweep
+    from distributed_llm_backend_benchmark_amd.parallel.collectives import OPS
+    from distributed_llm_backend_benchmark_amd.parallel.comm import init_distributed
+    from distributed_llm_backend_benchmark_amd.stats import stats1d, stats3d
+
+    comm = init_distributed("rccl")
+    try:
+        ops = [o for o in OPS if o != "alltoall_moe"]
+        run_1d_sweep(comm, ops=ops, sizes={"1KB": 256, "64KB": 16384}, warmup=2, iters=5,
+                     output_dir=str(tmp_path / "r1d"), validate=True, batched=True, graph=True)
+        run_3d_sweep(comm, ops=["allreduce", "allgather", "reduce_scatter"], batch_sizes=[1],
+                     seq_lengths=[128], hidden_dims=[2048], warmup=2, iters=5,
+                     output_dir=str(tmp_path / "r3d"), validate=True, wire_dtype="fp32")
+    finally:
+        comm.destroy()
+    files = sorted(os.listdir(tmp_path / "r1d"))
+    errs = [f for f in files if f.endswith(".error.json")]
+    assert not errs, [json.load(open(tmp_path / "r1d" / f))["error"] for f in errs]
+    for f in files:
+        d = json.load(open(tmp_path / "r1d" / f))
+        assert d["validated"] is True, f
+        assert d["timing_method"] == "hip_event"
+        assert len(d["timings"]) == 1 and len(d["timings"][0]) == 5
+    rows = stats1d.process_directory(str(tmp_path / "r1d"), str(tmp_path / "s1d"), verbose=False)
+    assert len(rows) == len(ops) * 2
+    rows3 = stats3d.process_directory(str(tmp_path / "r3d"), str(tmp_path / "s3d"), "rccl",
+                                      verbose=False)
+    assert {r["wire_dtype"] for r in rows3} == {"float32"}
+
+
+def _car_worker(rank, world, sizes):
+    import torch
+
+    from distributed_llm_backend_benchmark_amd.parallel.comm import init_distributed
+    from distributed_llm_backend_benchmark_amd.parallel.custom_allreduce import (ONESHOT, TWOSHOT,
+                                                                                CustomAllReduce)
+
+    comm = init_distributed("gloo", device="cuda")
+    car = CustomAllReduce(comm, capacity_bytes=8 << 20)
+    ok = []
+    for n in sizes:
+        for algo in (ONESHOT, TWOSHOT):
+            for it in range(3):   # several epochs: exercises the double-buffer parity
+                xs = [torch.randn(n, generator=torch.Generator(device="cuda").manual_seed(
+                    100 * r + it), device="cuda").to(torch.bfloat16) for r in range(world)]
+                ref = sum(x.float() for x in xs)
+                out = car.all_reduce(xs[rank].clone(), algo=algo)
+                torch.cuda.synchronize()
+                good = torch.allclose(out.float(), ref, rtol=2e-2, atol=5e-2)
+                ok.append((n, algo, it, bool(good), car.check_error()))
+            comm.barrier()
+    car.close()
+    comm.destroy()
+    return ok
+
+
+def test_custom_allreduce_two_ranks_one_gpu():
+    res = run_multiprocess(_car_worker, 2, args=([2048, 65536, 1 << 20],), timeout=300)
+    for r in res:
+        for n, algo, it, good, err in r:
+            assert good and err == 0, (n, algo, it, good, err)
+
+
+def test_bench_py_world1():
+    out = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--steps", "5",
+                          "--warmup", "2"], capture_output=True, text=True, timeout=600, cwd=REPO)
+    assert out.returncode == 0, out.stderr[-3000:]
+    line = [l for l in out.stdout.splitlines() if l.startswith("{")][-1]
+    rec = json.loads(line)
+    assert rec["n_gpus"] == 1 and rec["steps"] == 5 and rec["unit"] == "GB/s"
+    assert rec["ms_per_step"] > 0
+
+
+def test_tp_forward_world1_matches_torch():
+    from distributed_llm_backend_benchmark_amd.models.tp_transformer import LLM
+    from distributed_llm_backend_benchmark_amd.parallel.comm import init_distributed
+
+    comm = init_distributed("rccl")
+    try:
+        kw = dict(hidden_size=512, num_layers=2, num_heads=8, ffn_intermediate=2048, comm=comm,
+                  seed=3, init_std=0.02)
+        hip = LLM(kernels="hip", **kw)
+        ref = LLM(kernels="torch", **kw)
+        x = torch.randn(2, 128, 512, device="cuda", dtype=torch.bfloat16)
+        y1, y2 = hip(x), ref(x)
+        torch.testing.assert_close(y1.float(), y2.float(), rtol=5e-2, atol=5e-2)
+        for ad in ("fp32",):
+            hip32 = LLM(kernels="hip", allreduce_dtype=ad, **kw)
+            torch.testing.assert_close(hip32(x).float(), y2.float(), rtol=5e-2, atol=5e-2)
+    finally:
+        comm.destroy()
+
+
+def test_gpt2_ddp_step_world1():
+    from distributed_llm_backend_benchmark_amd.models.gpt2 import GPT2, GPT2Config
+    from distributed_llm_backend_benchmark_amd.parallel.ddp import FlatParamTrainer
+
+    cfg = GPT2Config(vocab_size=1024, block_size=256, n_layer=2, n_head=4, n_embd=256)
+    m = GPT2(cfg, device=torch.device("cuda"))
+    tr = FlatParamTrainer(m, None, lr=3e-3, bucket_mb=1)
+    idx = torch.randint(0, cfg.vocab_size, (4, 256), device="cuda")
+    losses = [tr.step(idx, idx) for _ in range(8)]
+    assert losses[-1] < losses[0] - 0.5, losses

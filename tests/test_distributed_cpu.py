@@ -1,0 +1,146 @@
+"""Multi-process CPU tests over Gloo (BASELINE config 1: "gloo backend world_size=2 on CPU").
+
+The reference's smoke tests need mpirun/deepspeed and a real backend (test/test_open.py,
+test/test_deepseed.py); here every collective, the sweep engine + JSON schema + timing gather,
+tensor parallelism and DDP are checked with world_size 2 (and 4) Gloo processes on localhost.
+"""
+
+import json
+import os
+
+import pytest
+import torch
+
+from mp_utils import run_multiprocess
+
+
+def _sweep_worker(rank, world, outdir):
+    from distributed_llm_backend_benchmark_amd.bench.sweep import run_1d_sweep, run_3d_sweep
+    from distributed_llm_backend_benchmark_amd.parallel.collectives import OPS
+    from distributed_llm_backend_benchmark_amd.parallel.comm import init_distributed
+
+    comm = init_distributed("gloo")
+    ops = list(OPS)
+    run_1d_sweep(comm, ops=ops, sizes={"1KB": 256, "4KiB": 2048}, dtype="fp32", warmup=2,
+                 iters=4, output_dir=os.path.join(outdir, "1d"), impl_name="gloo",
+                 validate=True, batched=True)
+    run_3d_sweep(comm, ops=["allreduce", "allgather", "reduce_scatter", "broadcast", "reduce",
+                            "gather", "alltoall"],
+                 batch_sizes=[1, 2], seq_lengths=[4], hidden_dims=[64], dtype="bf16",
+                 warmup=1, iters=3, output_dir=os.path.join(outdir, "3d"), impl_name="gloo",
+                 validate=True)
+    # resume: nothing rewritten
+    again = run_1d_sweep(comm, ops=["allreduce"], sizes={"1KB": 256}, dtype="fp32", warmup=1,
+                         iters=2, output_dir=os.path.join(outdir, "1d"), impl_name="gloo",
+                         resume=True)
+    comm.destroy()
+    return len(again)
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_gloo_sweeps_all_ops(tmp_path, world):
+    from distributed_llm_backend_benchmark_amd.stats import stats1d, stats3d
+
+    res = run_multiprocess(_sweep_worker, world, args=(str(tmp_path),), timeout=600)
+    assert res == [0] * world          # resume skipped the existing config
+    d1 = tmp_path / "1d"
+    files = sorted(os.listdir(d1))
+    errors = {f: json.load(open(d1 / f))["error"] for f in files if f.endswith(".error.json")}
+    assert not errors, errors
+    from distributed_llm_backend_benchmark_amd.parallel.collectives import OPS
+    assert len(files) == len(OPS) * 2
+    for f in files:
+        rec = json.load(open(d1 / f))
+        assert rec["validated"] is True, f
+        assert len(rec["timings"]) == world and all(len(t) == 4 for t in rec["timings"])
+        assert rec["timing_method"] == "host_perf_counter"
+        assert rec["batched_mean_s"] > 0
+    rows = stats1d.process_directory(str(d1), str(tmp_path / "s1d"), verbose=False)
+    assert len(rows) == len(files)
+    ar = [r for r in rows if r["operation"] == "allreduce" and r["data_size_name"] == "4KiB"][0]
+    assert ar["bytes"] == 8192 and ar["busbw_gbps"] > 0
+    d3 = tmp_path / "3d"
+    f3 = os.listdir(d3)
+    assert not [f for f in f3 if f.endswith(".error.json")], f3
+    assert len(f3) == 7 * 2
+    rows3 = stats3d.process_directory(str(d3), str(tmp_path / "s3d"), "gloo", verbose=False)
+    assert all(r["validated"] if "validated" in r else True for r in rows3)
+
+
+def _tp_worker(rank, world, attention):
+    from distributed_llm_backend_benchmark_amd.models.tp_transformer import LLM
+    from distributed_llm_backend_benchmark_amd.parallel.comm import Comm, init_distributed
+
+    comm = init_distributed("gloo")
+    kw = dict(hidden_size=128, num_layers=2, num_heads=4, ffn_intermediate=512, seed=11,
+              init_std=0.05, attention=attention)
+    dense = LLM(comm=Comm(0, 1, 0, "gloo", torch.device("cpu")), **kw)
+    tp = LLM(comm=comm, **kw)
+    tp.load_from_dense(dense.state_dict())
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(2, 16, 128, generator=g).to(torch.bfloat16)
+    y_ref = dense(x).float()
+    y_tp = tp(x).float()
+    err = float((y_ref - y_tp).abs().max())
+    tp32 = LLM(comm=comm, allreduce_dtype="fp32", **kw)
+    tp32.load_from_dense(dense.state_dict())
+    err32 = float((tp32(x).float() - y_ref).abs().max())
+    nbytes = tp.comm_bytes()
+    comm.destroy()
+    return err, err32, nbytes
+
+
+@pytest.mark.parametrize("attention", ["slice", "sdpa"])
+def test_tensor_parallel_matches_dense(attention):
+    res = run_multiprocess(_tp_worker, 2, args=(attention,), timeout=300)
+    for err, err32, nbytes in res:
+        assert err < 0.1 and err32 < 0.1, (err, err32)
+        assert nbytes == 2 * 2 * (2 * 16 * 128 * 2)   # 2 layers x 2 AR x [B,S,H] bf16
+
+
+def _ddp_worker(rank, world, bucket_mb, overlap, mode):
+    from distributed_llm_backend_benchmark_amd.models.gpt2 import GPT2, GPT2Config
+    from distributed_llm_backend_benchmark_amd.parallel.comm import init_distributed
+    from distributed_llm_backend_benchmark_amd.parallel.ddp import FlatParamTrainer
+
+    comm = init_distributed("gloo")
+    cfg = GPT2Config(vocab_size=256, block_size=32, n_layer=2, n_head=2, n_embd=64)
+    g = torch.Generator().manual_seed(0)
+    data = torch.randint(0, 256, (world * 2, 33), generator=g)
+    local = data[rank * 2:(rank + 1) * 2]
+    # reference gradient on the FULL batch in one process (mean over ranks == global mean)
+    ref = GPT2(cfg, seed=3)
+    loss = ref(data[:, :-1], data[:, 1:])
+    loss.backward()
+    ref_grads = {n: p.grad.float().clone() for n, p in ref.named_parameters()}
+    m = GPT2(cfg, seed=3)
+    tr = FlatParamTrainer(m, comm, lr=1e-3, bucket_mb=bucket_mb, overlap=overlap, mode=mode)
+    tr.zero_grad()
+    tr._reset()
+    l = m(local[:, :-1], local[:, 1:])
+    l.backward()
+    tr.finish()
+    errs = []
+    for n, p in m.named_parameters():
+        o = tr._offsets[id(p)]
+        gavg = tr.flat_grad[o:o + p.numel()].float().view_as(p) / world
+        errs.append(float((gavg - ref_grads[n]).abs().max()))
+    nb = len(tr.buckets)
+    tr.opt.step(tr.flat_grad, working_bf16=tr.flat_param, grad_scale=1.0 / world)
+    for _ in range(2):
+        tr.step(local[:, :-1], local[:, 1:])
+    # parameters must stay bit-identical across ranks
+    chk = comm.all_gather_object(float(tr.master.double().sum()))
+    comm.destroy()
+    return max(errs), nb, chk
+
+
+@pytest.mark.parametrize("bucket_mb,overlap,mode", [(0.05, True, "view"), (100, False, "view"),
+                                                    (0.05, True, "flatten")])
+def test_ddp_grads_match_full_batch(bucket_mb, overlap, mode):
+    res = run_multiprocess(_ddp_worker, 2, args=(bucket_mb, overlap, mode), timeout=300)
+    for err, nb, chk in res:
+        assert err < 2e-2, err
+        assert len(set(chk)) == 1
+    if bucket_mb < 1:
+        assert res[0][1] > 1

@@ -1,0 +1,256 @@
+"""Numerics of every gfx950 HIP kernel against a plain PyTorch fp32 reference of the same op."""
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _lib_loaded():
+    from distributed_llm_backend_benchmark_amd.ops import _lib
+
+    _lib.lib()  # must load: no silent fallback on a GPU box
+    yield
+
+
+def _randn(*shape, dtype=torch.bfloat16, seed=0, scale=1.0):
+    g = torch.Generator(device=DEV).manual_seed(seed)
+    return (torch.randn(*shape, generator=g, device=DEV) * scale).to(dtype)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16, torch.float32])
+@pytest.mark.parametrize("nsrc", [1, 2, 8, 16])
+@pytest.mark.parametrize("n", [7, 4096, 1000003])
+def test_reduce_sum(dtype, nsrc, n):
+    from distributed_llm_backend_benchmark_amd.ops import reduce_sum
+
+    srcs = [_randn(n, dtype=dtype, seed=i) for i in range(nsrc)]
+    ref = sum(s.float() for s in srcs) * 0.5
+    out = reduce_sum(srcs, out_dtype=torch.float32, scale=0.5)
+    torch.testing.assert_close(out, ref, rtol=1e-5, atol=1e-5)
+    out2 = reduce_sum(srcs, scale=0.5)
+    tol = 1e-2 if dtype != torch.float32 else 1e-5
+    torch.testing.assert_close(out2.float(), ref, rtol=tol, atol=tol * nsrc)
+
+
+@pytest.mark.parametrize("src,dst", [(torch.bfloat16, torch.float32), (torch.float32, torch.bfloat16),
+                                     (torch.float16, torch.float32), (torch.float32, torch.float16),
+                                     (torch.bfloat16, torch.float16)])
+@pytest.mark.parametrize("n", [1, 13, 65536 + 5])
+def test_cast(src, dst, n):
+    from distributed_llm_backend_benchmark_amd.ops import cast
+
+    x = _randn(n, dtype=src, seed=3)
+    torch.testing.assert_close(cast(x, dst), x.to(dst), rtol=0, atol=0)
+
+
+def test_cast_nan_inf_preserved():
+    from distributed_llm_backend_benchmark_amd.ops import cast
+
+    x = torch.tensor([float("nan"), float("inf"), -float("inf"), 1.0, -0.0] * 4, device=DEV)
+    y = cast(x, torch.bfloat16).float()
+    assert torch.isnan(y[0]) and y[1] == float("inf") and y[2] == -float("inf")
+
+
+@pytest.mark.parametrize("cols,ld", [(1024, 3072), (24, 72), (13, 40)])
+def test_pack_rows(cols, ld):
+    from distributed_llm_backend_benchmark_amd.ops import pack_rows
+
+    base = _randn(257, ld, seed=4)
+    view = base[:, :cols]
+    out = pack_rows(view, dtype=torch.float32)
+    torch.testing.assert_close(out, view.float(), rtol=0, atol=0)
+
+
+def test_chunk_copy_and_scale():
+    from distributed_llm_backend_benchmark_amd.ops import ChunkTable, ScaleTable, flatten_into
+
+    ts = [_randn(n, seed=i) for i, n in enumerate([1, 7, 1024, 300001, 64])]
+    flat = torch.zeros(sum(t.numel() for t in ts), dtype=torch.bfloat16, device=DEV)
+    tab = flatten_into(ts, flat)
+    tab.run()
+    torch.testing.assert_close(flat, torch.cat(ts), rtol=0, atol=0)
+    # unaligned byte copy
+    a = torch.arange(1001, dtype=torch.uint8, device=DEV)
+    b = torch.zeros(1001, dtype=torch.uint8, device=DEV)
+    ChunkTable([(a[1:], b[:-1])]).run()
+    assert torch.equal(b[:-1], a[1:])
+    outs = [torch.empty(t.numel(), dtype=torch.float32, device=DEV) for t in ts]
+    off, views = 0, []
+    for t in ts:
+        views.append(flat[off:off + t.numel()])
+        off += t.numel()
+    ScaleTable(list(zip(views, outs)), scale=0.125).run()
+    for t, o in zip(ts, outs):
+        torch.testing.assert_close(o, t.float() * 0.125, rtol=1e-6, atol=1e-6)
+
+
+@pytest.mark.parametrize("M,N,K", [(256, 256, 64), (4096, 1024, 4096), (300, 200, 128),
+                                   (8192, 768, 768), (128, 50304, 768)])
+def test_gemm_plain(M, N, K):
+    from distributed_llm_backend_benchmark_amd.ops import linear
+
+    x = _randn(M, K, seed=1, scale=0.5)
+    w = _randn(N, K, seed=2, scale=0.5)
+    ref = x.float() @ w.float().t()
+    y32 = linear(x, w, out_dtype=torch.float32)
+    torch.testing.assert_close(y32, ref, rtol=2e-3, atol=2e-3 * (K ** 0.5))
+    y = linear(x, w)
+    torch.testing.assert_close(y.float(), ref, rtol=2e-2, atol=2e-2 * (K ** 0.5))
+
+
+def test_gemm_asymmetric_identity():
+    """A = I with an asymmetric B catches a transposed C write (CDNA guide §3)."""
+    from distributed_llm_backend_benchmark_amd.ops import linear
+
+    n = 128
+    eye = torch.eye(n, device=DEV, dtype=torch.bfloat16)
+    b = (torch.arange(n * n, device=DEV, dtype=torch.float32).view(n, n) % 17).to(torch.bfloat16)
+    y = linear(eye, b, out_dtype=torch.float32)     # y = I @ b^T = b^T
+    torch.testing.assert_close(y, b.float().t(), rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("act", [None, "gelu", "gelu_tanh"])
+def test_gemm_epilogues(act):
+    from distributed_llm_backend_benchmark_amd.ops import linear
+
+    M, N, K = 512, 384, 256
+    x = _randn(M, K, seed=5, scale=0.3)
+    w = _randn(N, K, seed=6, scale=0.3)
+    b = _randn(N, seed=7)
+    r = _randn(M, N, seed=8)
+    pre = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+    u = x.float() @ w.float().t() + b.float()
+    if act == "gelu":
+        ref = F.gelu(u)
+    elif act == "gelu_tanh":
+        ref = F.gelu(u, approximate="tanh")
+    else:
+        ref = u
+    ref = ref + r.float()
+    y = linear(x, w, bias=b, act=act, residual=r, out_dtype=torch.float32, preact=pre)
+    torch.testing.assert_close(y, ref, rtol=2e-3, atol=3e-2)
+    torch.testing.assert_close(pre.float(), u, rtol=1e-2, atol=3e-2)
+
+
+def test_gemm_strided_A_view():
+    """The TP attention stub passes qkv[..., :H/P] (lda = 3H/P) straight into the GEMM."""
+    from distributed_llm_backend_benchmark_amd.ops import linear
+
+    qkv = _randn(256, 3 * 512, seed=9, scale=0.3)
+    a = qkv[:, :512]
+    w = _randn(640, 512, seed=10, scale=0.3)
+    torch.testing.assert_close(linear(a, w, out_dtype=torch.float32),
+                               a.float() @ w.float().t(), rtol=2e-3, atol=2e-2)
+
+
+@pytest.mark.parametrize("cols", [256, 768, 2048, 4096, 5120, 8192, 100])
+@pytest.mark.parametrize("with_res", [False, True])
+def test_layernorm_fwd(cols, with_res):
+    from distributed_llm_backend_benchmark_amd.ops import layernorm
+
+    rows = 333
+    x = _randn(rows, cols, seed=11, scale=2.0)
+    r = _randn(rows, cols, seed=12) if with_res else None
+    w = _randn(cols, seed=13)
+    b = _randn(cols, seed=14)
+    y, h = layernorm(x, w, b, 1e-5, residual=r)
+    hin = (x.float() + r.float()).to(torch.bfloat16).float() if with_res else x.float()
+    ref = F.layer_norm(hin, (cols,), w.float(), b.float(), 1e-5)
+    torch.testing.assert_close(y.float(), ref, rtol=2e-2, atol=3e-2)
+    if with_res:
+        torch.testing.assert_close(h.float(), hin, rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("cols", [768, 1024, 4096])
+@pytest.mark.parametrize("with_res", [False, True])
+def test_layernorm_bwd(cols, with_res):
+    from distributed_llm_backend_benchmark_amd.ops import layernorm
+
+    rows = 520
+    x = _randn(rows, cols, seed=15).requires_grad_(True)
+    r = _randn(rows, cols, seed=16).requires_grad_(True) if with_res else None
+    w = _randn(cols, seed=17).requires_grad_(True)
+    b = _randn(cols, seed=18).requires_grad_(True)
+    dy = _randn(rows, cols, seed=19)
+    dh = _randn(rows, cols, seed=20) if with_res else None
+    y, h = layernorm(x, w, b, 1e-5, residual=r)
+    loss = (y.float() * dy.float()).sum()
+    if with_res:
+        loss = loss + (h.float() * dh.float()).sum()
+    loss.backward()
+    # fp32 reference
+    xf = x.detach().float().requires_grad_(True)
+    rf = r.detach().float().requires_grad_(True) if with_res else None
+    wf = w.detach().float().requires_grad_(True)
+    bf = b.detach().float().requires_grad_(True)
+    hf = xf + rf if with_res else xf
+    yf = F.layer_norm(hf, (cols,), wf, bf, 1e-5)
+    lf = (yf * dy.float()).sum() + ((hf * dh.float()).sum() if with_res else 0)
+    lf.backward()
+    torch.testing.assert_close(x.grad.float(), xf.grad, rtol=3e-2, atol=3e-2)
+    torch.testing.assert_close(w.grad.float(), wf.grad, rtol=3e-2, atol=0.5)
+    torch.testing.assert_close(b.grad.float(), bf.grad, rtol=3e-2, atol=0.5)
+    if with_res:
+        torch.testing.assert_close(r.grad.float(), rf.grad, rtol=3e-2, atol=3e-2)
+
+
+@pytest.mark.parametrize("approx", ["none", "tanh"])
+def test_bias_gelu_fwd_bwd(approx):
+    from distributed_llm_backend_benchmark_amd.ops import bias_gelu
+
+    rows, cols = 700, 3072
+    x = _randn(rows, cols, seed=21, scale=2.0).requires_grad_(True)
+    b = _randn(cols, seed=22).requires_grad_(True)
+    dy = _randn(rows, cols, seed=23)
+    y = bias_gelu(x, b, approximate=approx)
+    (y.float() * dy.float()).sum().backward()
+    xf = x.detach().float().requires_grad_(True)
+    bf = b.detach().float().requires_grad_(True)
+    yf = F.gelu(xf + bf, approximate=approx)
+    (yf * dy.float()).sum().backward()
+    torch.testing.assert_close(y.float(), yf, rtol=2e-2, atol=2e-2)
+    torch.testing.assert_close(x.grad.float(), xf.grad, rtol=2e-2, atol=2e-2)
+    torch.testing.assert_close(b.grad.float(), bf.grad, rtol=2e-2, atol=0.5)
+
+
+def test_linear_train_grads():
+    from distributed_llm_backend_benchmark_amd.ops.linear_fn import linear_train
+
+    M, N, K = 512, 1024, 256
+    x = _randn(M, K, seed=24, scale=0.5).requires_grad_(True)
+    w = _randn(N, K, seed=25, scale=0.1).requires_grad_(True)
+    b = _randn(N, seed=26).requires_grad_(True)
+    dy = _randn(M, N, seed=27)
+    y = linear_train(x, w, b, act="gelu_tanh")
+    (y.float() * dy.float()).sum().backward()
+    xf, wf, bf = (t.detach().float().requires_grad_(True) for t in (x, w, b))
+    yf = F.gelu(xf @ wf.t() + bf, approximate="tanh")
+    (yf * dy.float()).sum().backward()
+    torch.testing.assert_close(y.float(), yf, rtol=2e-2, atol=2e-2)
+    torch.testing.assert_close(x.grad.float(), xf.grad, rtol=3e-2, atol=0.2)
+    torch.testing.assert_close(w.grad.float(), wf.grad, rtol=3e-2, atol=0.5)
+    torch.testing.assert_close(b.grad.float(), bf.grad, rtol=3e-2, atol=0.5)
+
+
+@pytest.mark.parametrize("gdt", [torch.bfloat16, torch.float32])
+def test_adamw(gdt):
+    from distributed_llm_backend_benchmark_amd.ops import FlatAdamW
+
+    n = 100003
+    p = _randn(n, dtype=torch.float32, seed=28)
+    pref = p.clone().requires_grad_(True)
+    opt = FlatAdamW(p, lr=1e-2, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.1)
+    ref = torch.optim.AdamW([pref], lr=1e-2, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.1)
+    shadow = torch.empty(n, dtype=torch.bfloat16, device=DEV)
+    for s in range(3):
+        g = _randn(n, dtype=gdt, seed=100 + s)
+        opt.step(g, working_bf16=shadow, grad_scale=0.5)
+        pref.grad = g.float() * 0.5
+        ref.step()
+    torch.testing.assert_close(p, pref.detach(), rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(shadow, p.to(torch.bfloat16), rtol=0, atol=0)
