@@ -1,0 +1,115 @@
+"""GPT-2-small DDP training microbenchmark (BASELINE config 5).
+
+Each rank trains the same GPT-2 on its own synthetic token batch; gradients are bucketed
+(contiguous slices of one flat bf16 gradient buffer) and all-reduced over RCCL while backward is
+still running (:mod:`..parallel.ddp`), then one fused AdamW kernel updates the fp32 masters and
+the bf16 working weights. Reported: tokens/s over the whole job (weak scaling: fixed
+micro-batch per GPU), ms/step (max over ranks), model TFLOP/s per GPU, and the same step with
+overlap disabled for comparison (``--compare-overlap``).
+
+Launch::
+
+    torchrun --nproc-per-node 8 --master-addr 127.0.0.1 -m \
+        distributed_llm_backend_benchmark_amd.cli.train_ddp --batch 16 --seq 1024
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+
+def parse_args(argv=None):
+    ap = argparse.ArgumentParser(description="GPT-2 DDP training microbenchmark")
+    ap.add_argument("--backend", default="auto", choices=["auto", "rccl", "gloo"])
+    ap.add_argument("--n-layer", type=int, default=12)
+    ap.add_argument("--n-head", type=int, default=12)
+    ap.add_argument("--n-embd", type=int, default=768)
+    ap.add_argument("--vocab", type=int, default=50304)
+    ap.add_argument("--batch", type=int, default=16, help="micro-batch per GPU")
+    ap.add_argument("--seq", type=int, default=1024)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--lr", type=float, default=3e-4)
+    ap.add_argument("--bucket-mb", type=float, default=64.0)
+    ap.add_argument("--mode", choices=["view", "flatten"], default="view")
+    ap.add_argument("--allreduce", choices=["rccl", "custom"], default="rccl")
+    ap.add_argument("--no-overlap", action="store_true")
+    ap.add_argument("--compare-overlap", action="store_true")
+    ap.add_argument("--output", default=None, help="write the result JSON here (rank 0)")
+    return ap.parse_args(argv)
+
+
+def run(args, comm, overlap: bool):
+    import torch
+
+    from ..data import SyntheticTokenDataset
+    from ..models.gpt2 import GPT2, GPT2Config
+    from ..parallel.ddp import FlatParamTrainer
+
+    cfg = GPT2Config(vocab_size=args.vocab, block_size=args.seq, n_layer=args.n_layer,
+                     n_head=args.n_head, n_embd=args.n_embd)
+    model = GPT2(cfg, device=comm.device)
+    tr = FlatParamTrainer(model, comm if comm.world_size > 1 else None, lr=args.lr,
+                          bucket_mb=args.bucket_mb, overlap=overlap, mode=args.mode,
+                          allreduce=args.allreduce)
+    data = SyntheticTokenDataset(args.batch, args.seq, cfg.vocab_size, rank=comm.rank,
+                                 device=comm.device)
+    for _ in range(args.warmup):
+        x, y = data.get_batch()
+        tr.step(x, y, sync_loss=False)
+    comm.barrier()
+    comm.sync()
+    t0 = time.perf_counter()
+    loss = None
+    for _ in range(args.steps):
+        x, y = data.get_batch()
+        loss = tr.step(x, y, sync_loss=False)
+    comm.sync()
+    dt = comm.allreduce_max(time.perf_counter() - t0)
+    res = {
+        "ms_per_step": dt / args.steps * 1e3,
+        "tokens_per_s": comm.world_size * args.batch * args.seq * args.steps / dt,
+        "loss": float(loss.item()) if loss is not None else None,
+        "params": model.num_parameters(),
+        "buckets": len(tr.buckets),
+        "tflops_per_gpu": model.flops_per_token(args.seq) * args.batch * args.seq
+        * args.steps / dt / 1e12,
+    }
+    tr.close()
+    del tr, model
+    if comm.is_gpu:
+        torch.cuda.empty_cache()
+    return res
+
+
+def main(argv=None) -> int:
+    args = parse_args(argv)
+    from ..parallel.comm import init_distributed
+
+    comm = init_distributed(args.backend, timeout_s=900)
+    main_res = run(args, comm, overlap=not args.no_overlap)
+    out = {"metric": "gpt2_ddp_tokens_per_s", "value": main_res["tokens_per_s"],
+           "n_gpus": comm.world_size, "overlap": not args.no_overlap, **main_res,
+           "config": {k: getattr(args, k) for k in ("n_layer", "n_head", "n_embd", "vocab",
+                                                    "batch", "seq", "bucket_mb", "mode",
+                                                    "allreduce")}}
+    if args.compare_overlap:
+        alt = run(args, comm, overlap=args.no_overlap)
+        out["other_overlap_setting"] = alt
+    if comm.rank == 0:
+        print(json.dumps(out), flush=True)
+        if args.output:
+            os.makedirs(os.path.dirname(os.path.abspath(args.output)), exist_ok=True)
+            with open(args.output, "w") as f:
+                json.dump(out, f, indent=2)
+    comm.barrier()
+    comm.destroy()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,93 @@
+"""Microbenchmarks of the gfx950 kernels vs their torch/hipBLASLt equivalents (device time via
+HIP events, median of N). Prints one JSON line per case; used to fill profiles/kernels.md."""
+import json
+import os
+import sys
+
+import torch
+import torch.nn.functional as F
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from distributed_llm_backend_benchmark_amd import ops  # noqa: E402
+
+
+def t_med(fn, iters=20, warm=3):
+    for _ in range(warm):
+        fn()
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(iters):
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        fn()
+        e.record()
+        e.synchronize()
+        ts.append(s.elapsed_time(e) * 1e-3)
+    ts.sort()
+    return ts[len(ts) // 2]
+
+
+def rnd(*s, dt=torch.bfloat16):
+    return torch.randn(*s, device="cuda").to(dt)
+
+
+def out(**kw):
+    print(json.dumps(kw), flush=True)
+
+
+which = sys.argv[1:] or ["gemm", "mem"]
+if "gemm" in which:
+    shapes = [("7B_qkv_P1", 4096, 12288, 4096), ("7B_out_P1", 4096, 4096, 4096),
+              ("7B_up_P1", 4096, 16384, 4096), ("7B_down_P1", 4096, 4096, 16384),
+              ("7B_up_P8", 4096, 2048, 4096), ("7B_down_P8", 4096, 4096, 2048),
+              ("sq4096", 4096, 4096, 4096), ("sq8192", 8192, 8192, 8192),
+              ("gpt2_fc", 16384, 3072, 768), ("gpt2_lmhead", 16384, 50304, 768)]
+    for name, M, N, K in shapes:
+        x, w = rnd(M, K), rnd(N, K)
+        fl = 2.0 * M * N * K
+        th = t_med(lambda: ops.linear(x, w))
+        tt = t_med(lambda: torch.matmul(x, w.t()))
+        tg = t_med(lambda: ops.linear(x, w, act="gelu"))
+        tgt = t_med(lambda: F.gelu(torch.matmul(x, w.t())))
+        out(kernel="gemm_bf16_nt", case=name, M=M, N=N, K=K, hip_tflops=fl / th / 1e12,
+            hipblaslt_tflops=fl / tt / 1e12, hip_us=th * 1e6, hipblaslt_us=tt * 1e6,
+            hip_gelu_us=tg * 1e6, torch_matmul_gelu_us=tgt * 1e6)
+if "mem" in which:
+    n = 1 << 28  # 256M elements
+    srcs = [rnd(n // 8) for _ in range(8)]
+    for k in (2, 8):
+        t = t_med(lambda: ops.reduce_sum(srcs[:k]))
+        b = (k + 1) * srcs[0].numel() * 2
+        tt = t_med(lambda: torch.stack(srcs[:k]).float().sum(0).to(torch.bfloat16))
+        out(kernel="reduce_sum", nsrc=k, bytes=b, hip_TBps=b / t / 1e12, torch_us=tt * 1e6,
+            hip_us=t * 1e6)
+    x = rnd(n // 4)
+    t = t_med(lambda: ops.cast(x, torch.float32))
+    tt = t_med(lambda: x.float())
+    out(kernel="cast_bf16_fp32", bytes=x.numel() * 6, hip_TBps=x.numel() * 6 / t / 1e12,
+        torch_TBps=x.numel() * 6 / tt / 1e12)
+    for rows, cols in ((16384, 768), (4096, 4096), (4096, 8192)):
+        a, r = rnd(rows, cols), rnd(rows, cols)
+        wv, bv = rnd(cols), rnd(cols)
+        t = t_med(lambda: ops.layernorm(a, wv, bv, residual=r))
+        tt = t_med(lambda: F.layer_norm(a + r, (cols,), wv, bv))
+        b = rows * cols * 2 * 4
+        out(kernel="add_layernorm_fwd", rows=rows, cols=cols, hip_TBps=b / t / 1e12,
+            hip_us=t * 1e6, torch_us=tt * 1e6)
+    a = rnd(16384, 3072)
+    bb = rnd(3072)
+    t = t_med(lambda: ops.bias_gelu(a, bb, "tanh"))
+    tt = t_med(lambda: F.gelu(a + bb, approximate="tanh"))
+    out(kernel="bias_gelu_fwd", hip_us=t * 1e6, torch_us=tt * 1e6,
+        hip_TBps=a.numel() * 4 / t / 1e12)
+    p = torch.randn(124_000_000, device="cuda")
+    opt = ops.FlatAdamW(p)
+    g = rnd(p.numel())
+    sh = torch.empty(p.numel(), dtype=torch.bfloat16, device="cuda")
+    t = t_med(lambda: opt.step(g, working_bf16=sh))
+    b = p.numel() * (4 * 6 + 2 + 2)
+    ref = torch.optim.AdamW([torch.nn.Parameter(p.clone())], fused=True)
+    ref.param_groups[0]["params"][0].grad = g.float()
+    tt = t_med(lambda: ref.step())
+    out(kernel="adamw_flat_124M", hip_us=t * 1e6, hip_TBps=b / t / 1e12,
+        torch_fused_adamw_us=tt * 1e6)
