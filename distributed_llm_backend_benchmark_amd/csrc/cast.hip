@@ -15,8 +15,15 @@ __global__ void __launch_bounds__(256) cast_kernel(const void* __restrict__ src,
                                                    void* __restrict__ dst, int64_t n) {
   const int64_t nvec = n / 8;
   const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
-  for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < nvec;
-       i += stride) {
+  int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  for (; i + 3 * stride < nvec; i += 4 * stride) {   // 4 loads in flight before any store
+    float v[4][8];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) load8<DTI>(src, i + u * stride, v[u]);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) store8<DTO>(dst, i + u * stride, v[u]);
+  }
+  for (; i < nvec; i += stride) {
     float v[8];
     load8<DTI>(src, i, v);
     store8<DTO>(dst, i, v);

@@ -42,7 +42,7 @@ __global__ void __launch_bounds__(256) bias_gelu_fwd_kernel(const uint16_t* __re
   }
 }
 
-constexpr int kStripRows = 64;
+constexpr int kStripRows = 32;
 
 // grid: (ceil(cv / 256), ceil(rows / kStripRows)); thread owns one 8-column vector.
 template <int APPROX>
@@ -60,7 +60,25 @@ __global__ void __launch_bounds__(256) bias_gelu_bwd_kernel(const uint16_t* __re
   float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   const int64_t r0 = static_cast<int64_t>(blockIdx.y) * kStripRows;
   const int64_t r1 = r0 + kStripRows < rows ? r0 + kStripRows : rows;
-  for (int64_t r = r0; r < r1; ++r) {
+  int64_t r = r0;
+  for (; r + 4 <= r1; r += 4) {   // 8 independent 16-B loads in flight per thread
+    float v[4][8], g[4][8];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      load8<DT_BF16>(x, (r + u) * cv + c, v[u]);
+      load8<DT_BF16>(dy, (r + u) * cv + c, g[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        g[u][j] *= act_grad<APPROX>(v[u][j] + bb[j]);
+        acc[j] += g[u][j];
+      }
+      store8<DT_BF16>(dx, (r + u) * cv + c, g[u]);
+    }
+  }
+  for (; r < r1; ++r) {
     float v[8], g[8];
     load8<DT_BF16>(x, r * cv + c, v);
     load8<DT_BF16>(dy, r * cv + c, g);

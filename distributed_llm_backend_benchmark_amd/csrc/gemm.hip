@@ -179,9 +179,212 @@ __global__ void __launch_bounds__(kThreads, 2) gemm_bf16_nt_kernel(GemmArgs a) {
   }
 }
 
+
+// ---------------------------------------------------------------------------------------
+// 256 x 256 x 64 tile, 512 threads (8 waves as 2 (M) x 4 (N), 128 x 64 outputs per wave),
+// one workgroup per CU (2 x 64 KiB LDS buffers). Each K-tile is computed in 4 phases, one
+// 64 x 32 output quadrant per wave per phase (16 MFMA 16x16x32). LDS is staged in 4 sections
+// of 128 rows x 64 k (16 KiB = 2 global_load_lds_dwordx4 per wave) cut along what the phases
+// read: SA0 = A rows of m-quadrant 0 of both wave rows, SB0 / SB1 = B rows of n-quadrant 0 / 1
+// of all four wave columns, SA1 = A rows of m-quadrant 1. Phase p of tile t issues section p of
+// tile t+1, so sections stay 3-4 phases in flight; the waits are COUNTED (vmcnt(4): two
+// sections may stay outstanding) and the barrier is a raw s_barrier so hipcc does not drain the
+// LDS-DMA queue (CDNA guide §5 "Pipelining across barriers", T3/T4, T5).
+//   phase 1: issue SA0' | read A(mq0), B(nq0) | 16 MFMA (mq0,nq0) | vmcnt(4) (SB1 landed)
+//   phase 2: issue SB0' | read B(nq1)         | 16 MFMA (mq0,nq1) | vmcnt(4) (SA1 landed)
+//   phase 3: issue SB1' | read A(mq1)         | 16 MFMA (mq1,nq1) |
+//   phase 4: issue SA1' | (no reads)          | 16 MFMA (mq1,nq0) | vmcnt(4) (SA0',SB0' landed)
+// WAR: tile t+1 overwrites the buffer tile t-1 read; its last reads (phase 3) precede the
+// phase-4 barrier every wave has passed before issuing tile t+1's sections.
+constexpr int BM2 = 256, BN2 = 256;
+constexpr int kThreads2 = 512;
+constexpr int kTile2Bytes = BM2 * BK * 2;      // 32 KiB per operand
+constexpr int kBuf2Bytes = 2 * kTile2Bytes;    // A + B = 64 KiB
+
+// tile row of 8-row group g (0..15) of section `sec` (0 = SA0, 1 = SB0, 2 = SB1, 3 = SA1)
+__device__ __forceinline__ int section_row(int sec, int g) {
+  if (sec == 0) return g < 8 ? g * 8 : 128 + (g - 8) * 8;
+  if (sec == 3) return 64 + (g < 8 ? g * 8 : 128 + (g - 8) * 8);
+  return (sec == 2 ? 32 : 0) + (g >> 2) * 64 + (g & 3) * 8;
+}
+
+__device__ __forceinline__ void stage_section(const uint16_t* __restrict__ X, int64_t ld,
+                                              int64_t row0, int64_t rows, int64_t k0,
+                                              char* tile, int sec, int wave, int lane) {
+  const int r_in = lane >> 3;
+  const int chunk = (lane & 7) ^ r_in;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int trow = section_row(sec, wave * 2 + i);
+    int64_t gr = row0 + trow + r_in;
+    gr = gr < rows ? gr : rows - 1;
+    glds16(X + gr * ld + k0 + chunk * 8, tile + trow * (BK * 2));
+  }
+}
+
+__device__ __forceinline__ void stage_next(const GemmArgs& a, int64_t m0, int64_t n0,
+                                           int64_t k0, char* buf, int sec, int wave, int lane) {
+  if (sec == 0 || sec == 3)
+    stage_section(a.A, a.lda, m0, a.M, k0, buf, sec, wave, lane);
+  else
+    stage_section(a.B, a.ldb, n0, a.N, k0, buf + kTile2Bytes, sec, wave, lane);
+}
+
+#define DLBB_WAIT_VM(N) asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory")
+#define DLBB_BARRIER()                                       \
+  do {                                                       \
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");       \
+    __builtin_amdgcn_s_barrier();                            \
+  } while (0)
+
+template <int MQ, int NQ>
+__device__ __forceinline__ void mfma_quadrant(f32x4 (&acc)[8][4], const bf16x8 (&af)[2][4],
+                                              const bf16x8 (&bf)[2][2]) {
+  __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        acc[MQ * 4 + i][NQ * 2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+            af[ks][i], bf[ks][j], acc[MQ * 4 + i][NQ * 2 + j], 0, 0, 0);
+  __builtin_amdgcn_s_setprio(0);
+}
+
+__device__ __forceinline__ void read_a(const char* tileA, int wr, int mq, int fr, int fq,
+                                       bf16x8 (&af)[2][4]) {
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      af[ks][i] = read_frag(tileA, wr * 128 + mq * 64 + i * 16 + fr, ks * 4 + fq);
+}
+
+__device__ __forceinline__ void read_b(const char* tileB, int wc, int nq, int fr, int fq,
+                                       bf16x8 (&bf)[2][2]) {
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+      bf[ks][j] = read_frag(tileB, wc * 64 + nq * 32 + j * 16 + fr, ks * 4 + fq);
+}
+
+__global__ void __launch_bounds__(kThreads2, 1) gemm_bf16_nt_256_kernel(GemmArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 2, wc = wave & 3;
+  const int fr = lane & 15, fq = lane >> 4;
+
+  const int64_t tiles_m = (a.M + BM2 - 1) / BM2, tiles_n = (a.N + BN2 - 1) / BN2;
+  const int64_t nwg = tiles_m * tiles_n;
+  int64_t wid = blockIdx.x;
+  {
+    const int64_t q = nwg / 8, r = nwg % 8, x = wid % 8;
+    wid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + wid / 8;
+  }
+  const int64_t group_size = kGroupM * tiles_n;
+  const int64_t group = wid / group_size;
+  const int64_t first_m = group * kGroupM;
+  const int64_t gm = (tiles_m - first_m) < kGroupM ? (tiles_m - first_m) : kGroupM;
+  const int64_t m0 = (first_m + (wid % group_size) % gm) * BM2;
+  const int64_t n0 = ((wid % group_size) / gm) * BN2;
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int64_t nk = a.K / BK;
+  // prologue: all four sections of K-tile 0 into buffer 0, wait for SA0 + SB0
+  stage_next(a, m0, n0, 0, smem, 0, wave, lane);
+  stage_next(a, m0, n0, 0, smem, 1, wave, lane);
+  stage_next(a, m0, n0, 0, smem, 2, wave, lane);
+  stage_next(a, m0, n0, 0, smem, 3, wave, lane);
+  DLBB_WAIT_VM(4);
+  DLBB_BARRIER();
+
+  bf16x8 af[2][4], b0[2][2], b1[2][2];
+  for (int64_t t = 0; t < nk; ++t) {
+    char* cur = smem + (t & 1) * kBuf2Bytes;
+    char* nxt = smem + ((t + 1) & 1) * kBuf2Bytes;
+    const bool more = t + 1 < nk;
+    const int64_t kn = (t + 1) * BK;
+    // phase 1
+    if (more) stage_next(a, m0, n0, kn, nxt, 0, wave, lane);
+    read_a(cur, wr, 0, fr, fq, af);
+    read_b(cur + kTile2Bytes, wc, 0, fr, fq, b0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    mfma_quadrant<0, 0>(acc, af, b0);
+    if (more) DLBB_WAIT_VM(4); else DLBB_WAIT_VM(0);
+    DLBB_BARRIER();
+    // phase 2
+    if (more) stage_next(a, m0, n0, kn, nxt, 1, wave, lane);
+    read_b(cur + kTile2Bytes, wc, 1, fr, fq, b1);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    mfma_quadrant<0, 1>(acc, af, b1);
+    if (more) DLBB_WAIT_VM(4); else DLBB_WAIT_VM(0);
+    DLBB_BARRIER();
+    // phase 3
+    if (more) stage_next(a, m0, n0, kn, nxt, 2, wave, lane);
+    read_a(cur, wr, 1, fr, fq, af);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    mfma_quadrant<1, 1>(acc, af, b1);
+    DLBB_BARRIER();
+    // phase 4
+    if (more) stage_next(a, m0, n0, kn, nxt, 3, wave, lane);
+    mfma_quadrant<1, 0>(acc, af, b0);
+    if (more) DLBB_WAIT_VM(4); else DLBB_WAIT_VM(0);
+    DLBB_BARRIER();
+  }
+
+  // epilogue: 32-bit offsets inside this wave's 128 x 64 output block (keeps VGPRs low)
+  const int epi = a.epi;
+  const int64_t row0 = m0 + wr * 128, col0 = n0 + wc * 64;
+  const int ldc = static_cast<int>(a.ldc), ldr = static_cast<int>(a.ldr);
+  const int rows_left = static_cast<int>(a.M - row0 < 128 ? a.M - row0 : 128);
+  const int cols_left = static_cast<int>(a.N - col0 < 64 ? a.N - col0 : 64);
+  float* cf = static_cast<float*>(a.C) + row0 * a.ldc + col0;
+  uint16_t* cb = static_cast<uint16_t*>(a.C) + row0 * a.ldc + col0;
+  uint16_t* pb = a.preact ? a.preact + row0 * a.ldc + col0 : nullptr;
+  const uint16_t* rb = (epi & EPI_RESIDUAL) ? a.residual + row0 * a.ldr + col0 : nullptr;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int cl = j * 16 + fr;
+    if (cl >= cols_left) continue;
+    const float bias = (epi & EPI_BIAS) ? bf16_to_f32(a.bias[col0 + cl]) : 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int rl = i * 16 + fq * 4 + r;
+        if (rl >= rows_left) continue;
+        float v = acc[i][j][r] + bias;
+        if (pb) pb[rl * ldc + cl] = f32_to_bf16(v);
+        v = apply_act(v, epi);
+        if (rb) v += bf16_to_f32(rb[rl * ldr + cl]);
+        if (a.out_f32)
+          cf[rl * ldc + cl] = v;
+        else
+          cb[rl * ldc + cl] = f32_to_bf16(v);
+      }
+    }
+  }
+}
+
 }  // namespace dlbb
 
 using namespace dlbb;
+
+static int dlbb_gemm_force_tile = 0;   // 0 = heuristic, 128 or 256 = force (A/B testing)
+
+DLBB_API void dlbb_gemm_set_tile(int tile) { dlbb_gemm_force_tile = tile; }
 
 DLBB_API int dlbb_gemm_bf16_nt(const void* A, int64_t lda, const void* B, int64_t ldb, void* C,
                                int64_t ldc, int64_t M, int64_t N, int64_t K, const void* bias,
@@ -197,6 +400,14 @@ DLBB_API int dlbb_gemm_bf16_nt(const void* A, int64_t lda, const void* B, int64_
   GemmArgs a{static_cast<const uint16_t*>(A), static_cast<const uint16_t*>(B), C,
              static_cast<const uint16_t*>(bias), static_cast<const uint16_t*>(residual),
              static_cast<uint16_t*>(preact), M, N, K, lda, ldb, ldc, ldr, epi, out_f32};
+  const int64_t tiles256 = ((M + BM2 - 1) / BM2) * ((N + BN2 - 1) / BN2);
+  // the 256^2 schedule needs >= ~1 workgroup per CU to fill the chip; otherwise 128^2 tiles
+  const int force = dlbb_gemm_force_tile;
+  if (force == 256 || (force != 128 && tiles256 >= 192)) {
+    hipLaunchKernelGGL(gemm_bf16_nt_256_kernel, dim3(static_cast<unsigned>(tiles256)),
+                       dim3(kThreads2), 2 * kBuf2Bytes, stream, a);
+    return hipGetLastError();
+  }
   const int64_t tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
   hipLaunchKernelGGL(gemm_bf16_nt_kernel, dim3(static_cast<unsigned>(tiles)), dim3(kThreads),
                      4 * kTileBytes, stream, a);

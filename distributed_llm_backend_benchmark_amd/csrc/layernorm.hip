@@ -215,15 +215,123 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(LnBwdArgs a) {
   }
 }
 
-// out[c] = sum_b part[b, c]  (fp32 accumulate, out in bf16 or fp32)
+// out[c] = sum_b part[b, c]  (fp32 accumulate, out in bf16 or fp32).
+// 256 threads = 8 row groups x 32 columns: every wave reads 2 x 128 contiguous bytes per
+// partial row, and each thread keeps 8 independent loads in flight (the naive
+// one-thread-per-column loop was latency-bound: 118 us for 512 x 768 partials).
 template <int DTO>
 __global__ void __launch_bounds__(256) col_reduce_kernel(const float* __restrict__ part,
                                                          int nparts, int cols, void* out) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= cols) return;
+  __shared__ float red[8][33];
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  const int c = blockIdx.x * 32 + tx;
   float s = 0.f;
-  for (int b = 0; b < nparts; ++b) s += part[static_cast<int64_t>(b) * cols + c];
-  Elem<DTO>::st(static_cast<typename Elem<DTO>::T*>(out), c, s);
+  if (c < cols) {
+    int b = ty;
+    for (; b + 56 < nparts; b += 64) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = part[static_cast<int64_t>(b + 8 * u) * cols + c];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s += v[u];
+    }
+    for (; b < nparts; b += 8) s += part[static_cast<int64_t>(b) * cols + c];
+  }
+  red[ty][tx] = s;
+  __syncthreads();
+  if (ty == 0 && c < cols) {
+    float t = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) t += red[k][tx];
+    Elem<DTO>::st(static_cast<typename Elem<DTO>::T*>(out), c, t);
+  }
+}
+
+// Block-per-row forward for wide rows (cols = T * 8 * VPT): 16-byte vectors, the row held in
+// registers, statistics reduced across the block's waves through LDS. Gives rows x T/64 waves
+// of parallelism where the wave-per-row kernel only has `rows` waves.
+template <int T, int VPT, int PDT>
+__global__ void __launch_bounds__(T) ln_fwd_row_kernel(LnFwdArgs a) {
+  __shared__ float red[2][T / 64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t row = blockIdx.x;
+  const int64_t base8 = row * (a.cols / 8);
+  float v[VPT][8];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) {
+    const int64_t c8 = i * T + threadIdx.x;
+    load8<DT_BF16>(a.x, base8 + c8, v[i]);
+    if (a.r) {
+      float rr[8];
+      load8<DT_BF16>(a.r, base8 + c8, rr);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[i][j] = round_bf16(v[i][j] + rr[j]);
+      if (a.h_out) store8<DT_BF16>(a.h_out, base8 + c8, v[i]);
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s += v[i][j];
+  }
+  s = wave_sum(s);
+  if (lane == 0) red[0][w] = s;
+  __syncthreads();
+  float tot = 0.f;
+#pragma unroll
+  for (int k = 0; k < T / 64; ++k) tot += red[0][k];
+  const float inv_c = 1.0f / static_cast<float>(a.cols);
+  const float mean = tot * inv_c;
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < VPT; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float d = v[i][j] - mean;
+      ss += d * d;
+    }
+  ss = wave_sum(ss);
+  if (lane == 0) red[1][w] = ss;
+  __syncthreads();
+  float vt = 0.f;
+#pragma unroll
+  for (int k = 0; k < T / 64; ++k) vt += red[1][k];
+  const float rstd = rsqrtf(vt * inv_c + a.eps);
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) {
+    const int c8 = i * T + threadIdx.x;
+    float g[8], b[8], o[8];
+    if constexpr (PDT == DT_F32) {
+      load8<DT_F32>(a.gamma, c8, g);
+      if (a.beta) load8<DT_F32>(a.beta, c8, b);
+    } else {
+      load8<DT_BF16>(a.gamma, c8, g);
+      if (a.beta) load8<DT_BF16>(a.beta, c8, b);
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = (v[i][j] - mean) * rstd * g[j] + (a.beta ? b[j] : 0.f);
+    store8<DT_BF16>(a.y, base8 + c8, o);
+  }
+  if (threadIdx.x == 0) {
+    if (a.mean) a.mean[row] = mean;
+    if (a.rstd) a.rstd[row] = rstd;
+  }
+}
+
+template <int T, int VPT, int PDT>
+static hipError_t fwd_row(const LnFwdArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL((ln_fwd_row_kernel<T, VPT, PDT>), dim3(a.rows), dim3(T), 0, s, a);
+  return hipGetLastError();
+}
+
+// returns hipErrorNotSupported when no (T, VPT) instance fits
+template <int PDT>
+static hipError_t fwd_row_dispatch(const LnFwdArgs& a, hipStream_t s) {
+  if (a.cols % 8 != 0) return hipErrorNotSupported;
+  const int nv = a.cols / 8;
+#define ROW(T, V) if (nv == T * V) return fwd_row<T, V, PDT>(a, s);
+  ROW(256, 1) ROW(256, 2) ROW(256, 3) ROW(256, 4) ROW(256, 5) ROW(256, 6) ROW(256, 8)
+  ROW(128, 3) ROW(128, 5) ROW(128, 7) ROW(64, 5) ROW(64, 7)
+#undef ROW
+  return hipErrorNotSupported;
 }
 
 template <int NV, int PDT>
@@ -234,6 +342,10 @@ static hipError_t fwd_nv(const LnFwdArgs& a, hipStream_t s) {
 
 template <int PDT>
 static hipError_t fwd_dispatch(const LnFwdArgs& a, hipStream_t s) {
+  if (a.cols >= 2048) {
+    hipError_t e = fwd_row_dispatch<PDT>(a, s);
+    if (e != hipErrorNotSupported) return e;
+  }
   if (a.cols % 256 == 0) {
     switch (a.cols / 256) {
       case 1: return fwd_nv<1, PDT>(a, s);
@@ -312,7 +424,7 @@ DLBB_API int dlbb_layernorm_bwd(const void* dy, const void* h, const void* gamma
   }
 #undef LB
   if (e != hipSuccess) return e;
-  const dim3 cg((cols + 255) / 256), cb(256);
+  const dim3 cg((cols + 31) / 32), cb(256);
   if (param_dtype == DT_F32) {
     hipLaunchKernelGGL((col_reduce_kernel<DT_F32>), cg, cb, 0, stream, pg, grid, cols, dgamma);
     if (dbeta)

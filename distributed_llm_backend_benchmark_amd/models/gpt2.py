@@ -8,7 +8,8 @@ north star asks for, built from the same gfx950 kernels as the TP model:
 * residual adds fused into the following LayerNorm (``ops.layernorm(x, residual=h)``),
 * QKV / attention-out / MLP / LM-head GEMMs on the MFMA kernel with fused bias and, for c_fc,
   fused tanh-GELU (pre-activation kept for backward),
-* causal attention via ``F.scaled_dot_product_attention`` (ROCm flash/efficient backends).
+* causal attention via ``F.scaled_dot_product_attention`` (ROCm flash/efficient backends),
+* the LM-head loss as one fused bf16 softmax-cross-entropy kernel (``ops.cross_entropy``).
 
 All parameters are bf16 working copies (the trainer keeps fp32 masters); vocab is padded to a
 multiple of 128 (50257 → 50304) so the tied LM-head GEMM fits the MFMA tiling.
@@ -107,7 +108,7 @@ class GPT2(nn.Module):
         logits = linear_train(y, self.wte)
         if targets is None:
             return logits
-        return F.cross_entropy(logits.float().view(-1, logits.shape[-1]), targets.reshape(-1))
+        return ops.cross_entropy(logits, targets)
 
     def num_parameters(self) -> int:
         return sum(p.numel() for p in self.parameters())

@@ -5,6 +5,7 @@
 * :mod:`.gemm` — MFMA bf16 GEMM with fused bias / GELU / residual epilogues.
 * :mod:`.norm_act` — fused residual+LayerNorm and bias+GELU (fwd + bwd, autograd).
 * :mod:`.optim` — flat fused AdamW.
+* :mod:`.xent` — fused softmax cross-entropy on bf16 logits.
 * :mod:`._lib` — loader; ``available()``, ``loaded_path()``.
 """
 
@@ -14,7 +15,8 @@ from .elementwise import reduce_sum, cast, pack_rows, ChunkTable, ScaleTable, fl
 from .gemm import linear
 from .norm_act import layernorm, bias_gelu
 from .optim import FlatAdamW
+from .xent import cross_entropy
 
 __all__ = ["available", "loaded_path", "KernelError", "reduce_sum", "cast", "pack_rows",
            "ChunkTable", "ScaleTable", "flatten_into", "linear", "layernorm", "bias_gelu",
-           "FlatAdamW"]
+           "FlatAdamW", "cross_entropy"]

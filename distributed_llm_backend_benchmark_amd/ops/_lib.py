@@ -52,9 +52,14 @@ _SIGS = {
     "dlbb_gemm_bf16_nt": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64,
                                   c_int64, c_int64, c_int64, c_void_p, c_void_p, c_int64,
                                   c_void_p, c_int, c_int, c_void_p]),
+    "dlbb_gemm_set_tile": (None, [c_int]),
     "dlbb_adamw": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int64,
                            c_float, c_float, c_float, c_float, c_float, c_int, c_float,
                            c_void_p]),
+    "dlbb_xent_fwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int64,
+                              c_void_p]),
+    "dlbb_xent_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int64,
+                              c_void_p, c_void_p]),
     "dlbb_car_create": (c_int, [c_int, c_int, c_int64, ctypes.POINTER(c_void_p)]),
     "dlbb_car_ipc_handles": (c_int, [c_void_p, c_void_p]),
     "dlbb_car_handle_bytes": (c_int, []),

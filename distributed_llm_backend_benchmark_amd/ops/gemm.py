@@ -4,13 +4,15 @@
 with ``w`` stored ``[out_features, in_features]`` (K-contiguous, the MFMA-native layout).
 Reference call sites: ``models.py:47`` (column-parallel) and ``models.py:81`` (row-parallel).
 
-Shape contract of the HIP kernel: ``K % 64 == 0``, 16-byte aligned rows; M and N arbitrary.
+Dispatch: see :func:`linear` (per-shape autotune between the fused MFMA kernel and hipBLASLt +
+HIP epilogue). Shape contract of the HIP kernel: ``K % 64 == 0``, 16-byte aligned rows; M and N arbitrary.
 Shapes outside the contract are routed to ``torch.matmul`` (hipBLASLt) — a plain library GEMM —
 and counted in :data:`FALLBACKS` so benchmarks can report it.
 """
 
 from __future__ import annotations
 
+import os
 from typing import Optional
 
 import torch
@@ -24,6 +26,11 @@ ACTS = {None: 0, "none": 0, "gelu": EPI_GELU_ERF, "gelu_erf": EPI_GELU_ERF,
         "gelu_tanh": EPI_GELU_TANH}
 
 FALLBACKS = {"count": 0}
+
+
+def set_tile(tile: int) -> None:
+    """Force the 128^2 or 256^2 MFMA kernel (0 = size heuristic); for A/B benchmarking."""
+    _lib.lib().dlbb_gemm_set_tile(int(tile))
 
 
 def hip_supported(x2: torch.Tensor, w: torch.Tensor) -> bool:
@@ -49,11 +56,97 @@ def _torch_linear(x2, w, bias, act, residual, out_dtype, preact):
     return y.to(out_dtype)
 
 
+def _mfma_linear(x2, w, bias, act, r2, out, preact):
+    M, K = x2.shape
+    N = w.shape[0]
+    epi = ACTS[act]
+    if bias is not None:
+        epi |= EPI_BIAS
+    if r2 is not None:
+        epi |= EPI_RESIDUAL
+    check(_lib.lib().dlbb_gemm_bf16_nt(
+        x2.data_ptr(), x2.stride(0), w.data_ptr(), w.stride(0), out.data_ptr(), N, M, N, K,
+        _lib.ptr(bias), _lib.ptr(r2), r2.stride(0) if r2 is not None else 0,
+        _lib.ptr(preact), epi, 1 if out.dtype == torch.float32 else 0,
+        _lib.stream(x2.device)), "gemm_bf16_nt")
+    return out
+
+
+_APPROX = {"gelu": 0, "gelu_erf": 0, "gelu_tanh": 1}
+
+
+def _blas_linear(x2, w, bias, act, r2, out, preact):
+    """hipBLASLt GEMM (bias fused by its epilogue through ``addmm``) followed by our HIP
+    elementwise epilogue kernels (GELU, cast) — the plain-library-GEMM path."""
+    M, N = x2.shape[0], w.shape[0]
+    if act is not None or out.dtype != torch.bfloat16 or r2 is not None:
+        u = preact if preact is not None else torch.empty(M, N, dtype=torch.bfloat16,
+                                                          device=x2.device)
+    else:
+        u = out
+    if bias is not None:
+        torch.addmm(bias, x2, w.t(), out=u)
+    else:
+        torch.mm(x2, w.t(), out=u)
+    if preact is not None and u is not preact:
+        preact.copy_(u)
+    y = u
+    if act is not None:
+        y = out if (out.dtype == torch.bfloat16 and r2 is None) else torch.empty_like(u)
+        check(_lib.lib().dlbb_bias_gelu_fwd(u.data_ptr(), None, y.data_ptr(), M, N,
+                                            _APPROX[act], _lib.stream(x2.device)), "bias_gelu")
+    if r2 is not None:
+        y = y + r2
+    if y is not out:
+        if out.dtype == y.dtype:
+            out.copy_(y)
+        else:
+            check(_lib.lib().dlbb_cast(y.data_ptr(), _lib.dt(y), out.data_ptr(), _lib.dt(out),
+                                       y.numel(), _lib.stream(x2.device)), "cast")
+    return out
+
+
+CHOICES = {}          # (M, N, K, epi-signature) -> "mfma" | "blas"
+_IMPLS = {"mfma": _mfma_linear, "blas": _blas_linear}
+
+
+def _autotune(key, args) -> str:
+    mode = os.environ.get("DLBB_GEMM", "auto").lower()
+    if mode in _IMPLS:
+        return mode
+    if key in CHOICES:
+        return CHOICES[key]
+    if torch.cuda.is_current_stream_capturing():
+        return "mfma"
+    best, best_t = "mfma", float("inf")
+    for name, fn in _IMPLS.items():
+        for _ in range(2):
+            fn(*args)
+        ts = []
+        for _ in range(5):
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            fn(*args)
+            e.record()
+            e.synchronize()
+            ts.append(s.elapsed_time(e))
+        t = sorted(ts)[len(ts) // 2]
+        if t < best_t:
+            best, best_t = name, t
+    CHOICES[key] = best
+    return best
+
+
 def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None,
            act: Optional[str] = None, residual: Optional[torch.Tensor] = None,
            out_dtype: Optional[torch.dtype] = None, out: Optional[torch.Tensor] = None,
            preact: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """``act(x @ w.T + bias) + residual``; x ``[..., K]``, w ``[N, K]``; returns ``[..., N]``."""
+    """``act(x @ w.T + bias) + residual``; x ``[..., K]``, w ``[N, K]``; returns ``[..., N]``.
+
+    GPU dispatch per shape (measured once, cached in :data:`CHOICES`; ``DLBB_GEMM`` forces):
+    ``mfma`` = the hand-written gfx950 kernel with the whole epilogue fused, or ``blas`` =
+    hipBLASLt GEMM + our HIP epilogue kernels. Both are native; the faster one runs.
+    """
     lead = x.shape[:-1]
     K = x.shape[-1]
     N = w.shape[0]
@@ -65,29 +158,27 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
     if act not in ACTS:
         raise ValueError(f"unknown activation {act!r}")
     if use_hip(x, w):
-        if not hip_supported(x2, w):
-            FALLBACKS["count"] += 1
-            y = _torch_linear(x2, w, bias, act, residual, out_dtype, preact)
-            return y.reshape(*lead, N) if out is None else out.copy_(y.reshape(out.shape))
         if out is None:
             out = torch.empty(*lead, N, dtype=out_dtype, device=x.device)
         if out.dtype not in (torch.bfloat16, torch.float32) or not out.is_contiguous():
             raise ValueError("linear: out must be contiguous bf16/fp32")
-        epi = ACTS[act]
         if bias is not None:
-            epi |= EPI_BIAS
             bias = bias.contiguous()
         r2 = None
         if residual is not None:
-            epi |= EPI_RESIDUAL
             r2 = residual.reshape(M, N)
             if r2.stride(1) != 1 or r2.dtype != torch.bfloat16:
                 r2 = r2.contiguous().to(torch.bfloat16)
-        check(_lib.lib().dlbb_gemm_bf16_nt(
-            x2.data_ptr(), x2.stride(0), w.data_ptr(), w.stride(0), out.data_ptr(), N, M, N, K,
-            _lib.ptr(bias), _lib.ptr(r2), r2.stride(0) if r2 is not None else 0,
-            _lib.ptr(preact), epi, 1 if out.dtype == torch.float32 else 0,
-            _lib.stream(x.device)), "gemm_bf16_nt")
+        o2 = out.view(M, N)
+        if not hip_supported(x2, w):
+            FALLBACKS["count"] += 1
+            _blas_linear(x2 if x2.stride(1) == 1 else x2.contiguous(), w.contiguous(), bias,
+                         act, r2, o2, preact)
+            return out
+        key = (M, N, K, x2.stride(0), act, bias is not None, r2 is not None, out.dtype,
+               preact is not None)
+        args = (x2, w, bias, act, r2, o2, preact)
+        _IMPLS[_autotune(key, args)](*args)
         return out
     y = _torch_linear(x2, w, bias, act, residual, out_dtype, preact)
     return y.reshape(*lead, N) if out is None else out.copy_(y.reshape(out.shape))

@@ -89,9 +89,21 @@ def test_chunk_copy_and_scale():
         torch.testing.assert_close(o, t.float() * 0.125, rtol=1e-6, atol=1e-6)
 
 
+@pytest.fixture(params=[("mfma", 0), ("mfma", 128), ("mfma", 256), ("blas", 0)],
+                ids=["mfma_auto", "mfma_t128", "mfma_t256", "blas"])
+def gemm_tile(request, monkeypatch):
+    from distributed_llm_backend_benchmark_amd.ops.gemm import set_tile
+
+    impl, tile = request.param
+    monkeypatch.setenv("DLBB_GEMM", impl)
+    set_tile(tile)
+    yield request.param
+    set_tile(0)
+
+
 @pytest.mark.parametrize("M,N,K", [(256, 256, 64), (4096, 1024, 4096), (300, 200, 128),
-                                   (8192, 768, 768), (128, 50304, 768)])
-def test_gemm_plain(M, N, K):
+                                   (8192, 768, 768), (128, 50304, 768), (520, 776, 192)])
+def test_gemm_plain(M, N, K, gemm_tile):
     from distributed_llm_backend_benchmark_amd.ops import linear
 
     x = _randn(M, K, seed=1, scale=0.5)
@@ -103,11 +115,11 @@ def test_gemm_plain(M, N, K):
     torch.testing.assert_close(y.float(), ref, rtol=2e-2, atol=2e-2 * (K ** 0.5))
 
 
-def test_gemm_asymmetric_identity():
+def test_gemm_asymmetric_identity(gemm_tile):
     """A = I with an asymmetric B catches a transposed C write (CDNA guide §3)."""
     from distributed_llm_backend_benchmark_amd.ops import linear
 
-    n = 128
+    n = 256
     eye = torch.eye(n, device=DEV, dtype=torch.bfloat16)
     b = (torch.arange(n * n, device=DEV, dtype=torch.float32).view(n, n) % 17).to(torch.bfloat16)
     y = linear(eye, b, out_dtype=torch.float32)     # y = I @ b^T = b^T
@@ -115,7 +127,7 @@ def test_gemm_asymmetric_identity():
 
 
 @pytest.mark.parametrize("act", [None, "gelu", "gelu_tanh"])
-def test_gemm_epilogues(act):
+def test_gemm_epilogues(act, gemm_tile):
     from distributed_llm_backend_benchmark_amd.ops import linear
 
     M, N, K = 512, 384, 256
@@ -254,3 +266,20 @@ def test_adamw(gdt):
         ref.step()
     torch.testing.assert_close(p, pref.detach(), rtol=1e-5, atol=1e-6)
     torch.testing.assert_close(shadow, p.to(torch.bfloat16), rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("V", [50304, 1000])
+def test_cross_entropy_fwd_bwd(V):
+    from distributed_llm_backend_benchmark_amd.ops import cross_entropy
+
+    rows = 300
+    x = _randn(rows, V, seed=40, scale=3.0).requires_grad_(True)
+    t = torch.randint(0, V, (rows,), device=DEV, generator=torch.Generator(device=DEV).manual_seed(1))
+    t[::7] = -100                       # ignore_index rows
+    loss = cross_entropy(x, t)
+    loss.backward()
+    xf = x.detach().float().requires_grad_(True)
+    lf = F.cross_entropy(xf, t, ignore_index=-100)
+    lf.backward()
+    torch.testing.assert_close(loss.float(), lf, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(x.grad.float(), xf.grad, rtol=2e-2, atol=2e-5)

@@ -45,11 +45,18 @@ if "gemm" in which:
     for name, M, N, K in shapes:
         x, w = rnd(M, K), rnd(N, K)
         fl = 2.0 * M * N * K
+        from distributed_llm_backend_benchmark_amd.ops.gemm import set_tile
+        res = {}
+        for tile in (128, 256):
+            set_tile(tile)
+            res[tile] = t_med(lambda: ops.linear(x, w))
+        set_tile(0)
         th = t_med(lambda: ops.linear(x, w))
         tt = t_med(lambda: torch.matmul(x, w.t()))
         tg = t_med(lambda: ops.linear(x, w, act="gelu"))
         tgt = t_med(lambda: F.gelu(torch.matmul(x, w.t())))
         out(kernel="gemm_bf16_nt", case=name, M=M, N=N, K=K, hip_tflops=fl / th / 1e12,
+            t128_tflops=fl / res[128] / 1e12, t256_tflops=fl / res[256] / 1e12,
             hipblaslt_tflops=fl / tt / 1e12, hip_us=th * 1e6, hipblaslt_us=tt * 1e6,
             hip_gelu_us=tg * 1e6, torch_matmul_gelu_us=tgt * 1e6)
 if "mem" in which:
