@@ -38,7 +38,9 @@ def parse(argv=None):
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--shape", default="8,2048,2048", help="B,S,H of the bf16 message")
-    ap.add_argument("--impl", default="rccl", choices=["rccl", "custom", "auto"])
+    ap.add_argument("--impl", default="best", choices=["best", "rccl", "custom"],
+                    help="best = time RCCL and the IPC xGMI kernel (if its self-test passed on "
+                         "every rank) during warmup and run the faster")
     ap.add_argument("--no-side", action="store_true", help="skip the 512 B / 8 MiB side runs")
     return ap.parse_args(argv)
 
@@ -73,9 +75,27 @@ def main(argv=None) -> int:
 
     B, S, H = (int(x) for x in args.shape.split(","))
     data = make_data((B, S, H), torch.bfloat16, comm.rank, comm.device)
-    op = make_op("allreduce", comm, data, impl=args.impl)
-    nbytes = op.message_bytes
+    cands = ["rccl"] if args.impl != "custom" else []
+    if args.impl in ("best", "custom") and P > 1 and comm.is_gpu:
+        from distributed_llm_backend_benchmark_amd.parallel.custom_allreduce import (
+            get_custom_allreduce)
 
+        car = get_custom_allreduce(comm)
+        if car is not None and car.healthy and car.supports(data.reshape(-1)):
+            cands.append("custom")
+        elif args.impl == "custom":
+            raise SystemExit("custom all-reduce unavailable (setup or self-test failed)")
+    trial = {}
+    op = None
+    for impl in cands:
+        cand = make_op("allreduce", comm, data, impl=impl)
+        for _ in range(max(1, args.warmup)):
+            cand.run()
+        comm.sync()
+        trial[impl] = _timed_steps(comm, cand, 10) / 10 if len(cands) > 1 else 0.0
+        if op is None or trial[impl] < trial[op.impl]:
+            op = cand
+    nbytes = op.message_bytes
     for _ in range(args.warmup):
         op.run()
     comm.sync()
@@ -91,7 +111,7 @@ def main(argv=None) -> int:
         tr = time_per_iteration(comm, small, iters=100, warmup=10)
         allt = comm.gather_floats(tr.timings)
         mid = make_op("allreduce", comm, make_data((4 * 1024 * 1024,), torch.bfloat16,
-                                                   comm.rank, comm.device), impl=args.impl)
+                                                   comm.rank, comm.device), impl=op.impl)
         for _ in range(5):
             mid.run()
         mid_t = _timed_steps(comm, mid, 20) / 20
@@ -128,7 +148,8 @@ def main(argv=None) -> int:
                 "hidden": H,
                 "message_bytes_per_rank": nbytes,
                 "parallelism": f"{'rccl' if comm.backend == 'nccl' else comm.backend}_world{P}",
-                "impl": getattr(op, "impl", args.impl),
+                "impl": op.impl,
+                "impl_trial_ms": {k: v * 1e3 for k, v in trial.items()} if len(trial) > 1 else None,
             },
             "algbw_GBps": alg,
             "baseline_busbw_GBps": REF_BUSBW_GBPS,

@@ -91,21 +91,38 @@ __device__ __forceinline__ bool wait_peers(const CarKernelArgs& a, int phase, ui
   return timed_out == 0;
 }
 
-template <int DT>
-__device__ __forceinline__ void sum_vec(const CarKernelArgs& a, char* const* bufs, int64_t off,
+// W = world size as a compile-time constant (2, 4, 8: every peer load issued before the adds,
+// fully unrolled) or 0 (runtime world). Peer pointers come straight from the kernel-argument
+// block with wave-uniform indices (scalar loads), never from a runtime-indexed local array.
+template <int DT, int W>
+__device__ __forceinline__ void sum_vec(const CarKernelArgs& a, int64_t half, int64_t off,
                                         float (&acc)[8]) {
-  // rotate the peer order per rank so ranks do not all hammer the same link first
-  load8<DT>(bufs[a.rank] + off, 0, acc);
-  for (int k = 1; k < a.world; ++k) {
-    const int p = (a.rank + k) % a.world;
-    float v[8];
-    load8<DT>(bufs[p] + off, 0, v);
+  if constexpr (W > 0) {
+    float v[W][8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) acc[j] += v[j];
+    for (int k = 0; k < W; ++k) {
+      const int p = (a.rank + k) & (W - 1);   // rotate so ranks start on different links
+      load8<DT>(a.data[p] + half + off, 0, v[k]);
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] = v[0][j];
+#pragma unroll
+    for (int k = 1; k < W; ++k)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += v[k][j];
+  } else {
+    load8<DT>(a.data[a.rank] + half + off, 0, acc);
+    for (int k = 1; k < a.world; ++k) {
+      const int p = (a.rank + k) % a.world;
+      float v[8];
+      load8<DT>(a.data[p] + half + off, 0, v);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += v[j];
+    }
   }
 }
 
-template <int DT>
+template <int DT, int W>
 __global__ void __launch_bounds__(kCarThreads) car_oneshot_kernel(CarKernelArgs a) {
   constexpr int64_t kVecBytes = 8 * Elem<DT>::kBytes;
   __shared__ uint32_t s_epoch;
@@ -126,16 +143,14 @@ __global__ void __launch_bounds__(kCarThreads) car_oneshot_kernel(CarKernelArgs 
   }
   signal_peers(a, 0, e);
   if (!wait_peers(a, 0, e)) return;
-  char* bufs[kMaxRanks];
-  for (int p = 0; p < a.world; ++p) bufs[p] = a.data[p] + half;
   for (int64_t v = v0 + threadIdx.x; v < v1; v += blockDim.x) {
     float acc[8];
-    sum_vec<DT>(a, bufs, v * kVecBytes, acc);
+    sum_vec<DT, W>(a, half, v * kVecBytes, acc);
     store8<DT>(a.out, v, acc);
   }
 }
 
-template <int DT>
+template <int DT, int W>
 __global__ void __launch_bounds__(kCarThreads) car_twoshot_kernel(CarKernelArgs a) {
   constexpr int64_t kVecBytes = 8 * Elem<DT>::kBytes;
   __shared__ uint32_t s_epoch;
@@ -162,21 +177,22 @@ __global__ void __launch_bounds__(kCarThreads) car_twoshot_kernel(CarKernelArgs 
   signal_peers(a, 0, e);
   if (!wait_peers(a, 0, e)) return;
   // reduce-scatter: my shard, sub-range b
-  char* bufs[kMaxRanks];
-  for (int p = 0; p < a.world; ++p) bufs[p] = a.data[p] + half;
   char* my_tmp = a.tmp[a.rank] + half;
   const int64_t mybase = a.rank * shard_vec;
   for (int64_t v = s0 + threadIdx.x; v < s1; v += blockDim.x) {
     float acc[8];
-    sum_vec<DT>(a, bufs, (mybase + v) * kVecBytes, acc);
+    sum_vec<DT, W>(a, half, (mybase + v) * kVecBytes, acc);
     store8<DT>(my_tmp, mybase + v, acc);
     store8<DT>(a.out, mybase + v, acc);
   }
   signal_peers(a, 1, e);
   if (!wait_peers(a, 1, e)) return;
   // all-gather: every other shard's sub-range b from its owner's tmp
-  for (int k = 1; k < a.world; ++k) {
-    const int p = (a.rank + k) % a.world;
+  const int world = W > 0 ? W : a.world;
+#pragma unroll
+  for (int k = 1; k < (W > 0 ? W : kMaxRanks); ++k) {
+    if (W == 0 && k >= world) break;
+    const int p = (a.rank + k) % world;
     const char* src = a.tmp[p] + half;
     const int64_t base = p * shard_vec;
     for (int64_t v = s0 + threadIdx.x; v < s1; v += blockDim.x) {
@@ -327,7 +343,14 @@ DLBB_API int dlbb_car_allreduce(void* h, const void* inp, void* out, int64_t n, 
   a.out = out;
   a.nbytes = nbytes;
   const dim3 g(nblocks), b(kCarThreads);
-#define CAR_L(KERN, D) hipLaunchKernelGGL((KERN<D>), g, b, 0, stream, a)
+#define CAR_W(KERN, D)                                                                  \
+  do {                                                                                  \
+    if (s->world == 2) hipLaunchKernelGGL((KERN<D, 2>), g, b, 0, stream, a);            \
+    else if (s->world == 4) hipLaunchKernelGGL((KERN<D, 4>), g, b, 0, stream, a);       \
+    else if (s->world == 8) hipLaunchKernelGGL((KERN<D, 8>), g, b, 0, stream, a);       \
+    else hipLaunchKernelGGL((KERN<D, 0>), g, b, 0, stream, a);                          \
+  } while (0)
+#define CAR_L(KERN, D) CAR_W(KERN, D)
   if (algo == 2) {
     if (dtype == DT_BF16) CAR_L(car_twoshot_kernel, DT_BF16);
     else if (dtype == DT_F16) CAR_L(car_twoshot_kernel, DT_F16);
@@ -337,6 +360,7 @@ DLBB_API int dlbb_car_allreduce(void* h, const void* inp, void* out, int64_t n, 
     else if (dtype == DT_F16) CAR_L(car_oneshot_kernel, DT_F16);
     else CAR_L(car_oneshot_kernel, DT_F32);
   }
+#undef CAR_W
 #undef CAR_L
   return hipGetLastError();
 }

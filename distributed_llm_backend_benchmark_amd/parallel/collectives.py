@@ -107,7 +107,7 @@ class AllReduce(CollectiveOp):
         self.buf = self.data.clone()
         impl = self.opts.get("impl", "rccl")
         self._custom = None
-        if impl in ("custom", "auto") and self.comm.is_gpu:
+        if impl in ("custom", "auto") and self.comm.is_gpu and self.comm.world_size > 1:
             from .custom_allreduce import get_custom_allreduce
 
             car = get_custom_allreduce(self.comm)

@@ -39,18 +39,32 @@ class CustomAllReduce:
             raise RuntimeError("custom all-reduce supports up to 8 ranks (one node)")
         self.comm = comm
         self.lib = _lib.lib()
-        h = ctypes.c_void_p()
-        _lib.check(self.lib.dlbb_car_create(comm.rank, comm.world_size, int(capacity_bytes),
-                                            ctypes.byref(h)), "car_create")
-        self.h = h
-        nb = self.lib.dlbb_car_handle_bytes()
-        buf = ctypes.create_string_buffer(nb)
-        _lib.check(self.lib.dlbb_car_ipc_handles(self.h, buf), "car_ipc_handles")
-        mine = (bytes(buf.raw), torch.cuda.current_device())
-        allh = comm.all_gather_object(mine)
+        self.h = None
+        # Every step that can fail locally is followed by an all-ranks agreement, so one rank's
+        # failure (allocation, IPC export/open, peer access) never leaves the others blocked in
+        # a collective.
+        mine, err = None, None
+        try:
+            h = ctypes.c_void_p()
+            _lib.check(self.lib.dlbb_car_create(comm.rank, comm.world_size, int(capacity_bytes),
+                                                ctypes.byref(h)), "car_create")
+            self.h = h
+            buf = ctypes.create_string_buffer(self.lib.dlbb_car_handle_bytes())
+            _lib.check(self.lib.dlbb_car_ipc_handles(self.h, buf), "car_ipc_handles")
+            mine = bytes(buf.raw)
+        except Exception as e:  # noqa: BLE001 - reported collectively below
+            err = e
+        allh = comm.all_gather_object((mine, torch.cuda.current_device(), repr(err)))
+        if any(x[0] is None for x in allh):
+            self.close()
+            raise RuntimeError(f"custom all-reduce setup failed: {[x[2] for x in allh]}")
         blob = b"".join(x[0] for x in allh)
         devs = (ctypes.c_int * comm.world_size)(*[int(x[1]) for x in allh])
-        _lib.check(self.lib.dlbb_car_open(self.h, blob, devs), "car_open")
+        rc = self.lib.dlbb_car_open(self.h, blob, devs)
+        oks = comm.all_gather_object(rc)
+        if any(r != 0 for r in oks):
+            self.close()
+            raise RuntimeError(f"custom all-reduce IPC open failed (hip rc per rank: {oks})")
         self.capacity = int(self.lib.dlbb_car_capacity(self.h))
         self.oneshot_max = oneshot_max_bytes
         self.auto_max = auto_max_bytes
@@ -105,7 +119,9 @@ class CustomAllReduce:
         pass for ``healthy``."""
         ok = True
         dev = self.comm.device
-        for n in (4096, 1 << 18):
+        for n in (4096, 1 << 18, 1 << 22):
+            if n * 2 > self.capacity:
+                continue
             g = torch.Generator(device=dev)
             g.manual_seed(1234 + self.comm.rank)
             x = torch.randn(n, generator=g, device=dev).to(torch.bfloat16)
@@ -113,12 +129,20 @@ class CustomAllReduce:
             if self.comm.world_size > 1:
                 dist.all_reduce(ref)
             for algo in (ONESHOT, TWOSHOT):
-                y = self.all_reduce(x.clone(), algo=algo)
-                torch.cuda.synchronize(dev)
-                good = torch.allclose(y.float(), ref, rtol=2e-2, atol=5e-2 * self.comm.world_size)
-                ok = ok and good and self.check_error() == 0
+                for _ in range(2):     # two epochs: both halves of the double buffer
+                    try:
+                        y = self.all_reduce(x.clone(), algo=algo)
+                        torch.cuda.synchronize(dev)
+                        good = torch.allclose(y.float(), ref, rtol=2e-2,
+                                              atol=5e-2 * self.comm.world_size)
+                        ok = ok and good and self.check_error() == 0
+                    except Exception:  # noqa: BLE001 - a failed launch is a failed test
+                        ok = False
         flags = self.comm.all_gather_object(bool(ok))
         self.healthy = all(flags)
+        if not self.healthy and self.comm.rank == 0:
+            print(f"[custom all-reduce] self-test failed on ranks "
+                  f"{[i for i, f in enumerate(flags) if not f]}: RCCL will be used", flush=True)
         return self.healthy
 
     def close(self) -> None:
@@ -139,11 +163,15 @@ def get_custom_allreduce(comm: Comm, self_test: bool = True) -> Optional[CustomA
     if os.environ.get("DLBB_CUSTOM_AR", "1") == "0" or not comm.is_gpu:
         return None
     key = id(comm)
-    inst = _INSTANCES.get(key)
-    if inst is None:
-        cap = int(os.environ.get("DLBB_CUSTOM_AR_CAP", str(64 << 20)))
-        inst = CustomAllReduce(comm, capacity_bytes=cap)
-        if self_test:
-            inst.self_test()
+    if key not in _INSTANCES:
+        cap = int(os.environ.get("DLBB_CUSTOM_AR_CAP", str(128 << 20)))
+        try:
+            inst = CustomAllReduce(comm, capacity_bytes=cap)
+            if self_test:
+                inst.self_test()
+        except RuntimeError as e:   # agreed on all ranks: fall back to RCCL everywhere
+            if comm.rank == 0:
+                print(f"[custom all-reduce disabled] {e}", flush=True)
+            inst = None
         _INSTANCES[key] = inst
-    return inst
+    return _INSTANCES[key]

@@ -110,7 +110,8 @@ def test_gemm_plain(M, N, K, gemm_tile):
     w = _randn(N, K, seed=2, scale=0.5)
     ref = x.float() @ w.float().t()
     y32 = linear(x, w, out_dtype=torch.float32)
-    torch.testing.assert_close(y32, ref, rtol=2e-3, atol=2e-3 * (K ** 0.5))
+    tol = 2e-3 if gemm_tile[0] == "mfma" else 2e-2     # blas path rounds to bf16 first
+    torch.testing.assert_close(y32, ref, rtol=tol, atol=tol * (K ** 0.5))
     y = linear(x, w)
     torch.testing.assert_close(y.float(), ref, rtol=2e-2, atol=2e-2 * (K ** 0.5))
 
@@ -145,7 +146,8 @@ def test_gemm_epilogues(act, gemm_tile):
         ref = u
     ref = ref + r.float()
     y = linear(x, w, bias=b, act=act, residual=r, out_dtype=torch.float32, preact=pre)
-    torch.testing.assert_close(y, ref, rtol=2e-3, atol=3e-2)
+    tol = 2e-3 if gemm_tile[0] == "mfma" else 2e-2
+    torch.testing.assert_close(y, ref, rtol=tol, atol=3e-2)
     torch.testing.assert_close(pre.float(), u, rtol=1e-2, atol=3e-2)
 
 
