@@ -38,6 +38,8 @@ def parse_args(argv=None):
     ap.add_argument("--mode", choices=["view", "flatten"], default="view")
     ap.add_argument("--allreduce", choices=["rccl", "custom"], default="rccl")
     ap.add_argument("--no-overlap", action="store_true")
+    ap.add_argument("--zero", action="store_true",
+                    help="ZeRO-2-style: reduce-scatter grads, sharded AdamW, all-gather params")
     ap.add_argument("--compare-overlap", action="store_true")
     ap.add_argument("--output", default=None, help="write the result JSON here (rank 0)")
     return ap.parse_args(argv)
@@ -53,9 +55,14 @@ def run(args, comm, overlap: bool):
     cfg = GPT2Config(vocab_size=args.vocab, block_size=args.seq, n_layer=args.n_layer,
                      n_head=args.n_head, n_embd=args.n_embd)
     model = GPT2(cfg, device=comm.device)
-    tr = FlatParamTrainer(model, comm if comm.world_size > 1 else None, lr=args.lr,
-                          bucket_mb=args.bucket_mb, overlap=overlap, mode=args.mode,
-                          allreduce=args.allreduce)
+    if args.zero:
+        from ..parallel.zero import ShardedTrainer
+
+        tr = ShardedTrainer(model, comm, lr=args.lr, bucket_mb=args.bucket_mb, overlap=overlap)
+    else:
+        tr = FlatParamTrainer(model, comm if comm.world_size > 1 else None, lr=args.lr,
+                              bucket_mb=args.bucket_mb, overlap=overlap, mode=args.mode,
+                              allreduce=args.allreduce)
     data = SyntheticTokenDataset(args.batch, args.seq, cfg.vocab_size, rank=comm.rank,
                                  device=comm.device)
     for _ in range(args.warmup):
@@ -96,7 +103,7 @@ def main(argv=None) -> int:
            "n_gpus": comm.world_size, "overlap": not args.no_overlap, **main_res,
            "config": {k: getattr(args, k) for k in ("n_layer", "n_head", "n_embd", "vocab",
                                                     "batch", "seq", "bucket_mb", "mode",
-                                                    "allreduce")}}
+                                                    "allreduce", "zero")}}
     if args.compare_overlap:
         alt = run(args, comm, overlap=args.no_overlap)
         out["other_overlap_setting"] = alt

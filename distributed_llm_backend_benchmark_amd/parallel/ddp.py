@@ -66,10 +66,19 @@ class FlatParamTrainer:
                 params.append(p)
         order = list(reversed(params))          # backward produces grads roughly in reverse
         dev = params[0].device
-        offs, total = [], 0
-        for p in order:
+        # layout: params back to back (each 64-element aligned), buckets closed at >= cap and
+        # padded to a multiple of `bucket_align` elements (ZeRO shards need P-divisible buckets)
+        cap = int(bucket_mb * (1 << 20) / torch.tensor([], dtype=grad_dtype).element_size())
+        balign = max(_ALIGN, self._bucket_align())
+        offs, spans, cur, start, total = [], [], [], 0, 0
+        for i, p in enumerate(order):
             offs.append(total)
             total += (p.numel() + _ALIGN - 1) // _ALIGN * _ALIGN
+            cur.append(p)
+            if total - start >= cap or i == len(order) - 1:
+                total = (total + balign - 1) // balign * balign
+                spans.append((start, total, cur))
+                cur, start = [], total
         self.numel = total
         self.flat_param = torch.zeros(total, dtype=torch.bfloat16, device=dev)
         self.flat_grad = torch.zeros(total, dtype=grad_dtype, device=dev)
@@ -78,22 +87,11 @@ class FlatParamTrainer:
                 view = self.flat_param[o:o + p.numel()].view_as(p)
                 view.copy_(p.data)
                 p.data = view
-        self.master = self.flat_param.float()
-        self.opt = FlatAdamW(self.master, lr=lr, betas=betas, weight_decay=weight_decay)
-        # buckets
-        cap = int(bucket_mb * (1 << 20) / self.flat_grad.element_size())
         self.buckets: List[_Bucket] = []
         self._bucket_of = {}
-        cur: List[torch.nn.Parameter] = []
-        start = 0
-        for p, o in zip(order, offs):
-            end = o + (p.numel() + _ALIGN - 1) // _ALIGN * _ALIGN
-            cur.append(p)
-            if end - start >= cap:
-                self._add_bucket(start, end, cur)
-                cur, start = [], end
-        if cur:
-            self._add_bucket(start, total, cur)
+        for st, en, ps in spans:
+            self._add_bucket(st, en, ps)
+        self._init_optimizer(lr, betas, weight_decay)
         self._offsets = {id(p): o for p, o in zip(order, offs)}
         self._params = order
         if mode == "view":
@@ -109,6 +107,17 @@ class FlatParamTrainer:
             self._car = get_custom_allreduce(comm)
             self._comm_stream = torch.cuda.Stream(dev, priority=-1)
         self.step_count = 0
+
+    # ------------------------------------------------------------------ hooks for subclasses
+    def _bucket_align(self) -> int:
+        return _ALIGN
+
+    def _init_optimizer(self, lr, betas, weight_decay) -> None:
+        self.master = self.flat_param.float()
+        self.opt = FlatAdamW(self.master, lr=lr, betas=betas, weight_decay=weight_decay)
+
+    def _optimizer_step(self) -> None:
+        self.opt.step(self.flat_grad, working_bf16=self.flat_param, grad_scale=1.0 / self.world)
 
     # ------------------------------------------------------------------ buckets
     def _add_bucket(self, start: int, end: int, params) -> None:
@@ -184,7 +193,7 @@ class FlatParamTrainer:
         loss.backward()
         self.finish()
         self.step_count += 1
-        self.opt.step(self.flat_grad, working_bf16=self.flat_param, grad_scale=1.0 / self.world)
+        self._optimizer_step()
         return float(loss.item()) if sync_loss else loss.detach()
 
     def close(self) -> None:

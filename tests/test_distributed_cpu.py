@@ -144,3 +144,37 @@ def test_ddp_grads_match_full_batch(bucket_mb, overlap, mode):
         assert len(set(chk)) == 1
     if bucket_mb < 1:
         assert res[0][1] > 1
+
+
+def _zero_worker(rank, world):
+    from distributed_llm_backend_benchmark_amd.models.gpt2 import GPT2, GPT2Config
+    from distributed_llm_backend_benchmark_amd.parallel.comm import init_distributed
+    from distributed_llm_backend_benchmark_amd.parallel.ddp import FlatParamTrainer
+    from distributed_llm_backend_benchmark_amd.parallel.zero import ShardedTrainer
+
+    comm = init_distributed("gloo")
+    cfg = GPT2Config(vocab_size=256, block_size=32, n_layer=2, n_head=2, n_embd=64)
+    g = torch.Generator().manual_seed(1)
+    data = torch.randint(0, 256, (world * 2, 33), generator=g)
+    local = data[rank * 2:(rank + 1) * 2]
+    md, mz = GPT2(cfg, seed=9), GPT2(cfg, seed=9)
+    ddp = FlatParamTrainer(md, comm, lr=1e-3, bucket_mb=0.05)
+    zero = ShardedTrainer(mz, comm, lr=1e-3, bucket_mb=0.05)
+    assert zero.shard_numel * world == zero.numel
+    for _ in range(3):
+        ld = ddp.step(local[:, :-1], local[:, 1:])
+        lz = zero.step(local[:, :-1], local[:, 1:])
+    # the all-gathered bf16 parameters must match DDP's, parameter by parameter
+    diff = max(float((a.float() - b.float()).abs().max())
+               for a, b in zip(md.parameters(), mz.parameters()))
+    # and the sharded optimizer really holds 1/world of the state
+    errs = [zero.master.numel() * world - zero.numel]
+    comm.destroy()
+    return diff, max(errs), ld, lz
+
+
+def test_zero2_matches_ddp():
+    res = run_multiprocess(_zero_worker, 2, timeout=300)
+    for diff, err, ld, lz in res:
+        assert diff < 2e-2 and err == 0, (diff, err)
+        assert abs(ld - lz) < 1e-2
