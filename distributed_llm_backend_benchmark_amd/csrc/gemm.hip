@@ -270,6 +270,7 @@ __device__ __forceinline__ void read_b(const char* tileB, int wc, int nq, int fr
       bf[ks][j] = read_frag(tileB, wc * 64 + nq * 32 + j * 16 + fr, ks * 4 + fq);
 }
 
+template <int MODE>   // 0 lock-step, 1 staggered, 2 staggered + whole next tile issued at phase 1
 __global__ void __launch_bounds__(kThreads2, 1) gemm_bf16_nt_256_kernel(GemmArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x;
@@ -308,6 +309,83 @@ __global__ void __launch_bounds__(kThreads2, 1) gemm_bf16_nt_256_kernel(GemmArgs
   DLBB_BARRIER();
 
   bf16x8 af[2][4], b0[2][2], b1[2][2];
+  if constexpr (MODE >= 1) {
+    // Two barriers per phase ([stage + ds_read] | barrier | [16 MFMA] | barrier) and wave
+    // row 1 one barrier behind wave row 0: on every SIMD one wave's LDS reads overlap its
+    // partner's MFMA cluster (CDNA guide 8-phase template, T3). With the groups offset, a
+    // section read at phase q must be waited for (by every wave) before the FIRST barrier of
+    // phase q-1. MODE 1 issues section p of tile t+1 at phase p (waits: vmcnt(4) at phases
+    // 1, 2, 4); MODE 2 issues all four sections at phase 1, so each has 3-5 phases to land
+    // (waits: vmcnt(10) / vmcnt(8) / - / vmcnt(4) at phases 1-4).
+    const bool lag = wr == 1;
+    if (lag) __builtin_amdgcn_s_barrier();
+    for (int64_t t = 0; t < nk; ++t) {
+      char* cur = smem + (t & 1) * kBuf2Bytes;
+      char* nxt = smem + ((t + 1) & 1) * kBuf2Bytes;
+      const bool more = t + 1 < nk;
+      const bool more0 = t > 0;          // MODE 2: tile t's own sections were issued at t-1 P1
+      const int64_t kn = (t + 1) * BK;
+      // phase 1
+      if (more) {
+        stage_next(a, m0, n0, kn, nxt, 0, wave, lane);
+        if constexpr (MODE == 2) {
+          stage_next(a, m0, n0, kn, nxt, 1, wave, lane);
+          stage_next(a, m0, n0, kn, nxt, 2, wave, lane);
+          stage_next(a, m0, n0, kn, nxt, 3, wave, lane);
+        }
+      }
+      read_a(cur, wr, 0, fr, fq, af);
+      read_b(cur + kTile2Bytes, wc, 0, fr, fq, b0);
+      if constexpr (MODE == 2) {
+        // queue [SB1, SA1 | next 4 sections]: retire SB1 (needed at phase 2)
+        if (more) DLBB_WAIT_VM(10); else DLBB_WAIT_VM(2);
+      } else {
+        if (more) DLBB_WAIT_VM(4); else DLBB_WAIT_VM(0);
+      }
+      (void)more0;
+      DLBB_BARRIER();
+      __builtin_amdgcn_sched_barrier(0);
+      mfma_quadrant<0, 0>(acc, af, b0);
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+      // phase 2
+      if constexpr (MODE == 1) {
+        if (more) stage_next(a, m0, n0, kn, nxt, 1, wave, lane);
+      }
+      read_b(cur + kTile2Bytes, wc, 1, fr, fq, b1);
+      if constexpr (MODE == 2) {
+        if (more) DLBB_WAIT_VM(8); else DLBB_WAIT_VM(0);   // retire SA1 (phase 3)
+      } else {
+        if (more) DLBB_WAIT_VM(4); else DLBB_WAIT_VM(0);
+      }
+      DLBB_BARRIER();
+      __builtin_amdgcn_sched_barrier(0);
+      mfma_quadrant<0, 1>(acc, af, b1);
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+      // phase 3
+      if constexpr (MODE == 1) {
+        if (more) stage_next(a, m0, n0, kn, nxt, 2, wave, lane);
+      }
+      read_a(cur, wr, 1, fr, fq, af);
+      DLBB_BARRIER();
+      __builtin_amdgcn_sched_barrier(0);
+      mfma_quadrant<1, 1>(acc, af, b1);
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+      // phase 4
+      if constexpr (MODE == 1) {
+        if (more) stage_next(a, m0, n0, kn, nxt, 3, wave, lane);
+      }
+      if (more) DLBB_WAIT_VM(4); else DLBB_WAIT_VM(0);       // retire SA0', SB0'
+      DLBB_BARRIER();
+      __builtin_amdgcn_sched_barrier(0);
+      mfma_quadrant<1, 0>(acc, af, b0);
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+    }
+    if (!lag) __builtin_amdgcn_s_barrier();   // equal barrier counts for both wave rows
+  } else {
   for (int64_t t = 0; t < nk; ++t) {
     char* cur = smem + (t & 1) * kBuf2Bytes;
     char* nxt = smem + ((t + 1) & 1) * kBuf2Bytes;
@@ -342,6 +420,7 @@ __global__ void __launch_bounds__(kThreads2, 1) gemm_bf16_nt_256_kernel(GemmArgs
     mfma_quadrant<1, 0>(acc, af, b0);
     if (more) DLBB_WAIT_VM(4); else DLBB_WAIT_VM(0);
     DLBB_BARRIER();
+  }
   }
 
   // epilogue: 32-bit offsets inside this wave's 128 x 64 output block (keeps VGPRs low)
@@ -384,7 +463,10 @@ using namespace dlbb;
 
 static int dlbb_gemm_force_tile = 0;   // 0 = heuristic, 128 or 256 = force (A/B testing)
 
+static int dlbb_gemm_stagger = 1;      // 256^2 schedule: 0 lock-step, 1 staggered (best), 2 + early issue
+
 DLBB_API void dlbb_gemm_set_tile(int tile) { dlbb_gemm_force_tile = tile; }
+DLBB_API void dlbb_gemm_set_stagger(int on) { dlbb_gemm_stagger = on; }
 
 DLBB_API int dlbb_gemm_bf16_nt(const void* A, int64_t lda, const void* B, int64_t ldb, void* C,
                                int64_t ldc, int64_t M, int64_t N, int64_t K, const void* bias,
@@ -404,8 +486,13 @@ DLBB_API int dlbb_gemm_bf16_nt(const void* A, int64_t lda, const void* B, int64_
   // the 256^2 schedule needs >= ~1 workgroup per CU to fill the chip; otherwise 128^2 tiles
   const int force = dlbb_gemm_force_tile;
   if (force == 256 || (force != 128 && tiles256 >= 192)) {
-    hipLaunchKernelGGL(gemm_bf16_nt_256_kernel, dim3(static_cast<unsigned>(tiles256)),
-                       dim3(kThreads2), 2 * kBuf2Bytes, stream, a);
+    const dim3 g(static_cast<unsigned>(tiles256)), b(kThreads2);
+    if (dlbb_gemm_stagger == 2)
+      hipLaunchKernelGGL(gemm_bf16_nt_256_kernel<2>, g, b, 2 * kBuf2Bytes, stream, a);
+    else if (dlbb_gemm_stagger == 1)
+      hipLaunchKernelGGL(gemm_bf16_nt_256_kernel<1>, g, b, 2 * kBuf2Bytes, stream, a);
+    else
+      hipLaunchKernelGGL(gemm_bf16_nt_256_kernel<0>, g, b, 2 * kBuf2Bytes, stream, a);
     return hipGetLastError();
   }
   const int64_t tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);

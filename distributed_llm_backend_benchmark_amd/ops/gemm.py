@@ -33,6 +33,12 @@ def set_tile(tile: int) -> None:
     _lib.lib().dlbb_gemm_set_tile(int(tile))
 
 
+def set_stagger(mode: int) -> None:
+    """256^2 kernel schedule: 0 lock-step, 1 staggered wave rows, 2 staggered + next tile
+    issued at phase 1. Default 1 (measured fastest: profiles/r01_gemm). For A/B benchmarking."""
+    _lib.lib().dlbb_gemm_set_stagger(int(mode))
+
+
 def hip_supported(x2: torch.Tensor, w: torch.Tensor) -> bool:
     K = x2.shape[1]
     return (x2.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and K % 64 == 0

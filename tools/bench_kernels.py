@@ -45,18 +45,26 @@ if "gemm" in which:
     for name, M, N, K in shapes:
         x, w = rnd(M, K), rnd(N, K)
         fl = 2.0 * M * N * K
-        from distributed_llm_backend_benchmark_amd.ops.gemm import set_tile
+        from distributed_llm_backend_benchmark_amd.ops.gemm import set_stagger, set_tile
+        os.environ["DLBB_GEMM"] = "mfma"
         res = {}
         for tile in (128, 256):
             set_tile(tile)
             res[tile] = t_med(lambda: ops.linear(x, w))
+        set_stagger(0)
+        res["256ls"] = t_med(lambda: ops.linear(x, w))
+        set_stagger(1)
+        res["256s1"] = t_med(lambda: ops.linear(x, w))
+        set_stagger(2)
         set_tile(0)
+        os.environ["DLBB_GEMM"] = "auto"
         th = t_med(lambda: ops.linear(x, w))
         tt = t_med(lambda: torch.matmul(x, w.t()))
         tg = t_med(lambda: ops.linear(x, w, act="gelu"))
         tgt = t_med(lambda: F.gelu(torch.matmul(x, w.t())))
         out(kernel="gemm_bf16_nt", case=name, M=M, N=N, K=K, hip_tflops=fl / th / 1e12,
             t128_tflops=fl / res[128] / 1e12, t256_tflops=fl / res[256] / 1e12,
+            t256_lockstep_tflops=fl / res["256ls"] / 1e12, t256_stag1_tflops=fl / res["256s1"] / 1e12,
             hipblaslt_tflops=fl / tt / 1e12, hip_us=th * 1e6, hipblaslt_us=tt * 1e6,
             hip_gelu_us=tg * 1e6, torch_matmul_gelu_us=tgt * 1e6)
 if "mem" in which:
