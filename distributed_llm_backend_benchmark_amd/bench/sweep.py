@@ -64,7 +64,10 @@ def _bench_one(comm: Comm, op_name: str, data: torch.Tensor, warmup: int, iters:
     if batched:
         mean = time_batched(comm, op, iters, warmup, graph=graph)
         out["batched_mean_s"] = comm.allreduce_max(mean)
-        out["batched_method"] = "hip_graph" if (graph and comm.is_gpu) else "back_to_back"
+        from .timing import graph_safe
+
+        out["batched_method"] = ("hip_graph" if (graph and comm.is_gpu and graph_safe(op))
+                                 else "back_to_back")
     del op
     return out
 

@@ -92,7 +92,7 @@ def time_batched(comm: Comm, op: CollectiveOp, iters: int, warmup: int,
         return (time.perf_counter() - t0) / iters
     stream = torch.cuda.current_stream(comm.device)
     runner = None
-    if graph:
+    if graph and graph_safe(op):
         runner = _capture(comm, op, iters)
     s = torch.cuda.Event(enable_timing=True)
     e = torch.cuda.Event(enable_timing=True)
@@ -109,6 +109,14 @@ def time_batched(comm: Comm, op: CollectiveOp, iters: int, warmup: int,
     return s.elapsed_time(e) * 1e-3 / iters
 
 
+def graph_safe(op: CollectiveOp) -> bool:
+    """HIP-graph capture is used only for ops that launch pure HIP kernels (the IPC xGMI
+    all-reduce). RCCL collectives captured through torch's ProcessGroupNCCL race its watchdog
+    thread's event queries on ROCm 7.0 / torch 2.10 (hipErrorCapturedEvent aborts the process),
+    so they are timed back to back instead."""
+    return getattr(op, "impl", None) == "custom"
+
+
 def _capture(comm: Comm, op: CollectiveOp, iters: int):
     """Capture ``iters`` calls into one HIP graph (launch overhead amortised)."""
     side = torch.cuda.Stream(comm.device)
@@ -118,7 +126,8 @@ def _capture(comm: Comm, op: CollectiveOp, iters: int):
     torch.cuda.current_stream(comm.device).wait_stream(side)
     comm.sync()
     g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g):
+    # thread_local: ProcessGroupNCCL's watchdog thread keeps querying events while we capture
+    with torch.cuda.graph(g, capture_error_mode="thread_local"):
         for _ in range(iters):
             op.run()
     comm.sync()
