@@ -40,6 +40,9 @@ def parse_args(argv=None):
     ap.add_argument("--warmup", type=int, default=None)
     ap.add_argument("--iters", type=int, default=None)
     ap.add_argument("--output-dir", default=None)
+    ap.add_argument("--graph", action="store_true",
+                    help="capture the forward in a HIP graph and replay it (world 1, or all "
+                         "all-reduces on the IPC kernel; RCCL collectives are not captured)")
     ap.add_argument("--ignore-world-size", action="store_true",
                     help="accept any world size (reference exits on mismatch, run_mpi.py:73-77)")
     return ap.parse_args(argv)
@@ -122,24 +125,48 @@ def main(argv=None) -> int:
     metrics.record_init_time(init_elapsed)
     gpu = comm.is_gpu
 
+    fwd_bytes = 0
     for _ in range(int(ex["warmup_iterations"])):
         batch = dataset.get_batch()
+        b0 = model.comm_bytes()
         t = time.perf_counter()
         model(batch)
         comm.sync()
         metrics.record_warmup_time(time.perf_counter() - t)
+        fwd_bytes = model.comm_bytes() - b0
     comm.barrier()
 
-    base_bytes = model.comm_bytes()
+    run_forward = lambda: model(dataset.get_batch())  # noqa: E731
+    use_graph = bool(args.graph or ex.get("graph", False)) and gpu
+    if use_graph and world > 1 and ex.get("allreduce") != "custom":
+        if rank == 0:
+            print("note: --graph needs world 1 or execution.allreduce=custom; running eagerly")
+        use_graph = False
+    if use_graph:
+        # HIP graph: one replay launches the whole forward (all GEMM / LN / all-reduce kernels);
+        # the autotuned GEMM choices were fixed by the eager warmup above.
+        static_in = dataset.get_batch()
+        side = torch.cuda.Stream(comm.device)
+        side.wait_stream(torch.cuda.current_stream(comm.device))
+        with torch.cuda.stream(side):
+            model(static_in)
+        torch.cuda.current_stream(comm.device).wait_stream(side)
+        comm.sync()
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph, capture_error_mode="thread_local"):
+            model(static_in)
+        graph.replay()
+        comm.sync()
+        run_forward = graph.replay
+
     ev = []
     for _ in range(int(ex["benchmark_iterations"])):
-        batch = dataset.get_batch()
         comm.barrier()                          # reference run_mpi.py:177
         if gpu:
             s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             s.record()
         t = time.perf_counter()
-        model(batch)
+        run_forward()
         if gpu:
             e.record()
         comm.sync()
@@ -147,8 +174,7 @@ def main(argv=None) -> int:
         metrics.record_forward_time(time.perf_counter() - t)
         if gpu:
             ev.append(s.elapsed_time(e) * 1e-3)
-    iters = int(ex["benchmark_iterations"])
-    ar_bytes = (model.comm_bytes() - base_bytes) // max(1, iters)
+    ar_bytes = fwd_bytes
     if ev:
         metrics.metrics["forward_device_times"] = ev
 
@@ -165,6 +191,7 @@ def main(argv=None) -> int:
             "allreduces_per_forward": 2 * int(config["model"]["num_layers"]),
             "forward_device_mean": float(np.mean(ev)) if ev else None,
             "kernels": ex.get("kernels"),
+            "hip_graph": use_graph,
             "gemm_fallbacks": __import__(
                 "distributed_llm_backend_benchmark_amd.ops.gemm", fromlist=["x"]).FALLBACKS["count"],
         }

@@ -37,6 +37,7 @@ constexpr int kMaxRanks = 8;
 constexpr int kMaxBlocks = 128;
 constexpr int kCarThreads = 512;
 constexpr unsigned kSpinLimit = 1u << 26;   // ~ seconds of polling, then give up
+constexpr uint32_t kMagic = 0xD1BB0000u;
 
 struct Signal {
   uint32_t flags[2][kMaxBlocks][kMaxRanks];   // written by peers (remote stores)
@@ -244,6 +245,12 @@ DLBB_API int dlbb_car_create(int rank, int world, int64_t cap_bytes, void** out)
     e = hipExtMallocWithFlags(reinterpret_cast<void**>(&s->sig), sizeof(Signal),
                               hipDeviceMallocUncached);
   if (e == hipSuccess) e = hipMemset(s->sig, 0, sizeof(Signal));
+  if (e == hipSuccess) {
+    // magic word identifying this rank's signal page: peers verify their IPC mapping with a
+    // copy-engine read before any kernel touches it (a bad mapping must not fault a kernel)
+    const uint32_t magic = kMagic | static_cast<uint32_t>(rank);
+    e = hipMemcpy(&s->sig->pad[0], &magic, sizeof(magic), hipMemcpyHostToDevice);
+  }
   if (e == hipSuccess) e = hipDeviceSynchronize();
   if (e != hipSuccess) {
     if (s->data) (void)hipFree(s->data);
@@ -304,6 +311,9 @@ DLBB_API int dlbb_car_open(void* h, const void* all_handles, const int* peer_dev
     s->peer_data[p] = static_cast<char*>(pd);
     s->peer_tmp[p] = static_cast<char*>(pt);
     s->peer_sig[p] = static_cast<Signal*>(ps);
+    uint32_t magic = 0;
+    CAR_CHECK(hipMemcpy(&magic, &s->peer_sig[p]->pad[0], sizeof(magic), hipMemcpyDeviceToHost));
+    if (magic != (kMagic | static_cast<uint32_t>(p))) return hipErrorInvalidHandle;
   }
   for (int p = 0; p < kMaxRanks; ++p) {
     s->args.data[p] = s->peer_data[p];
