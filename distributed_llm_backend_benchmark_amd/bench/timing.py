@@ -110,11 +110,12 @@ def time_batched(comm: Comm, op: CollectiveOp, iters: int, warmup: int,
 
 
 def graph_safe(op: CollectiveOp) -> bool:
-    """HIP-graph capture is used only for ops that launch pure HIP kernels (the IPC xGMI
-    all-reduce). RCCL collectives captured through torch's ProcessGroupNCCL race its watchdog
+    """HIP-graph capture is used for ops that do not go through torch's ProcessGroupNCCL: the
+    IPC xGMI all-reduce (pure HIP kernels) and the native RCCL engine (RCCL enqueued directly on
+    the capturing stream). RCCL collectives issued through ProcessGroupNCCL race its watchdog
     thread's event queries on ROCm 7.0 / torch 2.10 (hipErrorCapturedEvent aborts the process),
     so they are timed back to back instead."""
-    return getattr(op, "impl", None) == "custom"
+    return getattr(op, "impl", None) in ("custom", "native")
 
 
 def _capture(comm: Comm, op: CollectiveOp, iters: int):

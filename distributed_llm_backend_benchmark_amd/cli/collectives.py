@@ -56,6 +56,9 @@ def parse_args(argv=None):
     ap.add_argument("--validate", action="store_true", help="check results against closed forms")
     ap.add_argument("--resume", action="store_true", help="skip configs whose JSON exists")
     ap.add_argument("--allreduce-impl", default="rccl", choices=["rccl", "custom", "auto"])
+    ap.add_argument("--engine", default="torch", choices=["torch", "native"],
+                    help="torch = collectives through torch.distributed (ProcessGroupNCCL); "
+                         "native = our C++ RCCL engine enqueuing on the timing stream")
     ap.add_argument("--allreduce-algo", default=None, choices=["oneshot", "twoshot"])
     ap.add_argument("--allgather-form", default="tensor", choices=["tensor", "list"])
     ap.add_argument("--env", action="append", default=[],
@@ -86,10 +89,12 @@ def main(argv=None) -> int:
     else:
         ops = list(REFERENCE_1D_OPS) if args.mode == "1d" else list(REFERENCE_3D_OPS) + [
             "reduce_scatter", "alltoall"]
-    op_opts = {"impl": args.allreduce_impl, "form": args.allgather_form}
+    op_opts = {"impl": "native" if args.engine == "native" else args.allreduce_impl,
+               "form": args.allgather_form}
     if args.allreduce_algo:
         op_opts["algo"] = 1 if args.allreduce_algo == "oneshot" else 2
     extra = {"env": env} if env else {}
+    extra["engine"] = args.engine
     if comm.is_gpu:
         import torch
 

@@ -61,6 +61,17 @@ _SIGS = {
                               c_void_p]),
     "dlbb_xent_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int64,
                               c_void_p, c_void_p]),
+    "dlbb_rccl_unique_id_bytes": (c_int, []),
+    "dlbb_rccl_get_unique_id": (c_int, [c_void_p]),
+    "dlbb_rccl_init": (c_int, [c_void_p, c_int, c_int, ctypes.POINTER(c_void_p)]),
+    "dlbb_rccl_run": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_int64, c_int, c_int]),
+    "dlbb_rccl_enqueue": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_int64, c_int, c_int,
+                                  c_void_p]),
+    "dlbb_rccl_time_iters": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_int64, c_int, c_int,
+                                     c_int, c_int, ctypes.POINTER(ctypes.c_float)]),
+    "dlbb_rccl_time_batched": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_int64, c_int,
+                                       c_int, c_int, c_int, ctypes.POINTER(ctypes.c_float)]),
+    "dlbb_rccl_destroy": (c_int, [c_void_p]),
     "dlbb_car_create": (c_int, [c_int, c_int, c_int64, ctypes.POINTER(c_void_p)]),
     "dlbb_car_ipc_handles": (c_int, [c_void_p, c_void_p]),
     "dlbb_car_handle_bytes": (c_int, []),

@@ -24,6 +24,7 @@ BUILD = os.path.join(REPO, "build", "hip")
 LIB_NAME = "_dlbb_hip.so"
 LIB_PATH = os.path.join(PKG_DIR, LIB_NAME)
 ARCH = os.environ.get("DLBB_OFFLOAD_ARCH", "gfx950")
+ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 
 CFLAGS = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-Wall",
           "-Wno-unused-function", "-munsafe-fp-atomics"]
@@ -73,7 +74,8 @@ def build(force: bool = False, verbose: bool = False, jobs: int = 0) -> str:
     newest = max(os.path.getmtime(o) for o in objs)
     if force or not os.path.exists(LIB_PATH) or os.path.getmtime(LIB_PATH) < newest:
         tmp = LIB_PATH + f".tmp{os.getpid()}"
-        cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp, *objs]
+        cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp, *objs,
+               f"-L{ROCM}/lib", "-lrccl"]
         if verbose:
             print(" ".join(cmd), flush=True)
         r = subprocess.run(cmd, capture_output=True, text=True)

@@ -397,4 +397,11 @@ REFERENCE_3D_OPS = ["allreduce", "allgather", "broadcast", "gather", "reduce"]
 def make_op(name: str, comm: Comm, data: torch.Tensor, **opts) -> CollectiveOp:
     if name not in OPS:
         raise KeyError(f"unknown collective {name!r}; known: {sorted(OPS)}")
+    if opts.get("impl") == "native":
+        # our own RCCL communicator driven from C++, enqueued on the caller's stream
+        from .rccl_native import NATIVE_OPS
+
+        if name not in NATIVE_OPS:
+            raise KeyError(f"no native RCCL implementation of {name!r}")
+        return NATIVE_OPS[name](comm, data, **opts)
     return OPS[name](comm, data, **opts)

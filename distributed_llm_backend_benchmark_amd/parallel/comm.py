@@ -125,6 +125,11 @@ class Comm:
         return float(t.item())
 
     def destroy(self) -> None:
+        import sys
+
+        native = sys.modules.get(__package__ + ".rccl_native")
+        if native is not None:          # our own RCCL communicators go first
+            native.close_all()
         if self.owns_pg and dist.is_initialized():
             try:
                 dist.destroy_process_group()

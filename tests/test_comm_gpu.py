@@ -46,6 +46,39 @@ def test_rccl_world1_sweep(tmp_path):
     assert {r["wire_dtype"] for r in rows3} == {"float32"}
 
 
+def test_native_rccl_world1_sweep(tmp_path):
+    """Native C++ RCCL engine: every op validated, batched loop captured in a HIP graph, and
+    the C++ per-iteration / batched timing loops."""
+    from distributed_llm_backend_benchmark_amd.bench.sweep import run_1d_sweep
+    from distributed_llm_backend_benchmark_amd.parallel.collectives import make_data
+    from distributed_llm_backend_benchmark_amd.parallel.comm import init_distributed
+    from distributed_llm_backend_benchmark_amd.parallel.rccl_native import NATIVE_OPS, get_native
+
+    comm = init_distributed("rccl")
+    try:
+        ops = sorted(NATIVE_OPS)
+        run_1d_sweep(comm, ops=ops, sizes={"1KB": 256, "1MB": 1 << 19}, warmup=2, iters=5,
+                     output_dir=str(tmp_path / "n1d"), impl_name="native", validate=True,
+                     batched=True, graph=True, op_opts={"impl": "native"})
+        eng = get_native(comm)
+        x = make_data((4096,), torch.bfloat16, 0, comm.device)
+        ts = eng.time_iters("allreduce", x, x, x.numel(), iters=7, warmup=2)
+        assert len(ts) == 7 and all(0 < t < 0.1 for t in ts)
+        mean = eng.time_batched("allreduce", x, x, x.numel(), iters=20, warmup=2)
+        assert 0 < mean < 0.1
+    finally:
+        comm.destroy()
+    files = sorted(os.listdir(tmp_path / "n1d"))
+    errs = [f for f in files if f.endswith(".error.json")]
+    assert not errs, [json.load(open(tmp_path / "n1d" / f))["error"] for f in errs]
+    assert len(files) == len(ops) * 2
+    for f in files:
+        d = json.load(open(tmp_path / "n1d" / f))
+        assert d["validated"] is True, f
+        assert d["op_impl"] == "native"
+        assert d["batched_method"] == "hip_graph"
+
+
 def _car_worker(rank, world, sizes):
     import torch
 
