@@ -24,16 +24,20 @@ import torch
 
 from ..parallel.collectives import DTYPES, DTYPE_NAMES, make_data, make_op
 from ..parallel.comm import Comm
+from ..utils import faults, tracing
 from ..utils.io import save_json
 from . import schema
 from .timing import time_batched, time_per_iteration
 
 
-def _agree(comm: Comm, ok: bool) -> bool:
+def _agree(comm: Comm, exc: Optional[BaseException]) -> None:
     """All ranks agree that setup succeeded everywhere (avoid one rank entering a collective
-    alone and hanging until the PG timeout)."""
-    flags = comm.all_gather_object(bool(ok))
-    return all(flags)
+    alone and hanging until the PG timeout); on failure EVERY rank raises with the failing
+    ranks' errors, so rank 0's error record names the real cause."""
+    errs = comm.all_gather_object(None if exc is None else f"{type(exc).__name__}: {exc}")
+    bad = {r: e for r, e in enumerate(errs) if e is not None}
+    if bad:
+        raise RuntimeError(f"setup failed on rank(s) {sorted(bad)}: {bad}")
 
 
 def _validate(comm: Comm, op, shape, dtype, seed) -> bool:
@@ -111,15 +115,17 @@ def run_1d_sweep(comm: Comm, *, ops: Sequence[str], sizes: Dict[str, int], dtype
                     "num_ranks": comm.world_size, "data_size_name": size_name,
                     "num_elements": n, "dtype": dname}
             try:
-                ok, setup_exc = True, None
+                setup_exc = None
                 try:
+                    faults.maybe_fail("setup", op_name, size_name, comm.rank)
                     data = make_data((n,), tdt, comm.rank, comm.device, seed)
                 except Exception as e:  # OOM etc.
-                    ok, setup_exc = False, e
-                if not _agree(comm, ok):
-                    raise RuntimeError(f"setup failed on some rank: {setup_exc}")
-                r = _bench_one(comm, op_name, data, warmup, iters, timing, batched, graph,
-                               validate, seed, op_opts or {})
+                    setup_exc = e
+                _agree(comm, setup_exc)
+                faults.maybe_fail("run", op_name, size_name, comm.rank)
+                with tracing.range(f"{impl_name}/{op_name}/{size_name}"):
+                    r = _bench_one(comm, op_name, data, warmup, iters, timing, batched, graph,
+                                   validate, seed, op_opts or {})
                 rec = schema.result_1d(
                     impl=impl_name, backend=comm.backend_label, op=op_name,
                     ranks=comm.world_size, size_name=size_name, num_elements=r["num_elements"],
@@ -165,18 +171,21 @@ def run_3d_sweep(comm: Comm, *, ops: Sequence[str], batch_sizes: Iterable[int],
                             "num_ranks": comm.world_size,
                             "tensor_shape": {"batch": b, "seq_len": s, "hidden_dim": h}}
                     try:
-                        ok, setup_exc = True, None
+                        setup_exc = None
+                        shape_name = f"b{b}_s{s}_h{h}"
                         try:
+                            faults.maybe_fail("setup", op_name, shape_name, comm.rank)
                             data = make_data((b, s, h), tdt, comm.rank, comm.device, seed)
                             if wdt != tdt:
                                 from ..ops import cast as ops_cast
                                 data = ops_cast(data, wdt)
                         except Exception as e:
-                            ok, setup_exc = False, e
-                        if not _agree(comm, ok):
-                            raise RuntimeError(f"setup failed on some rank: {setup_exc}")
-                        r = _bench_one(comm, op_name, data, warmup, iters, timing, batched,
-                                       graph, validate, seed, op_opts or {})
+                            setup_exc = e
+                        _agree(comm, setup_exc)
+                        faults.maybe_fail("run", op_name, shape_name, comm.rank)
+                        with tracing.range(f"{impl_name}/{op_name}/{shape_name}"):
+                            r = _bench_one(comm, op_name, data, warmup, iters, timing, batched,
+                                           graph, validate, seed, op_opts or {})
                         rec = schema.result_3d(
                             impl=impl_name, backend=comm.backend_label, op=op_name,
                             ranks=comm.world_size, batch=b, seq_len=s, hidden_dim=h,

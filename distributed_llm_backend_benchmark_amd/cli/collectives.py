@@ -64,6 +64,10 @@ def parse_args(argv=None):
     ap.add_argument("--env", action="append", default=[],
                     help="KEY=VAL exported before the process group starts (RCCL knobs: "
                          "NCCL_ALGO, NCCL_PROTO, NCCL_MIN_NCHANNELS, NCCL_MAX_NCHANNELS, ...)")
+    ap.add_argument("--trace", action="store_true",
+                    help="emit roctx ranges (record with rocprofv3 --marker-trace)")
+    ap.add_argument("--torch-profile", default=None, metavar="DIR",
+                    help="torch.profiler Chrome trace per rank into DIR")
     ap.add_argument("--seed", type=int, default=42)
     ap.add_argument("--timeout", type=float, default=900.0, help="process-group timeout (s)")
     return ap.parse_args(argv)
@@ -100,25 +104,32 @@ def main(argv=None) -> int:
 
         extra["device"] = torch.cuda.get_device_name(comm.device)
     outdir = args.output_dir or os.path.join("results", args.mode, impl)
+    from ..utils import tracing
+
+    if args.trace:
+        tracing.enable()
+    timing = args.timing if args.timing != "host" else "host_perf_counter"
     try:
-        if args.mode == "1d":
-            dtype = args.dtype or "fp16"
-            elem = 4 if dtype in ("fp32", "float32") else 2
-            sizes = schema.resolve_1d_sizes(args.sizes, elem)
-            run_1d_sweep(comm, ops=ops, sizes=sizes, dtype=dtype, warmup=args.warmup,
-                         iters=args.iters, output_dir=outdir, impl_name=impl,
-                         timing=args.timing if args.timing != "host" else "host_perf_counter",
-                         batched=args.batched, graph=args.graph, validate=args.validate,
-                         resume=args.resume, seed=args.seed, op_opts=op_opts, extra=extra)
-        else:
-            run_3d_sweep(comm, ops=ops, batch_sizes=_ints(args.batch_sizes),
-                         seq_lengths=_ints(args.seq_lengths), hidden_dims=_ints(args.hidden_dims),
-                         dtype=args.dtype or "bf16", wire_dtype=args.wire_dtype,
-                         warmup=args.warmup, iters=args.iters, output_dir=outdir,
-                         impl_name=impl,
-                         timing=args.timing if args.timing != "host" else "host_perf_counter",
-                         batched=args.batched, graph=args.graph, validate=args.validate,
-                         resume=args.resume, seed=args.seed, op_opts=op_opts, extra=extra)
+        with tracing.torch_profile(args.torch_profile, comm.rank):
+            if args.mode == "1d":
+                dtype = args.dtype or "fp16"
+                elem = 4 if dtype in ("fp32", "float32") else 2
+                sizes = schema.resolve_1d_sizes(args.sizes, elem)
+                run_1d_sweep(comm, ops=ops, sizes=sizes, dtype=dtype, warmup=args.warmup,
+                             iters=args.iters, output_dir=outdir, impl_name=impl,
+                             timing=timing,
+                             batched=args.batched, graph=args.graph, validate=args.validate,
+                             resume=args.resume, seed=args.seed, op_opts=op_opts, extra=extra)
+            else:
+                run_3d_sweep(comm, ops=ops, batch_sizes=_ints(args.batch_sizes),
+                             seq_lengths=_ints(args.seq_lengths),
+                             hidden_dims=_ints(args.hidden_dims),
+                             dtype=args.dtype or "bf16", wire_dtype=args.wire_dtype,
+                             warmup=args.warmup, iters=args.iters, output_dir=outdir,
+                             impl_name=impl,
+                             timing=timing,
+                             batched=args.batched, graph=args.graph, validate=args.validate,
+                             resume=args.resume, seed=args.seed, op_opts=op_opts, extra=extra)
     finally:
         comm.barrier()
         comm.destroy()

@@ -43,6 +43,10 @@ def parse_args(argv=None):
     ap.add_argument("--graph", action="store_true",
                     help="capture the forward in a HIP graph and replay it (world 1, or all "
                          "all-reduces on the IPC kernel; RCCL collectives are not captured)")
+    ap.add_argument("--trace", action="store_true",
+                    help="emit roctx ranges (record with rocprofv3 --marker-trace)")
+    ap.add_argument("--torch-profile", default=None, metavar="DIR",
+                    help="torch.profiler Chrome trace per rank into DIR")
     ap.add_argument("--ignore-world-size", action="store_true",
                     help="accept any world size (reference exits on mismatch, run_mpi.py:73-77)")
     return ap.parse_args(argv)
@@ -159,6 +163,12 @@ def main(argv=None) -> int:
         comm.sync()
         run_forward = graph.replay
 
+    from ..utils import tracing
+
+    if args.trace:
+        tracing.enable()
+    prof = tracing.torch_profile(args.torch_profile, rank)
+    prof.__enter__()
     ev = []
     for _ in range(int(ex["benchmark_iterations"])):
         comm.barrier()                          # reference run_mpi.py:177
@@ -166,7 +176,8 @@ def main(argv=None) -> int:
             s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             s.record()
         t = time.perf_counter()
-        run_forward()
+        with tracing.range("tp_forward"):
+            run_forward()
         if gpu:
             e.record()
         comm.sync()
@@ -174,6 +185,7 @@ def main(argv=None) -> int:
         metrics.record_forward_time(time.perf_counter() - t)
         if gpu:
             ev.append(s.elapsed_time(e) * 1e-3)
+    prof.__exit__(None, None, None)
     ar_bytes = fwd_bytes
     if ev:
         metrics.metrics["forward_device_times"] = ev

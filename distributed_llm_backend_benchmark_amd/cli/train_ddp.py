@@ -41,6 +41,14 @@ def parse_args(argv=None):
     ap.add_argument("--zero", action="store_true",
                     help="ZeRO-2-style: reduce-scatter grads, sharded AdamW, all-gather params")
     ap.add_argument("--compare-overlap", action="store_true")
+    ap.add_argument("--save-checkpoint", default=None, metavar="DIR",
+                    help="after the timed steps, write master weights + AdamW state (safetensors)")
+    ap.add_argument("--resume-from", default=None, metavar="DIR",
+                    help="load a checkpoint written by --save-checkpoint before warmup")
+    ap.add_argument("--trace", action="store_true",
+                    help="emit roctx ranges (record with rocprofv3 --marker-trace)")
+    ap.add_argument("--torch-profile", default=None, metavar="DIR",
+                    help="torch.profiler Chrome trace per rank into DIR")
     ap.add_argument("--output", default=None, help="write the result JSON here (rank 0)")
     return ap.parse_args(argv)
 
@@ -65,6 +73,8 @@ def run(args, comm, overlap: bool):
                               allreduce=args.allreduce)
     data = SyntheticTokenDataset(args.batch, args.seq, cfg.vocab_size, rank=comm.rank,
                                  device=comm.device)
+    if args.resume_from:
+        tr.load_checkpoint(args.resume_from)
     for _ in range(args.warmup):
         x, y = data.get_batch()
         tr.step(x, y, sync_loss=False)
@@ -86,6 +96,10 @@ def run(args, comm, overlap: bool):
         "tflops_per_gpu": model.flops_per_token(args.seq) * args.batch * args.seq
         * args.steps / dt / 1e12,
     }
+    if args.save_checkpoint:
+        tr.save_checkpoint(args.save_checkpoint)
+        res["checkpoint"] = args.save_checkpoint
+    res["step_count"] = tr.step_count
     tr.close()
     del tr, model
     if comm.is_gpu:
@@ -97,8 +111,13 @@ def main(argv=None) -> int:
     args = parse_args(argv)
     from ..parallel.comm import init_distributed
 
+    from ..utils import tracing
+
     comm = init_distributed(args.backend, timeout_s=900)
-    main_res = run(args, comm, overlap=not args.no_overlap)
+    if args.trace:
+        tracing.enable()
+    with tracing.torch_profile(args.torch_profile, comm.rank):
+        main_res = run(args, comm, overlap=not args.no_overlap)
     out = {"metric": "gpt2_ddp_tokens_per_s", "value": main_res["tokens_per_s"],
            "n_gpus": comm.world_size, "overlap": not args.no_overlap, **main_res,
            "config": {k: getattr(args, k) for k in ("n_layer", "n_head", "n_embd", "vocab",

@@ -25,13 +25,16 @@ the MI355X-native replacement used by the GPT-2 DDP microbenchmark:
 
 from __future__ import annotations
 
-from typing import List, Optional
+import json
+import os
+from typing import Dict, List, Optional
 
 import torch
 import torch.distributed as dist
 
 from ..ops import FlatAdamW
 from ..ops.elementwise import ChunkTable
+from ..utils import tracing
 from .comm import Comm
 
 _ALIGN = 64  # elements: keeps every param view 128-B aligned (16-B MFMA/glds rows)
@@ -189,12 +192,77 @@ class FlatParamTrainer:
         """One full training step: forward, backward (+ overlapped all-reduce), AdamW."""
         self.zero_grad()
         self._reset()
-        loss = self.model(idx, targets)
-        loss.backward()
-        self.finish()
+        with tracing.range("fwd"):
+            loss = self.model(idx, targets)
+        with tracing.range("bwd+overlapped_grad_sync"):
+            loss.backward()
+        with tracing.range("grad_sync_tail"):
+            self.finish()
         self.step_count += 1
-        self._optimizer_step()
+        with tracing.range("optimizer"):
+            self._optimizer_step()
         return float(loss.item()) if sync_loss else loss.detach()
+
+    # ------------------------------------------------------------------ checkpoint / resume
+    # The reference has no checkpointing (SURVEY §5.4). Here the optimizer state is three flat
+    # fp32 buffers (+ the step counter), so a checkpoint is one safetensors file per state owner:
+    # rank 0 for replicated DDP, every rank for ZeRO shards. Layout = the flat bucket layout,
+    # which is a pure function of the model and (bucket_mb, world) — checked on load.
+    def _replicated_state(self) -> bool:
+        return True
+
+    def layout_signature(self) -> Dict:
+        return {"kind": type(self).__name__, "numel": int(self.numel),
+                "master_numel": int(self.master.numel()), "world": int(self.world),
+                "buckets": [[b.start, b.end] for b in self.buckets]}
+
+    def state_tensors(self) -> Dict[str, torch.Tensor]:
+        return {"master": self.master, "exp_avg": self.opt.m, "exp_avg_sq": self.opt.v}
+
+    def save_checkpoint(self, path: str) -> None:
+        from safetensors.torch import save_file
+
+        rank = self.comm.rank if self.comm is not None else 0
+        owner = (not self._replicated_state()) or rank == 0
+        meta = {**self.layout_signature(), "step": self.step_count, "adam_t": self.opt.t}
+        if owner:
+            os.makedirs(path, exist_ok=True)
+            name = os.path.join(path, f"rank{rank:05d}.safetensors")
+            tmp = name + ".tmp"
+            save_file({k: v.detach().contiguous().cpu() for k, v in self.state_tensors().items()},
+                      tmp, metadata={"meta": json.dumps(meta)})
+            os.replace(tmp, name)
+            if rank == 0:
+                with open(os.path.join(path, "meta.json.tmp"), "w") as f:
+                    json.dump(meta, f, indent=2)
+                os.replace(os.path.join(path, "meta.json.tmp"), os.path.join(path, "meta.json"))
+        if self.comm is not None:
+            self.comm.barrier()
+
+    @torch.no_grad()
+    def load_checkpoint(self, path: str) -> None:
+        from safetensors import safe_open
+
+        rank = self.comm.rank if self.comm is not None else 0
+        src_rank = 0 if self._replicated_state() else rank
+        name = os.path.join(path, f"rank{src_rank:05d}.safetensors")
+        with safe_open(name, framework="pt", device="cpu") as f:
+            meta = json.loads(f.metadata()["meta"])
+            want = self.layout_signature()
+            for k in ("kind", "numel", "master_numel", "buckets"):
+                if meta[k] != want[k]:
+                    raise ValueError(f"checkpoint {name}: {k} mismatch ({meta[k]} != {want[k]})")
+            if not self._replicated_state() and meta["world"] != want["world"]:
+                raise ValueError("sharded checkpoint written with world "
+                                 f"{meta['world']}, loading with {want['world']}")
+            for k, t in self.state_tensors().items():
+                t.copy_(f.get_tensor(k).to(t.device))
+        self.opt.t = int(meta["adam_t"])
+        self.step_count = int(meta["step"])
+        self._refresh_params()
+
+    def _refresh_params(self) -> None:
+        self.flat_param.copy_(self.master.to(torch.bfloat16))
 
     def close(self) -> None:
         for h in self._hooks:

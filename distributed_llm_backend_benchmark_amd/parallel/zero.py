@@ -71,6 +71,16 @@ class ShardedTrainer(FlatParamTrainer):
     def _optimizer_step(self) -> None:
         self.opt.step(self.grad_shard, working_bf16=self.param_shard,
                       grad_scale=1.0 / self.world)
+        self._gather_params()
+
+    def _replicated_state(self) -> bool:
+        return False
+
+    def _refresh_params(self) -> None:
+        self.param_shard.copy_(self.master.to(torch.bfloat16))
+        self._gather_params()
+
+    def _gather_params(self) -> None:
         works = []
         for b, (src, dst, n) in zip(self.buckets, self._chunks):
             shard = self.param_shard[dst:dst + n]

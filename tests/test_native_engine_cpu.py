@@ -30,3 +30,19 @@ def test_native_symbols_exported():
     for sym in ("dlbb_rccl_get_unique_id", "dlbb_rccl_init", "dlbb_rccl_enqueue",
                 "dlbb_rccl_time_iters", "dlbb_rccl_time_batched", "dlbb_rccl_destroy"):
         assert hasattr(lib, sym)
+
+
+def test_tracing_ranges_and_torch_profile(tmp_path):
+    from distributed_llm_backend_benchmark_amd.utils import tracing
+
+    with tracing.range("disabled"):          # no-op when disabled
+        pass
+    tracing.enable()
+    try:
+        with tracing.range("enabled"):
+            tracing.mark("m")
+    finally:
+        tracing.enable(False)
+    with tracing.torch_profile(str(tmp_path), rank=3):
+        torch.ones(8).sum()
+    assert (tmp_path / "trace_rank3.json").exists()
