@@ -48,6 +48,7 @@ struct GemmArgs {
   int64_t lda, ldb, ldc, ldr;
   int epi;
   int out_f32;
+  int vec_ok;              // 16-B aligned C / residual / preact / bias rows (vector epilogue)
 };
 
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
@@ -208,6 +209,16 @@ __device__ __forceinline__ int section_row(int sec, int g) {
   return (sec == 2 ? 32 : 0) + (g >> 2) * 64 + (g & 3) * 8;
 }
 
+// B rows are staged PERMUTED inside each 64-row block: LDS row (j*16 + t) holds output column
+// (t>>2)*16 + j*4 + (t&3) (bits [3:2] and [5:4] of the row index swapped). With the MFMA
+// operands swapped (D = W_rows x X_rows^T, so each lane holds 4 consecutive columns of one
+// output row) the four n-tiles j of a wave then give every lane 16 CONSECUTIVE columns of one
+// row: the epilogue stores 2 x 16 B per lane and row block instead of 16 scattered 2-B stores.
+__device__ __forceinline__ int perm_brow(int x) {
+  return (x & ~63) | (((x >> 2) & 3) << 4) | (((x >> 4) & 3) << 2) | (x & 3);
+}
+
+template <bool PERM>
 __device__ __forceinline__ void stage_section(const uint16_t* __restrict__ X, int64_t ld,
                                               int64_t row0, int64_t rows, int64_t k0,
                                               char* tile, int sec, int wave, int lane) {
@@ -216,7 +227,7 @@ __device__ __forceinline__ void stage_section(const uint16_t* __restrict__ X, in
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int trow = section_row(sec, wave * 2 + i);
-    int64_t gr = row0 + trow + r_in;
+    int64_t gr = row0 + (PERM ? perm_brow(trow + r_in) : trow + r_in);
     gr = gr < rows ? gr : rows - 1;
     glds16(X + gr * ld + k0 + chunk * 8, tile + trow * (BK * 2));
   }
@@ -225,9 +236,9 @@ __device__ __forceinline__ void stage_section(const uint16_t* __restrict__ X, in
 __device__ __forceinline__ void stage_next(const GemmArgs& a, int64_t m0, int64_t n0,
                                            int64_t k0, char* buf, int sec, int wave, int lane) {
   if (sec == 0 || sec == 3)
-    stage_section(a.A, a.lda, m0, a.M, k0, buf, sec, wave, lane);
+    stage_section<false>(a.A, a.lda, m0, a.M, k0, buf, sec, wave, lane);
   else
-    stage_section(a.B, a.ldb, n0, a.N, k0, buf + kTile2Bytes, sec, wave, lane);
+    stage_section<true>(a.B, a.ldb, n0, a.N, k0, buf + kTile2Bytes, sec, wave, lane);
 }
 
 #define DLBB_WAIT_VM(N) asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory")
@@ -248,7 +259,7 @@ __device__ __forceinline__ void mfma_quadrant(f32x4 (&acc)[8][4], const bf16x8 (
 #pragma unroll
       for (int j = 0; j < 2; ++j)
         acc[MQ * 4 + i][NQ * 2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-            af[ks][i], bf[ks][j], acc[MQ * 4 + i][NQ * 2 + j], 0, 0, 0);
+            bf[ks][j], af[ks][i], acc[MQ * 4 + i][NQ * 2 + j], 0, 0, 0);
   __builtin_amdgcn_s_setprio(0);
 }
 
@@ -270,7 +281,8 @@ __device__ __forceinline__ void read_b(const char* tileB, int wc, int nq, int fr
       bf[ks][j] = read_frag(tileB, wc * 64 + nq * 32 + j * 16 + fr, ks * 4 + fq);
 }
 
-template <int MODE>   // 0 lock-step, 1 staggered, 2 staggered + whole next tile issued at phase 1
+template <int MODE>   // 0 lock-step, 1 staggered, 2 staggered + whole next tile issued at phase 1,
+                      // 3 staggered + deep (one K-tile in flight) restaging
 __global__ void __launch_bounds__(kThreads2, 1) gemm_bf16_nt_256_kernel(GemmArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x;
@@ -301,15 +313,87 @@ __global__ void __launch_bounds__(kThreads2, 1) gemm_bf16_nt_256_kernel(GemmArgs
 
   const int64_t nk = a.K / BK;
   // prologue: all four sections of K-tile 0 into buffer 0, wait for SA0 + SB0
-  stage_next(a, m0, n0, 0, smem, 0, wave, lane);
-  stage_next(a, m0, n0, 0, smem, 1, wave, lane);
-  stage_next(a, m0, n0, 0, smem, 2, wave, lane);
-  stage_next(a, m0, n0, 0, smem, 3, wave, lane);
-  DLBB_WAIT_VM(4);
-  DLBB_BARRIER();
+  if constexpr (MODE != 3) {
+    stage_next(a, m0, n0, 0, smem, 0, wave, lane);
+    stage_next(a, m0, n0, 0, smem, 1, wave, lane);
+    stage_next(a, m0, n0, 0, smem, 2, wave, lane);
+    stage_next(a, m0, n0, 0, smem, 3, wave, lane);
+    DLBB_WAIT_VM(4);
+    DLBB_BARRIER();
+  }
 
   bf16x8 af[2][4], b0[2][2], b1[2][2];
-  if constexpr (MODE >= 1) {
+  if constexpr (MODE == 3) {
+    // Deep pipeline: a section is restaged for tile t+2 into the CURRENT buffer as soon as
+    // tile t's last read of it is two phases old, so four sections (one whole K-tile) stay in
+    // flight instead of two, with the same 128 KiB of LDS. Issue schedule in tile t:
+    //   ph1: S2(t+1)  ph2: S3(t+1)  ph3: S0(t+2)  ph4: S1(t+2)
+    // (S0 = A mq0, S1 = B nq0, S2 = B nq1, S3 = A mq1; last reads of tile t: S0,S1 @ph1,
+    // S2 @ph2, S3 @ph3.) Each phase: ds_reads first, then the section issue, the counted wait
+    // for the section read NEXT phase (retired before this phase's first barrier: with the
+    // wave rows staggered by one barrier that is the latest safe point), barrier, lgkmcnt(0),
+    // 16 MFMA, barrier.
+    const bool lag = wr == 1;
+    stage_next(a, m0, n0, 0, smem, 0, wave, lane);
+    stage_next(a, m0, n0, 0, smem, 1, wave, lane);
+    stage_next(a, m0, n0, 0, smem, 2, wave, lane);
+    stage_next(a, m0, n0, 0, smem, 3, wave, lane);
+    // + the first two sections of tile 1; then retire S0(0), S1(0) for phase 1
+    if (nk > 1) {
+      stage_next(a, m0, n0, BK, smem + kBuf2Bytes, 0, wave, lane);
+      stage_next(a, m0, n0, BK, smem + kBuf2Bytes, 1, wave, lane);
+      DLBB_WAIT_VM(8);
+    } else {
+      DLBB_WAIT_VM(4);
+    }
+    __builtin_amdgcn_s_barrier();
+    if (lag) __builtin_amdgcn_s_barrier();
+    for (int64_t t = 0; t < nk; ++t) {
+      char* cur = smem + (t & 1) * kBuf2Bytes;
+      char* nxt = smem + ((t + 1) & 1) * kBuf2Bytes;
+      const bool m1 = t + 1 < nk, m2 = t + 2 < nk;
+      // phase 1: MFMA (mq0, nq0); wait S2(t)
+      read_a(cur, wr, 0, fr, fq, af);
+      read_b(cur + kTile2Bytes, wc, 0, fr, fq, b0);
+      if (m1) { stage_next(a, m0, n0, (t + 1) * BK, nxt, 2, wave, lane); DLBB_WAIT_VM(8); }
+      else DLBB_WAIT_VM(2);
+      __builtin_amdgcn_s_barrier();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      mfma_quadrant<0, 0>(acc, af, b0);
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+      // phase 2: MFMA (mq0, nq1); wait S3(t)
+      read_b(cur + kTile2Bytes, wc, 1, fr, fq, b1);
+      if (m1) { stage_next(a, m0, n0, (t + 1) * BK, nxt, 3, wave, lane); DLBB_WAIT_VM(8); }
+      else DLBB_WAIT_VM(0);
+      __builtin_amdgcn_s_barrier();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      mfma_quadrant<0, 1>(acc, af, b1);
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+      // phase 3: MFMA (mq1, nq1); restage S0 for tile t+2
+      read_a(cur, wr, 1, fr, fq, af);
+      if (m2) stage_next(a, m0, n0, (t + 2) * BK, cur, 0, wave, lane);
+      __builtin_amdgcn_s_barrier();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      mfma_quadrant<1, 1>(acc, af, b1);
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+      // phase 4: MFMA (mq1, nq0); restage S1 for tile t+2; wait S0(t+1), S1(t+1)
+      if (m2) { stage_next(a, m0, n0, (t + 2) * BK, cur, 1, wave, lane); DLBB_WAIT_VM(8); }
+      else if (m1) DLBB_WAIT_VM(4);
+      else DLBB_WAIT_VM(0);
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      mfma_quadrant<1, 0>(acc, af, b0);
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+    }
+    if (!lag) __builtin_amdgcn_s_barrier();
+  } else if constexpr (MODE >= 1) {
     // Two barriers per phase ([stage + ds_read] | barrier | [16 MFMA] | barrier) and wave
     // row 1 one barrier behind wave row 0: on every SIMD one wave's LDS reads overlap its
     // partner's MFMA cluster (CDNA guide 8-phase template, T3). With the groups offset, a
@@ -423,35 +507,82 @@ __global__ void __launch_bounds__(kThreads2, 1) gemm_bf16_nt_256_kernel(GemmArgs
   }
   }
 
-  // epilogue: 32-bit offsets inside this wave's 128 x 64 output block (keeps VGPRs low)
+  // epilogue. Lane (fr, fq) holds output row rbase + i*16 + fr, columns cbase .. cbase+15
+  // (acc[i][j][r] = column j*4 + r, see perm_brow).
   const int epi = a.epi;
-  const int64_t row0 = m0 + wr * 128, col0 = n0 + wc * 64;
+  const int64_t cbase = n0 + wc * 64 + fq * 16;
+  const int cols_left = static_cast<int>(a.N - cbase < 16 ? a.N - cbase : 16);
+  if (cols_left <= 0) return;
+  const int64_t rbase = m0 + wr * 128 + fr;
+  const int rows_left = static_cast<int>(a.M - rbase);     // rows i*16 < rows_left are valid
+  const bool vec = a.vec_ok && cols_left == 16;
+  float bias[16];
+#pragma unroll
+  for (int c = 0; c < 16; ++c) bias[c] = 0.f;
+  if (epi & EPI_BIAS) {
+    if (vec) {
+      const u16x8* bp = reinterpret_cast<const u16x8*>(a.bias + cbase);
+      const u16x8 b0v = bp[0], b1v = bp[1];
+#pragma unroll
+      for (int c = 0; c < 8; ++c) { bias[c] = bf16_to_f32(b0v[c]); bias[8 + c] = bf16_to_f32(b1v[c]); }
+    } else {
+#pragma unroll
+      for (int c = 0; c < 16; ++c) if (c < cols_left) bias[c] = bf16_to_f32(a.bias[cbase + c]);
+    }
+  }
   const int ldc = static_cast<int>(a.ldc), ldr = static_cast<int>(a.ldr);
-  const int rows_left = static_cast<int>(a.M - row0 < 128 ? a.M - row0 : 128);
-  const int cols_left = static_cast<int>(a.N - col0 < 64 ? a.N - col0 : 64);
-  float* cf = static_cast<float*>(a.C) + row0 * a.ldc + col0;
-  uint16_t* cb = static_cast<uint16_t*>(a.C) + row0 * a.ldc + col0;
-  uint16_t* pb = a.preact ? a.preact + row0 * a.ldc + col0 : nullptr;
-  const uint16_t* rb = (epi & EPI_RESIDUAL) ? a.residual + row0 * a.ldr + col0 : nullptr;
+  float* cf = static_cast<float*>(a.C) + rbase * a.ldc + cbase;
+  uint16_t* cb = static_cast<uint16_t*>(a.C) + rbase * a.ldc + cbase;
+  uint16_t* pb = a.preact ? a.preact + rbase * a.ldc + cbase : nullptr;
+  const uint16_t* rb = (epi & EPI_RESIDUAL) ? a.residual + rbase * a.ldr + cbase : nullptr;
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int cl = j * 16 + fr;
-    if (cl >= cols_left) continue;
-    const float bias = (epi & EPI_BIAS) ? bf16_to_f32(a.bias[col0 + cl]) : 0.f;
+  for (int i = 0; i < 8; ++i) {
+    if (i * 16 >= rows_left) break;
+    float v[16];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
+    for (int j = 0; j < 4; ++j)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int rl = i * 16 + fq * 4 + r;
-        if (rl >= rows_left) continue;
-        float v = acc[i][j][r] + bias;
-        if (pb) pb[rl * ldc + cl] = f32_to_bf16(v);
-        v = apply_act(v, epi);
-        if (rb) v += bf16_to_f32(rb[rl * ldr + cl]);
-        if (a.out_f32)
-          cf[rl * ldc + cl] = v;
-        else
-          cb[rl * ldc + cl] = f32_to_bf16(v);
+      for (int r = 0; r < 4; ++r) v[j * 4 + r] = acc[i][j][r] + bias[j * 4 + r];
+    const int oc = i * 16 * ldc, orr = i * 16 * ldr;
+    if (vec) {
+      if (pb) {
+        u16x8 p0, p1;
+#pragma unroll
+        for (int c = 0; c < 8; ++c) { p0[c] = f32_to_bf16(v[c]); p1[c] = f32_to_bf16(v[8 + c]); }
+        reinterpret_cast<u16x8*>(pb + oc)[0] = p0;
+        reinterpret_cast<u16x8*>(pb + oc)[1] = p1;
+      }
+      if (epi & (EPI_GELU_ERF | EPI_GELU_TANH)) {
+#pragma unroll
+        for (int c = 0; c < 16; ++c) v[c] = apply_act(v[c], epi);
+      }
+      if (rb) {
+        const u16x8 r0 = reinterpret_cast<const u16x8*>(rb + orr)[0];
+        const u16x8 r1 = reinterpret_cast<const u16x8*>(rb + orr)[1];
+#pragma unroll
+        for (int c = 0; c < 8; ++c) { v[c] += bf16_to_f32(r0[c]); v[8 + c] += bf16_to_f32(r1[c]); }
+      }
+      if (a.out_f32) {
+        float4* o = reinterpret_cast<float4*>(cf + oc);
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          o[q] = make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+      } else {
+        u16x8 o0, o1;
+#pragma unroll
+        for (int c = 0; c < 8; ++c) { o0[c] = f32_to_bf16(v[c]); o1[c] = f32_to_bf16(v[8 + c]); }
+        reinterpret_cast<u16x8*>(cb + oc)[0] = o0;
+        reinterpret_cast<u16x8*>(cb + oc)[1] = o1;
+      }
+    } else {
+#pragma unroll
+      for (int c = 0; c < 16; ++c) {
+        if (c >= cols_left) break;
+        float x = v[c];
+        if (pb) pb[oc + c] = f32_to_bf16(x);
+        x = apply_act(x, epi);
+        if (rb) x += bf16_to_f32(rb[orr + c]);
+        if (a.out_f32) cf[oc + c] = x; else cb[oc + c] = f32_to_bf16(x);
       }
     }
   }
@@ -463,10 +594,11 @@ using namespace dlbb;
 
 static int dlbb_gemm_force_tile = 0;   // 0 = heuristic, 128 or 256 = force (A/B testing)
 
-static int dlbb_gemm_stagger = 1;      // 256^2 schedule: 0 lock-step, 1 staggered (best), 2 + early issue
+static int dlbb_gemm_stagger = 3;      // 256^2 schedule (set_stagger): 3 = deep restaging, measured fastest
 
 DLBB_API void dlbb_gemm_set_tile(int tile) { dlbb_gemm_force_tile = tile; }
 DLBB_API void dlbb_gemm_set_stagger(int on) { dlbb_gemm_stagger = on; }
+DLBB_API int dlbb_gemm_get_stagger() { return dlbb_gemm_stagger; }
 
 DLBB_API int dlbb_gemm_bf16_nt(const void* A, int64_t lda, const void* B, int64_t ldb, void* C,
                                int64_t ldc, int64_t M, int64_t N, int64_t K, const void* bias,
@@ -479,15 +611,22 @@ DLBB_API int dlbb_gemm_bf16_nt(const void* A, int64_t lda, const void* B, int64_
     return hipErrorInvalidValue;
   if ((epi & EPI_BIAS) && !bias) return hipErrorInvalidValue;
   if ((epi & EPI_RESIDUAL) && !residual) return hipErrorInvalidValue;
+  auto al16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+  const int vec_ok = (ldc % 8 == 0) && al16(C) && (!preact || al16(preact)) &&
+                     (!(epi & EPI_RESIDUAL) || (ldr % 8 == 0 && al16(residual))) &&
+                     (!(epi & EPI_BIAS) || al16(bias));
   GemmArgs a{static_cast<const uint16_t*>(A), static_cast<const uint16_t*>(B), C,
              static_cast<const uint16_t*>(bias), static_cast<const uint16_t*>(residual),
-             static_cast<uint16_t*>(preact), M, N, K, lda, ldb, ldc, ldr, epi, out_f32};
+             static_cast<uint16_t*>(preact), M, N, K, lda, ldb, ldc, ldr, epi, out_f32,
+             vec_ok};
   const int64_t tiles256 = ((M + BM2 - 1) / BM2) * ((N + BN2 - 1) / BN2);
   // the 256^2 schedule needs >= ~1 workgroup per CU to fill the chip; otherwise 128^2 tiles
   const int force = dlbb_gemm_force_tile;
   if (force == 256 || (force != 128 && tiles256 >= 192)) {
     const dim3 g(static_cast<unsigned>(tiles256)), b(kThreads2);
-    if (dlbb_gemm_stagger == 2)
+    if (dlbb_gemm_stagger == 3)
+      hipLaunchKernelGGL(gemm_bf16_nt_256_kernel<3>, g, b, 2 * kBuf2Bytes, stream, a);
+    else if (dlbb_gemm_stagger == 2)
       hipLaunchKernelGGL(gemm_bf16_nt_256_kernel<2>, g, b, 2 * kBuf2Bytes, stream, a);
     else if (dlbb_gemm_stagger == 1)
       hipLaunchKernelGGL(gemm_bf16_nt_256_kernel<1>, g, b, 2 * kBuf2Bytes, stream, a);

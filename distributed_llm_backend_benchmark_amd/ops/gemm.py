@@ -35,8 +35,13 @@ def set_tile(tile: int) -> None:
 
 def set_stagger(mode: int) -> None:
     """256^2 kernel schedule: 0 lock-step, 1 staggered wave rows, 2 staggered + next tile
-    issued at phase 1. Default 1 (measured fastest: profiles/r01_gemm). For A/B benchmarking."""
+    issued at phase 1, 3 staggered + deep restaging (one K-tile in flight). For A/B
+    benchmarking; the library default is the measured fastest (profiles/)."""
     _lib.lib().dlbb_gemm_set_stagger(int(mode))
+
+
+def get_stagger() -> int:
+    return int(_lib.lib().dlbb_gemm_get_stagger())
 
 
 def hip_supported(x2: torch.Tensor, w: torch.Tensor) -> bool:

@@ -89,16 +89,21 @@ def test_chunk_copy_and_scale():
         torch.testing.assert_close(o, t.float() * 0.125, rtol=1e-6, atol=1e-6)
 
 
-@pytest.fixture(params=[("mfma", 0), ("mfma", 128), ("mfma", 256), ("blas", 0)],
-                ids=["mfma_auto", "mfma_t128", "mfma_t256", "blas"])
+@pytest.fixture(params=[("mfma", 0, 1), ("mfma", 128, 1), ("mfma", 256, 1), ("mfma", 256, 0),
+                        ("mfma", 256, 2), ("mfma", 256, 3), ("blas", 0, 1)],
+                ids=["mfma_auto", "mfma_t128", "mfma_t256", "mfma_t256_lockstep",
+                     "mfma_t256_early", "mfma_t256_deep", "blas"])
 def gemm_tile(request, monkeypatch):
-    from distributed_llm_backend_benchmark_amd.ops.gemm import set_tile
+    from distributed_llm_backend_benchmark_amd.ops.gemm import get_stagger, set_stagger, set_tile
 
-    impl, tile = request.param
+    impl, tile, stagger = request.param
     monkeypatch.setenv("DLBB_GEMM", impl)
+    old = get_stagger()
     set_tile(tile)
+    set_stagger(stagger)
     yield request.param
     set_tile(0)
+    set_stagger(old)
 
 
 @pytest.mark.parametrize("M,N,K", [(256, 256, 64), (4096, 1024, 4096), (300, 200, 128),
