@@ -281,6 +281,189 @@ __device__ __forceinline__ void read_b(const char* tileB, int wc, int nq, int fr
       bf[ks][j] = read_frag(tileB, wc * 64 + nq * 32 + j * 16 + fr, ks * 4 + fq);
 }
 
+struct Tile256 {
+  int64_t m0, n0;
+};
+
+// virtual workgroup id -> output tile: XCD-aware bijective remap (T1), then GROUP_M ordering
+__device__ __forceinline__ Tile256 tile_of(const GemmArgs& a, int vb) {
+  // 32-bit index math (tile counts < 2^31): 64-bit divisions cost SGPRs and SALU time
+  const int tiles_m = static_cast<int>((a.M + BM2 - 1) / BM2);
+  const int tiles_n = static_cast<int>((a.N + BN2 - 1) / BN2);
+  const int nwg = tiles_m * tiles_n;
+  const int q = nwg >> 3, r = nwg & 7, x = vb & 7;
+  const int wid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (vb >> 3);
+  const int group_size = kGroupM * tiles_n;
+  const int group = wid / group_size;
+  const int first_m = group * kGroupM;
+  const int gm = (tiles_m - first_m) < kGroupM ? (tiles_m - first_m) : kGroupM;
+  const int in_group = wid - group * group_size;
+  return Tile256{static_cast<int64_t>(first_m + in_group % gm) * BM2,
+                 static_cast<int64_t>(in_group / gm) * BN2};
+}
+
+// Deep-pipeline prologue: all four sections of K-tile 0 and S0, S1 of K-tile 1 (6 sections).
+__device__ __forceinline__ void deep_prologue(const GemmArgs& a, int64_t m0, int64_t n0,
+                                              int64_t nk, char* smem, int wave, int lane) {
+  stage_next(a, m0, n0, 0, smem, 0, wave, lane);
+  stage_next(a, m0, n0, 0, smem, 1, wave, lane);
+  stage_next(a, m0, n0, 0, smem, 2, wave, lane);
+  stage_next(a, m0, n0, 0, smem, 3, wave, lane);
+  if (nk > 1) {
+    stage_next(a, m0, n0, BK, smem + kBuf2Bytes, 0, wave, lane);
+    stage_next(a, m0, n0, BK, smem + kBuf2Bytes, 1, wave, lane);
+  }
+}
+
+  // Deep pipeline: a section is restaged for tile t+2 into the CURRENT buffer as soon as
+  // tile t's last read of it is two phases old, so four sections (one whole K-tile) stay in
+  // flight instead of two, with the same 128 KiB of LDS. Issue schedule in tile t:
+  //   ph1: S2(t+1)  ph2: S3(t+1)  ph3: S0(t+2)  ph4: S1(t+2)
+  // (S0 = A mq0, S1 = B nq0, S2 = B nq1, S3 = A mq1; last reads of tile t: S0,S1 @ph1,
+  // S2 @ph2, S3 @ph3.) Each phase: ds_reads first, then the section issue, the counted wait
+  // for the section read NEXT phase (retired before this phase's first barrier: with the
+  // wave rows staggered by one barrier that is the latest safe point), barrier, lgkmcnt(0),
+  // 16 MFMA, barrier.
+// Entry: the prologue's S0(0), S1(0) retired and a barrier passed; the lagging wave row has
+// taken its extra barrier. Exit: every LDS read done; the wave rows are still staggered.
+__device__ __forceinline__ void deep_mainloop(const GemmArgs& a, f32x4 (&acc)[8][4], int64_t m0,
+                                              int64_t n0, int64_t nk, char* smem, int wave,
+                                              int lane) {
+  const int wr = wave >> 2, wc = wave & 3;
+  const int fr = lane & 15, fq = lane >> 4;
+  bf16x8 af[2][4], b0[2][2], b1[2][2];
+  for (int64_t t = 0; t < nk; ++t) {
+    char* cur = smem + (t & 1) * kBuf2Bytes;
+    char* nxt = smem + ((t + 1) & 1) * kBuf2Bytes;
+    const bool m1 = t + 1 < nk, m2 = t + 2 < nk;
+    // phase 1: MFMA (mq0, nq0); wait S2(t)
+    read_a(cur, wr, 0, fr, fq, af);
+    read_b(cur + kTile2Bytes, wc, 0, fr, fq, b0);
+    if (m1) { stage_next(a, m0, n0, (t + 1) * BK, nxt, 2, wave, lane); DLBB_WAIT_VM(8); }
+    else DLBB_WAIT_VM(2);
+    __builtin_amdgcn_s_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    mfma_quadrant<0, 0>(acc, af, b0);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    // phase 2: MFMA (mq0, nq1); wait S3(t)
+    read_b(cur + kTile2Bytes, wc, 1, fr, fq, b1);
+    if (m1) { stage_next(a, m0, n0, (t + 1) * BK, nxt, 3, wave, lane); DLBB_WAIT_VM(8); }
+    else DLBB_WAIT_VM(0);
+    __builtin_amdgcn_s_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    mfma_quadrant<0, 1>(acc, af, b1);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    // phase 3: MFMA (mq1, nq1); restage S0 for tile t+2
+    read_a(cur, wr, 1, fr, fq, af);
+    if (m2) stage_next(a, m0, n0, (t + 2) * BK, cur, 0, wave, lane);
+    __builtin_amdgcn_s_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    mfma_quadrant<1, 1>(acc, af, b1);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    // phase 4: MFMA (mq1, nq0); restage S1 for tile t+2; wait S0(t+1), S1(t+1)
+    if (m2) { stage_next(a, m0, n0, (t + 2) * BK, cur, 1, wave, lane); DLBB_WAIT_VM(8); }
+    else if (m1) DLBB_WAIT_VM(4);
+    else DLBB_WAIT_VM(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    mfma_quadrant<1, 0>(acc, af, b0);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+  }
+}
+
+// Epilogue of one 256^2 tile (global stores from registers; no LDS, no barriers).
+__device__ __forceinline__ void store_tile_256(const GemmArgs& a, const f32x4 (&acc)[8][4],
+                                               int64_t m0, int64_t n0, int wave, int lane) {
+  const int wr = wave >> 2, wc = wave & 3;
+  const int fr = lane & 15, fq = lane >> 4;
+  // epilogue. Lane (fr, fq) holds output row rbase + i*16 + fr, columns cbase .. cbase+15
+  // (acc[i][j][r] = column j*4 + r, see perm_brow).
+  const int epi = a.epi;
+  const int64_t cbase = n0 + wc * 64 + fq * 16;
+  const int cols_left = static_cast<int>(a.N - cbase < 16 ? a.N - cbase : 16);
+  if (cols_left <= 0) return;
+  const int64_t rbase = m0 + wr * 128 + fr;
+  const int rows_left = static_cast<int>(a.M - rbase);     // rows i*16 < rows_left are valid
+  const bool vec = a.vec_ok && cols_left == 16;
+  float bias[16];
+#pragma unroll
+  for (int c = 0; c < 16; ++c) bias[c] = 0.f;
+  if (epi & EPI_BIAS) {
+    if (vec) {
+      const u16x8* bp = reinterpret_cast<const u16x8*>(a.bias + cbase);
+      const u16x8 b0v = bp[0], b1v = bp[1];
+#pragma unroll
+      for (int c = 0; c < 8; ++c) { bias[c] = bf16_to_f32(b0v[c]); bias[8 + c] = bf16_to_f32(b1v[c]); }
+    } else {
+#pragma unroll
+      for (int c = 0; c < 16; ++c) if (c < cols_left) bias[c] = bf16_to_f32(a.bias[cbase + c]);
+    }
+  }
+  const int ldc = static_cast<int>(a.ldc), ldr = static_cast<int>(a.ldr);
+  float* cf = static_cast<float*>(a.C) + rbase * a.ldc + cbase;
+  uint16_t* cb = static_cast<uint16_t*>(a.C) + rbase * a.ldc + cbase;
+  uint16_t* pb = a.preact ? a.preact + rbase * a.ldc + cbase : nullptr;
+  const uint16_t* rb = (epi & EPI_RESIDUAL) ? a.residual + rbase * a.ldr + cbase : nullptr;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    if (i * 16 >= rows_left) break;
+    float v[16];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[j * 4 + r] = acc[i][j][r] + bias[j * 4 + r];
+    const int oc = i * 16 * ldc, orr = i * 16 * ldr;
+    if (vec) {
+      if (pb) {
+        u16x8 p0, p1;
+#pragma unroll
+        for (int c = 0; c < 8; ++c) { p0[c] = f32_to_bf16(v[c]); p1[c] = f32_to_bf16(v[8 + c]); }
+        reinterpret_cast<u16x8*>(pb + oc)[0] = p0;
+        reinterpret_cast<u16x8*>(pb + oc)[1] = p1;
+      }
+      if (epi & (EPI_GELU_ERF | EPI_GELU_TANH)) {
+#pragma unroll
+        for (int c = 0; c < 16; ++c) v[c] = apply_act(v[c], epi);
+      }
+      if (rb) {
+        const u16x8 r0 = reinterpret_cast<const u16x8*>(rb + orr)[0];
+        const u16x8 r1 = reinterpret_cast<const u16x8*>(rb + orr)[1];
+#pragma unroll
+        for (int c = 0; c < 8; ++c) { v[c] += bf16_to_f32(r0[c]); v[8 + c] += bf16_to_f32(r1[c]); }
+      }
+      if (a.out_f32) {
+        float4* o = reinterpret_cast<float4*>(cf + oc);
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          o[q] = make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+      } else {
+        u16x8 o0, o1;
+#pragma unroll
+        for (int c = 0; c < 8; ++c) { o0[c] = f32_to_bf16(v[c]); o1[c] = f32_to_bf16(v[8 + c]); }
+        reinterpret_cast<u16x8*>(cb + oc)[0] = o0;
+        reinterpret_cast<u16x8*>(cb + oc)[1] = o1;
+      }
+    } else {
+#pragma unroll
+      for (int c = 0; c < 16; ++c) {
+        if (c >= cols_left) break;
+        float x = v[c];
+        if (pb) pb[oc + c] = f32_to_bf16(x);
+        x = apply_act(x, epi);
+        if (rb) x += bf16_to_f32(rb[orr + c]);
+        if (a.out_f32) cf[oc + c] = x; else cb[oc + c] = f32_to_bf16(x);
+      }
+    }
+  }
+}
+
 template <int MODE>   // 0 lock-step, 1 staggered, 2 staggered + whole next tile issued at phase 1,
                       // 3 staggered + deep (one K-tile in flight) restaging
 __global__ void __launch_bounds__(kThreads2, 1) gemm_bf16_nt_256_kernel(GemmArgs a) {
@@ -291,19 +474,8 @@ __global__ void __launch_bounds__(kThreads2, 1) gemm_bf16_nt_256_kernel(GemmArgs
   const int wr = wave >> 2, wc = wave & 3;
   const int fr = lane & 15, fq = lane >> 4;
 
-  const int64_t tiles_m = (a.M + BM2 - 1) / BM2, tiles_n = (a.N + BN2 - 1) / BN2;
-  const int64_t nwg = tiles_m * tiles_n;
-  int64_t wid = blockIdx.x;
-  {
-    const int64_t q = nwg / 8, r = nwg % 8, x = wid % 8;
-    wid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + wid / 8;
-  }
-  const int64_t group_size = kGroupM * tiles_n;
-  const int64_t group = wid / group_size;
-  const int64_t first_m = group * kGroupM;
-  const int64_t gm = (tiles_m - first_m) < kGroupM ? (tiles_m - first_m) : kGroupM;
-  const int64_t m0 = (first_m + (wid % group_size) % gm) * BM2;
-  const int64_t n0 = ((wid % group_size) / gm) * BN2;
+  const Tile256 tl = tile_of(a, static_cast<int>(blockIdx.x));
+  const int64_t m0 = tl.m0, n0 = tl.n0;
 
   f32x4 acc[8][4];
 #pragma unroll
@@ -324,74 +496,12 @@ __global__ void __launch_bounds__(kThreads2, 1) gemm_bf16_nt_256_kernel(GemmArgs
 
   bf16x8 af[2][4], b0[2][2], b1[2][2];
   if constexpr (MODE == 3) {
-    // Deep pipeline: a section is restaged for tile t+2 into the CURRENT buffer as soon as
-    // tile t's last read of it is two phases old, so four sections (one whole K-tile) stay in
-    // flight instead of two, with the same 128 KiB of LDS. Issue schedule in tile t:
-    //   ph1: S2(t+1)  ph2: S3(t+1)  ph3: S0(t+2)  ph4: S1(t+2)
-    // (S0 = A mq0, S1 = B nq0, S2 = B nq1, S3 = A mq1; last reads of tile t: S0,S1 @ph1,
-    // S2 @ph2, S3 @ph3.) Each phase: ds_reads first, then the section issue, the counted wait
-    // for the section read NEXT phase (retired before this phase's first barrier: with the
-    // wave rows staggered by one barrier that is the latest safe point), barrier, lgkmcnt(0),
-    // 16 MFMA, barrier.
     const bool lag = wr == 1;
-    stage_next(a, m0, n0, 0, smem, 0, wave, lane);
-    stage_next(a, m0, n0, 0, smem, 1, wave, lane);
-    stage_next(a, m0, n0, 0, smem, 2, wave, lane);
-    stage_next(a, m0, n0, 0, smem, 3, wave, lane);
-    // + the first two sections of tile 1; then retire S0(0), S1(0) for phase 1
-    if (nk > 1) {
-      stage_next(a, m0, n0, BK, smem + kBuf2Bytes, 0, wave, lane);
-      stage_next(a, m0, n0, BK, smem + kBuf2Bytes, 1, wave, lane);
-      DLBB_WAIT_VM(8);
-    } else {
-      DLBB_WAIT_VM(4);
-    }
+    deep_prologue(a, m0, n0, nk, smem, wave, lane);
+    if (nk > 1) DLBB_WAIT_VM(8); else DLBB_WAIT_VM(4);   // retire S0(0), S1(0)
     __builtin_amdgcn_s_barrier();
     if (lag) __builtin_amdgcn_s_barrier();
-    for (int64_t t = 0; t < nk; ++t) {
-      char* cur = smem + (t & 1) * kBuf2Bytes;
-      char* nxt = smem + ((t + 1) & 1) * kBuf2Bytes;
-      const bool m1 = t + 1 < nk, m2 = t + 2 < nk;
-      // phase 1: MFMA (mq0, nq0); wait S2(t)
-      read_a(cur, wr, 0, fr, fq, af);
-      read_b(cur + kTile2Bytes, wc, 0, fr, fq, b0);
-      if (m1) { stage_next(a, m0, n0, (t + 1) * BK, nxt, 2, wave, lane); DLBB_WAIT_VM(8); }
-      else DLBB_WAIT_VM(2);
-      __builtin_amdgcn_s_barrier();
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_sched_barrier(0);
-      mfma_quadrant<0, 0>(acc, af, b0);
-      __builtin_amdgcn_sched_barrier(0);
-      __builtin_amdgcn_s_barrier();
-      // phase 2: MFMA (mq0, nq1); wait S3(t)
-      read_b(cur + kTile2Bytes, wc, 1, fr, fq, b1);
-      if (m1) { stage_next(a, m0, n0, (t + 1) * BK, nxt, 3, wave, lane); DLBB_WAIT_VM(8); }
-      else DLBB_WAIT_VM(0);
-      __builtin_amdgcn_s_barrier();
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_sched_barrier(0);
-      mfma_quadrant<0, 1>(acc, af, b1);
-      __builtin_amdgcn_sched_barrier(0);
-      __builtin_amdgcn_s_barrier();
-      // phase 3: MFMA (mq1, nq1); restage S0 for tile t+2
-      read_a(cur, wr, 1, fr, fq, af);
-      if (m2) stage_next(a, m0, n0, (t + 2) * BK, cur, 0, wave, lane);
-      __builtin_amdgcn_s_barrier();
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_sched_barrier(0);
-      mfma_quadrant<1, 1>(acc, af, b1);
-      __builtin_amdgcn_sched_barrier(0);
-      __builtin_amdgcn_s_barrier();
-      // phase 4: MFMA (mq1, nq0); restage S1 for tile t+2; wait S0(t+1), S1(t+1)
-      if (m2) { stage_next(a, m0, n0, (t + 2) * BK, cur, 1, wave, lane); DLBB_WAIT_VM(8); }
-      else if (m1) DLBB_WAIT_VM(4);
-      else DLBB_WAIT_VM(0);
-      __builtin_amdgcn_s_barrier();
-      __builtin_amdgcn_sched_barrier(0);
-      mfma_quadrant<1, 0>(acc, af, b0);
-      __builtin_amdgcn_sched_barrier(0);
-      __builtin_amdgcn_s_barrier();
-    }
+    deep_mainloop(a, acc, m0, n0, nk, smem, wave, lane);
     if (!lag) __builtin_amdgcn_s_barrier();
   } else if constexpr (MODE >= 1) {
     // Two barriers per phase ([stage + ds_read] | barrier | [16 MFMA] | barrier) and wave
@@ -507,84 +617,46 @@ __global__ void __launch_bounds__(kThreads2, 1) gemm_bf16_nt_256_kernel(GemmArgs
   }
   }
 
-  // epilogue. Lane (fr, fq) holds output row rbase + i*16 + fr, columns cbase .. cbase+15
-  // (acc[i][j][r] = column j*4 + r, see perm_brow).
-  const int epi = a.epi;
-  const int64_t cbase = n0 + wc * 64 + fq * 16;
-  const int cols_left = static_cast<int>(a.N - cbase < 16 ? a.N - cbase : 16);
-  if (cols_left <= 0) return;
-  const int64_t rbase = m0 + wr * 128 + fr;
-  const int rows_left = static_cast<int>(a.M - rbase);     // rows i*16 < rows_left are valid
-  const bool vec = a.vec_ok && cols_left == 16;
-  float bias[16];
+  store_tile_256(a, acc, m0, n0, wave, lane);
+}
+
+// Persistent form of the deep schedule: gridDim.x <= #CUs workgroups walk the virtual
+// workgroup ids vb = blockIdx.x, +gridDim.x, ... (same XCD chunk, same GROUP_M order as the
+// one-tile-per-workgroup launch). After a tile's main loop the NEXT tile's six prologue
+// sections are issued before this tile's epilogue stores, so the pipeline refill overlaps the
+// stores instead of following them (matters at small K: GPT-2's K = 768 is 12 K-tiles).
+__global__ void __launch_bounds__(kThreads2, 1) gemm_bf16_nt_256_persistent(GemmArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const bool lag = (wave >> 2) == 1;
+  const int nwg = static_cast<int>(((a.M + BM2 - 1) / BM2) * ((a.N + BN2 - 1) / BN2));
+  const int64_t nk = a.K / BK;
+  int vb = blockIdx.x;
+  if (vb >= nwg) return;
+  Tile256 tl = tile_of(a, vb);
+  deep_prologue(a, tl.m0, tl.n0, nk, smem, wave, lane);
+  if (nk > 1) DLBB_WAIT_VM(8); else DLBB_WAIT_VM(4);
+  __builtin_amdgcn_s_barrier();
+  f32x4 acc[8][4];
+  for (;;) {
 #pragma unroll
-  for (int c = 0; c < 16; ++c) bias[c] = 0.f;
-  if (epi & EPI_BIAS) {
-    if (vec) {
-      const u16x8* bp = reinterpret_cast<const u16x8*>(a.bias + cbase);
-      const u16x8 b0v = bp[0], b1v = bp[1];
+    for (int i = 0; i < 8; ++i)
 #pragma unroll
-      for (int c = 0; c < 8; ++c) { bias[c] = bf16_to_f32(b0v[c]); bias[8 + c] = bf16_to_f32(b1v[c]); }
-    } else {
-#pragma unroll
-      for (int c = 0; c < 16; ++c) if (c < cols_left) bias[c] = bf16_to_f32(a.bias[cbase + c]);
-    }
-  }
-  const int ldc = static_cast<int>(a.ldc), ldr = static_cast<int>(a.ldr);
-  float* cf = static_cast<float*>(a.C) + rbase * a.ldc + cbase;
-  uint16_t* cb = static_cast<uint16_t*>(a.C) + rbase * a.ldc + cbase;
-  uint16_t* pb = a.preact ? a.preact + rbase * a.ldc + cbase : nullptr;
-  const uint16_t* rb = (epi & EPI_RESIDUAL) ? a.residual + rbase * a.ldr + cbase : nullptr;
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    if (i * 16 >= rows_left) break;
-    float v[16];
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) v[j * 4 + r] = acc[i][j][r] + bias[j * 4 + r];
-    const int oc = i * 16 * ldc, orr = i * 16 * ldr;
-    if (vec) {
-      if (pb) {
-        u16x8 p0, p1;
-#pragma unroll
-        for (int c = 0; c < 8; ++c) { p0[c] = f32_to_bf16(v[c]); p1[c] = f32_to_bf16(v[8 + c]); }
-        reinterpret_cast<u16x8*>(pb + oc)[0] = p0;
-        reinterpret_cast<u16x8*>(pb + oc)[1] = p1;
-      }
-      if (epi & (EPI_GELU_ERF | EPI_GELU_TANH)) {
-#pragma unroll
-        for (int c = 0; c < 16; ++c) v[c] = apply_act(v[c], epi);
-      }
-      if (rb) {
-        const u16x8 r0 = reinterpret_cast<const u16x8*>(rb + orr)[0];
-        const u16x8 r1 = reinterpret_cast<const u16x8*>(rb + orr)[1];
-#pragma unroll
-        for (int c = 0; c < 8; ++c) { v[c] += bf16_to_f32(r0[c]); v[8 + c] += bf16_to_f32(r1[c]); }
-      }
-      if (a.out_f32) {
-        float4* o = reinterpret_cast<float4*>(cf + oc);
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-          o[q] = make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
-      } else {
-        u16x8 o0, o1;
-#pragma unroll
-        for (int c = 0; c < 8; ++c) { o0[c] = f32_to_bf16(v[c]); o1[c] = f32_to_bf16(v[8 + c]); }
-        reinterpret_cast<u16x8*>(cb + oc)[0] = o0;
-        reinterpret_cast<u16x8*>(cb + oc)[1] = o1;
-      }
-    } else {
-#pragma unroll
-      for (int c = 0; c < 16; ++c) {
-        if (c >= cols_left) break;
-        float x = v[c];
-        if (pb) pb[oc + c] = f32_to_bf16(x);
-        x = apply_act(x, epi);
-        if (rb) x += bf16_to_f32(rb[orr + c]);
-        if (a.out_f32) cf[oc + c] = x; else cb[oc + c] = f32_to_bf16(x);
-      }
-    }
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (lag) __builtin_amdgcn_s_barrier();
+    deep_mainloop(a, acc, tl.m0, tl.n0, nk, smem, wave, lane);
+    if (!lag) __builtin_amdgcn_s_barrier();     // rows re-aligned; every LDS read retired
+    const int vn = vb + static_cast<int>(gridDim.x);
+    const bool more = vn < nwg;
+    store_tile_256(a, acc, tl.m0, tl.n0, wave, lane);
+    if (!more) break;
+    const Tile256 tn = tile_of(a, vn);
+    deep_prologue(a, tn.m0, tn.n0, nk, smem, wave, lane);
+    DLBB_WAIT_VM(0);           // stores and prologue sections (stores and loads share vmcnt)
+    __builtin_amdgcn_s_barrier();
+    vb = vn;
+    tl = tn;
   }
 }
 
@@ -624,7 +696,22 @@ DLBB_API int dlbb_gemm_bf16_nt(const void* A, int64_t lda, const void* B, int64_
   const int force = dlbb_gemm_force_tile;
   if (force == 256 || (force != 128 && tiles256 >= 192)) {
     const dim3 g(static_cast<unsigned>(tiles256)), b(kThreads2);
-    if (dlbb_gemm_stagger == 3)
+    if (dlbb_gemm_stagger == 4) {
+      static int ncu[64] = {0};
+      int dev = 0;
+      (void)hipGetDevice(&dev);
+      if (dev < 0 || dev >= 64) dev = 0;
+      if (ncu[dev] == 0) {
+        int n = 0;
+        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+            n <= 0)
+          n = 256;
+        ncu[dev] = n;
+      }
+      const int64_t grid = tiles256 < ncu[dev] ? tiles256 : ncu[dev];
+      hipLaunchKernelGGL(gemm_bf16_nt_256_persistent, dim3(static_cast<unsigned>(grid)), b,
+                         2 * kBuf2Bytes, stream, a);
+    } else if (dlbb_gemm_stagger == 3)
       hipLaunchKernelGGL(gemm_bf16_nt_256_kernel<3>, g, b, 2 * kBuf2Bytes, stream, a);
     else if (dlbb_gemm_stagger == 2)
       hipLaunchKernelGGL(gemm_bf16_nt_256_kernel<2>, g, b, 2 * kBuf2Bytes, stream, a);

@@ -35,7 +35,8 @@ def set_tile(tile: int) -> None:
 
 def set_stagger(mode: int) -> None:
     """256^2 kernel schedule: 0 lock-step, 1 staggered wave rows, 2 staggered + next tile
-    issued at phase 1, 3 staggered + deep restaging (one K-tile in flight). For A/B
+    issued at phase 1, 3 staggered + deep restaging (one K-tile in flight), 4 = 3 as a
+    persistent kernel (next tile's prologue overlaps this tile's epilogue). For A/B
     benchmarking; the library default is the measured fastest (profiles/)."""
     _lib.lib().dlbb_gemm_set_stagger(int(mode))
 

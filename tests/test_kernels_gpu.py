@@ -90,9 +90,9 @@ def test_chunk_copy_and_scale():
 
 
 @pytest.fixture(params=[("mfma", 0, 1), ("mfma", 128, 1), ("mfma", 256, 1), ("mfma", 256, 0),
-                        ("mfma", 256, 2), ("mfma", 256, 3), ("blas", 0, 1)],
+                        ("mfma", 256, 2), ("mfma", 256, 3), ("mfma", 256, 4), ("blas", 0, 1)],
                 ids=["mfma_auto", "mfma_t128", "mfma_t256", "mfma_t256_lockstep",
-                     "mfma_t256_early", "mfma_t256_deep", "blas"])
+                     "mfma_t256_early", "mfma_t256_deep", "mfma_t256_persistent", "blas"])
 def gemm_tile(request, monkeypatch):
     from distributed_llm_backend_benchmark_amd.ops.gemm import get_stagger, set_stagger, set_tile
 
@@ -107,7 +107,8 @@ def gemm_tile(request, monkeypatch):
 
 
 @pytest.mark.parametrize("M,N,K", [(256, 256, 64), (4096, 1024, 4096), (300, 200, 128),
-                                   (8192, 768, 768), (128, 50304, 768), (520, 776, 192)])
+                                   (8192, 768, 768), (128, 50304, 768), (520, 776, 192),
+                                   (4096, 4352, 128), (2000, 9000, 64)])
 def test_gemm_plain(M, N, K, gemm_tile):
     from distributed_llm_backend_benchmark_amd.ops import linear
 
