@@ -164,15 +164,33 @@ __global__ void __launch_bounds__(kCarThreads) car_twoshot_kernel(CarKernelArgs 
   const int64_t s0 = blockIdx.x * per;
   const int64_t s1 = s0 + per < shard_vec ? s0 + per : shard_vec;
   char* mine = a.data[a.rank] + half;
-  // publish sub-range [s0, s1) of every shard
-  for (int p = 0; p < a.world; ++p) {
-    const int64_t base = p * shard_vec;
+  constexpr int kQ = kVecBytes / 16;
+  // publish sub-range [s0, s1) of every shard (W > 0: all W loads in flight per thread)
+  if constexpr (W > 0) {
     for (int64_t v = s0 + threadIdx.x; v < s1; v += blockDim.x) {
-      const int64_t off = (base + v) * kVecBytes;
+      u16x8 t[W][kQ];
 #pragma unroll
-      for (int q = 0; q < kVecBytes / 16; ++q)
-        reinterpret_cast<u16x8*>(mine + off)[q] =
-            reinterpret_cast<const u16x8*>(static_cast<const char*>(a.inp) + off)[q];
+      for (int p = 0; p < W; ++p)
+#pragma unroll
+        for (int q = 0; q < kQ; ++q)
+          t[p][q] = reinterpret_cast<const u16x8*>(
+              static_cast<const char*>(a.inp) + (p * shard_vec + v) * kVecBytes)[q];
+#pragma unroll
+      for (int p = 0; p < W; ++p)
+#pragma unroll
+        for (int q = 0; q < kQ; ++q)
+          reinterpret_cast<u16x8*>(mine + (p * shard_vec + v) * kVecBytes)[q] = t[p][q];
+    }
+  } else {
+    for (int p = 0; p < a.world; ++p) {
+      const int64_t base = p * shard_vec;
+      for (int64_t v = s0 + threadIdx.x; v < s1; v += blockDim.x) {
+        const int64_t off = (base + v) * kVecBytes;
+#pragma unroll
+        for (int q = 0; q < kQ; ++q)
+          reinterpret_cast<u16x8*>(mine + off)[q] =
+              reinterpret_cast<const u16x8*>(static_cast<const char*>(a.inp) + off)[q];
+      }
     }
   }
   signal_peers(a, 0, e);
@@ -188,20 +206,41 @@ __global__ void __launch_bounds__(kCarThreads) car_twoshot_kernel(CarKernelArgs 
   }
   signal_peers(a, 1, e);
   if (!wait_peers(a, 1, e)) return;
-  // all-gather: every other shard's sub-range b from its owner's tmp
-  const int world = W > 0 ? W : a.world;
-#pragma unroll
-  for (int k = 1; k < (W > 0 ? W : kMaxRanks); ++k) {
-    if (W == 0 && k >= world) break;
-    const int p = (a.rank + k) % world;
-    const char* src = a.tmp[p] + half;
-    const int64_t base = p * shard_vec;
+  // all-gather: every other shard's sub-range b from its owner's tmp. W > 0: the W-1 remote
+  // loads of a thread are all in flight before its stores (one per xGMI link), instead of one
+  // peer at a time.
+  if constexpr (W > 0) {
     for (int64_t v = s0 + threadIdx.x; v < s1; v += blockDim.x) {
-      const int64_t off = (base + v) * kVecBytes;
+      u16x8 t[W - 1][kQ];
 #pragma unroll
-      for (int q = 0; q < kVecBytes / 16; ++q)
-        reinterpret_cast<u16x8*>(static_cast<char*>(a.out) + off)[q] =
-            reinterpret_cast<const u16x8*>(src + off)[q];
+      for (int k = 1; k < W; ++k) {
+        const int p = (a.rank + k) & (W - 1);
+#pragma unroll
+        for (int q = 0; q < kQ; ++q)
+          t[k - 1][q] = reinterpret_cast<const u16x8*>(a.tmp[p] + half +
+                                                       (p * shard_vec + v) * kVecBytes)[q];
+      }
+#pragma unroll
+      for (int k = 1; k < W; ++k) {
+        const int p = (a.rank + k) & (W - 1);
+#pragma unroll
+        for (int q = 0; q < kQ; ++q)
+          reinterpret_cast<u16x8*>(static_cast<char*>(a.out) +
+                                   (p * shard_vec + v) * kVecBytes)[q] = t[k - 1][q];
+      }
+    }
+  } else {
+    for (int k = 1; k < a.world; ++k) {
+      const int p = (a.rank + k) % a.world;
+      const char* src = a.tmp[p] + half;
+      const int64_t base = p * shard_vec;
+      for (int64_t v = s0 + threadIdx.x; v < s1; v += blockDim.x) {
+        const int64_t off = (base + v) * kVecBytes;
+#pragma unroll
+        for (int q = 0; q < kQ; ++q)
+          reinterpret_cast<u16x8*>(static_cast<char*>(a.out) + off)[q] =
+              reinterpret_cast<const u16x8*>(src + off)[q];
+      }
     }
   }
 }
