@@ -143,3 +143,43 @@ def rank_statistics(per_rank_means: List[float]) -> Dict[str, object]:
         "variance_across_ranks": float(np.var(arr)),
         "coefficient_of_variation": float(np.std(arr) / mean) if mean > 0 else 0.0,
     }
+
+
+def gather_metrics_from_all_ranks(comm, local_summary: Dict[str, object]
+                                  ) -> Optional[Dict[str, object]]:
+    """Per-rank forward means (and p95s) to rank 0 with variance / CV.
+
+    Reference ``utils.py:172-209`` (``dist.gather`` of float32 scalars; defined but never called
+    there). Here it rides the job's process group through :class:`..parallel.comm.Comm`; returns
+    the statistics on rank 0 and ``None`` elsewhere."""
+    pairs = comm.all_gather_object((float(local_summary["forward_mean"]),
+                                    float(local_summary.get("forward_p95", 0.0))))
+    if comm.rank != 0:
+        return None
+    out = rank_statistics([m for m, _ in pairs])
+    out["forward_p95_per_rank"] = [p for _, p in pairs]
+    return out
+
+
+def run_experiment(model, dataset, config: Dict[str, object], metrics: "MetricsCollector",
+                   comm=None) -> "MetricsCollector":
+    """Warmup + timed forwards (reference ``utils.py:212-244``). The reference times each
+    forward with ``time.time()`` around an asynchronous call; here the timer synchronises the
+    device (``Timer(sync=True)``), and with ``comm`` every timed forward is bracketed by
+    barriers like ``run_mpi.py:177,183``."""
+    ex = config["execution"]
+    for _ in range(int(ex["warmup_iterations"])):
+        batch = dataset.get_batch()
+        with Timer(sync=True) as t:
+            model(batch)
+        metrics.record_warmup_time(t.elapsed)
+    for _ in range(int(ex["benchmark_iterations"])):
+        batch = dataset.get_batch()
+        if comm is not None:
+            comm.barrier()
+        with Timer(sync=True) as t:
+            model(batch)
+        if comm is not None:
+            comm.barrier()
+        metrics.record_forward_time(t.elapsed)
+    return metrics
