@@ -87,3 +87,24 @@ def test_bandwidth_conventions():
     assert busbw_gbps("broadcast", nb, t, P) == pytest.approx(nb / t / 1e9)
     assert busbw_gbps("allreduce", nb, t, 1) == 0.0
     assert legacy_bandwidth_gbps(4194304, 1.0, 2) == pytest.approx(4194304 * 4 / 2 ** 30)
+
+
+def test_compare_reference_against_itself_reproduces_baseline_numbers(tmp_path):
+    """The comparison table's reference side reproduces BASELINE.md's busBW figures."""
+    import glob
+
+    from distributed_llm_backend_benchmark_amd.stats import compare as C
+
+    fx = os.path.join(os.path.dirname(__file__), "fixtures", "reference")
+    ref1 = C.load_1d(sorted(glob.glob(os.path.join(fx, "1d", "csv", "*.csv"))))
+    rows = C.compare(ref1, ref1)
+    assert rows and all(abs(r["speedup_p50"] - 1.0) < 1e-12 for r in rows)
+    best = {(r["operation"], r["ref_num_ranks"], r["config"]): r for r in rows}
+    r = best[("allreduce", 2, "16MB")]            # BASELINE: oneCCL P=2 8 MiB -> 7.53 GB/s
+    assert r["ref_impl"] == "deepspeed_oneccl" and abs(r["ref_busbw_gbps"] - 7.53) < 0.01
+    assert abs(best[("allreduce", 2, "1KB")]["ref_p50_us"] - 22.9) < 0.05   # OpenMPI best
+    ref3 = C.load_3d(glob.glob(os.path.join(fx, "3d", "csv", "*.csv")))
+    r3 = {(r["operation"], r["ref_num_ranks"], r["config"]): r for r in C.compare(ref3, ref3)}
+    assert abs(r3[("allreduce", 8, "8/2048/2048")]["ref_busbw_gbps"] - 5.46) < 0.01
+    C.write_csv(rows, str(tmp_path / "c.csv"))
+    assert "| allreduce |" in C.markdown(rows)
