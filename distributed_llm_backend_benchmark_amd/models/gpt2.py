@@ -8,7 +8,7 @@ north star asks for, built from the same gfx950 kernels as the TP model:
 * residual adds fused into the following LayerNorm (``ops.layernorm(x, residual=h)``),
 * QKV / attention-out / MLP / LM-head GEMMs on the MFMA kernel with fused bias and, for c_fc,
   fused tanh-GELU (pre-activation kept for backward),
-* causal attention via ``F.scaled_dot_product_attention`` (ROCm flash/efficient backends),
+* causal attention: our gfx950 flash forward on the fused QKV (ops.causal_attention),
 * the LM-head loss as one fused bf16 softmax-cross-entropy kernel (``ops.cross_entropy``).
 
 All parameters are bf16 working copies (the trainer keeps fp32 masters); vocab is padded to a
@@ -76,9 +76,7 @@ class Block(nn.Module):
     def forward(self, y1, h):
         B, T, C = y1.shape
         qkv = linear_train(y1, self.attn_w, self.attn_b)
-        q, k, v = qkv.view(B, T, 3, self.n_head, C // self.n_head).permute(2, 0, 3, 1, 4).unbind(0)
-        att = F.scaled_dot_product_attention(q, k, v, is_causal=True)
-        att = att.transpose(1, 2).reshape(B, T, C)
+        att = ops.causal_attention(qkv, self.n_head)
         a = linear_train(att, self.attn_proj_w, self.attn_proj_b)
         y2, h = self.ln_2(a, residual=h)
         g = linear_train(y2, self.fc_w, self.fc_b, act="gelu_tanh")

@@ -16,7 +16,8 @@ from .gemm import linear
 from .norm_act import layernorm, bias_gelu
 from .optim import FlatAdamW
 from .xent import cross_entropy
+from .attention import causal_attention
 
-__all__ = ["available", "loaded_path", "KernelError", "reduce_sum", "cast", "pack_rows",
+__all__ = ["causal_attention", "available", "loaded_path", "KernelError", "reduce_sum", "cast", "pack_rows",
            "ChunkTable", "ScaleTable", "flatten_into", "linear", "layernorm", "bias_gelu",
            "FlatAdamW", "cross_entropy"]

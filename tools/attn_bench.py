@@ -1,0 +1,42 @@
+"""Device time of the causal attention forward (ours vs torch SDPA) and fwd+bwd, GPT-2 shape."""
+import json
+import math
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from distributed_llm_backend_benchmark_amd.ops import causal_attention  # noqa: E402
+from distributed_llm_backend_benchmark_amd.ops.attention import _torch_attention, attn_fwd  # noqa
+
+
+def t_best(fn, iters=20, rounds=5):
+    best = 1e9
+    for _ in range(rounds):
+        fn()
+        torch.cuda.synchronize()
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(iters):
+            fn()
+        e.record()
+        e.synchronize()
+        best = min(best, s.elapsed_time(e) / iters * 1e-3)
+    return best
+
+
+for B, T, H in ((16, 1024, 12), (8, 2048, 12), (4, 4096, 16)):
+    qkv = torch.randn(B, T, 3 * H * 64, device="cuda").to(torch.bfloat16)
+    fl = 4.0 * B * H * T * T * 64 / 2          # causal
+    t_ours = t_best(lambda: attn_fwd(qkv, H))
+    t_torch = t_best(lambda: _torch_attention(qkv, H))
+    x = qkv.clone().requires_grad_(True)
+    go = torch.randn(B, T, H * 64, device="cuda").to(torch.bfloat16)
+    t_fb_ours = t_best(lambda: causal_attention(x, H).backward(go), iters=5, rounds=3)
+    t_fb_torch = t_best(lambda: _torch_attention(x, H).backward(go), iters=5, rounds=3)
+    print(json.dumps({"B": B, "T": T, "H": H, "D": 64, "fwd_us_ours": t_ours * 1e6,
+                      "fwd_us_torch": t_torch * 1e6, "fwd_tflops_ours": fl / t_ours / 1e12,
+                      "fwd_tflops_torch": fl / t_torch / 1e12,
+                      "fwd_bwd_us_ours": t_fb_ours * 1e6, "fwd_bwd_us_torch": t_fb_torch * 1e6}),
+          flush=True)
