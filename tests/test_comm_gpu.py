@@ -97,7 +97,7 @@ def _car_worker(rank, world, sizes):
                 ref = sum(x.float() for x in xs)
                 out = car.all_reduce(xs[rank].clone(), algo=algo)
                 torch.cuda.synchronize()
-                good = torch.allclose(out.float(), ref, rtol=2e-2, atol=5e-2)
+                good = torch.allclose(out.float(), ref, rtol=2e-2, atol=5e-2 * world)
                 ok.append((n, algo, it, bool(good), car.check_error()))
             comm.barrier()
     car.close()
@@ -105,8 +105,11 @@ def _car_worker(rank, world, sizes):
     return ok
 
 
-def test_custom_allreduce_two_ranks_one_gpu():
-    res = run_multiprocess(_car_worker, 2, args=([2048, 65536, 1 << 20],), timeout=300)
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_custom_allreduce_ranks_on_one_gpu(world):
+    """The IPC protocol (flags, epochs, both buffer halves) with 2/4/8 ranks sharing one GPU —
+    the compile-time W = 2/4/8 kernels the driver's 8-GPU node runs."""
+    res = run_multiprocess(_car_worker, world, args=([2048, 65536, 1 << 20],), timeout=600)
     for r in res:
         for n, algo, it, good, err in r:
             assert good and err == 0, (n, algo, it, good, err)
