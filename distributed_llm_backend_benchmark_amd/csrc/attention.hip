@@ -219,6 +219,335 @@ __global__ void __launch_bounds__(kAttnThreads, 2) attn_fwd_d64_kernel(AttnArgs 
   }
 }
 
+
+// ===================================================================================== backward
+// dS = P * (dP - delta), delta = rowsum(dO * O), P recomputed from Q, K and the forward's LSE.
+// Two kernels, no atomics (CDNA guide §B "Attention backward": a dQ sum across key blocks by
+// float atomics would cost dQ-bytes / 1.3 TB/s — ~100+ us at GPT-2's shape):
+//   dkdv: a workgroup owns 128 keys (wave: 32, key on the MFMA lane) and sweeps 32-query
+//         slices; S = Q K^T and dP = dO V^T come out with the key on the lane, so P and dS are
+//         directly the B operands of dV^T += dO^T P and dK^T += Q^T dS (Q / dO slice images
+//         read by rows AND transposed: one swizzle serves both, bswz).
+//   dq:   a workgroup owns 128 queries (wave: 32, query on the lane) and sweeps 64-key tiles
+//         like the forward: S^T = K Q^T, dP^T = V dO^T, then dQ^T += K^T dS^T (K image read
+//         transposed).
+// Both write straight into the fused dQKV gradient [B, T, 3, H, D].
+
+// one swizzle for row reads (ds_read_b128, 32x32x16 A operand) and transposed reads
+// (ds_read_b64_tr_b16) of a [rows][64 x bf16] image: t = pair index, bit 2 flipped on odd t
+__device__ __forceinline__ int bswz(int r) {
+  const int t = (r >> 1) & 7;
+  return t ^ ((t & 1) << 2);
+}
+
+struct AttnBwdArgs {
+  const uint16_t* qkv;     // [B, T, 3, H, D]
+  const uint16_t* dout;    // [B, T, H, D] (row stride ldo)
+  const float* lse;        // [B, H, T] natural log
+  const float* delta;      // [B, H, T]
+  uint16_t* dqkv;          // [B, T, 3, H, D] (row stride ld)
+  int64_t ld, ldo;
+  int B, T, H;
+  float scale_log2;        // log2(e) / sqrt(D)
+  float scale;             // 1 / sqrt(D)
+};
+
+// delta[b, h, t] = sum_d dO[b, t, h, d] * O[b, t, h, d]; one thread per (b, t, h) row of 64
+__global__ void __launch_bounds__(256) attn_bwd_delta_kernel(const uint16_t* __restrict__ dout,
+                                                             const uint16_t* __restrict__ out,
+                                                             int64_t ldo, float* __restrict__ delta,
+                                                             int B, int T, int H) {
+  const int64_t row = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  const int64_t nrows = static_cast<int64_t>(B) * T * H;
+  if (row >= nrows) return;
+  const int h = static_cast<int>(row % H);
+  const int64_t bt = row / H;
+  const uint16_t* g = dout + bt * ldo + h * kAttnD;
+  const uint16_t* o = out + bt * ldo + h * kAttnD;
+  float acc = 0.f;
+#pragma unroll
+  for (int c = 0; c < kAttnD / 8; ++c) {
+    float x[8], y[8];
+    load8<DT_BF16>(g, c, x);
+    load8<DT_BF16>(o, c, y);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc += x[j] * y[j];
+  }
+  const int64_t b = bt / T, t = bt % T;
+  delta[(b * H + h) * T + t] = acc;
+}
+
+// transposed operand read of a [rows][64] bf16 image (bswz): A operand of a 32x32x16 MFMA whose
+// k index is the image row: lane (col = colbase + (lane & 31), hi) gets rows
+// rowbase + 8 (j>>2) + 4 hi + (j&3), j = 0..7 — matching an accumulator reused as B operand.
+__device__ __forceinline__ bf16x8 tr_operand(const char* img, int rowbase, int colbase, int lane) {
+  const int g = lane >> 4, i16 = lane & 15;
+  const int tq = i16 >> 2, tp = i16 & 3;
+  bf16x8 f;
+#pragma unroll
+  for (int half = 0; half < 2; ++half) {
+    const int row = rowbase + 8 * half + 4 * (g >> 1) + tq;
+    const int col = colbase + 16 * (g & 1) + 4 * tp;
+    const int off = row * 128 + (((col >> 3) ^ bswz(row)) << 4) + (col & 7) * 2;
+    const i16x4 t = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4_ptr)(img + off));
+#pragma unroll
+    for (int u = 0; u < 4; ++u) f[4 * half + u] = t[u];
+  }
+  return f;
+}
+
+__device__ __forceinline__ bf16x8 row_operand(const char* img, int row, int chunk) {
+  return *reinterpret_cast<const bf16x8*>(img + row * 128 + ((chunk ^ bswz(row)) << 4));
+}
+
+__device__ __forceinline__ bf16x8 acc_to_bf16(const f32x16& x, int st) {
+  bf16x8 f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) f[j] = __builtin_bit_cast(short, static_cast<__bf16>(x[8 * st + j]));
+  return f;
+}
+
+// stage 32 rows x 128 B of a [T, ...] bf16 matrix (row stride ld, column offset col0) into an
+// image with the bswz layout; wave w issues rows [8w, 8w + 8). Rows >= T are clamped.
+__device__ __forceinline__ void stage32(const uint16_t* base, int64_t ld, int row0, int T,
+                                        char* img, int wave, int lane) {
+  const int r_in = lane >> 3, slot = lane & 7;
+  const int row = wave * 8 + r_in;
+  int t = row0 + row;
+  t = t < T ? t : T - 1;
+  attn_glds16(base + static_cast<int64_t>(t) * ld + (slot ^ bswz(row)) * 8, img + wave * 8 * 128);
+}
+
+constexpr int kBwdKeys = 128;
+constexpr int kSlice = 32;
+constexpr int kSliceImg = kSlice * 128;     // 4 KiB
+
+__global__ void __launch_bounds__(kAttnThreads, 2) attn_bwd_dkdv_d64_kernel(AttnBwdArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int r = lane & 31, hi = lane >> 5;
+  const int h = blockIdx.y, b = blockIdx.z;
+  const int kb0 = blockIdx.x * kBwdKeys;            // block 0 = most query slices: first
+  const int kw = kb0 + wave * 32;
+  const int mykey = kw + r;
+  const uint16_t* base_bt = a.qkv + static_cast<int64_t>(b) * a.T * a.ld;
+  const uint16_t* dout_bt = a.dout + static_cast<int64_t>(b) * a.T * a.ldo;
+  const int hoff = h * kAttnD;
+  const int64_t bh = static_cast<int64_t>(b) * a.H + h;
+
+  bf16x8 kf[4], vf[4];
+  {
+    const int kk = mykey < a.T ? mykey : a.T - 1;
+    const uint16_t* kp = base_bt + static_cast<int64_t>(kk) * a.ld + kAttnD * a.H + hoff + 8 * hi;
+    const uint16_t* vp = kp + kAttnD * a.H;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      kf[ks] = *reinterpret_cast<const bf16x8*>(kp + 16 * ks);
+      vf[ks] = *reinterpret_cast<const bf16x8*>(vp + 16 * ks);
+    }
+  }
+  f32x16 dv[2], dk[2];
+#pragma unroll
+  for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) { dv[dt][e] = 0.f; dk[dt][e] = 0.f; }
+
+  const int ns = (a.T - kb0 + kSlice - 1) / kSlice;
+  auto imgQ = [&](int c) { return smem + c * 2 * kSliceImg; };
+  auto imgG = [&](int c) { return smem + c * 2 * kSliceImg + kSliceImg; };
+  stage32(base_bt + hoff, a.ld, kb0, a.T, imgQ(0), wave, lane);
+  stage32(dout_bt + hoff, a.ldo, kb0, a.T, imgG(0), wave, lane);
+  for (int i = 0; i < ns; ++i) {
+    const int cur = i & 1;
+    const int qs = kb0 + i * kSlice;
+    if (i + 1 < ns) {
+      stage32(base_bt + hoff, a.ld, qs + kSlice, a.T, imgQ(cur ^ 1), wave, lane);
+      stage32(dout_bt + hoff, a.ldo, qs + kSlice, a.T, imgG(cur ^ 1), wave, lane);
+      asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    if (qs + kSlice - 1 >= kw) {                    // wave-uniform: some query >= some key
+      const char* iq = imgQ(cur);
+      const char* ig = imgG(cur);
+      // per-row constants for rows q = qs + 8 g + 4 hi + u (register e = 4 g + u)
+      float l2[16], dl[16];
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4)
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          int q = qs + 8 * g4 + 4 * hi + u;
+          q = q < a.T ? q : a.T - 1;
+          l2[4 * g4 + u] = a.lse[bh * a.T + q] * 1.4426950408889634f;
+          dl[4 * g4 + u] = a.delta[bh * a.T + q];
+        }
+      f32x16 s, dp;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) { s[e] = 0.f; dp[e] = 0.f; }
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_operand(iq, r, 2 * ks + hi), kf[ks], s,
+                                                    0, 0, 0);
+        dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_operand(ig, r, 2 * ks + hi), vf[ks],
+                                                     dp, 0, 0, 0);
+      }
+      const bool diag = qs < kw + 31;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int q = qs + (e & 3) + 8 * (e >> 2) + 4 * hi;
+        float p = __builtin_amdgcn_exp2f(s[e] * a.scale_log2 - l2[e]);
+        if ((diag && mykey > q) || q >= a.T) p = 0.f;
+        s[e] = p;
+        dp[e] = p * (dp[e] - dl[e]);
+      }
+#pragma unroll
+      for (int st = 0; st < 2; ++st) {
+        const bf16x8 pb = acc_to_bf16(s, st);
+        const bf16x8 db = acc_to_bf16(dp, st);
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt) {
+          dv[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_operand(ig, 16 * st, 32 * dt, lane),
+                                                           pb, dv[dt], 0, 0, 0);
+          dk[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_operand(iq, 16 * st, 32 * dt, lane),
+                                                           db, dk[dt], 0, 0, 0);
+        }
+      }
+    }
+    __builtin_amdgcn_s_barrier();
+  }
+  if (mykey < a.T) {
+    uint16_t* dkp = a.dqkv + (static_cast<int64_t>(b) * a.T + mykey) * a.ld + kAttnD * a.H + hoff;
+    uint16_t* dvp = dkp + kAttnD * a.H;
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+      for (int gg = 0; gg < 4; ++gg) {
+        u16x4 wk, wv;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          wk[u] = f32_to_bf16(dk[dt][4 * gg + u] * a.scale);
+          wv[u] = f32_to_bf16(dv[dt][4 * gg + u]);
+        }
+        *reinterpret_cast<u16x4*>(dkp + dt * 32 + 8 * gg + 4 * hi) = wk;
+        *reinterpret_cast<u16x4*>(dvp + dt * 32 + 8 * gg + 4 * hi) = wv;
+      }
+  }
+}
+
+// K and V tiles of 64 keys in the bswz layout (both read by rows; K also transposed)
+__device__ __forceinline__ void stage_kv64(const AttnBwdArgs& a, const uint16_t* base_bt, int k0,
+                                           int hoff, char* tk, char* tv, int wave, int lane) {
+  const int r_in = lane >> 3, slot = lane & 7;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int row = wave * 16 + i * 8 + r_in;
+    int key = k0 + row;
+    key = key < a.T ? key : a.T - 1;
+    const uint16_t* src = base_bt + static_cast<int64_t>(key) * a.ld + hoff + (slot ^ bswz(row)) * 8;
+    attn_glds16(src + kAttnD * a.H, tk + (wave * 16 + i * 8) * 128);
+    attn_glds16(src + 2 * kAttnD * a.H, tv + (wave * 16 + i * 8) * 128);
+  }
+}
+
+__global__ void __launch_bounds__(kAttnThreads, 2) attn_bwd_dq_d64_kernel(AttnBwdArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int nqb = (a.T + kQB - 1) / kQB;
+  const int qb = nqb - 1 - static_cast<int>(blockIdx.x);
+  const int h = blockIdx.y, b = blockIdx.z;
+  const int q0 = qb * kQB;
+  const int qw = q0 + wave * 32;
+  const int r = lane & 31, hi = lane >> 5;
+  const uint16_t* base_bt = a.qkv + static_cast<int64_t>(b) * a.T * a.ld;
+  const int hoff = h * kAttnD;
+  const int64_t bh = static_cast<int64_t>(b) * a.H + h;
+  const int qme = qw + r;
+  const int qc = qme < a.T ? qme : a.T - 1;
+
+  bf16x8 qf[4], gf[4];
+  {
+    const uint16_t* qp = base_bt + static_cast<int64_t>(qc) * a.ld + hoff + 8 * hi;
+    const uint16_t* gp = a.dout + (static_cast<int64_t>(b) * a.T + qc) * a.ldo + hoff + 8 * hi;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      qf[ks] = *reinterpret_cast<const bf16x8*>(qp + 16 * ks);
+      gf[ks] = *reinterpret_cast<const bf16x8*>(gp + 16 * ks);
+    }
+  }
+  const float l2 = a.lse[bh * a.T + qc] * 1.4426950408889634f;
+  const float dl = a.delta[bh * a.T + qc];
+  f32x16 dq[2];
+#pragma unroll
+  for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) dq[dt][e] = 0.f;
+  const int q_hi = qw + 31;
+  const int last_key = (q0 + kQB - 1) < (a.T - 1) ? (q0 + kQB - 1) : (a.T - 1);
+  const int nt = last_key / kKB + 1;
+  auto tileK = [&](int c) { return smem + c * 2 * kTileKV; };
+  auto tileV = [&](int c) { return smem + c * 2 * kTileKV + kTileKV; };
+  stage_kv64(a, base_bt, 0, hoff, tileK(0), tileV(0), wave, lane);
+  for (int kt = 0; kt < nt; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nt) {
+      stage_kv64(a, base_bt, (kt + 1) * kKB, hoff, tileK(cur ^ 1), tileV(cur ^ 1), wave, lane);
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    const int k0 = kt * kKB;
+    if (k0 <= q_hi) {
+      const char* tk = tileK(cur);
+      const char* tv = tileV(cur);
+      const bool diag = k0 + kKB - 1 > qw;
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        f32x16 s, dp;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) { s[e] = 0.f; dp[e] = 0.f; }
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) {
+          s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_operand(tk, kk * 32 + r, 2 * ks + hi),
+                                                      qf[ks], s, 0, 0, 0);
+          dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_operand(tv, kk * 32 + r, 2 * ks + hi),
+                                                       gf[ks], dp, 0, 0, 0);
+        }
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int key = k0 + kk * 32 + (e & 3) + 8 * (e >> 2) + 4 * hi;
+          float p = __builtin_amdgcn_exp2f(s[e] * a.scale_log2 - l2);
+          if (diag && key > qme) p = 0.f;
+          dp[e] = p * (dp[e] - dl);
+        }
+#pragma unroll
+        for (int st = 0; st < 2; ++st) {
+          const bf16x8 db = acc_to_bf16(dp, st);
+#pragma unroll
+          for (int dt = 0; dt < 2; ++dt)
+            dq[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+                tr_operand(tk, kk * 32 + 16 * st, 32 * dt, lane), db, dq[dt], 0, 0, 0);
+        }
+      }
+    }
+    __builtin_amdgcn_s_barrier();
+  }
+  if (qme < a.T) {
+    uint16_t* dqp = a.dqkv + (static_cast<int64_t>(b) * a.T + qme) * a.ld + hoff;
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+      for (int gg = 0; gg < 4; ++gg) {
+        u16x4 w;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) w[u] = f32_to_bf16(dq[dt][4 * gg + u] * a.scale);
+        *reinterpret_cast<u16x4*>(dqp + dt * 32 + 8 * gg + 4 * hi) = w;
+      }
+  }
+}
 }  // namespace dlbb
 
 using namespace dlbb;
@@ -237,5 +566,29 @@ DLBB_API int dlbb_attn_fwd(const void* qkv, int64_t ld, void* out, int64_t ldo, 
              B, T, H, scale * 1.4426950408889634f};
   const dim3 grid((T + kQB - 1) / kQB, H, B);
   hipLaunchKernelGGL(attn_fwd_d64_kernel, grid, dim3(kAttnThreads), 4 * kTileKV, stream, a);
+  return hipGetLastError();
+}
+
+// Backward of dlbb_attn_fwd. dout / out: [B, T, H, 64] (row stride ldo); lse: forward's;
+// delta: [B, H, T] fp32 workspace; dqkv: [B, T, 3, H, 64] (row stride ld, written fully).
+DLBB_API int dlbb_attn_bwd(const void* qkv, int64_t ld, const void* out, const void* dout,
+                           int64_t ldo, const float* lse, float* delta, void* dqkv, int B, int T,
+                           int H, int D, float scale, hipStream_t stream) {
+  if (B <= 0 || T <= 0 || H <= 0) return hipSuccess;
+  if (D != kAttnD) return hipErrorInvalidValue;
+  if (ld % 8 || ldo % 8 || ld < 3 * H * D || ldo < H * D) return hipErrorInvalidValue;
+  auto mis16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) != 0; };
+  if (mis16(qkv) || mis16(out) || mis16(dout) || mis16(dqkv)) return hipErrorInvalidValue;
+  const int64_t rows = static_cast<int64_t>(B) * T * H;
+  hipLaunchKernelGGL(attn_bwd_delta_kernel, dim3(static_cast<unsigned>((rows + 255) / 256)),
+                     dim3(256), 0, stream, static_cast<const uint16_t*>(dout),
+                     static_cast<const uint16_t*>(out), ldo, delta, B, T, H);
+  AttnBwdArgs a{static_cast<const uint16_t*>(qkv), static_cast<const uint16_t*>(dout), lse, delta,
+                static_cast<uint16_t*>(dqkv), ld, ldo, B, T, H,
+                scale * 1.4426950408889634f, scale};
+  hipLaunchKernelGGL(attn_bwd_dkdv_d64_kernel, dim3((T + kBwdKeys - 1) / kBwdKeys, H, B),
+                     dim3(kAttnThreads), 4 * kSliceImg, stream, a);
+  hipLaunchKernelGGL(attn_bwd_dq_d64_kernel, dim3((T + kQB - 1) / kQB, H, B),
+                     dim3(kAttnThreads), 4 * kTileKV, stream, a);
   return hipGetLastError();
 }

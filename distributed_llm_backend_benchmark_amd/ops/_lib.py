@@ -64,6 +64,8 @@ _SIGS = {
                               c_void_p, c_void_p]),
     "dlbb_attn_fwd": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int, c_int,
                               c_int, c_int, c_float, c_void_p]),
+    "dlbb_attn_bwd": (c_int, [c_void_p, c_int64, c_void_p, c_void_p, c_int64, c_void_p,
+                              c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_float, c_void_p]),
     "dlbb_rccl_unique_id_bytes": (c_int, []),
     "dlbb_rccl_get_unique_id": (c_int, [c_void_p]),
     "dlbb_rccl_init": (c_int, [c_void_p, c_int, c_int, ctypes.POINTER(c_void_p)]),

@@ -3,10 +3,10 @@
 ``causal_attention(qkv, n_head)`` takes GPT-2's fused ``[B, T, 3C]`` QKV GEMM output and returns
 ``[B, T, C]`` (heads interleaved, ready for the projection GEMM). The forward is our gfx950
 flash kernel (head dim 64); it reads Q/K/V straight out of ``qkv`` — no unbind/transpose copies
-— and emits the per-row log-sum-exp. The backward hands (dO, Q, K, V, O, LSE) to the stack's
-flash-attention backward (``aten._scaled_dot_product_flash_attention_backward``, same LSE
-convention: natural log, ``[B, H, T]`` fp32) and packs dQ/dK/dV into the fused ``[B, T, 3C]``
-gradient with three row-strided copies of our pack kernel instead of a generic cat.
+— and emits the per-row log-sum-exp. The backward is ours too (delta = rowsum(dO * O), then a
+key-block kernel for dK/dV and a query-block kernel for dQ, no atomics), writing the fused
+``[B, T, 3C]`` gradient directly. ``attn_bwd_library`` (the stack's flash backward on our
+forward's O / LSE — same natural-log ``[B, H, T]`` convention) is kept as the A/B baseline.
 
 Other head dims, CPU tensors and ``DLBB_KERNELS=torch`` use ``F.scaled_dot_product_attention``.
 """
@@ -66,28 +66,46 @@ class _CausalAttention(torch.autograd.Function):
     @staticmethod
     def backward(ctx, gout):
         qkv, out, lse = ctx.saved_tensors
-        H = ctx.n_head
-        B, T, C3 = qkv.shape
-        C = C3 // 3
-        D = C // H
-        q, k, v = _views(qkv, H)
-        o4 = out.view(B, T, H, D).transpose(1, 2)
-        g4 = gout.reshape(B, T, H, D).transpose(1, 2)
-        seed = torch.zeros((), dtype=torch.int64, device=qkv.device)
-        dq, dk, dv = torch.ops.aten._scaled_dot_product_flash_attention_backward(
-            g4, q, k, v, o4, lse, None, None, T, T, 0.0, True, seed, seed,
-            scale=1.0 / math.sqrt(D))
-        dqkv = torch.empty_like(qkv)
-        lib = _lib.lib()
-        st = _lib.stream(qkv.device)
-        for j, g in enumerate((dq, dk, dv)):
-            g2 = g.transpose(1, 2)                     # [B, T, H, D] view
-            if not g2.is_contiguous():
-                g2 = g2.contiguous()
-            check(lib.dlbb_pack_rows(g2.data_ptr(), _lib.DT_BF16, C,
-                                     dqkv.data_ptr() + j * C * 2, _lib.DT_BF16, C3, B * T, C, st),
-                  "pack_rows(dqkv)")
-        return dqkv, None
+        return attn_bwd(qkv, out, lse, gout, ctx.n_head), None
+
+
+def attn_bwd(qkv: torch.Tensor, out: torch.Tensor, lse: torch.Tensor, gout: torch.Tensor,
+             n_head: int) -> torch.Tensor:
+    """Raw backward: dQKV [B, T, 3C] (dkdv + dq kernels, no atomics)."""
+    B, T, C3 = qkv.shape
+    C = C3 // 3
+    D = C // n_head
+    gout = gout.contiguous()
+    dqkv = torch.empty_like(qkv)
+    delta = torch.empty(B, n_head, T, dtype=torch.float32, device=qkv.device)
+    check(_lib.lib().dlbb_attn_bwd(qkv.data_ptr(), C3, out.data_ptr(), gout.data_ptr(), C,
+                                   lse.data_ptr(), delta.data_ptr(), dqkv.data_ptr(), B, T, n_head,
+                                   D, 1.0 / math.sqrt(D), _lib.stream(qkv.device)), "attn_bwd")
+    return dqkv
+
+
+def attn_bwd_library(qkv, out, lse, gout, n_head: int) -> torch.Tensor:
+    """The stack's flash backward on our forward's (O, LSE), dQ/dK/dV packed into [B, T, 3C]
+    (A/B baseline for :func:`attn_bwd`)."""
+    B, T, C3 = qkv.shape
+    C = C3 // 3
+    D = C // n_head
+    q, k, v = _views(qkv, n_head)
+    o4 = out.view(B, T, n_head, D).transpose(1, 2)
+    g4 = gout.reshape(B, T, n_head, D).transpose(1, 2)
+    seed = torch.zeros((), dtype=torch.int64, device=qkv.device)
+    dq, dk, dv = torch.ops.aten._scaled_dot_product_flash_attention_backward(
+        g4, q, k, v, o4, lse, None, None, T, T, 0.0, True, seed, seed, scale=1.0 / math.sqrt(D))
+    dqkv = torch.empty_like(qkv)
+    lib = _lib.lib()
+    st = _lib.stream(qkv.device)
+    for j, g in enumerate((dq, dk, dv)):
+        g2 = g.transpose(1, 2)
+        if not g2.is_contiguous():
+            g2 = g2.contiguous()
+        check(lib.dlbb_pack_rows(g2.data_ptr(), _lib.DT_BF16, C, dqkv.data_ptr() + j * C * 2,
+                                 _lib.DT_BF16, C3, B * T, C, st), "pack_rows(dqkv)")
+    return dqkv
 
 
 def causal_attention(qkv: torch.Tensor, n_head: int) -> torch.Tensor:

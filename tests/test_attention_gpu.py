@@ -70,3 +70,29 @@ def test_causal_attention_autograd_matches_sdpa():
     y2.backward(gout)
     torch.testing.assert_close(y1.float(), y2.float(), rtol=2e-2, atol=2e-2)
     torch.testing.assert_close(x1.grad.float(), x2.grad.float(), rtol=3e-2, atol=3e-2)
+
+
+def _ref_grads(qkv, gout, H):
+    x = qkv.float().clone().requires_grad_(True)
+    y, _ = _ref(x, H)
+    y.backward(gout.float())
+    return y.detach(), x.grad
+
+
+@pytest.mark.parametrize("B,T,H", [(1, 64, 1), (2, 200, 2), (1, 256, 3), (2, 1024, 2),
+                                   (1, 333, 2)])
+def test_attn_bwd_matches_fp32_reference(B, T, H):
+    from distributed_llm_backend_benchmark_amd.ops.attention import attn_bwd, attn_fwd
+
+    g = torch.Generator(device="cuda").manual_seed(7 * T + H)
+    qkv = torch.randn(B, T, 3 * H * 64, device="cuda", generator=g).to(torch.bfloat16)
+    gout = torch.randn(B, T, H * 64, device="cuda", generator=g).to(torch.bfloat16)
+    out, lse = attn_fwd(qkv, H)
+    d = attn_bwd(qkv, out, lse, gout, H)
+    _, ref = _ref_grads(qkv, gout, H)
+    C = H * 64
+    for j, name in enumerate("qkv"):
+        got, want = d[..., j * C:(j + 1) * C].float(), ref[..., j * C:(j + 1) * C]
+        err = float((got - want).abs().max())
+        scale = float(want.abs().max())
+        assert err <= 0.03 * scale + 0.02, (name, err, scale)
