@@ -138,37 +138,41 @@ __global__ void __launch_bounds__(kAttnThreads, 2) attn_fwd_d64_kernel(AttnArgs 
       }
       // ---- scale, causal mask, online softmax (lane = one query; keys in registers)
       const bool diag = k0 + kKB - 1 > qw;          // some key of this tile beyond some query
-      float mx = -INFINITY;
+      float mx = -INFINITY;                          // max of the RAW scores (scale > 0)
+      if (diag) {
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+          for (int e = 0; e < 16; ++e) {
+            const int key = k0 + kk * 32 + (e & 3) + 8 * (e >> 2) + 4 * hi;
+            if (key > qme) s[kk][e] = -INFINITY;
+          }
+      }
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
-        for (int e = 0; e < 16; ++e) {
-          float v = s[kk][e] * a.scale_log2;
-          if (diag) {
-            const int key = k0 + kk * 32 + (e & 3) + 8 * (e >> 2) + 4 * hi;
-            if (key > qme) v = -INFINITY;
-          }
-          s[kk][e] = v;
-          mx = fmaxf(mx, v);
-        }
+        for (int e = 0; e < 16; ++e) mx = fmaxf(mx, s[kk][e]);
       mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      const float mn = fmaxf(m, mx);
+      const float mn = fmaxf(m, mx * a.scale_log2);
       const float alpha = __builtin_amdgcn_exp2f(m - mn);   // m = -inf on the first tile -> 0
+      const bool rescale = m != mn;
       m = mn;
       float ls = 0.f;
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
-          const float p = __builtin_amdgcn_exp2f(s[kk][e] - mn);
+          const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(s[kk][e], a.scale_log2, -mn));
           s[kk][e] = p;
           ls += p;
         }
       l = l * alpha + ls;
+      if (__any(rescale)) {                          // wave-uniform skip when no max moved
 #pragma unroll
-      for (int dt = 0; dt < 2; ++dt)
+        for (int dt = 0; dt < 2; ++dt)
 #pragma unroll
-        for (int e = 0; e < 16; ++e) o[dt][e] *= alpha;
+          for (int e = 0; e < 16; ++e) o[dt][e] *= alpha;
+      }
       // ---- O^T += V^T P^T: k-step = 16 keys; P^T element j <-> key 16 s + 8 (j>>2) + 4 hi + (j&3)
       const int g = lane >> 4, i16 = lane & 15;
       const int tq = i16 >> 2, tp = i16 & 3;        // tr-read lane role: block row / col group
@@ -372,17 +376,33 @@ __global__ void __launch_bounds__(kAttnThreads, 2) attn_bwd_dkdv_d64_kernel(Attn
     if (qs + kSlice - 1 >= kw) {                    // wave-uniform: some query >= some key
       const char* iq = imgQ(cur);
       const char* ig = imgG(cur);
-      // per-row constants for rows q = qs + 8 g + 4 hi + u (register e = 4 g + u)
+      // per-row constants for rows q = qs + 8 g + 4 hi + u (register e = 4 g + u): 4 rows per
+      // float4 when the slice is whole (the tail slice clamps row by row)
       float l2[16], dl[16];
+      const float* lrow = a.lse + bh * a.T;
+      const float* drow = a.delta + bh * a.T;
+      if (qs + kSlice <= a.T && (a.T & 3) == 0) {
 #pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4)
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          int q = qs + 8 * g4 + 4 * hi + u;
-          q = q < a.T ? q : a.T - 1;
-          l2[4 * g4 + u] = a.lse[bh * a.T + q] * 1.4426950408889634f;
-          dl[4 * g4 + u] = a.delta[bh * a.T + q];
+        for (int g4 = 0; g4 < 4; ++g4) {
+          const float4 lv = *reinterpret_cast<const float4*>(lrow + qs + 8 * g4 + 4 * hi);
+          const float4 dv4 = *reinterpret_cast<const float4*>(drow + qs + 8 * g4 + 4 * hi);
+          l2[4 * g4 + 0] = lv.x; l2[4 * g4 + 1] = lv.y; l2[4 * g4 + 2] = lv.z; l2[4 * g4 + 3] = lv.w;
+          dl[4 * g4 + 0] = dv4.x; dl[4 * g4 + 1] = dv4.y; dl[4 * g4 + 2] = dv4.z;
+          dl[4 * g4 + 3] = dv4.w;
         }
+      } else {
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4)
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            int q = qs + 8 * g4 + 4 * hi + u;
+            q = q < a.T ? q : a.T - 1;
+            l2[4 * g4 + u] = lrow[q];
+            dl[4 * g4 + u] = drow[q];
+          }
+      }
+#pragma unroll
+      for (int e = 0; e < 16; ++e) l2[e] *= 1.4426950408889634f;
       f32x16 s, dp;
 #pragma unroll
       for (int e = 0; e < 16; ++e) { s[e] = 0.f; dp[e] = 0.f; }
