@@ -311,20 +311,24 @@ __device__ __forceinline__ bf16x8 acc_to_bf16(const f32x16& x, int st) {
   return f;
 }
 
-// stage 32 rows x 128 B of a [T, ...] bf16 matrix (row stride ld, column offset col0) into an
-// image with the bswz layout; wave w issues rows [8w, 8w + 8). Rows >= T are clamped.
-__device__ __forceinline__ void stage32(const uint16_t* base, int64_t ld, int row0, int T,
+// stage 64 rows x 128 B of a [T, ...] bf16 matrix (row stride ld) into an image with the bswz
+// layout; wave w issues rows [16w, 16w + 16) (2 instructions). Rows >= T are clamped.
+__device__ __forceinline__ void stage64(const uint16_t* base, int64_t ld, int row0, int T,
                                         char* img, int wave, int lane) {
   const int r_in = lane >> 3, slot = lane & 7;
-  const int row = wave * 8 + r_in;
-  int t = row0 + row;
-  t = t < T ? t : T - 1;
-  attn_glds16(base + static_cast<int64_t>(t) * ld + (slot ^ bswz(row)) * 8, img + wave * 8 * 128);
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int row = wave * 16 + i * 8 + r_in;
+    int t = row0 + row;
+    t = t < T ? t : T - 1;
+    attn_glds16(base + static_cast<int64_t>(t) * ld + (slot ^ bswz(row)) * 8,
+                img + (wave * 16 + i * 8) * 128);
+  }
 }
 
 constexpr int kBwdKeys = 128;
-constexpr int kSlice = 32;
-constexpr int kSliceImg = kSlice * 128;     // 4 KiB
+constexpr int kSlice = 64;                   // queries staged per barrier pair (2 x 32)
+constexpr int kSliceImg = kSlice * 128;      // 8 KiB
 
 __global__ void __launch_bounds__(kAttnThreads, 2) attn_bwd_dkdv_d64_kernel(AttnBwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -339,6 +343,8 @@ __global__ void __launch_bounds__(kAttnThreads, 2) attn_bwd_dkdv_d64_kernel(Attn
   const uint16_t* dout_bt = a.dout + static_cast<int64_t>(b) * a.T * a.ldo;
   const int hoff = h * kAttnD;
   const int64_t bh = static_cast<int64_t>(b) * a.H + h;
+  const float* lrow = a.lse + bh * a.T;
+  const float* drow = a.delta + bh * a.T;
 
   bf16x8 kf[4], vf[4];
   {
@@ -360,32 +366,34 @@ __global__ void __launch_bounds__(kAttnThreads, 2) attn_bwd_dkdv_d64_kernel(Attn
   const int ns = (a.T - kb0 + kSlice - 1) / kSlice;
   auto imgQ = [&](int c) { return smem + c * 2 * kSliceImg; };
   auto imgG = [&](int c) { return smem + c * 2 * kSliceImg + kSliceImg; };
-  stage32(base_bt + hoff, a.ld, kb0, a.T, imgQ(0), wave, lane);
-  stage32(dout_bt + hoff, a.ldo, kb0, a.T, imgG(0), wave, lane);
+  stage64(base_bt + hoff, a.ld, kb0, a.T, imgQ(0), wave, lane);
+  stage64(dout_bt + hoff, a.ldo, kb0, a.T, imgG(0), wave, lane);
   for (int i = 0; i < ns; ++i) {
     const int cur = i & 1;
     const int qs = kb0 + i * kSlice;
     if (i + 1 < ns) {
-      stage32(base_bt + hoff, a.ld, qs + kSlice, a.T, imgQ(cur ^ 1), wave, lane);
-      stage32(dout_bt + hoff, a.ldo, qs + kSlice, a.T, imgG(cur ^ 1), wave, lane);
-      asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      stage64(base_bt + hoff, a.ld, qs + kSlice, a.T, imgQ(cur ^ 1), wave, lane);
+      stage64(dout_bt + hoff, a.ldo, qs + kSlice, a.T, imgG(cur ^ 1), wave, lane);
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     __builtin_amdgcn_s_barrier();
-    if (qs + kSlice - 1 >= kw) {                    // wave-uniform: some query >= some key
-      const char* iq = imgQ(cur);
-      const char* ig = imgG(cur);
-      // per-row constants for rows q = qs + 8 g + 4 hi + u (register e = 4 g + u): 4 rows per
-      // float4 when the slice is whole (the tail slice clamps row by row)
+    const char* iq = imgQ(cur);
+    const char* ig = imgG(cur);
+#pragma unroll
+    for (int sub = 0; sub < 2; ++sub) {
+      const int qsub = qs + 32 * sub;
+      if (qsub + 31 < kw) continue;                 // wave-uniform: every query < every key
+      const int rb = 32 * sub;                      // image row base of this 32-query block
+      // per-row constants for rows q = qsub + 8 g + 4 hi + u (register e = 4 g + u): 4 rows
+      // per float4 when the block is whole (a tail block clamps row by row)
       float l2[16], dl[16];
-      const float* lrow = a.lse + bh * a.T;
-      const float* drow = a.delta + bh * a.T;
-      if (qs + kSlice <= a.T && (a.T & 3) == 0) {
+      if (qsub + 32 <= a.T && (a.T & 3) == 0) {
 #pragma unroll
         for (int g4 = 0; g4 < 4; ++g4) {
-          const float4 lv = *reinterpret_cast<const float4*>(lrow + qs + 8 * g4 + 4 * hi);
-          const float4 dv4 = *reinterpret_cast<const float4*>(drow + qs + 8 * g4 + 4 * hi);
+          const float4 lv = *reinterpret_cast<const float4*>(lrow + qsub + 8 * g4 + 4 * hi);
+          const float4 dv4 = *reinterpret_cast<const float4*>(drow + qsub + 8 * g4 + 4 * hi);
           l2[4 * g4 + 0] = lv.x; l2[4 * g4 + 1] = lv.y; l2[4 * g4 + 2] = lv.z; l2[4 * g4 + 3] = lv.w;
           dl[4 * g4 + 0] = dv4.x; dl[4 * g4 + 1] = dv4.y; dl[4 * g4 + 2] = dv4.z;
           dl[4 * g4 + 3] = dv4.w;
@@ -395,29 +403,28 @@ __global__ void __launch_bounds__(kAttnThreads, 2) attn_bwd_dkdv_d64_kernel(Attn
         for (int g4 = 0; g4 < 4; ++g4)
 #pragma unroll
           for (int u = 0; u < 4; ++u) {
-            int q = qs + 8 * g4 + 4 * hi + u;
+            int q = qsub + 8 * g4 + 4 * hi + u;
             q = q < a.T ? q : a.T - 1;
             l2[4 * g4 + u] = lrow[q];
             dl[4 * g4 + u] = drow[q];
           }
       }
-#pragma unroll
-      for (int e = 0; e < 16; ++e) l2[e] *= 1.4426950408889634f;
       f32x16 s, dp;
 #pragma unroll
       for (int e = 0; e < 16; ++e) { s[e] = 0.f; dp[e] = 0.f; }
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) {
-        s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_operand(iq, r, 2 * ks + hi), kf[ks], s,
-                                                    0, 0, 0);
-        dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_operand(ig, r, 2 * ks + hi), vf[ks],
+        s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_operand(iq, rb + r, 2 * ks + hi), kf[ks],
+                                                    s, 0, 0, 0);
+        dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_operand(ig, rb + r, 2 * ks + hi), vf[ks],
                                                      dp, 0, 0, 0);
       }
-      const bool diag = qs < kw + 31;
+      const bool diag = qsub < kw + 31;
 #pragma unroll
       for (int e = 0; e < 16; ++e) {
-        const int q = qs + (e & 3) + 8 * (e >> 2) + 4 * hi;
-        float p = __builtin_amdgcn_exp2f(s[e] * a.scale_log2 - l2[e]);
+        const int q = qsub + (e & 3) + 8 * (e >> 2) + 4 * hi;
+        float p = __builtin_amdgcn_exp2f(
+            __builtin_fmaf(s[e], a.scale_log2, -l2[e] * 1.4426950408889634f));
         if ((diag && mykey > q) || q >= a.T) p = 0.f;
         s[e] = p;
         dp[e] = p * (dp[e] - dl[e]);
@@ -428,10 +435,10 @@ __global__ void __launch_bounds__(kAttnThreads, 2) attn_bwd_dkdv_d64_kernel(Attn
         const bf16x8 db = acc_to_bf16(dp, st);
 #pragma unroll
         for (int dt = 0; dt < 2; ++dt) {
-          dv[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_operand(ig, 16 * st, 32 * dt, lane),
-                                                           pb, dv[dt], 0, 0, 0);
-          dk[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_operand(iq, 16 * st, 32 * dt, lane),
-                                                           db, dk[dt], 0, 0, 0);
+          dv[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+              tr_operand(ig, rb + 16 * st, 32 * dt, lane), pb, dv[dt], 0, 0, 0);
+          dk[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+              tr_operand(iq, rb + 16 * st, 32 * dt, lane), db, dk[dt], 0, 0, 0);
         }
       }
     }
