@@ -48,6 +48,7 @@ class _Bucket:
         self.launched = False
         self.work = None
         self.table: Optional[ChunkTable] = None
+        self.table_key = None
 
 
 class FlatParamTrainer:
@@ -151,11 +152,16 @@ class FlatParamTrainer:
     def _launch(self, b: _Bucket) -> None:
         b.launched = True
         if self.mode == "flatten":
-            if b.table is None:
+            # autograd allocates fresh .grad tensors each step: the table is keyed by their
+            # addresses (the caching allocator usually hands back the same blocks, so it is
+            # rebuilt only when a block moved)
+            key = tuple(p.grad.data_ptr() for p in b.params)
+            if b.table is None or b.table_key != key:
                 pairs = [(p.grad.reshape(-1), self.flat_grad[self._offsets[id(p)]:
                                                               self._offsets[id(p)] + p.numel()])
                          for p in b.params]
                 b.table = ChunkTable(pairs)
+                b.table_key = key
             b.table.run()
         if self.world == 1:
             return
