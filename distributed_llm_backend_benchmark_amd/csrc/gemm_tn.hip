@@ -1,0 +1,203 @@
+// Weight-gradient GEMM, gfx950: dW[N][K] = sum_m dY[m][N] * X[m][K]   (reduction over ROWS).
+//
+// Training backward of every linear (GPT-2, TP model): dW = dY^T X with M = tokens (16 K) and a
+// small output (768 x 768 .. 3072 x 768). The library picks 128^2..256^2 tiles without enough
+// split-K and reaches 210-530 TFLOP/s on these shapes (profiles/r01_gpt2). Here:
+//   * both operands are row-major over the reduction index m, so MFMA fragments (8 consecutive m
+//     of one column) come from ds_read_b64_tr_b16 transposed reads of [64 m][128 col] LDS tiles
+//     staged by LDS-DMA (global_load_lds 16 B) — no transpose pass over the activations;
+//   * LDS image swizzle: 16-B chunk c of row m lives in slot c ^ 2 h(m), h(m) = (m & 3) |
+//     ((m >> 3) & 1) << 2, which makes the 8 rows a 32-lane half reads hit 8 disjoint 32-B bank
+//     groups (conflict-free; a plain 256-B-row image is 8-way);
+//   * split-K over m: fp32 partials [split][N][K], then one reduce + bf16 cast kernel
+//     (deterministic; no float atomics).
+// 128 x 128 output tile per workgroup, 4 waves in 2 x 2 (64 x 64 each = 4 x 4 MFMA 16x16x32),
+// BK = 64 rows of m per stage, two LDS buffers.
+#include "common.h"
+
+namespace dlbb {
+
+namespace tn {
+
+constexpr int BN = 128, BKO = 128, BM = 64;       // output rows (N), output cols (K), reduction
+constexpr int kThreads = 256;
+constexpr int kTile = BM * 128 * 2;               // 16 KiB per operand tile
+
+typedef short i16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) void* lds_vptr_t;
+typedef __attribute__((address_space(3))) i16x4* lds_i16x4_ptr;
+
+__device__ __forceinline__ int swz(int m) { return ((m & 3) | (((m >> 3) & 1) << 2)) << 1; }
+
+struct Args {
+  const uint16_t* A;   // [M][lda]  (dY)
+  const uint16_t* B;   // [M][ldb]  (X)
+  float* ws;           // [split][N][K]
+  int64_t lda, ldb;
+  int M, N, K;
+  int m_per_split;
+};
+
+// Stage rows [m0, m0 + 64) x cols [c0, c0 + 128) of a row-major matrix into a swizzled image.
+// One wave-instruction = 4 rows x 256 B; wave w issues rows [16 w, 16 w + 16) (4 instructions).
+__device__ __forceinline__ void stage(const uint16_t* X, int64_t ld, int m0, int c0, char* img,
+                                      int wave, int lane) {
+  const int rq = lane >> 4, slot = lane & 15;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int row = wave * 16 + i * 4 + rq;
+    const int chunk = slot ^ swz(row);
+    const uint16_t* src = X + static_cast<int64_t>(m0 + row) * ld + c0 + chunk * 8;
+    __builtin_amdgcn_global_load_lds(src, (lds_vptr_t)(img + (wave * 16 + i * 4) * 256), 16, 0,
+                                     0);
+  }
+}
+
+// MFMA 16x16x32 operand from a [64 m][128 col] image: lane l gets column colbase + (l & 15),
+// rows kbase + 8 (l >> 4) + j, j = 0..7 (two transposed reads of 4 rows each).
+__device__ __forceinline__ bf16x8 frag(const char* img, int kbase, int colbase, int lane) {
+  const int g = lane >> 4, i16 = lane & 15;
+  const int q = i16 >> 2, p = i16 & 3;
+  bf16x8 f;
+#pragma unroll
+  for (int half = 0; half < 2; ++half) {
+    const int row = kbase + 8 * g + 4 * half + q;
+    const int col = colbase + 4 * p;
+    const int off = row * 256 + (((col >> 3) ^ swz(row)) << 4) + (col & 7) * 2;
+    const i16x4 t = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4_ptr)(img + off));
+#pragma unroll
+    for (int u = 0; u < 4; ++u) f[4 * half + u] = t[u];
+  }
+  return f;
+}
+
+__global__ void __launch_bounds__(kThreads, 2) wgrad_kernel(Args a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int tiles_k = a.K / BKO;
+  const int tn = blockIdx.x / tiles_k, tk = blockIdx.x % tiles_k;
+  const int n0 = tn * BN, k0 = tk * BKO;
+  const int split = blockIdx.y;
+  const int mb = split * a.m_per_split;
+  const int me = mb + a.m_per_split < a.M ? mb + a.m_per_split : a.M;
+  const int nsteps = (me - mb) / BM;
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto imgA = [&](int c) { return smem + c * 2 * kTile; };
+  auto imgB = [&](int c) { return smem + c * 2 * kTile + kTile; };
+  if (nsteps > 0) {
+    stage(a.A, a.lda, mb, n0, imgA(0), wave, lane);
+    stage(a.B, a.ldb, mb, k0, imgB(0), wave, lane);
+  }
+  for (int s = 0; s < nsteps; ++s) {
+    const int cur = s & 1;
+    if (s + 1 < nsteps) {
+      stage(a.A, a.lda, mb + (s + 1) * BM, n0, imgA(cur ^ 1), wave, lane);
+      stage(a.B, a.ldb, mb + (s + 1) * BM, k0, imgB(cur ^ 1), wave, lane);
+      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    const char* ia = imgA(cur);
+    const char* ib = imgB(cur);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 af[4], bfr[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[i] = frag(ia, 32 * ks, wm * 64 + i * 16, lane);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bfr[j] = frag(ib, 32 * ks, wn * 64 + j * 16, lane);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+    }
+    __builtin_amdgcn_s_barrier();
+  }
+  // D map: col = lane & 15 (output k), row = 4 (lane >> 4) + r (output n)
+  float* w = a.ws + static_cast<int64_t>(split) * a.N * a.K;
+  const int fr = lane & 15, fq = lane >> 4;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int n = n0 + wm * 64 + i * 16 + fq * 4 + r;
+        const int k = k0 + wn * 64 + j * 16 + fr;
+        w[static_cast<int64_t>(n) * a.K + k] = acc[i][j][r];
+      }
+}
+
+// out[i] = sum_s ws[s][i] (+ out[i] if accumulate), bf16 or fp32 output; 8 elements / thread
+template <int DTO>
+__global__ void __launch_bounds__(256) split_reduce_kernel(const float* __restrict__ ws,
+                                                           void* __restrict__ out, int64_t n,
+                                                           int split, int accumulate) {
+  const int64_t nv = n / 8;
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
+  for (int64_t v = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; v < nv;
+       v += stride) {
+    float acc[8];
+    load8<DT_F32>(ws, v, acc);
+    for (int s = 1; s < split; ++s) {
+      float t[8];
+      load8<DT_F32>(ws + static_cast<int64_t>(s) * n, v, t);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += t[j];
+    }
+    if (accumulate) {
+      float o[8];
+      load8<DTO>(out, v, o);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += o[j];
+    }
+    store8<DTO>(out, v, acc);
+  }
+}
+
+}  // namespace tn
+}  // namespace dlbb
+
+using namespace dlbb;
+
+// dW[N][K] = A^T B with A = [M][lda] (N columns used), B = [M][ldb] (K columns used), bf16.
+// Requires M % 64 == 0, N % 128 == 0, K % 128 == 0, lda/ldb % 8 == 0, 16-B aligned bases.
+// ws: fp32 workspace of split * N * K floats. out: bf16 (dt_out 1) or fp32 (0), dense [N][K].
+DLBB_API int dlbb_gemm_wgrad(const void* A, int64_t lda, const void* B, int64_t ldb, void* out,
+                             int dt_out, int accumulate, float* ws, int M, int N, int K,
+                             int split, hipStream_t stream) {
+  using namespace dlbb::tn;
+  if (M <= 0 || N <= 0 || K <= 0) return hipSuccess;
+  if (M % BM || N % BN || K % BKO || lda % 8 || ldb % 8 || split < 1) return hipErrorInvalidValue;
+  if ((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(B) |
+       reinterpret_cast<uintptr_t>(ws)) & 15)
+    return hipErrorInvalidValue;
+  int per = (M / split + BM - 1) / BM * BM;
+  if (per <= 0) per = BM;
+  split = (M + per - 1) / per;
+  Args a{static_cast<const uint16_t*>(A), static_cast<const uint16_t*>(B), ws, lda, ldb, M, N, K,
+         per};
+  const dim3 grid((N / BN) * (K / BKO), split);
+  hipLaunchKernelGGL(wgrad_kernel, grid, dim3(kThreads), 4 * kTile, stream, a);
+  const int64_t n = static_cast<int64_t>(N) * K;
+  const int g = stream_grid(n / 8, 256);
+  if (dt_out == DT_BF16)
+    hipLaunchKernelGGL(split_reduce_kernel<DT_BF16>, dim3(g), dim3(256), 0, stream, ws, out, n,
+                       split, accumulate);
+  else
+    hipLaunchKernelGGL(split_reduce_kernel<DT_F32>, dim3(g), dim3(256), 0, stream, ws, out, n,
+                       split, accumulate);
+  return hipGetLastError();
+}

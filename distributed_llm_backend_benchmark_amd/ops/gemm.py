@@ -194,3 +194,87 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
         return out
     y = _torch_linear(x2, w, bias, act, residual, out_dtype, preact)
     return y.reshape(*lead, N) if out is None else out.copy_(y.reshape(out.shape))
+
+
+def wgrad_supported(dy2: torch.Tensor, x2: torch.Tensor) -> bool:
+    M, N = dy2.shape
+    K = x2.shape[1]
+    return (dy2.dtype == torch.bfloat16 and x2.dtype == torch.bfloat16 and x2.shape[0] == M
+            and M % 64 == 0 and N % 128 == 0 and K % 128 == 0 and dy2.stride(1) == 1
+            and x2.stride(1) == 1 and dy2.stride(0) % 8 == 0 and x2.stride(0) % 8 == 0
+            and dy2.data_ptr() % 16 == 0 and x2.data_ptr() % 16 == 0)
+
+
+def _wgrad_hip(dy2, x2, out, accumulate, split=None):
+    M, N = dy2.shape
+    K = x2.shape[1]
+    tiles = (N // 128) * (K // 128)
+    if split is None:
+        split = max(1, min(M // 256, -(-512 // tiles)))
+    ws = torch.empty(split * N * K, dtype=torch.float32, device=dy2.device)
+    check(_lib.lib().dlbb_gemm_wgrad(dy2.data_ptr(), dy2.stride(0), x2.data_ptr(), x2.stride(0),
+                                     out.data_ptr(), _lib.dt(out), int(accumulate), ws.data_ptr(),
+                                     M, N, K, split, _lib.stream(dy2.device)), "gemm_wgrad")
+
+
+def _wgrad_blas(dy2, x2, out, accumulate, split=None):
+    if accumulate:
+        out.add_(torch.matmul(dy2.t(), x2).to(out.dtype))
+    elif out.dtype == dy2.dtype:
+        torch.matmul(dy2.t(), x2, out=out)
+    else:
+        out.copy_(torch.matmul(dy2.t(), x2))
+
+
+WGRAD_CHOICES = {}    # (M, N, K, out dtype) -> "mfma" | "blas"
+_WGRAD_IMPLS = {"mfma": _wgrad_hip, "blas": _wgrad_blas}
+
+
+def _wgrad_choice(dy2, x2, out) -> str:
+    mode = os.environ.get("DLBB_GEMM", "auto").lower()
+    if mode in _WGRAD_IMPLS:
+        return mode
+    key = (dy2.shape[0], dy2.shape[1], x2.shape[1], out.dtype)
+    if key in WGRAD_CHOICES:
+        return WGRAD_CHOICES[key]
+    if torch.cuda.is_current_stream_capturing():
+        return "mfma"
+    scratch = torch.empty_like(out)
+    best, best_t = "mfma", float("inf")
+    for name, fn in _WGRAD_IMPLS.items():
+        for _ in range(2):
+            fn(dy2, x2, scratch, False)
+        ts = []
+        for _ in range(5):
+            s0, e0 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s0.record()
+            fn(dy2, x2, scratch, False)
+            e0.record()
+            e0.synchronize()
+            ts.append(s0.elapsed_time(e0))
+        t = sorted(ts)[len(ts) // 2]
+        if t < best_t:
+            best, best_t = name, t
+    WGRAD_CHOICES[key] = best
+    return best
+
+
+def wgrad(dy2: torch.Tensor, x2: torch.Tensor, out: Optional[torch.Tensor] = None,
+          accumulate: bool = False, split: Optional[int] = None) -> torch.Tensor:
+    """Weight gradient ``dW = dy2^T @ x2`` ([N, K]) for row-major ``dy2 [M, N]``, ``x2 [M, K]``.
+
+    HIP path (``csrc/gemm_tn.hip``): transposed-read MFMA tiles, split-K over M with fp32
+    partials and one reduce/cast pass; ``accumulate=True`` adds into ``out``. Per shape the
+    faster of this kernel and the library GEMM is measured once and cached
+    (:data:`WGRAD_CHOICES`; ``DLBB_GEMM=mfma|blas`` forces; an explicit ``split`` forces ours)."""
+    M, N = dy2.shape
+    K = x2.shape[1]
+    if out is None:
+        out = torch.empty(N, K, dtype=dy2.dtype, device=dy2.device)
+    if (use_hip(dy2, x2) and wgrad_supported(dy2, x2) and out.is_contiguous()
+            and out.dtype in (torch.bfloat16, torch.float32)):
+        choice = "mfma" if split is not None else _wgrad_choice(dy2, x2, out)
+        _WGRAD_IMPLS[choice](dy2, x2, out, accumulate, split)
+        return out
+    _wgrad_blas(dy2, x2, out, accumulate)
+    return out

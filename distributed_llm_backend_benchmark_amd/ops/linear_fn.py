@@ -3,8 +3,9 @@
 Forward: ``y = act(x @ W^T + b)`` through the hand-written MFMA kernel (``csrc/gemm.hip``);
 with an activation the epilogue also stores the pre-activation ``u`` (needed by the GELU
 backward). Backward: ``dU = dY * act'(u)`` and ``db = colsum(dU)`` in one pass of the bias-GELU
-backward kernel (``csrc/gelu.hip``); ``dX = dU @ W`` and ``dW = dU^T @ X`` are plain library
-GEMMs (hipBLASLt through ``torch.matmul``), as allowed for unfused GEMMs.
+backward kernel (``csrc/gelu.hip``); ``dX = dU @ W`` is a plain library GEMM (hipBLASLt through
+``torch.matmul``, as allowed for unfused GEMMs); ``dW = dU^T @ X`` goes through
+:func:`.gemm.wgrad` (our split-K transposed-read MFMA kernel or the library, per-shape autotune).
 """
 
 from __future__ import annotations
@@ -16,7 +17,7 @@ import torch.nn.functional as F
 
 from . import _lib
 from ._lib import check, use_hip
-from .gemm import hip_supported, linear as _linear
+from .gemm import hip_supported, linear as _linear, wgrad
 
 _APPROX = {"gelu": 0, "gelu_erf": 0, "gelu_tanh": 1}
 
@@ -61,7 +62,7 @@ class _LinearFn(torch.autograd.Function):
             if ctx.has_bias:
                 db = du.sum(0, dtype=torch.float32).to(w.dtype)
         dx = torch.matmul(du, w) if ctx.needs_input_grad[0] else None
-        dw = torch.matmul(du.t(), x2) if ctx.needs_input_grad[1] else None
+        dw = wgrad(du, x2) if ctx.needs_input_grad[1] else None
         if dx is not None:
             dx = dx.view(*ctx.lead, K)
         return dx, dw, db, None

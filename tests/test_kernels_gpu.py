@@ -291,3 +291,36 @@ def test_cross_entropy_fwd_bwd(V):
     lf.backward()
     torch.testing.assert_close(loss.float(), lf, rtol=1e-4, atol=1e-4)
     torch.testing.assert_close(x.grad.float(), xf.grad, rtol=2e-2, atol=2e-5)
+
+
+@pytest.mark.parametrize("M,N,K", [(64, 128, 128), (16384, 768, 768), (4096, 2304, 768),
+                                   (1024, 256, 3072), (320, 384, 256)])
+@pytest.mark.parametrize("split", [None, 1, 3])
+def test_wgrad_matches_fp32(M, N, K, split):
+    from distributed_llm_backend_benchmark_amd.ops.gemm import wgrad
+
+    dy = _randn(M, N, seed=21, scale=0.5)
+    x = _randn(M, K, seed=22, scale=0.5)
+    ref = dy.float().t() @ x.float()
+    out32 = torch.empty(N, K, dtype=torch.float32, device=DEV)
+    wgrad(dy, x, out=out32, split=split)
+    torch.testing.assert_close(out32, ref, rtol=2e-3, atol=2e-3 * (M ** 0.5))
+    acc = torch.ones(N, K, dtype=torch.float32, device=DEV)
+    wgrad(dy, x, out=acc, accumulate=True, split=split)
+    torch.testing.assert_close(acc, ref + 1, rtol=2e-3, atol=2e-3 * (M ** 0.5))
+    y = wgrad(dy, x, split=split)
+    torch.testing.assert_close(y.float(), ref, rtol=2e-2, atol=2e-2 * (M ** 0.5))
+
+
+def test_wgrad_asymmetric():
+    """dY = one-hot columns: dW rows must be the right X rows (catches swapped maps)."""
+    from distributed_llm_backend_benchmark_amd.ops.gemm import wgrad
+
+    M, N, K = 128, 128, 128
+    dy = torch.zeros(M, N, device=DEV)
+    dy[torch.arange(M), (torch.arange(M) * 7) % N] = 1.0
+    x = (torch.arange(M * K, device=DEV, dtype=torch.float32).view(M, K) % 13)
+    dy, x = dy.to(torch.bfloat16), x.to(torch.bfloat16)
+    out = torch.empty(N, K, dtype=torch.float32, device=DEV)
+    wgrad(dy, x, out=out)
+    torch.testing.assert_close(out, dy.float().t() @ x.float(), rtol=0, atol=0)
