@@ -30,7 +30,7 @@ def parse_args(argv=None):
     ap.add_argument("--config", required=True, help="YAML config (reference schema)")
     ap.add_argument("--backend", default="rccl", choices=["rccl", "gloo", "nccl"],
                     help="process-group backend; also names the output file")
-    ap.add_argument("--allreduce", choices=["auto", "rccl", "custom"], default=None,
+    ap.add_argument("--allreduce", choices=["auto", "rccl", "custom", "native"], default=None,
                     help="override execution.allreduce")
     ap.add_argument("--allreduce-dtype", choices=["bf16", "fp32"], default=None)
     ap.add_argument("--attention", choices=["slice", "sdpa"], default=None)
@@ -41,8 +41,9 @@ def parse_args(argv=None):
     ap.add_argument("--iters", type=int, default=None)
     ap.add_argument("--output-dir", default=None)
     ap.add_argument("--graph", action="store_true",
-                    help="capture the forward in a HIP graph and replay it (world 1, or all "
-                         "all-reduces on the IPC kernel; RCCL collectives are not captured)")
+                    help="capture the forward in a HIP graph and replay it (world 1, or "
+                         "all-reduces not issued through ProcessGroupNCCL: custom / native / "
+                         "auto)")
     ap.add_argument("--trace", action="store_true",
                     help="emit roctx ranges (record with rocprofv3 --marker-trace)")
     ap.add_argument("--torch-profile", default=None, metavar="DIR",
@@ -142,9 +143,10 @@ def main(argv=None) -> int:
 
     run_forward = lambda: model(dataset.get_batch())  # noqa: E731
     use_graph = bool(args.graph or ex.get("graph", False)) and gpu
-    if use_graph and world > 1 and ex.get("allreduce") != "custom":
+    if use_graph and world > 1 and ex.get("allreduce") not in ("custom", "native", "auto"):
         if rank == 0:
-            print("note: --graph needs world 1 or execution.allreduce=custom; running eagerly")
+            print("note: --graph needs world 1 or execution.allreduce custom|native|auto; "
+                  "running eagerly")
         use_graph = False
     if use_graph:
         # HIP graph: one replay launches the whole forward (all GEMM / LN / all-reduce kernels);

@@ -75,10 +75,21 @@ class RowParallelLinear(nn.Module):
         self.weight = _randn_weight(out_features, self.in_per_rank, comm.device, dtype,
                                     generator, std)
         self._car = None
+        self._native = None
         if allreduce in ("custom", "auto") and comm.is_gpu and comm.world_size > 1:
             from .custom_allreduce import get_custom_allreduce
 
             self._car = get_custom_allreduce(comm)
+        if allreduce in ("native", "auto") and comm.is_gpu and comm.world_size > 1:
+            # RCCL enqueued on the compute stream by our engine: no ProcessGroupNCCL stream hop
+            # and HIP-graph capturable (run_tp --graph at world > 1)
+            from .rccl_native import get_native
+
+            try:
+                self._native = get_native(comm)
+            except RuntimeError:
+                if allreduce == "native":
+                    raise
         self.comm_bytes = 0   # bytes all-reduced by this layer (accounting)
 
     def _all_reduce(self, t: torch.Tensor) -> None:
@@ -89,6 +100,8 @@ class RowParallelLinear(nn.Module):
         if car is not None and (self.allreduce == "custom" or car.should_use(t)) \
                 and car.supports(t):
             car.all_reduce_(t)
+        elif self._native is not None and t.is_contiguous():
+            self._native.enqueue("allreduce", t, t, t.numel())
         else:
             dist.all_reduce(t)
 

@@ -10,7 +10,9 @@ Additions (all optional, defaults keep reference behaviour):
 * ``parallelism.backend``: ``rccl`` | ``gloo`` | ``auto`` (process-group backend).
 * ``parallelism.world_size: auto`` accepts whatever world the launcher created.
 * ``parallelism.cores_per_rank`` is accepted and recorded; on GPU it is a no-op.
-* ``execution.allreduce``: ``rccl`` | ``custom`` | ``auto`` (row-parallel all-reduce path).
+* ``execution.allreduce``: ``rccl`` (torch ProcessGroupNCCL) | ``native`` (our C++ RCCL engine
+  on the compute stream) | ``custom`` (IPC xGMI kernel) | ``auto`` (custom below its crossover,
+  native above) — the row-parallel all-reduce path.
 * ``execution.allreduce_dtype``: ``bf16`` (on-device, default) | ``fp32`` (reference wire format,
   ``models.py:84``).
 * ``execution.attention``: ``slice`` (reference stub ``models.py:162-167``) | ``sdpa``.
@@ -95,8 +97,9 @@ def validate_config(config: Dict[str, Any]) -> Dict[str, Any]:
         if int(m[k]) <= 0:
             raise ConfigError(f"model.{k} must be positive")
     ex = cfg["execution"]
-    if ex["allreduce"] not in ("auto", "rccl", "custom", "torch"):
-        raise ConfigError(f"execution.allreduce must be auto|rccl|custom|torch, got {ex['allreduce']!r}")
+    if ex["allreduce"] not in ("auto", "rccl", "custom", "native", "torch"):
+        raise ConfigError("execution.allreduce must be auto|rccl|custom|native|torch, got "
+                          f"{ex['allreduce']!r}")
     if ex["allreduce_dtype"] not in ("bf16", "fp32"):
         raise ConfigError("execution.allreduce_dtype must be bf16|fp32")
     if ex["attention"] not in ("slice", "sdpa"):
