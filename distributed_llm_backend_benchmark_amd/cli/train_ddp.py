@@ -36,7 +36,9 @@ def parse_args(argv=None):
     ap.add_argument("--lr", type=float, default=3e-4)
     ap.add_argument("--bucket-mb", type=float, default=64.0)
     ap.add_argument("--mode", choices=["view", "flatten"], default="view")
-    ap.add_argument("--allreduce", choices=["rccl", "custom"], default="rccl")
+    ap.add_argument("--allreduce", choices=["rccl", "custom", "native"], default="rccl",
+                    help="bucket all-reduce: torch ProcessGroupNCCL, IPC xGMI kernel, or our "
+                         "C++ RCCL engine on a dedicated stream")
     ap.add_argument("--no-overlap", action="store_true")
     ap.add_argument("--zero", action="store_true",
                     help="ZeRO-2-style: reduce-scatter grads, sharded AdamW, all-gather params")

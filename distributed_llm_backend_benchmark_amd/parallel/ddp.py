@@ -19,8 +19,9 @@ the MI355X-native replacement used by the GPT-2 DDP microbenchmark:
   producing kernels by an event), strictly in bucket order on every rank (identical collective
   order — RCCL would hang otherwise). ``finish()`` waits the works; the optimizer consumes the
   reduced flat gradient with the 1/world average fused into the AdamW kernel.
-* ``allreduce="custom"`` routes buckets that fit through the IPC xGMI kernel on a dedicated
-  comm stream instead.
+* ``allreduce="custom"`` routes buckets that fit through the IPC xGMI kernel, and
+  ``allreduce="native"`` through our own RCCL communicator (``rccl_native``), both on a
+  dedicated high-priority comm stream instead of ProcessGroupNCCL's.
 """
 
 from __future__ import annotations
@@ -105,10 +106,16 @@ class FlatParamTrainer:
         self._next = 0
         self._comm_stream = None
         self._car = None
+        self._native = None
         if allreduce == "custom" and comm is not None and comm.is_gpu and self.world > 1:
             from .custom_allreduce import get_custom_allreduce
 
             self._car = get_custom_allreduce(comm)
+            self._comm_stream = torch.cuda.Stream(dev, priority=-1)
+        if allreduce == "native" and comm is not None and comm.is_gpu and self.world > 1:
+            from .rccl_native import get_native
+
+            self._native = get_native(comm)
             self._comm_stream = torch.cuda.Stream(dev, priority=-1)
         self.step_count = 0
 
@@ -171,7 +178,14 @@ class FlatParamTrainer:
             cs.wait_stream(torch.cuda.current_stream(buf.device))
             with torch.cuda.stream(cs):
                 self._car.all_reduce_(buf)
-            b.work = "custom"
+            b.work = "stream"
+        elif self._native is not None:
+            # our RCCL communicator on a dedicated high-priority stream, ordered after the
+            # producing backward kernels; finish() joins the stream
+            cs = self._comm_stream
+            cs.wait_stream(torch.cuda.current_stream(buf.device))
+            self._native.enqueue("allreduce", buf, buf, buf.numel(), stream=cs.cuda_stream)
+            b.work = "stream"
         else:
             b.work = dist.all_reduce(buf, async_op=True)
 
@@ -181,7 +195,7 @@ class FlatParamTrainer:
             self._launch(self.buckets[self._next])
             self._next += 1
         for b in self.buckets:
-            if b.work == "custom":
+            if b.work == "stream":
                 torch.cuda.current_stream(self.flat_grad.device).wait_stream(self._comm_stream)
             elif b.work is not None:
                 b.work.wait()
