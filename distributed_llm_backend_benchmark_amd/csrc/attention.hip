@@ -110,13 +110,12 @@ __global__ void __launch_bounds__(kAttnThreads, 2) attn_fwd_d64_kernel(AttnArgs 
   attn_stage(a, base_bt, 0, hoff, tileK(0), tileV(0), wave, lane);
   for (int kt = 0; kt < nt; ++kt) {
     const int cur = kt & 1;
-    if (kt + 1 < nt) {
-      attn_stage(a, base_bt, (kt + 1) * kKB, hoff, tileK(cur ^ 1), tileV(cur ^ 1), wave, lane);
-      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
+    // one barrier per tile: it both publishes tile kt (every wave's DMA retired) and frees
+    // buffer cur^1 (every wave finished tile kt-1), so the restage goes right after it
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
+    if (kt + 1 < nt)
+      attn_stage(a, base_bt, (kt + 1) * kKB, hoff, tileK(cur ^ 1), tileV(cur ^ 1), wave, lane);
     const int k0 = kt * kKB;
     if (k0 <= q_hi) {                               // wave-uniform: tile has keys <= a query
       const char* tk = tileK(cur);
@@ -200,7 +199,6 @@ __global__ void __launch_bounds__(kAttnThreads, 2) attn_fwd_d64_kernel(AttnArgs 
           }
         }
     }
-    __builtin_amdgcn_s_barrier();                   // buffer cur is restaged next iteration
   }
 
   // ---- finalize: l over both lane halves, O / l, store O [B,T,H,D] and LSE
@@ -371,14 +369,12 @@ __global__ void __launch_bounds__(kAttnThreads, 2) attn_bwd_dkdv_d64_kernel(Attn
   for (int i = 0; i < ns; ++i) {
     const int cur = i & 1;
     const int qs = kb0 + i * kSlice;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();                   // publishes slice i, frees buffer cur^1
     if (i + 1 < ns) {
       stage64(base_bt + hoff, a.ld, qs + kSlice, a.T, imgQ(cur ^ 1), wave, lane);
       stage64(dout_bt + hoff, a.ldo, qs + kSlice, a.T, imgG(cur ^ 1), wave, lane);
-      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
-    __builtin_amdgcn_s_barrier();
     const char* iq = imgQ(cur);
     const char* ig = imgG(cur);
 #pragma unroll
@@ -442,7 +438,6 @@ __global__ void __launch_bounds__(kAttnThreads, 2) attn_bwd_dkdv_d64_kernel(Attn
         }
       }
     }
-    __builtin_amdgcn_s_barrier();
   }
   if (mykey < a.T) {
     uint16_t* dkp = a.dqkv + (static_cast<int64_t>(b) * a.T + mykey) * a.ld + kAttnD * a.H + hoff;
@@ -519,13 +514,10 @@ __global__ void __launch_bounds__(kAttnThreads, 2) attn_bwd_dq_d64_kernel(AttnBw
   stage_kv64(a, base_bt, 0, hoff, tileK(0), tileV(0), wave, lane);
   for (int kt = 0; kt < nt; ++kt) {
     const int cur = kt & 1;
-    if (kt + 1 < nt) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();                   // publishes tile kt, frees buffer cur^1
+    if (kt + 1 < nt)
       stage_kv64(a, base_bt, (kt + 1) * kKB, hoff, tileK(cur ^ 1), tileV(cur ^ 1), wave, lane);
-      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __builtin_amdgcn_s_barrier();
     const int k0 = kt * kKB;
     if (k0 <= q_hi) {
       const char* tk = tileK(cur);
@@ -560,7 +552,6 @@ __global__ void __launch_bounds__(kAttnThreads, 2) attn_bwd_dq_d64_kernel(AttnBw
         }
       }
     }
-    __builtin_amdgcn_s_barrier();
   }
   if (qme < a.T) {
     uint16_t* dqp = a.dqkv + (static_cast<int64_t>(b) * a.T + qme) * a.ld + hoff;
