@@ -277,8 +277,8 @@ DLBB_API int dlbb_car_create(int rank, int world, int64_t cap_bytes, void** out)
   s->rank = rank;
   s->world = world;
   s->cap = cap_bytes;
-  CAR_CHECK(hipGetDevice(&s->device));
-  hipError_t e = hipMalloc(reinterpret_cast<void**>(&s->data), 2 * cap_bytes);
+  hipError_t e = hipGetDevice(&s->device);   // (no early return: s must not leak)
+  if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&s->data), 2 * cap_bytes);
   if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&s->tmp), 2 * cap_bytes);
   if (e == hipSuccess)
     e = hipExtMallocWithFlags(reinterpret_cast<void**>(&s->sig), sizeof(Signal),
