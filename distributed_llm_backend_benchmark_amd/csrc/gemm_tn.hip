@@ -12,14 +12,14 @@
 //   * split-K over m: fp32 partials [split][N][K], then one reduce + bf16 cast kernel
 //     (deterministic; no float atomics).
 // 128 x 128 output tile per workgroup, 4 waves in 2 x 2 (64 x 64 each = 4 x 4 MFMA 16x16x32),
-// BK = 64 rows of m per stage, two LDS buffers.
+// BM = 32 rows of m per stage, two LDS buffers (32 KiB: three workgroups per CU).
 #include "common.h"
 
 namespace dlbb {
 
 namespace tn {
 
-constexpr int BN = 128, BKO = 128, BM = 64;       // output rows (N), output cols (K), reduction
+constexpr int BN = 128, BKO = 128, BM = 32;       // output rows (N), output cols (K), reduction
 constexpr int kThreads = 256;
 constexpr int kTile = BM * 128 * 2;               // 16 KiB per operand tile
 
@@ -38,18 +38,18 @@ struct Args {
   int m_per_split;
 };
 
-// Stage rows [m0, m0 + 64) x cols [c0, c0 + 128) of a row-major matrix into a swizzled image.
-// One wave-instruction = 4 rows x 256 B; wave w issues rows [16 w, 16 w + 16) (4 instructions).
+// Stage rows [m0, m0 + BM) x cols [c0, c0 + 128) of a row-major matrix into a swizzled image.
+// One wave-instruction = 4 rows x 256 B; wave w issues rows [BM/4 w, BM/4 (w + 1)).
 __device__ __forceinline__ void stage(const uint16_t* X, int64_t ld, int m0, int c0, char* img,
                                       int wave, int lane) {
   const int rq = lane >> 4, slot = lane & 15;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int row = wave * 16 + i * 4 + rq;
+  for (int i = 0; i < BM / 16; ++i) {
+    const int row = wave * (BM / 4) + i * 4 + rq;
     const int chunk = slot ^ swz(row);
     const uint16_t* src = X + static_cast<int64_t>(m0 + row) * ld + c0 + chunk * 8;
-    __builtin_amdgcn_global_load_lds(src, (lds_vptr_t)(img + (wave * 16 + i * 4) * 256), 16, 0,
-                                     0);
+    __builtin_amdgcn_global_load_lds(src, (lds_vptr_t)(img + (wave * (BM / 4) + i * 4) * 256),
+                                     16, 0, 0);
   }
 }
 
@@ -71,7 +71,7 @@ __device__ __forceinline__ bf16x8 frag(const char* img, int kbase, int colbase, 
   return f;
 }
 
-__global__ void __launch_bounds__(kThreads, 2) wgrad_kernel(Args a) {
+__global__ void __launch_bounds__(kThreads, 3) wgrad_kernel(Args a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -98,18 +98,18 @@ __global__ void __launch_bounds__(kThreads, 2) wgrad_kernel(Args a) {
   }
   for (int s = 0; s < nsteps; ++s) {
     const int cur = s & 1;
+    // one barrier per stage: it publishes stage s (every wave's DMA retired) and frees buffer
+    // cur^1 (every wave finished stage s-1), so the next stage is issued right after it
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
     if (s + 1 < nsteps) {
       stage(a.A, a.lda, mb + (s + 1) * BM, n0, imgA(cur ^ 1), wave, lane);
       stage(a.B, a.ldb, mb + (s + 1) * BM, k0, imgB(cur ^ 1), wave, lane);
-      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
-    __builtin_amdgcn_s_barrier();
     const char* ia = imgA(cur);
     const char* ib = imgB(cur);
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
+    for (int ks = 0; ks < BM / 32; ++ks) {
       bf16x8 af[4], bfr[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) af[i] = frag(ia, 32 * ks, wm * 64 + i * 16, lane);
@@ -123,7 +123,6 @@ __global__ void __launch_bounds__(kThreads, 2) wgrad_kernel(Args a) {
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
       __builtin_amdgcn_s_setprio(0);
     }
-    __builtin_amdgcn_s_barrier();
   }
   // D map: col = lane & 15 (output k), row = 4 (lane >> 4) + r (output n)
   float* w = a.ws + static_cast<int64_t>(split) * a.N * a.K;
@@ -173,7 +172,7 @@ __global__ void __launch_bounds__(256) split_reduce_kernel(const float* __restri
 using namespace dlbb;
 
 // dW[N][K] = A^T B with A = [M][lda] (N columns used), B = [M][ldb] (K columns used), bf16.
-// Requires M % 64 == 0, N % 128 == 0, K % 128 == 0, lda/ldb % 8 == 0, 16-B aligned bases.
+// Requires M % 32 == 0, N % 128 == 0, K % 128 == 0, lda/ldb % 8 == 0, 16-B aligned bases.
 // ws: fp32 workspace of split * N * K floats. out: bf16 (dt_out 1) or fp32 (0), dense [N][K].
 DLBB_API int dlbb_gemm_wgrad(const void* A, int64_t lda, const void* B, int64_t ldb, void* out,
                              int dt_out, int accumulate, float* ws, int M, int N, int K,

@@ -200,7 +200,7 @@ def wgrad_supported(dy2: torch.Tensor, x2: torch.Tensor) -> bool:
     M, N = dy2.shape
     K = x2.shape[1]
     return (dy2.dtype == torch.bfloat16 and x2.dtype == torch.bfloat16 and x2.shape[0] == M
-            and M % 64 == 0 and N % 128 == 0 and K % 128 == 0 and dy2.stride(1) == 1
+            and M % 32 == 0 and N % 128 == 0 and K % 128 == 0 and dy2.stride(1) == 1
             and x2.stride(1) == 1 and dy2.stride(0) % 8 == 0 and x2.stride(0) % 8 == 0
             and dy2.data_ptr() % 16 == 0 and x2.data_ptr() % 16 == 0)
 

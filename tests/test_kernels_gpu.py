@@ -297,7 +297,7 @@ def test_cross_entropy_fwd_bwd(V):
 
 
 @pytest.mark.parametrize("M,N,K", [(64, 128, 128), (16384, 768, 768), (4096, 2304, 768),
-                                   (1024, 256, 3072), (320, 384, 256)])
+                                   (1024, 256, 3072), (320, 384, 256), (96, 128, 256)])
 @pytest.mark.parametrize("split", [None, 1, 3])
 def test_wgrad_matches_fp32(M, N, K, split):
     from distributed_llm_backend_benchmark_amd.ops.gemm import wgrad

@@ -42,10 +42,16 @@ for name, N_out, K_in in (("qkv", 3 * C, C), ("proj", C, C), ("fc", 4 * C, C), (
     from distributed_llm_backend_benchmark_amd.ops.gemm import wgrad
     t_dw_ours = t_best(lambda: wgrad(dy, x))
     dw_err = float((wgrad(dy, x).float() - torch.matmul(dy.t(), x).float()).abs().max())
+    tiles = (N_out // 128) * (K_in // 128)
+    splits = {}
+    for target in (256, 512, 1024, 2048):
+        sp = max(1, min(M // 256, -(-target // tiles)))
+        splits[f"wgs{target}_split{sp}"] = round(t_best(lambda: wgrad(dy, x, split=sp)) * 1e6, 1)
     print(json.dumps({"gemm": name, "dX_shape": [M, K_in, N_out], "dX_blas_us": t_dx_blas * 1e6,
                       "dX_ours_us": None if t_dx_ours is None else t_dx_ours * 1e6,
                       "transpose_us": t_tr * 1e6, "dX_blas_tflops": fl / t_dx_blas / 1e12,
                       "dX_ours_tflops": None if t_dx_ours is None else fl / t_dx_ours / 1e12,
                       "dW_blas_us": t_dw_blas * 1e6, "dW_blas_tflops": fl / t_dw_blas / 1e12,
                       "dW_ours_us": t_dw_ours * 1e6, "dW_ours_tflops": fl / t_dw_ours / 1e12,
-                      "dW_max_err": dw_err, "max_err": err}), flush=True)
+                      "dW_max_err": dw_err, "dW_ours_by_split_us": splits,
+                      "max_err": err}), flush=True)
