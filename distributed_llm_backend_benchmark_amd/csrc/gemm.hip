@@ -60,6 +60,11 @@ __device__ __forceinline__ void glds16(const void* g, char* lds_base_wave_unifor
 
 // Stage a 128 x 64 bf16 tile of a K-contiguous matrix into LDS (16 KiB).
 // Wave w issues 4 instructions; instruction i covers tile rows [w*32 + i*8, +8).
+__device__ __forceinline__ int perm_brow(int x) {
+  return (x & ~63) | (((x >> 2) & 3) << 4) | (((x >> 4) & 3) << 2) | (x & 3);
+}
+
+template <bool PERM>   // PERM: B rows in the perm_brow order (swapped-operand epilogue)
 __device__ __forceinline__ void stage_tile(const uint16_t* __restrict__ X, int64_t ld,
                                            int64_t row0, int64_t rows, int64_t k0, char* lds,
                                            int wave, int lane) {
@@ -69,7 +74,7 @@ __device__ __forceinline__ void stage_tile(const uint16_t* __restrict__ X, int64
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int trow = wave * 32 + i * 8;
-    int64_t gr = row0 + trow + r_in;
+    int64_t gr = row0 + (PERM ? perm_brow(trow + r_in) : trow + r_in);
     gr = gr < rows ? gr : rows - 1;              // ragged edge: clamp (stores are masked)
     const uint16_t* src = X + gr * ld + k0 + chunk * 8;
     glds16(src, lds + trow * (BK * 2));
@@ -85,99 +90,6 @@ __device__ __forceinline__ float apply_act(float v, int epi) {
   if (epi & EPI_GELU_ERF) return gelu_erf(v);
   if (epi & EPI_GELU_TANH) return gelu_tanh(v);
   return v;
-}
-
-__global__ void __launch_bounds__(kThreads, 2) gemm_bf16_nt_kernel(GemmArgs a) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave >> 1, wn = wave & 1;
-
-  // ---- workgroup -> tile: XCD-aware bijective remap, then GROUP_M swizzle
-  const int64_t tiles_m = (a.M + BM - 1) / BM, tiles_n = (a.N + BN - 1) / BN;
-  const int64_t nwg = tiles_m * tiles_n;
-  int64_t wid = blockIdx.x;
-  {
-    const int64_t q = nwg / 8, r = nwg % 8, x = wid % 8;
-    wid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + wid / 8;
-  }
-  const int64_t group_size = kGroupM * tiles_n;
-  const int64_t group = wid / group_size;
-  const int64_t first_m = group * kGroupM;
-  const int64_t gm = (tiles_m - first_m) < kGroupM ? (tiles_m - first_m) : kGroupM;
-  const int64_t tm = first_m + (wid % group_size) % gm;
-  const int64_t tn = (wid % group_size) / gm;
-  const int64_t m0 = tm * BM, n0 = tn * BN;
-
-  // buffer c: A at smem + c * 2 * kTileBytes, B right after it
-  auto bufA = [&](int c) { return smem + c * 2 * kTileBytes; };
-  auto bufB = [&](int c) { return smem + c * 2 * kTileBytes + kTileBytes; };
-
-  f32x4 acc[4][4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  const int64_t nk = a.K / BK;
-  stage_tile(a.A, a.lda, m0, a.M, 0, bufA(0), wave, lane);
-  stage_tile(a.B, a.ldb, n0, a.N, 0, bufB(0), wave, lane);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-
-  const int fr = lane & 15, fq = lane >> 4;
-  for (int64_t kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < nk) {
-      stage_tile(a.A, a.lda, m0, a.M, (kt + 1) * BK, bufA(cur ^ 1), wave, lane);
-      stage_tile(a.B, a.ldb, n0, a.N, (kt + 1) * BK, bufB(cur ^ 1), wave, lane);
-    }
-    const char* la = bufA(cur);
-    const char* lb = bufB(cur);
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      bf16x8 af[4], bfr[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) af[i] = read_frag(la, wm * 64 + i * 16 + fr, ks * 4 + fq);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) bfr[j] = read_frag(lb, wn * 64 + j * 16 + fr, ks * 4 + fq);
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
-      __builtin_amdgcn_s_setprio(0);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-  }
-
-  // ---- epilogue: C/D map of 16x16x32: col = lane & 15, row = 4 * (lane >> 4) + reg
-  const int epi = a.epi;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int64_t col = n0 + wn * 64 + j * 16 + fr;
-    if (col >= a.N) continue;
-    const float bias = (epi & EPI_BIAS) ? bf16_to_f32(a.bias[col]) : 0.f;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int64_t row = m0 + wm * 64 + i * 16 + fq * 4 + r;
-        if (row >= a.M) continue;
-        float v = acc[i][j][r] + bias;
-        if (a.preact) a.preact[row * a.ldc + col] = f32_to_bf16(v);
-        v = apply_act(v, epi);
-        if (epi & EPI_RESIDUAL) v += bf16_to_f32(a.residual[row * a.ldr + col]);
-        if (a.out_f32)
-          static_cast<float*>(a.C)[row * a.ldc + col] = v;
-        else
-          static_cast<uint16_t*>(a.C)[row * a.ldc + col] = f32_to_bf16(v);
-      }
-    }
-  }
 }
 
 
@@ -214,9 +126,6 @@ __device__ __forceinline__ int section_row(int sec, int g) {
 // operands swapped (D = W_rows x X_rows^T, so each lane holds 4 consecutive columns of one
 // output row) the four n-tiles j of a wave then give every lane 16 CONSECUTIVE columns of one
 // row: the epilogue stores 2 x 16 B per lane and row block instead of 16 scattered 2-B stores.
-__device__ __forceinline__ int perm_brow(int x) {
-  return (x & ~63) | (((x >> 2) & 3) << 4) | (((x >> 4) & 3) << 2) | (x & 3);
-}
 
 template <bool PERM>
 __device__ __forceinline__ void stage_section(const uint16_t* __restrict__ X, int64_t ld,
@@ -379,17 +288,19 @@ __device__ __forceinline__ void deep_mainloop(const GemmArgs& a, f32x4 (&acc)[8]
 }
 
 // Epilogue of one 256^2 tile (global stores from registers; no LDS, no barriers).
-__device__ __forceinline__ void store_tile_256(const GemmArgs& a, const f32x4 (&acc)[8][4],
-                                               int64_t m0, int64_t n0, int wave, int lane) {
-  const int wr = wave >> 2, wc = wave & 3;
+// Epilogue of one wave's MI*16 x 64 output block at (row0, col0) — global stores from
+// registers (no LDS, no barriers). Requires the swapped-operand MFMA + perm_brow B staging.
+template <int MI>
+__device__ __forceinline__ void store_tile(const GemmArgs& a, const f32x4 (&acc)[MI][4],
+                                           int64_t row0, int64_t col0, int lane) {
   const int fr = lane & 15, fq = lane >> 4;
   // epilogue. Lane (fr, fq) holds output row rbase + i*16 + fr, columns cbase .. cbase+15
   // (acc[i][j][r] = column j*4 + r, see perm_brow).
   const int epi = a.epi;
-  const int64_t cbase = n0 + wc * 64 + fq * 16;
+  const int64_t cbase = col0 + fq * 16;
   const int cols_left = static_cast<int>(a.N - cbase < 16 ? a.N - cbase : 16);
   if (cols_left <= 0) return;
-  const int64_t rbase = m0 + wr * 128 + fr;
+  const int64_t rbase = row0 + fr;
   const int rows_left = static_cast<int>(a.M - rbase);     // rows i*16 < rows_left are valid
   const bool vec = a.vec_ok && cols_left == 16;
   float bias[16];
@@ -412,7 +323,7 @@ __device__ __forceinline__ void store_tile_256(const GemmArgs& a, const f32x4 (&
   uint16_t* pb = a.preact ? a.preact + rbase * a.ldc + cbase : nullptr;
   const uint16_t* rb = (epi & EPI_RESIDUAL) ? a.residual + rbase * a.ldr + cbase : nullptr;
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
+  for (int i = 0; i < MI; ++i) {
     if (i * 16 >= rows_left) break;
     float v[16];
 #pragma unroll
@@ -463,6 +374,84 @@ __device__ __forceinline__ void store_tile_256(const GemmArgs& a, const f32x4 (&
     }
   }
 }
+__device__ __forceinline__ void store_tile_256(const GemmArgs& a, const f32x4 (&acc)[8][4],
+                                               int64_t m0, int64_t n0, int wave, int lane) {
+  store_tile<8>(a, acc, m0 + (wave >> 2) * 128, n0 + (wave & 3) * 64, lane);
+}
+
+// 128 x 128 x 64 tile, 4 waves (2 x 2, 64 x 64 each), two LDS buffers, 2 workgroups per CU:
+// the small-grid path (fewer than ~192 256^2 tiles).
+__global__ void __launch_bounds__(kThreads, 2) gemm_bf16_nt_kernel(GemmArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+
+  // ---- workgroup -> tile: XCD-aware bijective remap, then GROUP_M swizzle
+  const int64_t tiles_m = (a.M + BM - 1) / BM, tiles_n = (a.N + BN - 1) / BN;
+  const int64_t nwg = tiles_m * tiles_n;
+  int64_t wid = blockIdx.x;
+  {
+    const int64_t q = nwg / 8, r = nwg % 8, x = wid % 8;
+    wid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + wid / 8;
+  }
+  const int64_t group_size = kGroupM * tiles_n;
+  const int64_t group = wid / group_size;
+  const int64_t first_m = group * kGroupM;
+  const int64_t gm = (tiles_m - first_m) < kGroupM ? (tiles_m - first_m) : kGroupM;
+  const int64_t tm = first_m + (wid % group_size) % gm;
+  const int64_t tn = (wid % group_size) / gm;
+  const int64_t m0 = tm * BM, n0 = tn * BN;
+
+  // buffer c: A at smem + c * 2 * kTileBytes, B right after it
+  auto bufA = [&](int c) { return smem + c * 2 * kTileBytes; };
+  auto bufB = [&](int c) { return smem + c * 2 * kTileBytes + kTileBytes; };
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int64_t nk = a.K / BK;
+  stage_tile<false>(a.A, a.lda, m0, a.M, 0, bufA(0), wave, lane);
+  stage_tile<true>(a.B, a.ldb, n0, a.N, 0, bufB(0), wave, lane);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  const int fr = lane & 15, fq = lane >> 4;
+  for (int64_t kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) {
+      stage_tile<false>(a.A, a.lda, m0, a.M, (kt + 1) * BK, bufA(cur ^ 1), wave, lane);
+      stage_tile<true>(a.B, a.ldb, n0, a.N, (kt + 1) * BK, bufB(cur ^ 1), wave, lane);
+    }
+    const char* la = bufA(cur);
+    const char* lb = bufB(cur);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 af[4], bfr[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[i] = read_frag(la, wm * 64 + i * 16 + fr, ks * 4 + fq);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bfr[j] = read_frag(lb, wn * 64 + j * 16 + fr, ks * 4 + fq);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+
+  // ---- epilogue: swapped operands + permuted B rows -> 16 consecutive columns per lane
+  store_tile<4>(a, acc, m0 + wm * 64, n0 + wn * 64, lane);
+}
+
 
 template <int MODE>   // 0 lock-step, 1 staggered, 2 staggered + whole next tile issued at phase 1,
                       // 3 staggered + deep (one K-tile in flight) restaging

@@ -17,7 +17,9 @@ from distributed_llm_backend_benchmark_amd.ops.gemm import set_stagger, set_tile
 SHAPES = [("sq4096", 4096, 4096, 4096), ("sq8192", 8192, 8192, 8192),
           ("7B_qkv_P1", 4096, 12288, 4096), ("7B_up_P1", 4096, 16384, 4096),
           ("7B_down_P1", 4096, 4096, 16384), ("gpt2_lmhead", 16384, 50304, 768),
-          ("gpt2_fc", 16384, 3072, 768)]
+          ("gpt2_fc", 16384, 3072, 768), ("7B_qkv_P8", 4096, 1536, 4096),
+          ("7B_up_P8", 4096, 2048, 4096), ("7B_down_P8", 4096, 4096, 2048),
+          ("1B_qkv_P8", 1024, 768, 2048)]
 
 
 def timed(fn, iters):
@@ -38,10 +40,11 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--shapes", default=None)
+    ap.add_argument("--tile", type=int, default=256, help="force the 128^2 or 256^2 kernel")
     args = ap.parse_args()
     modes = [int(m) for m in args.modes.split(",")]
     os.environ["DLBB_GEMM"] = "mfma"
-    set_tile(256)
+    set_tile(args.tile)
     shapes = [s for s in SHAPES if not args.shapes or s[0] in args.shapes.split(",")]
     for name, M, N, K in shapes:
         g = torch.Generator(device="cuda").manual_seed(0)
