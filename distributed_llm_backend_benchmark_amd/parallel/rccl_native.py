@@ -65,9 +65,11 @@ class NativeRCCL:
     def enqueue(self, op: str, send: torch.Tensor, recv: torch.Tensor, count: int,
                 root: int = 0, stream: Optional[int] = None) -> None:
         """Enqueue on ``stream`` (default: torch's current stream) without synchronising."""
+        # NB: torch's default stream has handle 0 (the null stream) — a valid target, passed
+        # through as is (the C side never reinterprets 0 as "engine stream")
         st = _lib.stream(send.device) if stream is None else stream
         rc = self.lib.dlbb_rccl_enqueue(self.h, OP_CODES[op], send.data_ptr(), recv.data_ptr(),
-                                        int(count), _lib.dt(send), int(root), st)
+                                        int(count), _lib.dt(send), int(root), st, 0)
         if rc != 0:
             raise RuntimeError(f"native RCCL {op} failed: rc={rc}")
 
