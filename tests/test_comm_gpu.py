@@ -66,6 +66,21 @@ def test_native_rccl_world1_sweep(tmp_path):
         assert len(ts) == 7 and all(0 < t < 0.1 for t in ts)
         mean = eng.time_batched("allreduce", x, x, x.numel(), iters=20, warmup=2)
         assert 0 < mean < 0.1
+        # stream ordering: an op enqueued from torch's DEFAULT stream (handle 0) must run on it —
+        # events around a 256 MiB single-rank copy see the copy (>= 512 MiB of HBM traffic)
+        from distributed_llm_backend_benchmark_amd.parallel.collectives import make_op
+
+        big = make_data((1 << 27,), torch.bfloat16, 0, comm.device)
+        op = make_op("sendrecv", comm, big, impl="native")
+        assert torch.cuda.current_stream().cuda_stream == 0
+        op.recv.zero_()
+        s0, e0 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s0.record()
+        op.run()
+        e0.record()
+        e0.synchronize()
+        assert s0.elapsed_time(e0) > 0.03, s0.elapsed_time(e0)      # ms
+        assert torch.equal(op.recv[-4096:], big[-4096:])
     finally:
         comm.destroy()
     files = sorted(os.listdir(tmp_path / "n1d"))
