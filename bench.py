@@ -69,7 +69,15 @@ def main(argv=None) -> int:
     from distributed_llm_backend_benchmark_amd.stats.bandwidth import algbw_gbps, busbw_gbps
 
     backend = "rccl" if torch.cuda.is_available() else "gloo"
-    comm = init_distributed(backend, timeout_s=900)
+    # DLBB_BENCH_BACKEND=gloo with GPUs visible: gloo process group over GPU tensors — lets
+    # several ranks share one GPU to rehearse the multi-rank path (IPC kernel, candidate
+    # agreement, native-engine refusal of duplicate GPUs); never used for reported numbers
+    override = os.environ.get("DLBB_BENCH_BACKEND")
+    if override:
+        comm = init_distributed(override, timeout_s=900,
+                                device="cuda" if torch.cuda.is_available() else None)
+    else:
+        comm = init_distributed(backend, timeout_s=900)
     P = comm.world_size
     if args.gpus != P and comm.rank == 0:
         print(f"note: --gpus {args.gpus} but world size is {P}; using {P}", file=sys.stderr)

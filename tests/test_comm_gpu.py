@@ -140,6 +140,23 @@ def test_bench_py_world1():
     assert rec["ms_per_step"] > 0
 
 
+def test_bench_py_two_ranks_rehearsal():
+    """bench.py's multi-rank path (candidate agreement, IPC kernel, native-engine refusal of a
+    shared GPU) with 2 ranks on one GPU over a gloo process group (DLBB_BENCH_BACKEND=gloo)."""
+    from conftest import free_port
+
+    env = dict(os.environ, DLBB_BENCH_BACKEND="gloo", HSA_ENABLE_IPC_MODE_LEGACY="0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
+           os.path.join(REPO, "bench.py"), "--gpus", "2", "--steps", "5", "--warmup", "2"]
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=REPO, env=env)
+    assert out.returncode == 0, out.stderr[-3000:]
+    rec = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][-1])
+    assert rec["n_gpus"] == 2 and rec["value"] > 0 and rec["vs_baseline"] is not None
+    assert rec["config"]["impl"] in ("custom", "rccl")
+    assert rec["p50_latency_us_512B"] > 0
+
+
 def test_tp_forward_world1_matches_torch():
     from distributed_llm_backend_benchmark_amd.models.tp_transformer import LLM
     from distributed_llm_backend_benchmark_amd.parallel.comm import init_distributed
