@@ -18,6 +18,7 @@
 #include <string.h>
 
 #include <new>
+#include <vector>
 
 #define DLBB_API extern "C" __attribute__((visibility("default")))
 
@@ -165,6 +166,32 @@ DLBB_API int dlbb_rccl_enqueue(void* h, int op, const void* send, void* recv, in
   Engine* e = static_cast<Engine*>(h);
   hipStream_t st = own_stream ? e->stream : static_cast<hipStream_t>(stream);
   const ncclResult_t r = enqueue_on(e, op, send, recv, static_cast<size_t>(count), dt, root, st);
+  return r == ncclSuccess ? 0 : 1000 + static_cast<int>(r);
+}
+
+// Uneven all-to-all (MoE token dispatch): counts / displacements in elements, one entry per
+// peer (host arrays of nranks size_t). Single rank: the self block is a stream-ordered copy.
+DLBB_API int dlbb_rccl_alltoallv(void* h, const void* send, const int64_t* sendcounts,
+                                 const int64_t* sdispls, void* recv, const int64_t* recvcounts,
+                                 const int64_t* rdispls, int dt, void* stream) {
+  Engine* e = static_cast<Engine*>(h);
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const size_t es = elem_size(dt);
+  if (e->nranks == 1) {
+    if (sendcounts[0] == 0) return 0;
+    return hipMemcpyAsync(static_cast<char*>(recv) + rdispls[0] * es,
+                          static_cast<const char*>(send) + sdispls[0] * es, sendcounts[0] * es,
+                          hipMemcpyDeviceToDevice, st) == hipSuccess ? 0 : 3;
+  }
+  std::vector<size_t> sc(e->nranks), sd(e->nranks), rc(e->nranks), rd(e->nranks);
+  for (int p = 0; p < e->nranks; ++p) {
+    sc[p] = static_cast<size_t>(sendcounts[p]);
+    sd[p] = static_cast<size_t>(sdispls[p]);
+    rc[p] = static_cast<size_t>(recvcounts[p]);
+    rd[p] = static_cast<size_t>(rdispls[p]);
+  }
+  const ncclResult_t r = ncclAllToAllv(send, sc.data(), sd.data(), recv, rc.data(), rd.data(),
+                                       to_nccl(dt), e->comm, st);
   return r == ncclSuccess ? 0 : 1000 + static_cast<int>(r);
 }
 

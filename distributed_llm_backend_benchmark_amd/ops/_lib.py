@@ -74,6 +74,8 @@ _SIGS = {
     "dlbb_rccl_run": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_int64, c_int, c_int]),
     "dlbb_rccl_enqueue": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_int64, c_int, c_int,
                                   c_void_p, c_int]),
+    "dlbb_rccl_alltoallv": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                    c_void_p, c_int, c_void_p]),
     "dlbb_rccl_time_iters": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_int64, c_int, c_int,
                                      c_int, c_int, ctypes.POINTER(ctypes.c_float)]),
     "dlbb_rccl_time_batched": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_int64, c_int,

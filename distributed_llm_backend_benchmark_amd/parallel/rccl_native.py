@@ -73,6 +73,30 @@ class NativeRCCL:
         if rc != 0:
             raise RuntimeError(f"native RCCL {op} failed: rc={rc}")
 
+    def alltoallv(self, send: torch.Tensor, send_splits, recv: torch.Tensor, recv_splits,
+                  stream: Optional[int] = None) -> None:
+        """Uneven all-to-all: ``send_splits[p]`` elements go to peer p, ``recv_splits[p]``
+        arrive from it (contiguous blocks in rank order), enqueued on ``stream``."""
+        P = self.comm.world_size
+
+        def arr(vals):
+            return (ctypes.c_int64 * P)(*[int(v) for v in vals])
+
+        def displs(splits):
+            out, acc = [], 0
+            for v in splits:
+                out.append(acc)
+                acc += int(v)
+            return out
+
+        st = _lib.stream(send.device) if stream is None else stream
+        rc = self.lib.dlbb_rccl_alltoallv(self.h, send.data_ptr(), arr(send_splits),
+                                          arr(displs(send_splits)), recv.data_ptr(),
+                                          arr(recv_splits), arr(displs(recv_splits)),
+                                          _lib.dt(send), st)
+        if rc != 0:
+            raise RuntimeError(f"native RCCL alltoallv failed: rc={rc}")
+
     def time_iters(self, op: str, send: torch.Tensor, recv: torch.Tensor, count: int,
                    iters: int, warmup: int, root: int = 0) -> List[float]:
         """Per-iteration device seconds, device barrier before each (C++ loop)."""
@@ -253,6 +277,19 @@ class NativeSendRecv(_Native, C.SendRecv):
         return self.flat, self.recv.view(-1), self.flat.numel(), 0
 
 
-NATIVE_OPS = {c.code: c for c in (NativeAllReduce, NativeAllGather, NativeReduceScatter,
+class NativeAllToAllMoE(_Native, C.AllToAllMoE):
+    """Uneven MoE-shaped all-to-all (``ncclAllToAllv``) with the registry op's split matrix."""
+
+    code = "alltoall_moe"
+
+    def setup(self):
+        C.AllToAllMoE.setup(self)
+        self.engine = self._engine()
+
+    def run(self):
+        self.engine.alltoallv(self.inp, self.in_splits, self.out, self.out_splits)
+
+
+NATIVE_OPS = {c.code: c for c in (NativeAllToAllMoE, NativeAllReduce, NativeAllGather, NativeReduceScatter,
                                   NativeBroadcast, NativeReduce, NativeGather, NativeScatter,
                                   NativeAllToAll, NativeSendRecv)}
