@@ -43,6 +43,9 @@ def parse_args(argv=None):
     ap.add_argument("--zero", action="store_true",
                     help="ZeRO-2-style: reduce-scatter grads, sharded AdamW, all-gather params")
     ap.add_argument("--compare-overlap", action="store_true")
+    ap.add_argument("--graph", action="store_true",
+                    help="capture the whole training step in a HIP graph after warmup and replay "
+                         "it (world 1, or --allreduce native|custom)")
     ap.add_argument("--save-checkpoint", default=None, metavar="DIR",
                     help="after the timed steps, write master weights + AdamW state (safetensors)")
     ap.add_argument("--resume-from", default=None, metavar="DIR",
@@ -80,13 +83,17 @@ def run(args, comm, overlap: bool):
     for _ in range(args.warmup):
         x, y = data.get_batch()
         tr.step(x, y, sync_loss=False)
+    step_fn = lambda x, y: tr.step(x, y, sync_loss=False)  # noqa: E731
+    if args.graph:
+        x, y = data.get_batch()
+        step_fn = tr.capture_step(x, y)
     comm.barrier()
     comm.sync()
     t0 = time.perf_counter()
     loss = None
     for _ in range(args.steps):
         x, y = data.get_batch()
-        loss = tr.step(x, y, sync_loss=False)
+        loss = step_fn(x, y)
     comm.sync()
     dt = comm.allreduce_max(time.perf_counter() - t0)
     res = {
@@ -95,6 +102,7 @@ def run(args, comm, overlap: bool):
         "loss": float(loss.item()) if loss is not None else None,
         "params": model.num_parameters(),
         "buckets": len(tr.buckets),
+        "hip_graph": bool(args.graph),
         "tflops_per_gpu": model.flops_per_token(args.seq) * args.batch * args.seq
         * args.steps / dt / 1e12,
     }

@@ -21,14 +21,21 @@ struct AdamArgs {
   float lr, beta1, beta2, eps, weight_decay;
   float bc1, bc2;     // 1 - beta^t
   float grad_scale;
+  const int* step_dev;   // optional: step count read on the device (HIP-graph replayable)
 };
 
 template <int GDT>
 __global__ void __launch_bounds__(256) adamw_kernel(AdamArgs a) {
   const int64_t nvec = a.n / 8;
   const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
-  const float step = a.lr / a.bc1;
-  const float inv_bc2 = 1.0f / a.bc2;
+  float bc1 = a.bc1, bc2 = a.bc2;
+  if (a.step_dev) {            // graph replay: the step advances in device memory
+    const float t = static_cast<float>(*a.step_dev);
+    bc1 = 1.f - powf(a.beta1, t);
+    bc2 = 1.f - powf(a.beta2, t);
+  }
+  const float step = a.lr / bc1;
+  const float inv_bc2 = 1.0f / bc2;
   auto body = [&](float& p, float& m, float& v, float g) {
     g *= a.grad_scale;
     m = a.beta1 * m + (1.f - a.beta1) * g;
@@ -66,15 +73,8 @@ __global__ void __launch_bounds__(256) adamw_kernel(AdamArgs a) {
 
 using namespace dlbb;
 
-DLBB_API int dlbb_adamw(float* p, float* m, float* v, const void* g, int grad_dtype,
-                        void* p_bf16, int64_t n, float lr, float beta1, float beta2, float eps,
-                        float weight_decay, int step, float grad_scale, hipStream_t stream) {
-  if (n <= 0) return hipSuccess;
-  if (step < 1) return hipErrorInvalidValue;
-  AdamArgs a{p, m, v, g, static_cast<uint16_t*>(p_bf16), n, lr, beta1, beta2, eps,
-             weight_decay, 1.f - powf(beta1, static_cast<float>(step)),
-             1.f - powf(beta2, static_cast<float>(step)), grad_scale};
-  const int grid = stream_grid((n + 7) / 8, 256);
+static int launch_adamw(const AdamArgs& a, int grad_dtype, hipStream_t stream) {
+  const int grid = stream_grid((a.n + 7) / 8, 256);
   if (grad_dtype == DT_BF16)
     hipLaunchKernelGGL(adamw_kernel<DT_BF16>, dim3(grid), dim3(256), 0, stream, a);
   else if (grad_dtype == DT_F32)
@@ -82,4 +82,28 @@ DLBB_API int dlbb_adamw(float* p, float* m, float* v, const void* g, int grad_dt
   else
     return hipErrorInvalidValue;
   return hipGetLastError();
+}
+
+DLBB_API int dlbb_adamw(float* p, float* m, float* v, const void* g, int grad_dtype,
+                        void* p_bf16, int64_t n, float lr, float beta1, float beta2, float eps,
+                        float weight_decay, int step, float grad_scale, hipStream_t stream) {
+  if (n <= 0) return hipSuccess;
+  if (step < 1) return hipErrorInvalidValue;
+  AdamArgs a{p, m, v, g, static_cast<uint16_t*>(p_bf16), n, lr, beta1, beta2, eps,
+             weight_decay, 1.f - powf(beta1, static_cast<float>(step)),
+             1.f - powf(beta2, static_cast<float>(step)), grad_scale, nullptr};
+  return launch_adamw(a, grad_dtype, stream);
+}
+
+// Same update with the step count (>= 1) read from device memory `step_dev` — the form a HIP
+// graph can replay (the caller advances the counter on the stream before each update).
+DLBB_API int dlbb_adamw_devstep(float* p, float* m, float* v, const void* g, int grad_dtype,
+                                void* p_bf16, int64_t n, float lr, float beta1, float beta2,
+                                float eps, float weight_decay, const int* step_dev,
+                                float grad_scale, hipStream_t stream) {
+  if (n <= 0) return hipSuccess;
+  if (!step_dev) return hipErrorInvalidValue;
+  AdamArgs a{p, m, v, g, static_cast<uint16_t*>(p_bf16), n, lr, beta1, beta2, eps,
+             weight_decay, 1.f, 1.f, grad_scale, step_dev};
+  return launch_adamw(a, grad_dtype, stream);
 }

@@ -58,6 +58,9 @@ _SIGS = {
     "dlbb_adamw": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int64,
                            c_float, c_float, c_float, c_float, c_float, c_int, c_float,
                            c_void_p]),
+    "dlbb_adamw_devstep": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p,
+                                   c_int64, c_float, c_float, c_float, c_float, c_float,
+                                   c_void_p, c_float, c_void_p]),
     "dlbb_xent_fwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int64,
                               c_void_p]),
     "dlbb_xent_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int64,

@@ -26,6 +26,14 @@ class FlatAdamW:
         self.v = torch.zeros_like(master)
         self.lr, self.betas, self.eps, self.wd = lr, betas, eps, weight_decay
         self.t = 0
+        self.t_dev: Optional[torch.Tensor] = None   # device step counter (HIP-graph mode)
+
+    def enable_device_step(self) -> None:
+        """Keep the step count in device memory: every update first advances it on the stream
+        and the kernel reads it — so a captured HIP graph replays with the right bias
+        correction. ``t`` stays a host mirror (advance it per replay)."""
+        if self.t_dev is None:
+            self.t_dev = torch.full((1,), self.t, dtype=torch.int32, device=self.p.device)
 
     @torch.no_grad()
     def step(self, grad: torch.Tensor, working_bf16: Optional[torch.Tensor] = None,
@@ -34,6 +42,14 @@ class FlatAdamW:
         b1, b2 = self.betas
         if grad.numel() != self.p.numel():
             raise ValueError("grad / master size mismatch")
+        if use_hip(self.p, grad) and self.t_dev is not None:
+            self.t_dev.add_(1)
+            check(_lib.lib().dlbb_adamw_devstep(
+                self.p.data_ptr(), self.m.data_ptr(), self.v.data_ptr(), grad.data_ptr(),
+                dt(grad), _lib.ptr(working_bf16), self.p.numel(), self.lr, b1, b2, self.eps,
+                self.wd, self.t_dev.data_ptr(), float(grad_scale), _lib.stream(self.p.device)),
+                "adamw_devstep")
+            return
         if use_hip(self.p, grad):
             check(_lib.lib().dlbb_adamw(
                 self.p.data_ptr(), self.m.data_ptr(), self.v.data_ptr(), grad.data_ptr(),

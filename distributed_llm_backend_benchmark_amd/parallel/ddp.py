@@ -223,6 +223,46 @@ class FlatParamTrainer:
             self._optimizer_step()
         return float(loss.item()) if sync_loss else loss.detach()
 
+    # ------------------------------------------------------------------ HIP graph
+    def capture_step(self, idx: torch.Tensor, targets: torch.Tensor):
+        """Capture one whole training step (forward, backward with its bucket reductions, AdamW)
+        into a HIP graph and return ``replay(idx, targets) -> loss`` (a device tensor).
+
+        Capturable when nothing in the step goes through ProcessGroupNCCL (its watchdog breaks
+        capture on this stack): world 1, or bucket reductions on the native RCCL engine /
+        the IPC kernel. The optimizer's step count moves to device memory. One eager step is run
+        first (a real training step) to settle lazily created state; GEMM choices are already
+        cached by earlier eager steps."""
+        if self.world > 1 and self._native is None and self._car is None:
+            raise RuntimeError("graph capture needs world 1 or allreduce='native'|'custom'")
+        self.opt.enable_device_step()
+        dev = self.flat_param.device
+        static_idx, static_tgt = idx.clone(), targets.clone()
+        cur = torch.cuda.current_stream(dev)
+        side = torch.cuda.Stream(dev)
+        side.wait_stream(cur)
+        with torch.cuda.stream(side):
+            self.step(static_idx, static_tgt, sync_loss=False)
+        cur.wait_stream(side)
+        torch.cuda.synchronize(dev)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph, capture_error_mode="thread_local"):
+            static_loss = self.step(static_idx, static_tgt, sync_loss=False)
+        # capture recorded the step without running it: undo the host-side bookkeeping
+        self.step_count -= 1
+        self.opt.t -= 1
+
+        def replay(x: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
+            static_idx.copy_(x)
+            static_tgt.copy_(y)
+            graph.replay()
+            self.step_count += 1
+            self.opt.t += 1
+            return static_loss
+
+        replay.graph = graph
+        return replay
+
     # ------------------------------------------------------------------ checkpoint / resume
     # The reference has no checkpointing (SURVEY §5.4). Here the optimizer state is three flat
     # fp32 buffers (+ the step counter), so a checkpoint is one safetensors file per state owner:
