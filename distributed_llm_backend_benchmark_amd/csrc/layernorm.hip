@@ -47,28 +47,48 @@ __device__ __forceinline__ void st4(uint16_t* p, int64_t i4, const float (&v)[4]
 }
 __device__ __forceinline__ float round_bf16(float f) { return bf16_to_f32(f32_to_bf16(f)); }
 
-// NV = number of 4-element vectors per lane; cols == NV * 256.
+template <int PDT>
+__device__ __forceinline__ void ldp4(const void* p, int c4, float (&v)[4]) {
+  if constexpr (PDT == DT_F32) {
+    const float4 t = reinterpret_cast<const float4*>(p)[c4];
+    v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
+  } else {
+    ld4(static_cast<const uint16_t*>(p), c4, v);
+  }
+}
+
+// NV = number of 4-element vectors per lane; cols == NV * 256. All loads of the row (x and r)
+// are issued before any store (restrict-qualified: a store to h_out cannot alias the next
+// loads, which had serialised the row into NV load round trips).
 template <int NV, int PDT>
 __global__ void __launch_bounds__(256) ln_fwd_kernel(LnFwdArgs a) {
   const int lane = threadIdx.x & 63;
   const int64_t row = static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6);
   if (row >= a.rows) return;
+  const uint16_t* __restrict__ xp = a.x;
+  const uint16_t* __restrict__ rp = a.r;
+  uint16_t* __restrict__ hp = a.h_out;
+  uint16_t* __restrict__ yp = a.y;
   const int64_t base4 = row * (a.cols / 4);
-  float v[NV][4];
+  float v[NV][4], rr[NV][4];
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    ld4(xp, base4 + i * 64 + lane, v[i]);
+    if (rp) ld4(rp, base4 + i * 64 + lane, rr[i]);
+  }
   float s = 0.f;
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
-    const int64_t c4 = i * 64 + lane;
-    ld4(a.x, base4 + c4, v[i]);
-    if (a.r) {
-      float rr[4];
-      ld4(a.r, base4 + c4, rr);
+    if (rp) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) v[i][j] = round_bf16(v[i][j] + rr[j]);
-      if (a.h_out) st4(a.h_out, base4 + c4, v[i]);
+      for (int j = 0; j < 4; ++j) v[i][j] = round_bf16(v[i][j] + rr[i][j]);
     }
 #pragma unroll
     for (int j = 0; j < 4; ++j) s += v[i][j];
+  }
+  if (rp && hp) {
+#pragma unroll
+    for (int i = 0; i < NV; ++i) st4(hp, base4 + i * 64 + lane, v[i]);
   }
   const float inv_c = 1.0f / static_cast<float>(a.cols);
   const float mean = wave_sum(s) * inv_c;
@@ -83,15 +103,12 @@ __global__ void __launch_bounds__(256) ln_fwd_kernel(LnFwdArgs a) {
   const float rstd = rsqrtf(wave_sum(ss) * inv_c + a.eps);
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
-    const int c = (i * 64 + lane) * 4;
-    float o[4];
+    float g[4], b[4] = {0.f, 0.f, 0.f, 0.f}, o[4];
+    ldp4<PDT>(a.gamma, i * 64 + lane, g);
+    if (a.beta) ldp4<PDT>(a.beta, i * 64 + lane, b);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const float g = ldp<PDT>(a.gamma, c + j);
-      const float b = a.beta ? ldp<PDT>(a.beta, c + j) : 0.f;
-      o[j] = (v[i][j] - mean) * rstd * g + b;
-    }
-    st4(a.y, base4 + i * 64 + lane, o);
+    for (int j = 0; j < 4; ++j) o[j] = (v[i][j] - mean) * rstd * g[j] + b[j];
+    st4(yp, base4 + i * 64 + lane, o);
   }
   if (lane == 0) {
     if (a.mean) a.mean[row] = mean;
@@ -167,6 +184,10 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(LnBwdArgs a) {
     for (int j = 0; j < 4; ++j) gam[i][j] = ldp<PDT>(a.gamma, (i * 64 + lane) * 4 + j);
   const float inv_c = 1.0f / static_cast<float>(a.cols);
   const int64_t nwaves = static_cast<int64_t>(gridDim.x) * 4;
+  const uint16_t* __restrict__ hp = a.h;
+  const uint16_t* __restrict__ dyp = a.dy;
+  const uint16_t* __restrict__ drp = a.dres;
+  uint16_t* __restrict__ dxp = a.dx;
   for (int64_t row = static_cast<int64_t>(blockIdx.x) * 4 + w; row < a.rows; row += nwaves) {
     const int64_t base4 = row * (a.cols / 4);
     const float mu = a.mean[row], rs = a.rstd[row];
@@ -175,8 +196,8 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(LnBwdArgs a) {
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
       float hv[4], dyv[4];
-      ld4(a.h, base4 + i * 64 + lane, hv);
-      ld4(a.dy, base4 + i * 64 + lane, dyv);
+      ld4(hp, base4 + i * 64 + lane, hv);
+      ld4(dyp, base4 + i * 64 + lane, dyv);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         xh[i][j] = (hv[j] - mu) * rs;
@@ -187,15 +208,23 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(LnBwdArgs a) {
         db[i][j] += dyv[j];
       }
     }
+    float dr[NV][4];
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {           // every load of the row before any store
+      if (drp) {
+        ld4(drp, base4 + i * 64 + lane, dr[i]);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) dr[i][j] = 0.f;
+      }
+    }
     const float c1 = wave_sum(s1) * inv_c, c2 = wave_sum(s2) * inv_c;
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
       float o[4];
-      float dr[4] = {0.f, 0.f, 0.f, 0.f};
-      if (a.dres) ld4(a.dres, base4 + i * 64 + lane, dr);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) o[j] = rs * (g[i][j] - xh[i][j] * c1 - c2) + dr[j];
-      st4(a.dx, base4 + i * 64 + lane, o);
+      for (int j = 0; j < 4; ++j) o[j] = rs * (g[i][j] - xh[i][j] * c1 - c2) + dr[i][j];
+      st4(dxp, base4 + i * 64 + lane, o);
     }
   }
   // cross-wave reduction of the dgamma/dbeta partials through LDS

@@ -106,3 +106,19 @@ if "mem" in which:
     tt = t_med(lambda: ref.step())
     out(kernel="adamw_flat_124M", hip_us=t * 1e6, hip_TBps=b / t / 1e12,
         torch_fused_adamw_us=tt * 1e6)
+if "ln" in which:
+    # GPT-2 small LayerNorm shapes: rows = B*T = 16384, cols = 768 (bf16 params, fused residual)
+    for rows, cols in ((16384, 768), (16384, 1024), (4096, 4096)):
+        a, r = rnd(rows, cols), rnd(rows, cols)
+        wv, bv = rnd(cols), rnd(cols)
+        t_res = t_med(lambda: ops.layernorm(a, wv, bv, residual=r), iters=50)
+        t_plain = t_med(lambda: ops.layernorm(a, wv, bv), iters=50)
+        ar = a.clone().requires_grad_(True)
+        wr, br = wv.clone().requires_grad_(True), bv.clone().requires_grad_(True)
+        y, _ = ops.layernorm(ar, wr, br)
+        dy = rnd(rows, cols)
+        t_bwd = t_med(lambda: torch.autograd.grad(y, [ar, wr, br], dy, retain_graph=True),
+                      iters=50)
+        out(kernel="layernorm", rows=rows, cols=cols, fwd_res_us=t_res * 1e6,
+            fwd_res_TBps=rows * cols * 2 * 4 / t_res / 1e12, fwd_us=t_plain * 1e6,
+            bwd_us=t_bwd * 1e6, bwd_TBps=rows * cols * 2 * 3 / t_bwd / 1e12)
