@@ -10,7 +10,11 @@
 //     ((m >> 3) & 1) << 2, which makes the 8 rows a 32-lane half reads hit 8 disjoint 32-B bank
 //     groups (conflict-free; a plain 256-B-row image is 8-way);
 //   * split-K over m: fp32 partials [split][N][K], then one reduce + bf16 cast kernel
-//     (deterministic; no float atomics).
+//     (deterministic; no float atomics);
+//   * optional fused bias gradient db[n] = sum_m dY[m][n]: the workgroups of output column
+//     block 0 also multiply their dY fragments by an all-ones B operand (two extra MFMAs per
+//     k-step per wave, the fragments are already in registers), partials [split][N] go through
+//     the same reduce kernel — replaces a separate column-sum pass over dY.
 // 128 x 128 output tile per workgroup, 4 waves in 2 x 2 (64 x 64 each = 4 x 4 MFMA 16x16x32),
 // BM = 32 rows of m per stage, two LDS buffers (32 KiB: three workgroups per CU).
 #include "common.h"
@@ -36,6 +40,7 @@ struct Args {
   int64_t lda, ldb;
   int M, N, K;
   int m_per_split;
+  int nsplit;          // fused db partials (BIAS) at ws + nsplit * N * K (tk == 0 blocks)
 };
 
 // Stage rows [m0, m0 + BM) x cols [c0, c0 + 128) of a row-major matrix into a swizzled image.
@@ -71,6 +76,9 @@ __device__ __forceinline__ bf16x8 frag(const char* img, int kbase, int colbase, 
   return f;
 }
 
+// BIAS: a separate instantiation (two extra accumulators + the ones operand: 112 -> 122 VGPRs,
+// still 4 waves/SIMD).
+template <bool BIAS>
 __global__ void __launch_bounds__(kThreads, 3) wgrad_kernel(Args a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = threadIdx.x & 63;
@@ -89,6 +97,12 @@ __global__ void __launch_bounds__(kThreads, 3) wgrad_kernel(Args a) {
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // bias: wave (wm, wn) of a column-block-0 workgroup sums fragments i = 2 wn, 2 wn + 1
+  const bool do_bias = BIAS && tk == 0;
+  f32x4 bacc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+  bf16x8 ones;
+#pragma unroll
+  for (int u = 0; u < 8; ++u) ones[u] = static_cast<short>(0x3F80);
 
   auto imgA = [&](int c) { return smem + c * 2 * kTile; };
   auto imgB = [&](int c) { return smem + c * 2 * kTile + kTile; };
@@ -121,6 +135,16 @@ __global__ void __launch_bounds__(kThreads, 3) wgrad_kernel(Args a) {
 #pragma unroll
         for (int j = 0; j < 4; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      if (do_bias) {   // wave-uniform branches on wn (a runtime index into af[] would
+                       // become v_cndmask chains over every fragment register)
+        if (wn == 0) {
+          bacc[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0], ones, bacc[0], 0, 0, 0);
+          bacc[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[1], ones, bacc[1], 0, 0, 0);
+        } else {
+          bacc[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[2], ones, bacc[0], 0, 0, 0);
+          bacc[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[3], ones, bacc[1], 0, 0, 0);
+        }
+      }
       __builtin_amdgcn_s_setprio(0);
     }
   }
@@ -137,32 +161,46 @@ __global__ void __launch_bounds__(kThreads, 3) wgrad_kernel(Args a) {
         const int k = k0 + wn * 64 + j * 16 + fr;
         w[static_cast<int64_t>(n) * a.K + k] = acc[i][j][r];
       }
+  if (do_bias && fr == 0) {   // every D column holds the same sum; lanes 0/16/32/48 write
+    float* wb = a.ws + static_cast<int64_t>(a.nsplit) * a.N * a.K +
+                static_cast<int64_t>(split) * a.N;
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) wb[n0 + wm * 64 + (2 * wn + h) * 16 + fq * 4 + r] = bacc[h][r];
+  }
 }
 
-// out[i] = sum_s ws[s][i] (+ out[i] if accumulate), bf16 or fp32 output; 8 elements / thread
+// out[i] = sum_s ws[s][i] (+ out[i] if accumulate), bf16 or fp32 output; 8 elements / thread.
+// Vectors past n / 8 reduce the bias partials ([split][nb] after the weight partials) into outb.
 template <int DTO>
 __global__ void __launch_bounds__(256) split_reduce_kernel(const float* __restrict__ ws,
                                                            void* __restrict__ out, int64_t n,
+                                                           void* __restrict__ outb, int64_t nb,
                                                            int split, int accumulate) {
-  const int64_t nv = n / 8;
+  const int64_t nv = n / 8, nvb = nb / 8;
   const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
-  for (int64_t v = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; v < nv;
+  for (int64_t v = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; v < nv + nvb;
        v += stride) {
+    const bool is_b = v >= nv;
+    const float* src = is_b ? ws + split * n : ws;
+    const int64_t ld = is_b ? nb : n, vi = is_b ? v - nv : v;
+    void* dst = is_b ? outb : out;
     float acc[8];
-    load8<DT_F32>(ws, v, acc);
+    load8<DT_F32>(src, vi, acc);
     for (int s = 1; s < split; ++s) {
       float t[8];
-      load8<DT_F32>(ws + static_cast<int64_t>(s) * n, v, t);
+      load8<DT_F32>(src + static_cast<int64_t>(s) * ld, vi, t);
 #pragma unroll
       for (int j = 0; j < 8; ++j) acc[j] += t[j];
     }
     if (accumulate) {
       float o[8];
-      load8<DTO>(out, v, o);
+      load8<DTO>(dst, vi, o);
 #pragma unroll
       for (int j = 0; j < 8; ++j) acc[j] += o[j];
     }
-    store8<DTO>(out, v, acc);
+    store8<DTO>(dst, vi, acc);
   }
 }
 
@@ -173,10 +211,11 @@ using namespace dlbb;
 
 // dW[N][K] = A^T B with A = [M][lda] (N columns used), B = [M][ldb] (K columns used), bf16.
 // Requires M % 32 == 0, N % 128 == 0, K % 128 == 0, lda/ldb % 8 == 0, 16-B aligned bases.
-// ws: fp32 workspace of split * N * K floats. out: bf16 (dt_out 1) or fp32 (0), dense [N][K].
+// ws: fp32 workspace of split * (N * K + N) floats. out: bf16 (dt_out 1) or fp32 (0), dense
+// [N][K]. out_bias (optional, same dtype as out, N elements): fused db = column sums of A.
 DLBB_API int dlbb_gemm_wgrad(const void* A, int64_t lda, const void* B, int64_t ldb, void* out,
                              int dt_out, int accumulate, float* ws, int M, int N, int K,
-                             int split, hipStream_t stream) {
+                             int split, void* out_bias, hipStream_t stream) {
   using namespace dlbb::tn;
   if (M <= 0 || N <= 0 || K <= 0) return hipSuccess;
   if (M % BM || N % BN || K % BKO || lda % 8 || ldb % 8 || split < 1) return hipErrorInvalidValue;
@@ -187,16 +226,20 @@ DLBB_API int dlbb_gemm_wgrad(const void* A, int64_t lda, const void* B, int64_t 
   if (per <= 0) per = BM;
   split = (M + per - 1) / per;
   Args a{static_cast<const uint16_t*>(A), static_cast<const uint16_t*>(B), ws, lda, ldb, M, N, K,
-         per};
+         per, split};
   const dim3 grid((N / BN) * (K / BKO), split);
-  hipLaunchKernelGGL(wgrad_kernel, grid, dim3(kThreads), 4 * kTile, stream, a);
+  if (out_bias)
+    hipLaunchKernelGGL(wgrad_kernel<true>, grid, dim3(kThreads), 4 * kTile, stream, a);
+  else
+    hipLaunchKernelGGL(wgrad_kernel<false>, grid, dim3(kThreads), 4 * kTile, stream, a);
   const int64_t n = static_cast<int64_t>(N) * K;
-  const int g = stream_grid(n / 8, 256);
+  const int64_t nb = out_bias ? N : 0;
+  const int g = stream_grid((n + nb) / 8, 256);
   if (dt_out == DT_BF16)
     hipLaunchKernelGGL(split_reduce_kernel<DT_BF16>, dim3(g), dim3(256), 0, stream, ws, out, n,
-                       split, accumulate);
+                       out_bias, nb, split, accumulate);
   else
     hipLaunchKernelGGL(split_reduce_kernel<DT_F32>, dim3(g), dim3(256), 0, stream, ws, out, n,
-                       split, accumulate);
+                       out_bias, nb, split, accumulate);
   return hipGetLastError();
 }

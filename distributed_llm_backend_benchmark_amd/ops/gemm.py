@@ -205,50 +205,58 @@ def wgrad_supported(dy2: torch.Tensor, x2: torch.Tensor) -> bool:
             and dy2.data_ptr() % 16 == 0 and x2.data_ptr() % 16 == 0)
 
 
-def _wgrad_hip(dy2, x2, out, accumulate, split=None):
+def _wgrad_hip(dy2, x2, out, accumulate, split=None, bias_out=None):
     M, N = dy2.shape
     K = x2.shape[1]
     tiles = (N // 128) * (K // 128)
     if split is None:
         split = max(1, min(M // 256, -(-512 // tiles)))
-    ws = torch.empty(split * N * K, dtype=torch.float32, device=dy2.device)
+    ws = torch.empty(split * (N * K + N), dtype=torch.float32, device=dy2.device)
     check(_lib.lib().dlbb_gemm_wgrad(dy2.data_ptr(), dy2.stride(0), x2.data_ptr(), x2.stride(0),
                                      out.data_ptr(), _lib.dt(out), int(accumulate), ws.data_ptr(),
-                                     M, N, K, split, _lib.stream(dy2.device)), "gemm_wgrad")
+                                     M, N, K, split, _lib.ptr(bias_out),
+                                     _lib.stream(dy2.device)), "gemm_wgrad")
 
 
-def _wgrad_blas(dy2, x2, out, accumulate, split=None):
+def _wgrad_blas(dy2, x2, out, accumulate, split=None, bias_out=None):
     if accumulate:
         out.add_(torch.matmul(dy2.t(), x2).to(out.dtype))
     elif out.dtype == dy2.dtype:
         torch.matmul(dy2.t(), x2, out=out)
     else:
         out.copy_(torch.matmul(dy2.t(), x2))
+    if bias_out is not None:
+        db = dy2.sum(0, dtype=torch.float32)
+        if accumulate:
+            bias_out.add_(db.to(bias_out.dtype))
+        else:
+            bias_out.copy_(db)
 
 
-WGRAD_CHOICES = {}    # (M, N, K, out dtype) -> "mfma" | "blas"
+WGRAD_CHOICES = {}    # (M, N, K, out dtype, fused bias) -> "mfma" | "blas"
 _WGRAD_IMPLS = {"mfma": _wgrad_hip, "blas": _wgrad_blas}
 
 
-def _wgrad_choice(dy2, x2, out) -> str:
+def _wgrad_choice(dy2, x2, out, bias_out=None) -> str:
     mode = os.environ.get("DLBB_GEMM", "auto").lower()
     if mode in _WGRAD_IMPLS:
         return mode
-    key = (dy2.shape[0], dy2.shape[1], x2.shape[1], out.dtype)
+    key = (dy2.shape[0], dy2.shape[1], x2.shape[1], out.dtype, bias_out is not None)
     if key in WGRAD_CHOICES:
         return WGRAD_CHOICES[key]
     if torch.cuda.is_current_stream_capturing():
         return "mfma"
     scratch = torch.empty_like(out)
+    scratch_b = torch.empty_like(bias_out) if bias_out is not None else None
     best, best_t = "mfma", float("inf")
     for name, fn in _WGRAD_IMPLS.items():
         for _ in range(2):
-            fn(dy2, x2, scratch, False)
+            fn(dy2, x2, scratch, False, None, scratch_b)
         ts = []
         for _ in range(5):
             s0, e0 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             s0.record()
-            fn(dy2, x2, scratch, False)
+            fn(dy2, x2, scratch, False, None, scratch_b)
             e0.record()
             e0.synchronize()
             ts.append(s0.elapsed_time(e0))
@@ -260,21 +268,26 @@ def _wgrad_choice(dy2, x2, out) -> str:
 
 
 def wgrad(dy2: torch.Tensor, x2: torch.Tensor, out: Optional[torch.Tensor] = None,
-          accumulate: bool = False, split: Optional[int] = None) -> torch.Tensor:
+          accumulate: bool = False, split: Optional[int] = None,
+          bias_out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Weight gradient ``dW = dy2^T @ x2`` ([N, K]) for row-major ``dy2 [M, N]``, ``x2 [M, K]``.
 
     HIP path (``csrc/gemm_tn.hip``): transposed-read MFMA tiles, split-K over M with fp32
-    partials and one reduce/cast pass; ``accumulate=True`` adds into ``out``. Per shape the
-    faster of this kernel and the library GEMM is measured once and cached
-    (:data:`WGRAD_CHOICES`; ``DLBB_GEMM=mfma|blas`` forces; an explicit ``split`` forces ours)."""
+    partials and one reduce/cast pass; ``accumulate=True`` adds into ``out``. ``bias_out``
+    ([N], same dtype as ``out``) also receives the bias gradient ``dy2.sum(0)`` — fused into
+    the same kernels on the HIP path. Per shape the faster of this kernel and the library GEMM
+    is measured once and cached (:data:`WGRAD_CHOICES`; ``DLBB_GEMM=mfma|blas`` forces; an
+    explicit ``split`` forces ours)."""
     M, N = dy2.shape
     K = x2.shape[1]
     if out is None:
         out = torch.empty(N, K, dtype=dy2.dtype, device=dy2.device)
-    if (use_hip(dy2, x2) and wgrad_supported(dy2, x2) and out.is_contiguous()
+    fused_ok = bias_out is None or (bias_out.is_contiguous() and bias_out.dtype == out.dtype
+                                    and bias_out.numel() == N)
+    if (use_hip(dy2, x2) and wgrad_supported(dy2, x2) and out.is_contiguous() and fused_ok
             and out.dtype in (torch.bfloat16, torch.float32)):
-        choice = "mfma" if split is not None else _wgrad_choice(dy2, x2, out)
-        _WGRAD_IMPLS[choice](dy2, x2, out, accumulate, split)
+        choice = "mfma" if split is not None else _wgrad_choice(dy2, x2, out, bias_out)
+        _WGRAD_IMPLS[choice](dy2, x2, out, accumulate, split, bias_out)
         return out
-    _wgrad_blas(dy2, x2, out, accumulate)
+    _wgrad_blas(dy2, x2, out, accumulate, None, bias_out)
     return out

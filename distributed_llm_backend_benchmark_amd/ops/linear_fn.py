@@ -5,7 +5,8 @@ with an activation the epilogue also stores the pre-activation ``u`` (needed by 
 backward). Backward: ``dU = dY * act'(u)`` and ``db = colsum(dU)`` in one pass of the bias-GELU
 backward kernel (``csrc/gelu.hip``); ``dX = dU @ W`` is a plain library GEMM (hipBLASLt through
 ``torch.matmul``, as allowed for unfused GEMMs); ``dW = dU^T @ X`` goes through
-:func:`.gemm.wgrad` (our split-K transposed-read MFMA kernel or the library, per-shape autotune).
+:func:`.gemm.wgrad` (our split-K transposed-read MFMA kernel or the library, per-shape autotune),
+which also produces ``db = colsum(dU)`` (an all-ones MFMA operand in the same kernel).
 """
 
 from __future__ import annotations
@@ -48,21 +49,31 @@ class _LinearFn(torch.autograd.Function):
         dy2 = dy.reshape(M, N)
         if not dy2.is_contiguous():
             dy2 = dy2.contiguous()
+        want_db = ctx.has_bias and ctx.needs_input_grad[2]
+        fuse_db = want_db and ctx.needs_input_grad[1]   # db rides on the wgrad kernels
         db = None
         if ctx.act is not None:
             du = torch.empty_like(u)
-            ws = torch.zeros(N, dtype=torch.float32, device=u.device) if ctx.has_bias else None
+            ws = (torch.zeros(N, dtype=torch.float32, device=u.device)
+                  if want_db and not fuse_db else None)
             check(_lib.lib().dlbb_bias_gelu_bwd(dy2.data_ptr(), u.data_ptr(), None, du.data_ptr(),
                                                 _lib.ptr(ws), M, N, _APPROX[ctx.act],
                                                 _lib.stream(u.device)), "bias_gelu_bwd")
-            if ctx.has_bias:
+            if ws is not None:
                 db = ws.to(w.dtype)
         else:
             du = dy2
-            if ctx.has_bias:
+            if want_db and not fuse_db:
                 db = du.sum(0, dtype=torch.float32).to(w.dtype)
         dx = torch.matmul(du, w) if ctx.needs_input_grad[0] else None
-        dw = wgrad(du, x2) if ctx.needs_input_grad[1] else None
+        dw = None
+        if ctx.needs_input_grad[1]:
+            dw = torch.empty(N, K, dtype=du.dtype, device=du.device)
+            if fuse_db:
+                db = torch.empty(N, dtype=du.dtype, device=du.device)
+            wgrad(du, x2, out=dw, bias_out=db)
+            if db is not None and db.dtype != w.dtype:
+                db = db.to(w.dtype)
         if dx is not None:
             dx = dx.view(*ctx.lead, K)
         return dx, dw, db, None

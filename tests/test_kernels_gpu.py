@@ -313,6 +313,15 @@ def test_wgrad_matches_fp32(M, N, K, split):
     torch.testing.assert_close(acc, ref + 1, rtol=2e-3, atol=2e-3 * (M ** 0.5))
     y = wgrad(dy, x, split=split)
     torch.testing.assert_close(y.float(), ref, rtol=2e-2, atol=2e-2 * (M ** 0.5))
+    # fused bias gradient (all-ones MFMA operand in the column-block-0 workgroups)
+    refb = dy.float().sum(0)
+    w32, b32 = torch.empty(N, K, device=DEV), torch.empty(N, device=DEV)
+    wgrad(dy, x, out=w32, split=split, bias_out=b32)
+    torch.testing.assert_close(w32, ref, rtol=2e-3, atol=2e-3 * (M ** 0.5))
+    torch.testing.assert_close(b32, refb, rtol=2e-3, atol=2e-3 * (M ** 0.5))
+    b32.fill_(1.0)
+    wgrad(dy, x, out=w32, accumulate=True, split=split, bias_out=b32)
+    torch.testing.assert_close(b32, refb + 1, rtol=2e-3, atol=2e-3 * (M ** 0.5))
 
 
 def test_wgrad_asymmetric():
@@ -327,3 +336,23 @@ def test_wgrad_asymmetric():
     out = torch.empty(N, K, dtype=torch.float32, device=DEV)
     wgrad(dy, x, out=out)
     torch.testing.assert_close(out, dy.float().t() @ x.float(), rtol=0, atol=0)
+
+
+def test_linear_train_frozen_weight_bias_grad():
+    """Weight frozen, bias trained: db cannot ride on the (skipped) wgrad kernels."""
+    from distributed_llm_backend_benchmark_amd.ops.linear_fn import linear_train
+
+    M, N, K = 256, 512, 256
+    x = _randn(M, K, seed=34, scale=0.5).requires_grad_(True)
+    w = _randn(N, K, seed=35, scale=0.1)
+    for act in (None, "gelu_tanh"):
+        b = _randn(N, seed=36).requires_grad_(True)
+        dy = _randn(M, N, seed=37)
+        y = linear_train(x, w, b, act=act)
+        (y.float() * dy.float()).sum().backward()
+        bf = b.detach().float().requires_grad_(True)
+        yf = x.detach().float() @ w.float().t() + bf
+        if act:
+            yf = F.gelu(yf, approximate="tanh")
+        (yf * dy.float()).sum().backward()
+        torch.testing.assert_close(b.grad.float(), bf.grad, rtol=3e-2, atol=0.5)

@@ -122,3 +122,27 @@ if "ln" in which:
         out(kernel="layernorm", rows=rows, cols=cols, fwd_res_us=t_res * 1e6,
             fwd_res_TBps=rows * cols * 2 * 4 / t_res / 1e12, fwd_us=t_plain * 1e6,
             bwd_us=t_bwd * 1e6, bwd_TBps=rows * cols * 2 * 3 / t_bwd / 1e12)
+if "wgrad" in which:
+    from distributed_llm_backend_benchmark_amd.ops.gemm import wgrad
+    for N, K in ((2304, 768), (768, 768), (3072, 768), (768, 3072)):
+        M = 16384
+        dy, x = rnd(M, N), rnd(M, K)
+        w_out, b_out = torch.empty(N, K, device="cuda", dtype=torch.bfloat16), \
+            torch.empty(N, device="cuda", dtype=torch.bfloat16)
+        t_w = t_med(lambda: wgrad(dy, x, out=w_out), iters=30)
+        t_wb = t_med(lambda: wgrad(dy, x, out=w_out, bias_out=b_out), iters=30)
+        t_sum = t_med(lambda: dy.sum(0, dtype=torch.float32).to(torch.bfloat16), iters=30)
+        out(kernel="wgrad", M=M, N=N, K=K, wgrad_us=t_w * 1e6, wgrad_fused_bias_us=t_wb * 1e6,
+            torch_colsum_us=t_sum * 1e6, tflops=2 * M * N * K / t_w / 1e12)
+if "gelu" in which:
+    a, bb, g = rnd(16384, 3072), rnd(3072), rnd(16384, 3072)
+    from distributed_llm_backend_benchmark_amd.ops import _lib as L
+    du = torch.empty_like(a)
+    ws = torch.zeros(3072, dtype=torch.float32, device="cuda")
+    t_f = t_med(lambda: ops.bias_gelu(a, bb, "tanh"), iters=30)
+    t_b = t_med(lambda: L.lib().dlbb_bias_gelu_bwd(g.data_ptr(), a.data_ptr(), None, du.data_ptr(),
+                                                   None, 16384, 3072, 1, L.stream(a.device)), iters=30)
+    t_bd = t_med(lambda: L.lib().dlbb_bias_gelu_bwd(g.data_ptr(), a.data_ptr(), None, du.data_ptr(),
+                                                    ws.data_ptr(), 16384, 3072, 1, L.stream(a.device)), iters=30)
+    out(kernel="bias_gelu_tanh", fwd_us=t_f * 1e6, fwd_TBps=a.numel() * 4 / t_f / 1e12,
+        bwd_us=t_b * 1e6, bwd_db_us=t_bd * 1e6, bwd_TBps=a.numel() * 6 / t_b / 1e12)
