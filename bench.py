@@ -84,35 +84,44 @@ def main(argv=None) -> int:
 
     B, S, H = (int(x) for x in args.shape.split(","))
     data = make_data((B, S, H), torch.bfloat16, comm.rank, comm.device)
-    cands = [args.impl] if args.impl in ("rccl", "native") else []
-    if args.impl == "best":
-        cands = ["rccl", "native"] if comm.is_gpu else ["rccl"]
+    # candidates: (label, impl, opts); every rank builds the same list (the custom kernel's
+    # health flags are agreed collectively), so trial construction stays collective-safe
+    cands = []
+    if args.impl in ("best", "rccl"):
+        cands.append(("rccl", "rccl", {}))
+    if args.impl in ("best", "native") and comm.is_gpu:
+        cands.append(("native", "native", {}))
     if args.impl in ("best", "custom") and P > 1 and comm.is_gpu:
         from distributed_llm_backend_benchmark_amd.parallel.custom_allreduce import (
             get_custom_allreduce)
 
         car = get_custom_allreduce(comm)
-        if car is not None and car.healthy and car.supports(data.reshape(-1)):
-            cands.append("custom")
-        elif args.impl == "custom":
+        flat = data.reshape(-1)
+        if car is not None and car.healthy and car.supports(flat):
+            cands += [("custom", "custom", {}), ("custom/nb256", "custom", {"nblocks": 256})]
+        if car is not None and car.reg_healthy and car.supports_registered(flat):
+            # in place on an IPC-registered buffer: no copy-in / staging pass
+            cands += [(f"custom_reg/nb{nb}", "custom_reg", {"nblocks": nb})
+                      for nb in (64, 128, 256)]
+        if args.impl == "custom" and not cands:
             raise SystemExit("custom all-reduce unavailable (setup or self-test failed)")
     trial = {}
-    op = None
-    for impl in cands:
+    op, op_label = None, None
+    for label, impl, opts in cands:
         try:
-            cand = make_op("allreduce", comm, data, impl=impl)
-        except RuntimeError as e:      # e.g. native engine init failed on some rank
+            cand = make_op("allreduce", comm, data, impl=impl, **opts)
+        except RuntimeError as e:      # e.g. native engine init failed (agreed on all ranks)
             if args.impl != "best":
                 raise
             if comm.rank == 0:
-                print(f"note: {impl} all-reduce unavailable: {e}", file=sys.stderr)
+                print(f"note: {label} all-reduce unavailable: {e}", file=sys.stderr)
             continue
         for _ in range(max(1, args.warmup)):
             cand.run()
         comm.sync()
-        trial[impl] = _timed_steps(comm, cand, 10) / 10 if len(cands) > 1 else 0.0
-        if op is None or trial[impl] < trial[op.impl]:
-            op = cand
+        trial[label] = _timed_steps(comm, cand, 10) / 10 if len(cands) > 1 else 0.0
+        if op is None or trial[label] < trial[op_label]:
+            op, op_label = cand, label
     nbytes = op.message_bytes
     for _ in range(args.warmup):
         op.run()
@@ -185,7 +194,7 @@ def main(argv=None) -> int:
                 "hidden": H,
                 "message_bytes_per_rank": nbytes,
                 "parallelism": f"{'rccl' if comm.backend == 'nccl' else comm.backend}_world{P}",
-                "impl": op.impl,
+                "impl": op_label,
                 "impl_trial_ms": {k: v * 1e3 for k, v in trial.items()} if len(trial) > 1 else None,
             },
             "algbw_GBps": alg,

@@ -15,6 +15,14 @@
 //   two-shot : copy sub-range b of every shard -> buffer[e&1] ; signal/wait phase 0 ;
 //              reduce sub-range b of MY shard from all peers -> my tmp[e&1] and out ;
 //              signal/wait phase 1 ; gather sub-range b of every peer shard from peer tmp -> out
+//   two-shot, registered (in place on a user buffer every rank IPC-mapped once with
+//   dlbb_car_reg_open — no copy-in, no tmp): signal/wait phase 0 (inputs ready) ; reduce
+//              sub-range b of MY shard from every rank's buffer into my buffer ; signal/wait
+//              phase 1 ; gather sub-range b of every peer shard from its owner's buffer ;
+//              signal/wait phase 2 (no peer still reads my buffer when my stream moves on)
+// Epochs: every call advances the epoch of ALL kMaxBlocks workgroup slots by one (block 0 also
+// bumps the slots beyond this call's grid), so the epoch - and with it the buffer half - is the
+// same in every workgroup of a call even when consecutive calls use different grid sizes.
 // Double buffering by epoch parity + the ">= e" wait makes one barrier per phase sufficient:
 // a rank reaches epoch e+2 (and overwrites buffer[e&1]) only after every peer signalled e+1,
 // i.e. finished reading epoch e.
@@ -30,17 +38,18 @@
 #include <string.h>
 
 #include <new>
+#include <vector>
 
 namespace dlbb {
 
 constexpr int kMaxRanks = 8;
-constexpr int kMaxBlocks = 128;
+constexpr int kMaxBlocks = 256;
 constexpr int kCarThreads = 512;
 constexpr unsigned kSpinLimit = 1u << 26;   // ~ seconds of polling, then give up
 constexpr uint32_t kMagic = 0xD1BB0000u;
 
 struct Signal {
-  uint32_t flags[2][kMaxBlocks][kMaxRanks];   // written by peers (remote stores)
+  uint32_t flags[3][kMaxBlocks][kMaxRanks];   // written by peers (remote stores)
   uint32_t epoch[kMaxBlocks];                 // local per-workgroup call counter
   uint32_t error;                             // nonzero: a wait timed out
   uint32_t pad[3];
@@ -92,6 +101,20 @@ __device__ __forceinline__ bool wait_peers(const CarKernelArgs& a, int phase, ui
   return timed_out == 0;
 }
 
+// Advance this call's epoch (see header): each workgroup bumps its own slot, block 0 also the
+// slots no workgroup of this grid owns. Returns the epoch of the calling workgroup.
+__device__ __forceinline__ uint32_t begin_epoch(const CarKernelArgs& a) {
+  __shared__ uint32_t s_epoch;
+  Signal* s = a.sig[a.rank];
+  if (threadIdx.x == 0) s_epoch = ++s->epoch[blockIdx.x];
+  if (blockIdx.x == 0)
+    for (unsigned b = gridDim.x + threadIdx.x; b < static_cast<unsigned>(kMaxBlocks);
+         b += blockDim.x)
+      ++s->epoch[b];
+  __syncthreads();
+  return s_epoch;
+}
+
 // W = world size as a compile-time constant (2, 4, 8: every peer load issued before the adds,
 // fully unrolled) or 0 (runtime world). Peer pointers come straight from the kernel-argument
 // block with wave-uniform indices (scalar loads), never from a runtime-indexed local array.
@@ -126,10 +149,7 @@ __device__ __forceinline__ void sum_vec(const CarKernelArgs& a, int64_t half, in
 template <int DT, int W>
 __global__ void __launch_bounds__(kCarThreads) car_oneshot_kernel(CarKernelArgs a) {
   constexpr int64_t kVecBytes = 8 * Elem<DT>::kBytes;
-  __shared__ uint32_t s_epoch;
-  if (threadIdx.x == 0) s_epoch = ++a.sig[a.rank]->epoch[blockIdx.x];
-  __syncthreads();
-  const uint32_t e = s_epoch;
+  const uint32_t e = begin_epoch(a);
   const int64_t half = (e & 1) * a.cap;
   const int64_t nvec = a.nbytes / kVecBytes;
   const int64_t per = (nvec + gridDim.x - 1) / gridDim.x;
@@ -154,10 +174,7 @@ __global__ void __launch_bounds__(kCarThreads) car_oneshot_kernel(CarKernelArgs 
 template <int DT, int W>
 __global__ void __launch_bounds__(kCarThreads) car_twoshot_kernel(CarKernelArgs a) {
   constexpr int64_t kVecBytes = 8 * Elem<DT>::kBytes;
-  __shared__ uint32_t s_epoch;
-  if (threadIdx.x == 0) s_epoch = ++a.sig[a.rank]->epoch[blockIdx.x];
-  __syncthreads();
-  const uint32_t e = s_epoch;
+  const uint32_t e = begin_epoch(a);
   const int64_t half = (e & 1) * a.cap;
   const int64_t shard_vec = a.nbytes / kVecBytes / a.world;      // vectors per shard
   const int64_t per = (shard_vec + gridDim.x - 1) / gridDim.x;
@@ -245,6 +262,77 @@ __global__ void __launch_bounds__(kCarThreads) car_twoshot_kernel(CarKernelArgs 
   }
 }
 
+// Registered two-shot, in place (see header). a.data[p] = rank p's registered buffer (no halves).
+// Disjointness: in phase 1 a rank writes only shard `rank` of its own buffer, which peers do not
+// read in phase 1 (peer q reads shard q); in phase 2 it writes shards p != rank of its own buffer,
+// and peers only read shard `rank` of it. Workgroup b of every rank owns sub-range b of every
+// shard, so the per-workgroup flags order exactly the producer/consumer pairs.
+template <int DT, int W>
+__global__ void __launch_bounds__(kCarThreads) car_twoshot_reg_kernel(CarKernelArgs a) {
+  constexpr int64_t kVecBytes = 8 * Elem<DT>::kBytes;
+  constexpr int kQ = kVecBytes / 16;
+  const uint32_t e = begin_epoch(a);
+  const int64_t shard_vec = a.nbytes / kVecBytes / a.world;
+  const int64_t per = (shard_vec + gridDim.x - 1) / gridDim.x;
+  const int64_t s0 = blockIdx.x * per;
+  const int64_t s1 = s0 + per < shard_vec ? s0 + per : shard_vec;
+  char* mine = a.data[a.rank];
+  signal_peers(a, 0, e);                       // my input is complete (stream order)
+  if (!wait_peers(a, 0, e)) return;
+  const int64_t mybase = a.rank * shard_vec;
+  for (int64_t v = s0 + threadIdx.x; v < s1; v += blockDim.x) {
+    float acc[8];
+    sum_vec<DT, W>(a, 0, (mybase + v) * kVecBytes, acc);
+    store8<DT>(mine, mybase + v, acc);
+  }
+  signal_peers(a, 1, e);
+  if (!wait_peers(a, 1, e)) return;
+  if constexpr (W > 0) {
+    for (int64_t v = s0 + threadIdx.x; v < s1; v += blockDim.x) {
+      u16x8 t[W - 1][kQ];
+#pragma unroll
+      for (int k = 1; k < W; ++k) {
+        const int p = (a.rank + k) & (W - 1);
+#pragma unroll
+        for (int q = 0; q < kQ; ++q)
+          t[k - 1][q] = reinterpret_cast<const u16x8*>(a.data[p] +
+                                                       (p * shard_vec + v) * kVecBytes)[q];
+      }
+#pragma unroll
+      for (int k = 1; k < W; ++k) {
+        const int p = (a.rank + k) & (W - 1);
+#pragma unroll
+        for (int q = 0; q < kQ; ++q)
+          reinterpret_cast<u16x8*>(mine + (p * shard_vec + v) * kVecBytes)[q] = t[k - 1][q];
+      }
+    }
+  } else {
+    for (int k = 1; k < a.world; ++k) {
+      const int p = (a.rank + k) % a.world;
+      for (int64_t v = s0 + threadIdx.x; v < s1; v += blockDim.x) {
+        const int64_t off = (p * shard_vec + v) * kVecBytes;
+#pragma unroll
+        for (int q = 0; q < kQ; ++q)
+          reinterpret_cast<u16x8*>(mine + off)[q] =
+              reinterpret_cast<const u16x8*>(a.data[p] + off)[q];
+      }
+    }
+  }
+  signal_peers(a, 2, e);                       // done reading every peer's buffer
+  wait_peers(a, 2, e);
+}
+
+struct RegBuf {
+  char* ptr[kMaxRanks] = {};    // every rank's registered buffer (mine at [rank])
+  int64_t bytes = 0;
+};
+
+struct OpenedMap {               // one hipIpcOpenMemHandle per (peer, allocation)
+  int peer;
+  hipIpcMemHandle_t handle;
+  char* base;
+};
+
 struct CarState {
   int rank = 0, world = 1, device = 0;
   int64_t cap = 0;
@@ -256,6 +344,8 @@ struct CarState {
   char* peer_data[kMaxRanks] = {};
   char* peer_tmp[kMaxRanks] = {};
   Signal* peer_sig[kMaxRanks] = {};
+  std::vector<RegBuf> regs;
+  std::vector<OpenedMap> opened_maps;
 };
 
 }  // namespace dlbb
@@ -414,6 +504,92 @@ DLBB_API int dlbb_car_allreduce(void* h, const void* inp, void* out, int64_t n, 
   return hipGetLastError();
 }
 
+// ---- registered buffers -----------------------------------------------------------------------
+// Export the IPC handle of the allocation that contains `ptr` (e.g. a torch caching-allocator
+// segment) and ptr's offset in it.
+DLBB_API int dlbb_car_reg_export(void* h, const void* ptr, void* out_handle, int64_t* out_offset) {
+  (void)h;
+  void* base = nullptr;
+  size_t size = 0;
+  CAR_CHECK(hipMemGetAddressRange(&base, &size, const_cast<void*>(ptr)));
+  hipIpcMemHandle_t hd;
+  CAR_CHECK(hipIpcGetMemHandle(&hd, base));
+  memcpy(out_handle, &hd, 64);
+  *out_offset = static_cast<const char*>(ptr) - static_cast<char*>(base);
+  return hipSuccess;
+}
+
+// Map every peer's exported buffer (all_handles: world x 64 bytes, offsets: world) and record
+// the registration; *out_id indexes it for dlbb_car_allreduce_reg. A peer allocation already
+// mapped by an earlier registration is reused (one open per allocation and peer).
+DLBB_API int dlbb_car_reg_open(void* h, const void* ptr, int64_t nbytes, const void* all_handles,
+                               const int64_t* offsets, int* out_id) {
+  CarState* s = static_cast<CarState*>(h);
+  if (!s->opened) return hipErrorNotInitialized;
+  RegBuf r;
+  r.bytes = nbytes;
+  const char* hs = static_cast<const char*>(all_handles);
+  for (int p = 0; p < s->world; ++p) {
+    if (p == s->rank) {
+      r.ptr[p] = static_cast<char*>(const_cast<void*>(ptr));
+      continue;
+    }
+    hipIpcMemHandle_t hd;
+    memcpy(&hd, hs + p * 64, 64);
+    char* base = nullptr;
+    for (const OpenedMap& m : s->opened_maps)
+      if (m.peer == p && memcmp(&m.handle, &hd, sizeof(hd)) == 0) base = m.base;
+    if (!base) {
+      void* pd = nullptr;
+      CAR_CHECK(hipIpcOpenMemHandle(&pd, hd, hipIpcMemLazyEnablePeerAccess));
+      base = static_cast<char*>(pd);
+      s->opened_maps.push_back(OpenedMap{p, hd, base});
+    }
+    r.ptr[p] = base + offsets[p];
+    // copy-engine read of the first and last byte: a bad mapping fails here, not in a kernel
+    char probe[2];
+    CAR_CHECK(hipMemcpy(&probe[0], r.ptr[p], 1, hipMemcpyDeviceToHost));
+    CAR_CHECK(hipMemcpy(&probe[1], r.ptr[p] + nbytes - 1, 1, hipMemcpyDeviceToHost));
+  }
+  s->regs.push_back(r);
+  *out_id = static_cast<int>(s->regs.size()) - 1;
+  return hipSuccess;
+}
+
+// In-place all-reduce of registration `id` (n elements from its start; n * esize must be a
+// multiple of 16 * world and at most the registered size).
+DLBB_API int dlbb_car_allreduce_reg(void* h, int id, int64_t n, int dtype, int nblocks,
+                                    hipStream_t stream) {
+  CarState* s = static_cast<CarState*>(h);
+  if (!s->opened || id < 0 || id >= static_cast<int>(s->regs.size())) return hipErrorInvalidValue;
+  const RegBuf& r = s->regs[id];
+  const int64_t esz = dtype == DT_F32 ? 4 : 2;
+  const int64_t nbytes = n * esz;
+  if (nbytes <= 0) return hipSuccess;
+  if (nbytes > r.bytes || nbytes % (8 * esz * s->world) != 0) return hipErrorInvalidValue;
+  if (s->world == 1) return hipSuccess;
+  if (nblocks < 1) nblocks = 1;
+  if (nblocks > kMaxBlocks) nblocks = kMaxBlocks;
+  CarKernelArgs a = s->args;
+  for (int p = 0; p < kMaxRanks; ++p) a.data[p] = r.ptr[p];
+  a.inp = r.ptr[s->rank];
+  a.out = r.ptr[s->rank];
+  a.nbytes = nbytes;
+  const dim3 g(nblocks), b(kCarThreads);
+#define CAR_RW(D)                                                                            \
+  do {                                                                                       \
+    if (s->world == 2) hipLaunchKernelGGL((car_twoshot_reg_kernel<D, 2>), g, b, 0, stream, a); \
+    else if (s->world == 4) hipLaunchKernelGGL((car_twoshot_reg_kernel<D, 4>), g, b, 0, stream, a); \
+    else if (s->world == 8) hipLaunchKernelGGL((car_twoshot_reg_kernel<D, 8>), g, b, 0, stream, a); \
+    else hipLaunchKernelGGL((car_twoshot_reg_kernel<D, 0>), g, b, 0, stream, a);            \
+  } while (0)
+  if (dtype == DT_BF16) CAR_RW(DT_BF16);
+  else if (dtype == DT_F16) CAR_RW(DT_F16);
+  else CAR_RW(DT_F32);
+#undef CAR_RW
+  return hipGetLastError();
+}
+
 // Reads (and clears) the device-side timeout flag. Synchronous: call outside timed regions.
 DLBB_API int dlbb_car_error(void* h) {
   CarState* s = static_cast<CarState*>(h);
@@ -436,6 +612,7 @@ DLBB_API int dlbb_car_destroy(void* h) {
     if (s->peer_tmp[p]) (void)hipIpcCloseMemHandle(s->peer_tmp[p]);
     if (s->peer_sig[p]) (void)hipIpcCloseMemHandle(s->peer_sig[p]);
   }
+  for (const OpenedMap& m : s->opened_maps) (void)hipIpcCloseMemHandle(m.base);
   (void)hipFree(s->data);
   (void)hipFree(s->tmp);
   (void)hipFree(s->sig);

@@ -107,11 +107,22 @@ class AllReduce(CollectiveOp):
         self.buf = self.data.clone()
         impl = self.opts.get("impl", "rccl")
         self._custom = None
-        if impl in ("custom", "auto") and self.comm.is_gpu and self.comm.world_size > 1:
+        self._reg_id = None
+        self.nblocks = self.opts.get("nblocks")
+        multi_gpu = self.comm.is_gpu and self.comm.world_size > 1
+        if impl in ("custom", "custom_reg", "auto") and multi_gpu:
             from .custom_allreduce import get_custom_allreduce
 
             car = get_custom_allreduce(self.comm)
-            if impl == "custom":
+            if impl == "custom_reg":
+                # in place on self.buf, IPC-mapped once on every rank (collective; raises on
+                # every rank alike)
+                if car is None or not car.reg_healthy or not car.supports_registered(self.buf):
+                    raise RuntimeError("registered custom all-reduce unavailable for "
+                                       f"{self.buf.numel()} x {self.buf.dtype}")
+                self._reg_id = car.register(self.buf)
+                self._custom = car
+            elif impl == "custom":
                 if car is None or not car.healthy:
                     raise RuntimeError("custom all-reduce unavailable or failed its self-test")
                 if not car.supports(self.buf):
@@ -121,14 +132,17 @@ class AllReduce(CollectiveOp):
             elif car is not None and car.should_use(self.buf):
                 self._custom = car
         self.algo = self.opts.get("algo")
-        self.impl = "custom" if self._custom is not None else "rccl"
+        self.impl = ("custom_reg" if self._reg_id is not None
+                     else "custom" if self._custom is not None else "rccl")
 
     def reset(self):
         self.buf.copy_(self.data)
 
     def run(self):
-        if self._custom is not None:
-            self._custom.all_reduce_(self.buf, algo=self.algo)
+        if self._reg_id is not None:
+            self._custom.all_reduce_registered(self.buf, self._reg_id, nblocks=self.nblocks)
+        elif self._custom is not None:
+            self._custom.all_reduce_(self.buf, algo=self.algo, nblocks=self.nblocks)
         else:
             dist.all_reduce(self.buf, op=dist.ReduceOp.SUM)
 

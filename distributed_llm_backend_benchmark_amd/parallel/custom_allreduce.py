@@ -5,6 +5,9 @@ The oneCCL algorithm sweep of the reference (``CCL_ALLREDUCE`` ∈ direct/ring/2
 node: RCCL (ring/tree, default), ``oneshot`` (every rank reads all peers' full buffers over its
 7 dedicated xGMI links — the "direct" analogue, lowest latency) and ``twoshot`` (direct
 reduce-scatter + direct all-gather — the "2d"/rabenseifner analogue, all links busy).
+``register(t)`` IPC-maps a user tensor on every rank once; ``all_reduce_registered`` then runs
+the two-shot in place on it (no copy-in, no staging buffer: the bandwidth path for large,
+long-lived buffers such as gradient buckets or a benchmark's message).
 
 Setup: each rank allocates its IPC regions, the 192-byte handles and device ordinals are
 exchanged once through the process group (``all_gather_object``), peers are opened with
@@ -70,6 +73,9 @@ class CustomAllReduce:
         self.auto_max = auto_max_bytes
         self.nblocks = nblocks
         self.healthy = False
+        self.reg_healthy = False
+        self._regs: Dict[tuple, int] = {}
+        self._reg_keep = []
 
     # ------------------------------------------------------------------ policy
     def supports(self, t: torch.Tensor) -> bool:
@@ -91,13 +97,62 @@ class CustomAllReduce:
     def blocks_for(self, nbytes: int, algo: int) -> int:
         if self.nblocks:
             return self.nblocks
-        # ~64 KiB of message per workgroup, 1..128 workgroups
+        # ~64 KiB of message per workgroup, 1..128 workgroups (256 via nblocks=)
         per = max(1, nbytes // (64 << 10))
         return int(min(128, max(1, per if algo == TWOSHOT else min(per, 32))))
 
+    # ------------------------------------------------------------------ registration
+    def register(self, t: torch.Tensor) -> int:
+        """Collective: IPC-map tensor ``t`` of every rank (same numel / dtype everywhere) for
+        :meth:`all_reduce_registered`. Every local failure is agreed on by all ranks (then
+        every rank raises). Registered tensors are kept alive by this object."""
+        if not self.supports_registered(t):
+            raise ValueError(f"cannot register {t.numel()} x {t.dtype}")
+        key = (t.data_ptr(), t.numel() * t.element_size())
+        if key in self._regs:
+            return self._regs[key]
+        mine, err = None, None
+        try:
+            hb = ctypes.create_string_buffer(64)
+            off = ctypes.c_int64()
+            _lib.check(self.lib.dlbb_car_reg_export(self.h, t.data_ptr(), hb,
+                                                    ctypes.byref(off)), "car_reg_export")
+            mine = (bytes(hb.raw), int(off.value))
+        except Exception as e:  # noqa: BLE001 - reported collectively below
+            err = e
+        allh = self.comm.all_gather_object((mine, repr(err)))
+        if any(x[0] is None for x in allh):
+            raise RuntimeError(f"custom all-reduce registration failed: {[x[1] for x in allh]}")
+        blob = b"".join(x[0][0] for x in allh)
+        offs = (ctypes.c_int64 * self.comm.world_size)(*[x[0][1] for x in allh])
+        rid = ctypes.c_int(-1)
+        rc = self.lib.dlbb_car_reg_open(self.h, t.data_ptr(), key[1], blob, offs,
+                                        ctypes.byref(rid))
+        oks = self.comm.all_gather_object(rc)
+        if any(r != 0 for r in oks):
+            raise RuntimeError(f"custom all-reduce registration open failed (hip rc: {oks})")
+        self._regs[key] = int(rid.value)
+        self._reg_keep.append(t)
+        return int(rid.value)
+
+    def supports_registered(self, t: torch.Tensor) -> bool:
+        if t.dtype not in (torch.bfloat16, torch.float16, torch.float32) or not t.is_contiguous():
+            return False
+        nbytes = t.numel() * t.element_size()
+        return nbytes > 0 and nbytes % (8 * t.element_size() * self.comm.world_size) == 0
+
+    def all_reduce_registered(self, t: torch.Tensor, rid: int,
+                              nblocks: Optional[int] = None) -> torch.Tensor:
+        """In-place two-shot on registration ``rid`` (``t`` must be the registered tensor)."""
+        nbytes = t.numel() * t.element_size()
+        nb = nblocks or self.nblocks or int(min(256, max(1, nbytes // (256 << 10))))
+        _lib.check(self.lib.dlbb_car_allreduce_reg(self.h, rid, t.numel(), _lib.dt(t), nb,
+                                                   _lib.stream(t.device)), "car_allreduce_reg")
+        return t
+
     # ------------------------------------------------------------------ ops
     def all_reduce(self, inp: torch.Tensor, out: Optional[torch.Tensor] = None,
-                   algo: Optional[int] = None) -> torch.Tensor:
+                   algo: Optional[int] = None, nblocks: Optional[int] = None) -> torch.Tensor:
         if not self.supports(inp):
             raise ValueError(f"custom all-reduce cannot take {inp.numel()} x {inp.dtype}")
         out = inp if out is None else out
@@ -105,11 +160,12 @@ class CustomAllReduce:
         a = algo or self.algo_for(nbytes, 8 * inp.element_size())
         _lib.check(self.lib.dlbb_car_allreduce(
             self.h, inp.data_ptr(), out.data_ptr(), inp.numel(), _lib.dt(inp), a,
-            self.blocks_for(nbytes, a), _lib.stream(inp.device)), "car_allreduce")
+            nblocks or self.blocks_for(nbytes, a), _lib.stream(inp.device)), "car_allreduce")
         return out
 
-    def all_reduce_(self, t: torch.Tensor, algo: Optional[int] = None) -> torch.Tensor:
-        return self.all_reduce(t, t, algo)
+    def all_reduce_(self, t: torch.Tensor, algo: Optional[int] = None,
+                    nblocks: Optional[int] = None) -> torch.Tensor:
+        return self.all_reduce(t, t, algo, nblocks)
 
     def check_error(self) -> int:
         return int(self.lib.dlbb_car_error(self.h))
@@ -143,7 +199,38 @@ class CustomAllReduce:
         if not self.healthy and self.comm.rank == 0:
             print(f"[custom all-reduce] self-test failed on ranks "
                   f"{[i for i, f in enumerate(flags) if not f]}: RCCL will be used", flush=True)
+        if self.healthy:
+            self._self_test_registered()
         return self.healthy
+
+    def _self_test_registered(self) -> None:
+        """Registered in-place two-shot vs RCCL (two calls: reuse of one registration);
+        ``reg_healthy`` only if it passes on every rank."""
+        dev, W = self.comm.device, self.comm.world_size
+        ok = True
+        try:
+            n = 1 << 20
+            buf = torch.empty(n, device=dev, dtype=torch.bfloat16)
+            rid = self.register(buf)
+            for it in range(2):
+                g = torch.Generator(device=dev)
+                g.manual_seed(777 + 31 * it + self.comm.rank)
+                x = torch.randn(n, generator=g, device=dev).to(torch.bfloat16)
+                ref = x.float().clone()
+                if W > 1:
+                    dist.all_reduce(ref)
+                buf.copy_(x)
+                self.all_reduce_registered(buf, rid)
+                torch.cuda.synchronize(dev)
+                ok = ok and bool(torch.allclose(buf.float(), ref, rtol=2e-2, atol=5e-2 * W))
+                ok = ok and self.check_error() == 0
+        except Exception:  # noqa: BLE001 - a failed registration/launch is a failed test
+            ok = False
+        flags = self.comm.all_gather_object(bool(ok))
+        self.reg_healthy = all(flags)
+        if not self.reg_healthy and self.comm.rank == 0:
+            print("[custom all-reduce] registered-buffer self-test failed on ranks "
+                  f"{[i for i, f in enumerate(flags) if not f]}", flush=True)
 
     def close(self) -> None:
         if getattr(self, "h", None):

@@ -19,7 +19,8 @@ the MI355X-native replacement used by the GPT-2 DDP microbenchmark:
   producing kernels by an event), strictly in bucket order on every rank (identical collective
   order — RCCL would hang otherwise). ``finish()`` waits the works; the optimizer consumes the
   reduced flat gradient with the 1/world average fused into the AdamW kernel.
-* ``allreduce="custom"`` routes buckets that fit through the IPC xGMI kernel, and
+* ``allreduce="custom"`` routes buckets through the IPC xGMI kernel (in place on the
+  IPC-registered bucket when the registered self-test passed, else via its staging buffer), and
   ``allreduce="native"`` through our own RCCL communicator (``rccl_native``), both on a
   dedicated high-priority comm stream instead of ProcessGroupNCCL's.
 """
@@ -107,11 +108,19 @@ class FlatParamTrainer:
         self._comm_stream = None
         self._car = None
         self._native = None
+        self._bucket_reg: Dict[int, int] = {}
         if allreduce == "custom" and comm is not None and comm.is_gpu and self.world > 1:
             from .custom_allreduce import get_custom_allreduce
 
             self._car = get_custom_allreduce(comm)
             self._comm_stream = torch.cuda.Stream(dev, priority=-1)
+            # buckets are fixed slices of flat_grad: IPC-map them once, then every bucket
+            # all-reduce is the in-place two-shot (no staging copy, no capacity limit)
+            if self._car is not None and self._car.reg_healthy:
+                for b in self.buckets:
+                    buf = self.flat_grad[b.start:b.end]
+                    if self._car.supports_registered(buf):
+                        self._bucket_reg[b.idx] = self._car.register(buf)
         if allreduce == "native" and comm is not None and comm.is_gpu and self.world > 1:
             from .rccl_native import get_native
 
@@ -173,7 +182,13 @@ class FlatParamTrainer:
         if self.world == 1:
             return
         buf = self.flat_grad[b.start:b.end]
-        if self._car is not None and self._car.healthy and self._car.supports(buf):
+        if b.idx in self._bucket_reg:
+            cs = self._comm_stream
+            cs.wait_stream(torch.cuda.current_stream(buf.device))
+            with torch.cuda.stream(cs):
+                self._car.all_reduce_registered(buf, self._bucket_reg[b.idx])
+            b.work = "stream"
+        elif self._car is not None and self._car.healthy and self._car.supports(buf):
             cs = self._comm_stream
             cs.wait_stream(torch.cuda.current_stream(buf.device))
             with torch.cuda.stream(cs):

@@ -130,6 +130,95 @@ def test_custom_allreduce_ranks_on_one_gpu(world):
             assert good and err == 0, (n, algo, it, good, err)
 
 
+def _car_reg_worker(rank, world, n):
+    import torch
+
+    from distributed_llm_backend_benchmark_amd.parallel.comm import init_distributed
+    from distributed_llm_backend_benchmark_amd.parallel.custom_allreduce import (ONESHOT, TWOSHOT,
+                                                                                CustomAllReduce)
+
+    comm = init_distributed("gloo", device="cuda")
+    car = CustomAllReduce(comm, capacity_bytes=8 << 20)
+    car.self_test()
+    ok = [("self_test", car.healthy, car.reg_healthy)]
+    buf = torch.empty(n, device="cuda", dtype=torch.bfloat16)
+    rid = car.register(buf)
+    assert car.register(buf) == rid            # idempotent
+    # interleave registered calls (grid sizes 1..256) with staging-buffer calls of other grid
+    # sizes: the epoch (and buffer half) must stay consistent across workgroups and calls
+    plan = [("reg", 256), ("copy2", 7), ("reg", 64), ("copy1", 3), ("reg", 1), ("copy2", 128),
+            ("reg", 200), ("reg", 256), ("copy1", 32), ("reg", 33)]
+    for it, (kind, nb) in enumerate(plan):
+        xs = [torch.randn(n, generator=torch.Generator(device="cuda").manual_seed(
+            1000 * r + it), device="cuda").to(torch.bfloat16) for r in range(world)]
+        ref = sum(x.float() for x in xs)
+        if kind == "reg":
+            buf.copy_(xs[rank])
+            out = car.all_reduce_registered(buf, rid, nblocks=nb)
+        else:
+            out = car.all_reduce(xs[rank].clone(), algo=ONESHOT if kind == "copy1" else TWOSHOT,
+                                 nblocks=nb)
+        torch.cuda.synchronize()
+        good = torch.allclose(out.float(), ref, rtol=2e-2, atol=5e-2 * world)
+        ok.append((kind, nb, bool(good), car.check_error()))
+    comm.barrier()
+    car.close()
+    comm.destroy()
+    return ok
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_custom_allreduce_registered_ranks_on_one_gpu(world):
+    """Registered in-place two-shot (IPC-mapped user buffers, 3 flag phases) with 2/4/8 ranks
+    sharing one GPU, interleaved with staging-buffer calls of different grid sizes."""
+    res = run_multiprocess(_car_reg_worker, world, args=(world * 8 * 4096 + world * 8 * 3,),
+                           timeout=600)
+    for r in res:
+        assert r[0] == ("self_test", True, True), r[0]
+        for kind, nb, good, err in r[1:]:
+            assert good and err == 0, (kind, nb, good, err)
+
+
+def _ddp_custom_worker(rank, world):
+    import torch
+
+    from distributed_llm_backend_benchmark_amd.models.gpt2 import GPT2, GPT2Config
+    from distributed_llm_backend_benchmark_amd.parallel.comm import init_distributed
+    from distributed_llm_backend_benchmark_amd.parallel.ddp import FlatParamTrainer
+
+    comm = init_distributed("gloo", device="cuda")
+    cfg = GPT2Config(vocab_size=512, block_size=64, n_layer=2, n_head=4, n_embd=256)
+    g = torch.Generator().manual_seed(0)
+    data = torch.randint(0, 512, (world * 2, 65), generator=g).cuda()
+    local = data[rank * 2:(rank + 1) * 2]
+    out = {}
+    for ar in ("rccl", "custom"):          # "rccl" = the process group's all_reduce (gloo here)
+        m = GPT2(cfg, device=torch.device("cuda"), seed=3)
+        tr = FlatParamTrainer(m, comm, lr=1e-3, bucket_mb=0.5, allreduce=ar)
+        nreg = len(tr._bucket_reg)
+        for _ in range(3):
+            tr.step(local[:, :-1], local[:, 1:])
+        torch.cuda.synchronize()
+        out[ar] = (tr.master.clone(), nreg, len(tr.buckets))
+        tr.close()
+    ref, _, nb = out["rccl"]
+    got, nreg, _ = out["custom"]
+    sums = comm.all_gather_object(float(got.double().sum()))
+    comm.destroy()
+    return float((got - ref).abs().max()), nreg, nb, sums
+
+
+def test_ddp_custom_registered_buckets_ranks_on_one_gpu():
+    """DDP with allreduce="custom": every bucket IPC-registered and all-reduced in place by the
+    two-shot kernel on the comm stream; 2 ranks sharing one GPU; the result tracks the process
+    group's all-reduce and stays identical across ranks."""
+    res = run_multiprocess(_ddp_custom_worker, 2, timeout=600)
+    for err, nreg, nb, sums in res:
+        assert nreg == nb and nb > 1, (nreg, nb)
+        assert err < 1e-3, err
+        assert len(set(sums)) == 1, sums
+
+
 def test_bench_py_world1():
     out = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--steps", "5",
                           "--warmup", "2"], capture_output=True, text=True, timeout=600, cwd=REPO)
@@ -153,7 +242,7 @@ def test_bench_py_two_ranks_rehearsal():
     assert out.returncode == 0, out.stderr[-3000:]
     rec = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][-1])
     assert rec["n_gpus"] == 2 and rec["value"] > 0 and rec["vs_baseline"] is not None
-    assert rec["config"]["impl"] in ("custom", "rccl")
+    assert rec["config"]["impl"].split("/")[0] in ("custom", "custom_reg", "rccl")
     assert rec["p50_latency_us_512B"] > 0
 
 
