@@ -72,6 +72,11 @@ class Block(nn.Module):
         self.fc_b = _param((4 * d,), 0.0, device, gen)
         self.mlp_proj_w = _param((d, 4 * d), proj_std, device, gen)
         self.mlp_proj_b = _param((d,), 0.0, device, gen)
+        # used exactly once per forward (by linear_train): a trainer may accumulate their
+        # gradients in-kernel into its flat buffer (ops.linear_fn gradient sinks)
+        for p in (self.attn_w, self.attn_b, self.attn_proj_w, self.attn_proj_b, self.fc_w,
+                  self.fc_b, self.mlp_proj_w, self.mlp_proj_b):
+            p._dlbb_single_use = True
 
     def forward(self, y1, h):
         B, T, C = y1.shape

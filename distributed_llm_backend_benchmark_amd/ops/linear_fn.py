@@ -7,6 +7,12 @@ backward kernel (``csrc/gelu.hip``); ``dX = dU @ W`` is a plain library GEMM (hi
 ``torch.matmul``, as allowed for unfused GEMMs); ``dW = dU^T @ X`` goes through
 :func:`.gemm.wgrad` (our split-K transposed-read MFMA kernel or the library, per-shape autotune),
 which also produces ``db = colsum(dU)`` (an all-ones MFMA operand in the same kernel).
+
+Gradient sinks: a trainer that keeps ``.grad`` as views of a flat bucket buffer can mark a
+parameter with ``_dlbb_grad_sink = callback`` (only for parameters used ONCE per forward — the
+model opts in with ``_dlbb_single_use``). The backward then accumulates dW / db straight into
+``param.grad`` inside the weight-gradient kernel's reduce pass, calls ``callback(param)`` and
+returns no gradient for it — no separate gradient tensor and no AccumulateGrad add kernel.
 """
 
 from __future__ import annotations
@@ -37,6 +43,7 @@ class _LinearFn(torch.autograd.Function):
         y = _linear(x2, w, bias=b, act=act, preact=u)
         ctx.save_for_backward(x2, w, u)
         ctx.has_bias = b is not None
+        ctx.weight, ctx.bias = w, b   # leaf parameters: only read for their grad sinks
         ctx.act = act
         ctx.lead = x.shape[:-1]
         return y.view(*x.shape[:-1], N)
@@ -67,6 +74,17 @@ class _LinearFn(torch.autograd.Function):
                 db = du.sum(0, dtype=torch.float32).to(w.dtype)
         dx = torch.matmul(du, w) if ctx.needs_input_grad[0] else None
         dw = None
+        w_sink = _sink(ctx.weight) if ctx.needs_input_grad[1] else None
+        b_sink = _sink(ctx.bias) if fuse_db else None
+        if w_sink is not None and (not want_db or b_sink is not None):
+            wgrad(du, x2, out=ctx.weight.grad, accumulate=True,
+                  bias_out=ctx.bias.grad if want_db else None)
+            w_sink(ctx.weight)
+            if want_db:
+                b_sink(ctx.bias)
+            if dx is not None:
+                dx = dx.view(*ctx.lead, K)
+            return dx, None, None, None
         if ctx.needs_input_grad[1]:
             dw = torch.empty(N, K, dtype=du.dtype, device=du.device)
             if fuse_db:
@@ -77,6 +95,15 @@ class _LinearFn(torch.autograd.Function):
         if dx is not None:
             dx = dx.view(*ctx.lead, K)
         return dx, dw, db, None
+
+
+def _sink(p: Optional[torch.Tensor]):
+    """The parameter's gradient-sink callback if its .grad can take an in-kernel accumulate."""
+    cb = getattr(p, "_dlbb_grad_sink", None) if p is not None else None
+    g = p.grad if cb is not None else None
+    if g is None or g.dtype != p.dtype or g.shape != p.shape or not g.is_contiguous():
+        return None
+    return cb
 
 
 def linear_train(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor] = None,

@@ -39,6 +39,7 @@ from ..ops.elementwise import ChunkTable
 from ..utils import tracing
 from .comm import Comm
 
+_GRAD_SINKS = os.environ.get("DLBB_GRAD_SINKS", "1") != "0"   # A/B switch for the sinks
 _ALIGN = 64  # elements: keeps every param view 128-B aligned (16-B MFMA/glds rows)
 
 
@@ -103,8 +104,13 @@ class FlatParamTrainer:
         if mode == "view":
             for p, o in zip(order, offs):
                 p.grad = self.flat_grad[o:o + p.numel()].view_as(p)
+                # single-use params (model opt-in): backward accumulates into the bucket view
+                # in-kernel and reports readiness itself (ops.linear_fn gradient sinks)
+                if getattr(p, "_dlbb_single_use", False) and _GRAD_SINKS:
+                    p._dlbb_grad_sink = self._on_grad
         self._hooks = [p.register_post_accumulate_grad_hook(self._on_grad) for p in order]
         self._next = 0
+        self._seen = set()
         self._comm_stream = None
         self._car = None
         self._native = None
@@ -150,8 +156,14 @@ class FlatParamTrainer:
         for b in self.buckets:
             b.ready, b.launched, b.work = 0, False, None
         self._next = 0
+        self._seen.clear()
 
     def _on_grad(self, p: torch.nn.Parameter) -> None:
+        # a param is counted once per step: a gradient-sink param reports itself from inside its
+        # backward, and autograd may still run its post-accumulate hook (with no gradient)
+        if id(p) in self._seen:
+            return
+        self._seen.add(id(p))
         b = self._bucket_of[id(p)]
         b.ready += 1
         if self.overlap and b.ready == len(b.params):
@@ -342,3 +354,6 @@ class FlatParamTrainer:
     def close(self) -> None:
         for h in self._hooks:
             h.remove()
+        for p in self._params:
+            if hasattr(p, "_dlbb_grad_sink"):
+                del p._dlbb_grad_sink

@@ -191,31 +191,38 @@ def _ddp_custom_worker(rank, world):
     g = torch.Generator().manual_seed(0)
     data = torch.randint(0, 512, (world * 2, 65), generator=g).cuda()
     local = data[rank * 2:(rank + 1) * 2]
-    out = {}
+    grads, info = {}, {}
     for ar in ("rccl", "custom"):          # "rccl" = the process group's all_reduce (gloo here)
         m = GPT2(cfg, device=torch.device("cuda"), seed=3)
         tr = FlatParamTrainer(m, comm, lr=1e-3, bucket_mb=0.5, allreduce=ar)
-        nreg = len(tr._bucket_reg)
+        tr.zero_grad()
+        tr._reset()
+        m(local[:, :-1], local[:, 1:]).backward()
+        tr.finish()
+        torch.cuda.synchronize()
+        grads[ar] = tr.flat_grad.float().clone()
         for _ in range(3):
             tr.step(local[:, :-1], local[:, 1:])
         torch.cuda.synchronize()
-        out[ar] = (tr.master.clone(), nreg, len(tr.buckets))
+        info[ar] = (len(tr._bucket_reg), len(tr.buckets),
+                    comm.all_gather_object(float(tr.master.double().sum())))
         tr.close()
-    ref, _, nb = out["rccl"]
-    got, nreg, _ = out["custom"]
-    sums = comm.all_gather_object(float(got.double().sum()))
+    # hipBLASLt may pick split-K kernels whose reduction order varies run to run: compare the
+    # reduced gradients to bf16 resolution, not bit-exactly
+    scale = float(grads["rccl"].abs().max())
+    err = float((grads["custom"] - grads["rccl"]).abs().max()) / scale
     comm.destroy()
-    return float((got - ref).abs().max()), nreg, nb, sums
+    return err, info["custom"]
 
 
 def test_ddp_custom_registered_buckets_ranks_on_one_gpu():
     """DDP with allreduce="custom": every bucket IPC-registered and all-reduced in place by the
-    two-shot kernel on the comm stream; 2 ranks sharing one GPU; the result tracks the process
-    group's all-reduce and stays identical across ranks."""
+    two-shot kernel on the comm stream; 2 ranks sharing one GPU. The reduced gradients match the
+    process group's all-reduce and the trained weights stay identical across ranks."""
     res = run_multiprocess(_ddp_custom_worker, 2, timeout=600)
-    for err, nreg, nb, sums in res:
+    for err, (nreg, nb, sums) in res:
         assert nreg == nb and nb > 1, (nreg, nb)
-        assert err < 1e-3, err
+        assert err < 1e-2, err
         assert len(set(sums)) == 1, sums
 
 
@@ -276,6 +283,39 @@ def test_gpt2_ddp_step_world1():
     idx = torch.randint(0, cfg.vocab_size, (4, 256), device="cuda")
     losses = [tr.step(idx, idx) for _ in range(8)]
     assert losses[-1] < losses[0] - 0.5, losses
+
+
+def test_gpt2_grad_sinks_match_autograd():
+    """Gradient sinks: block linears accumulate dW/db in-kernel into the trainer's flat buckets
+    (no AccumulateGrad); every other param goes through autograd. The flat gradients must
+    equal a plain autograd backward of the same model, and every bucket must be counted
+    complete exactly once during backward."""
+    from distributed_llm_backend_benchmark_amd.models.gpt2 import GPT2, GPT2Config
+    from distributed_llm_backend_benchmark_amd.parallel.ddp import FlatParamTrainer
+
+    cfg = GPT2Config(vocab_size=1024, block_size=256, n_layer=2, n_head=4, n_embd=256)
+    dev = torch.device("cuda")
+    idx = torch.randint(0, cfg.vocab_size, (4, 256), device=dev)
+    ref = GPT2(cfg, device=dev, seed=11)
+    ref(idx, idx).backward()
+    m = GPT2(cfg, device=dev, seed=11)
+    tr = FlatParamTrainer(m, None, lr=1e-3, bucket_mb=0.25)
+    assert sum(hasattr(p, "_dlbb_grad_sink") for p in m.parameters()) == 8 * cfg.n_layer
+    for _ in range(2):                      # second pass: buffers reused, zeroed, re-counted
+        tr.zero_grad()
+        tr._reset()
+        m(idx, idx).backward()
+        assert all(b.ready == len(b.params) for b in tr.buckets), [
+            (b.ready, len(b.params)) for b in tr.buckets]
+        tr.finish()
+        torch.cuda.synchronize()
+        for (n, p), (_, q) in zip(m.named_parameters(), ref.named_parameters()):
+            o = tr._offsets[id(p)]
+            g = tr.flat_grad[o:o + p.numel()].float().view_as(p)
+            err = (g - q.grad.float()).abs().max().item()
+            assert err <= 2e-2 * max(1.0, q.grad.float().abs().max().item()), (n, err)
+    tr.close()
+    assert not any(hasattr(p, "_dlbb_grad_sink") for p in m.parameters())
 
 
 def test_zero2_and_checkpoint_world1_gpu(tmp_path):
