@@ -77,17 +77,27 @@ __device__ __forceinline__ bf16x8 frag(const char* img, int kbase, int colbase, 
 }
 
 // BIAS: a separate instantiation (two extra accumulators + the ones operand: 112 -> 122 VGPRs,
-// still 4 waves/SIMD).
-template <bool BIAS>
+// still 4 waves/SIMD). NB: LDS ring depth (stages) — NB - 1 stages of DMA in flight while one
+// is consumed (NB = 2: 32 KiB, 3 workgroups/CU; 3: 48 KiB, 3/CU; 4: 64 KiB, 2/CU).
+template <bool BIAS, int NB>
 __global__ void __launch_bounds__(kThreads, 3) wgrad_kernel(Args a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = wave >> 1, wn = wave & 1;
+  // workgroup -> (split, tile): XCD-aware bijective remap (guide T1; blockIdx % 8 labels the
+  // blocks that share an L2), then split-major / row-block-major order, so the ~1/8 of the grid
+  // that shares an XCD is a contiguous run of tiles of one split: its dY column blocks are
+  // re-read by the tiles_k workgroups of a row and its X blocks by every row — from that L2
+  // instead of from the Infinity Cache / HBM (the default round-robin puts neighbours on
+  // different XCDs, so every workgroup fetched its panels from beyond L2).
   const int tiles_k = a.K / BKO;
-  const int tn = blockIdx.x / tiles_k, tk = blockIdx.x % tiles_k;
+  const int tiles = (a.N / BN) * tiles_k;
+  const int nwg = gridDim.x, xcd = blockIdx.x % 8, q = nwg / 8, r = nwg % 8;
+  const int wid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + blockIdx.x / 8;
+  const int split = wid / tiles, t = wid % tiles;
+  const int tn = t / tiles_k, tk = t % tiles_k;
   const int n0 = tn * BN, k0 = tk * BKO;
-  const int split = blockIdx.y;
   const int mb = split * a.m_per_split;
   const int me = mb + a.m_per_split < a.M ? mb + a.m_per_split : a.M;
   const int nsteps = (me - mb) / BM;
@@ -106,19 +116,30 @@ __global__ void __launch_bounds__(kThreads, 3) wgrad_kernel(Args a) {
 
   auto imgA = [&](int c) { return smem + c * 2 * kTile; };
   auto imgB = [&](int c) { return smem + c * 2 * kTile + kTile; };
-  if (nsteps > 0) {
-    stage(a.A, a.lda, mb, n0, imgA(0), wave, lane);
-    stage(a.B, a.ldb, mb, k0, imgB(0), wave, lane);
-  }
+  constexpr int kLoadsPerStage = 2 * (BM / 16);   // global_load_lds per wave per stage
+#pragma unroll
+  for (int p = 0; p < NB - 1; ++p)
+    if (p < nsteps) {
+      stage(a.A, a.lda, mb + p * BM, n0, imgA(p), wave, lane);
+      stage(a.B, a.ldb, mb + p * BM, k0, imgB(p), wave, lane);
+    }
   for (int s = 0; s < nsteps; ++s) {
-    const int cur = s & 1;
-    // one barrier per stage: it publishes stage s (every wave's DMA retired) and frees buffer
-    // cur^1 (every wave finished stage s-1), so the next stage is issued right after it
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int cur = s % NB;
+    // stage s landed: later stages (up to NB - 2 of them) may still be in flight
+    const int ahead = nsteps - 1 - s < NB - 2 ? nsteps - 1 - s : NB - 2;
+    if (NB >= 4 && ahead >= 2)
+      asm volatile("s_waitcnt vmcnt(%0)" :: "n"(2 * kLoadsPerStage) : "memory");
+    else if (NB >= 3 && ahead >= 1)
+      asm volatile("s_waitcnt vmcnt(%0)" :: "n"(kLoadsPerStage) : "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // one barrier per stage: it publishes stage s (every wave's DMA of it retired) and frees
+    // the buffer of stage s - 1 (every wave finished it), which stage s + NB - 1 now refills
     __builtin_amdgcn_s_barrier();
-    if (s + 1 < nsteps) {
-      stage(a.A, a.lda, mb + (s + 1) * BM, n0, imgA(cur ^ 1), wave, lane);
-      stage(a.B, a.ldb, mb + (s + 1) * BM, k0, imgB(cur ^ 1), wave, lane);
+    if (s + NB - 1 < nsteps) {
+      const int nxt = (s + NB - 1) % NB;
+      stage(a.A, a.lda, mb + (s + NB - 1) * BM, n0, imgA(nxt), wave, lane);
+      stage(a.B, a.ldb, mb + (s + NB - 1) * BM, k0, imgB(nxt), wave, lane);
     }
     const char* ia = imgA(cur);
     const char* ib = imgB(cur);
@@ -209,6 +230,11 @@ __global__ void __launch_bounds__(256) split_reduce_kernel(const float* __restri
 
 using namespace dlbb;
 
+// LDS ring depth of the wgrad kernel (A/B: dlbb_gemm_wgrad_set_stages)
+static int g_wgrad_stages = 2;
+
+DLBB_API void dlbb_gemm_wgrad_set_stages(int nb) { g_wgrad_stages = nb >= 2 && nb <= 4 ? nb : 2; }
+
 // dW[N][K] = A^T B with A = [M][lda] (N columns used), B = [M][ldb] (K columns used), bf16.
 // Requires M % 32 == 0, N % 128 == 0, K % 128 == 0, lda/ldb % 8 == 0, 16-B aligned bases.
 // ws: fp32 workspace of split * (N * K + N) floats. out: bf16 (dt_out 1) or fp32 (0), dense
@@ -227,11 +253,20 @@ DLBB_API int dlbb_gemm_wgrad(const void* A, int64_t lda, const void* B, int64_t 
   split = (M + per - 1) / per;
   Args a{static_cast<const uint16_t*>(A), static_cast<const uint16_t*>(B), ws, lda, ldb, M, N, K,
          per, split};
-  const dim3 grid((N / BN) * (K / BKO), split);
-  if (out_bias)
-    hipLaunchKernelGGL(wgrad_kernel<true>, grid, dim3(kThreads), 4 * kTile, stream, a);
-  else
-    hipLaunchKernelGGL(wgrad_kernel<false>, grid, dim3(kThreads), 4 * kTile, stream, a);
+  const dim3 grid((N / BN) * (K / BKO) * split);
+#define WG_LAUNCH(BIASV, NBV)                                                               \
+  hipLaunchKernelGGL((wgrad_kernel<BIASV, NBV>), grid, dim3(kThreads), NBV * 2 * kTile, stream, a)
+  const int stages = g_wgrad_stages;
+  if (out_bias) {
+    if (stages == 4) WG_LAUNCH(true, 4);
+    else if (stages == 3) WG_LAUNCH(true, 3);
+    else WG_LAUNCH(true, 2);
+  } else {
+    if (stages == 4) WG_LAUNCH(false, 4);
+    else if (stages == 3) WG_LAUNCH(false, 3);
+    else WG_LAUNCH(false, 2);
+  }
+#undef WG_LAUNCH
   const int64_t n = static_cast<int64_t>(N) * K;
   const int64_t nb = out_bias ? N : 0;
   const int g = stream_grid((n + nb) / 8, 256);

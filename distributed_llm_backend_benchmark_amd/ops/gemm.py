@@ -41,6 +41,11 @@ def set_stagger(mode: int) -> None:
     _lib.lib().dlbb_gemm_set_stagger(int(mode))
 
 
+def set_wgrad_stages(nb: int) -> None:
+    """LDS ring depth of the weight-gradient kernel (2, 3 or 4 stages); for A/B benchmarking."""
+    _lib.lib().dlbb_gemm_wgrad_set_stages(int(nb))
+
+
 def get_stagger() -> int:
     return int(_lib.lib().dlbb_gemm_get_stagger())
 
@@ -210,7 +215,9 @@ def _wgrad_hip(dy2, x2, out, accumulate, split=None, bias_out=None):
     K = x2.shape[1]
     tiles = (N // 128) * (K // 128)
     if split is None:
-        split = max(1, min(M // 256, -(-512 // tiles)))
+        # about one resident wave of workgroups (3 per CU x 256 CUs): measured best with the
+        # XCD-aware tile order (profiles/r01_gpt2/wgrad_split_xcd.jsonl)
+        split = max(1, min(M // 256, -(-768 // tiles)))
     ws = torch.empty(split * (N * K + N), dtype=torch.float32, device=dy2.device)
     check(_lib.lib().dlbb_gemm_wgrad(dy2.data_ptr(), dy2.stride(0), x2.data_ptr(), x2.stride(0),
                                      out.data_ptr(), _lib.dt(out), int(accumulate), ws.data_ptr(),
