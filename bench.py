@@ -173,6 +173,30 @@ def main(argv=None) -> int:
                 "ref_busbw_GBps_8MiB": REF_BUSBW_8MIB,
             }
 
+    # BASELINE configs 3/4 on the same [B,S,H] message at P > 1: all-gather, reduce-scatter and
+    # all-to-all through RCCL and through the direct one-hop IPC kernels (side measurements)
+    coll = {}
+    if not args.no_side and P > 1:
+        for name in ("allgather", "reduce_scatter", "alltoall"):
+            res = {}
+            for label, opts in (("rccl", {}), ("direct_ipc", {"direct": True})):
+                if label == "direct_ipc" and not comm.is_gpu:
+                    continue
+                try:
+                    cop = make_op(name, comm, data, **opts)
+                except RuntimeError as e:   # agreed on every rank (health flags are collective)
+                    if comm.rank == 0:
+                        print(f"note: {name}/{label} unavailable: {e}", file=sys.stderr)
+                    continue
+                for _ in range(3):
+                    cop.run()
+                comm.sync()
+                t = _timed_steps(comm, cop, 10) / 10
+                res[label] = {"busbw_GBps": busbw_gbps(name, cop.message_bytes, t, P),
+                              "ms": t * 1e3}
+                del cop
+            coll[name] = res
+
     if comm.rank == 0:
         rec = {
             "metric": "all-reduce bus BW (GB/s)",
@@ -203,6 +227,8 @@ def main(argv=None) -> int:
                      "vs_baseline is null (reference has no single-rank data)"),
             **side,
         }
+        if coll:
+            rec["collectives_same_message"] = coll
         print(json.dumps(rec), flush=True)
     comm.barrier()
     comm.destroy()

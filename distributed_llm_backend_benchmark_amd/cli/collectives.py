@@ -60,6 +60,10 @@ def parse_args(argv=None):
                     help="torch = collectives through torch.distributed (ProcessGroupNCCL); "
                          "native = our C++ RCCL engine enqueuing on the timing stream")
     ap.add_argument("--allreduce-algo", default=None, choices=["oneshot", "twoshot"])
+    ap.add_argument("--direct-ipc", action="store_true",
+                    help="allgather / reduce_scatter / alltoall through the direct one-hop IPC "
+                         "kernels (each GPU pulls from all peers over its xGMI links) instead "
+                         "of RCCL")
     ap.add_argument("--allgather-form", default="tensor", choices=["tensor", "list"])
     ap.add_argument("--env", action="append", default=[],
                     help="KEY=VAL exported before the process group starts (RCCL knobs: "
@@ -94,7 +98,7 @@ def main(argv=None) -> int:
         ops = list(REFERENCE_1D_OPS) if args.mode == "1d" else list(REFERENCE_3D_OPS) + [
             "reduce_scatter", "alltoall"]
     op_opts = {"impl": "native" if args.engine == "native" else args.allreduce_impl,
-               "form": args.allgather_form}
+               "form": args.allgather_form, "direct": args.direct_ipc}
     if args.allreduce_algo:
         op_opts["algo"] = 1 if args.allreduce_algo == "oneshot" else 2
     extra = {"env": env} if env else {}

@@ -322,6 +322,82 @@ __global__ void __launch_bounds__(kCarThreads) car_twoshot_reg_kernel(CarKernelA
   wait_peers(a, 2, e);
 }
 
+// ---- direct (one-hop) collectives on registered inputs --------------------------------------
+// Every GPU reads its peers' registered input buffers over its own xGMI link to each of them, so
+// all 7 links of a GPU carry traffic at once (an RCCL ring uses one link in and one out per
+// channel). Entry barrier: every rank's input is complete; exit barrier: no peer still reads my
+// input when my stream moves on (the caller may overwrite it). Workgroup b moves sub-range b of
+// every peer's chunk with the loads from all peers in flight together.
+//   all-gather : out[p * chunk .. ] = in_p[0 .. chunk)
+//   all-to-all : out[p * chunk .. ] = in_p[rank * chunk .. ]   (equal splits)
+template <int W, bool A2A>
+__global__ void __launch_bounds__(kCarThreads) car_pull_kernel(CarKernelArgs a) {
+  const uint32_t e = begin_epoch(a);
+  const int64_t chunk = a.nbytes;                    // bytes per peer chunk, multiple of 16
+  const int64_t nvec = chunk / 16;
+  const int64_t per = (nvec + gridDim.x - 1) / gridDim.x;
+  const int64_t v0 = blockIdx.x * per;
+  const int64_t v1 = v0 + per < nvec ? v0 + per : nvec;
+  const int64_t src_off = A2A ? a.rank * chunk : 0;
+  char* out = static_cast<char*>(a.out);
+  signal_peers(a, 0, e);
+  if (!wait_peers(a, 0, e)) return;
+  if constexpr (W > 0) {
+    for (int64_t v = v0 + threadIdx.x; v < v1; v += blockDim.x) {
+      u16x8 t[W];
+#pragma unroll
+      for (int k = 0; k < W; ++k) {
+        const int p = (a.rank + k) & (W - 1);
+        t[k] = reinterpret_cast<const u16x8*>(a.data[p] + src_off)[v];
+      }
+#pragma unroll
+      for (int k = 0; k < W; ++k) {
+        const int p = (a.rank + k) & (W - 1);
+        reinterpret_cast<u16x8*>(out + p * chunk)[v] = t[k];
+      }
+    }
+  } else {
+    for (int k = 0; k < a.world; ++k) {
+      const int p = (a.rank + k) % a.world;
+      for (int64_t v = v0 + threadIdx.x; v < v1; v += blockDim.x)
+        reinterpret_cast<u16x8*>(out + p * chunk)[v] =
+            reinterpret_cast<const u16x8*>(a.data[p] + src_off)[v];
+    }
+  }
+  signal_peers(a, 2, e);
+  wait_peers(a, 2, e);
+}
+
+//   reduce-scatter : out[0 .. n/P) = sum_p in_p[rank * n/P .. ]   (fp32 accumulation)
+template <int DT, int W>
+__global__ void __launch_bounds__(kCarThreads) car_rs_kernel(CarKernelArgs a) {
+  constexpr int64_t kVecBytes = 8 * Elem<DT>::kBytes;
+  const uint32_t e = begin_epoch(a);
+  const int64_t shard_vec = a.nbytes / kVecBytes / a.world;
+  const int64_t per = (shard_vec + gridDim.x - 1) / gridDim.x;
+  const int64_t s0 = blockIdx.x * per;
+  const int64_t s1 = s0 + per < shard_vec ? s0 + per : shard_vec;
+  signal_peers(a, 0, e);
+  if (!wait_peers(a, 0, e)) return;
+  const int64_t mybase = a.rank * shard_vec;
+  for (int64_t v = s0 + threadIdx.x; v < s1; v += blockDim.x) {
+    float acc[8];
+    sum_vec<DT, W>(a, 0, (mybase + v) * kVecBytes, acc);
+    store8<DT>(a.out, v, acc);
+  }
+  signal_peers(a, 2, e);
+  wait_peers(a, 2, e);
+}
+
+template <int W>
+void launch_direct(int kind, int dtype, dim3 g, dim3 b, hipStream_t st, const CarKernelArgs& a) {
+  if (kind == 0) hipLaunchKernelGGL((car_pull_kernel<W, false>), g, b, 0, st, a);
+  else if (kind == 1) hipLaunchKernelGGL((car_pull_kernel<W, true>), g, b, 0, st, a);
+  else if (dtype == DT_BF16) hipLaunchKernelGGL((car_rs_kernel<DT_BF16, W>), g, b, 0, st, a);
+  else if (dtype == DT_F16) hipLaunchKernelGGL((car_rs_kernel<DT_F16, W>), g, b, 0, st, a);
+  else hipLaunchKernelGGL((car_rs_kernel<DT_F32, W>), g, b, 0, st, a);
+}
+
 struct RegBuf {
   char* ptr[kMaxRanks] = {};    // every rank's registered buffer (mine at [rank])
   int64_t bytes = 0;
@@ -587,6 +663,37 @@ DLBB_API int dlbb_car_allreduce_reg(void* h, int id, int64_t n, int dtype, int n
   else if (dtype == DT_F16) CAR_RW(DT_F16);
   else CAR_RW(DT_F32);
 #undef CAR_RW
+  return hipGetLastError();
+}
+
+// Direct collectives on registration `id` (this rank's registered input; out is local).
+//   kind 0 = all-gather  : bytes = chunk bytes per rank (<= registered), out = world x chunk
+//   kind 1 = all-to-all  : bytes = chunk bytes per peer (world x chunk <= registered)
+//   kind 2 = reduce-scatter (dtype): bytes = whole input (multiple of 16 x world), out = bytes/world
+DLBB_API int dlbb_car_direct_reg(void* h, int id, int kind, int64_t bytes, int dtype, void* out,
+                                 int nblocks, hipStream_t stream) {
+  CarState* s = static_cast<CarState*>(h);
+  if (!s->opened || id < 0 || id >= static_cast<int>(s->regs.size()) || !out)
+    return hipErrorInvalidValue;
+  const RegBuf& r = s->regs[id];
+  if (bytes <= 0) return hipSuccess;
+  if (kind == 0 && (bytes % 16 || bytes > r.bytes)) return hipErrorInvalidValue;
+  if (kind == 1 && (bytes % 16 || bytes * s->world > r.bytes)) return hipErrorInvalidValue;
+  if (kind == 2 && (bytes % (16 * s->world) || bytes > r.bytes)) return hipErrorInvalidValue;
+  if (kind < 0 || kind > 2) return hipErrorInvalidValue;
+  if (nblocks < 1) nblocks = 1;
+  if (nblocks > kMaxBlocks) nblocks = kMaxBlocks;
+  CarKernelArgs a = s->args;
+  for (int p = 0; p < kMaxRanks; ++p) a.data[p] = r.ptr[p];
+  a.inp = r.ptr[s->rank];
+  a.out = out;
+  a.nbytes = bytes;
+  const dim3 g(nblocks), b(kCarThreads);
+  const int w = s->world == 2 || s->world == 4 || s->world == 8 ? s->world : 0;
+  if (w == 2) launch_direct<2>(kind, dtype, g, b, stream, a);
+  else if (w == 4) launch_direct<4>(kind, dtype, g, b, stream, a);
+  else if (w == 8) launch_direct<8>(kind, dtype, g, b, stream, a);
+  else launch_direct<0>(kind, dtype, g, b, stream, a);
   return hipGetLastError();
 }
 

@@ -20,6 +20,9 @@ alltoall_moe     —                                      uneven token splits (t
 sendrecv         ``1d/openmpi.py:189-193``                ring ``batch_isend_irecv``
 ================ ====================================== =========================================
 
+``direct=True`` routes allgather / reduce_scatter / alltoall through the one-hop IPC kernels of
+:mod:`.custom_allreduce` (every GPU pulls from all 7 peers at once over xGMI) instead of RCCL.
+
 Each op separates ``reset()`` (restores in-place buffers, reference ``data.clone()`` at
 ``1d/dsccl.py:62``; never timed) from ``run()`` (the timed collective), reports its message
 bytes, and can validate its result against a closed form computed from every rank's seeded
@@ -50,6 +53,22 @@ def make_data(shape, dtype: torch.dtype, rank: int, device: torch.device,
     g = torch.Generator(device=device)
     g.manual_seed(seed + rank)
     return torch.randn(*shape, generator=g, device=device, dtype=torch.float32).to(dtype)
+
+
+def _direct_ipc(comm: Comm, t: torch.Tensor, multiple: int):
+    """(kernel object, registration id) for the direct IPC collectives on ``t`` (registered on
+    every rank — collective). ``multiple``: element count granularity the kernel needs (16-byte
+    vectors per chunk). Raises alike on every rank when unavailable."""
+    if not (comm.is_gpu and comm.world_size > 1):
+        raise RuntimeError("direct IPC collectives need world > 1 on HIP devices")
+    if t.numel() % multiple:
+        raise RuntimeError(f"direct IPC collective needs a multiple of {multiple} elements")
+    from .custom_allreduce import get_custom_allreduce
+
+    car = get_custom_allreduce(comm)
+    if car is None or not car.reg_healthy:
+        raise RuntimeError("IPC kernels unavailable or failed their self-test")
+    return car, car.register(t)
 
 
 class CollectiveOp:
@@ -162,14 +181,23 @@ class AllGather(CollectiveOp):
     def setup(self):
         self.form = self.opts.get("form", "tensor")
         n = self.data.numel()
+        self.impl, self._car = "rccl", None
         if self.form == "list":
             self.outs = [torch.empty_like(self.data) for _ in range(self.P)]
         else:
             self.out = torch.empty(self.P * n, dtype=self.data.dtype, device=self.data.device)
             self.flat = self.data.reshape(-1)
             self._tensor_ok = True
+            if self.opts.get("direct"):     # direct one-hop pulls over xGMI
+                self._car, self._rid = _direct_ipc(self.comm, self.flat,
+                                                   16 // self.data.element_size())
+                self.impl = "custom"
 
     def run(self):
+        if self._car is not None:
+            self._car.all_gather_registered(self.flat, self._rid, self.out,
+                                            nblocks=self.opts.get("nblocks"))
+            return
         if self.form == "list":
             dist.all_gather(self.outs, self.data)
             return
@@ -199,12 +227,21 @@ class ReduceScatter(CollectiveOp):
         self.inp = self.data.reshape(-1)[:n].contiguous()
         self.out = torch.empty(n // self.P, dtype=self.data.dtype, device=self.data.device)
         self._native = True
+        self.impl, self._car = "rccl", None
+        if self.opts.get("direct"):
+            self._car, self._rid = _direct_ipc(self.comm, self.inp,
+                                               16 // self.inp.element_size() * self.P)
+            self.impl = "custom"
 
     @property
     def message_bytes(self):
         return self.inp.numel() * self.inp.element_size()
 
     def run(self):
+        if self._car is not None:
+            self._car.reduce_scatter_registered(self.inp, self._rid, self.out,
+                                                nblocks=self.opts.get("nblocks"))
+            return
         if self._native:
             try:
                 dist.reduce_scatter_tensor(self.out, self.inp, op=dist.ReduceOp.SUM)
@@ -308,12 +345,21 @@ class AllToAll(CollectiveOp):
         n = self.data.numel() - self.data.numel() % self.P
         self.inp = self.data.reshape(-1)[:n].contiguous()
         self.out = torch.empty_like(self.inp)
+        self.impl, self._car = "rccl", None
+        if self.opts.get("direct"):
+            self._car, self._rid = _direct_ipc(self.comm, self.inp,
+                                               16 // self.inp.element_size() * self.P)
+            self.impl = "custom"
 
     @property
     def message_bytes(self):
         return self.inp.numel() * self.inp.element_size()
 
     def run(self):
+        if self._car is not None:
+            self._car.all_to_all_registered(self.inp, self._rid, self.out,
+                                            nblocks=self.opts.get("nblocks"))
+            return
         dist.all_to_all_single(self.out, self.inp)
 
     def expected(self, all_inputs):

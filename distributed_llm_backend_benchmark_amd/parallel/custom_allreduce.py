@@ -7,7 +7,9 @@ node: RCCL (ring/tree, default), ``oneshot`` (every rank reads all peers' full b
 reduce-scatter + direct all-gather — the "2d"/rabenseifner analogue, all links busy).
 ``register(t)`` IPC-maps a user tensor on every rank once; ``all_reduce_registered`` then runs
 the two-shot in place on it (no copy-in, no staging buffer: the bandwidth path for large,
-long-lived buffers such as gradient buckets or a benchmark's message).
+long-lived buffers such as gradient buckets or a benchmark's message). The same registration
+serves the direct one-hop ``all_gather_registered`` / ``reduce_scatter_registered`` /
+``all_to_all_registered`` kernels: each GPU pulls its peers' data over its 7 xGMI links at once.
 
 Setup: each rank allocates its IPC regions, the 192-byte handles and device ordinals are
 exchanged once through the process group (``all_gather_object``), peers are opened with
@@ -28,6 +30,7 @@ from ..ops import _lib
 from .comm import Comm
 
 ONESHOT, TWOSHOT = 1, 2
+DIRECT_AG, DIRECT_A2A, DIRECT_RS = 0, 1, 2
 
 _INSTANCES: Dict[int, "CustomAllReduce"] = {}
 
@@ -106,7 +109,8 @@ class CustomAllReduce:
         """Collective: IPC-map tensor ``t`` of every rank (same numel / dtype everywhere) for
         :meth:`all_reduce_registered`. Every local failure is agreed on by all ranks (then
         every rank raises). Registered tensors are kept alive by this object."""
-        if not self.supports_registered(t):
+        if (t.dtype not in (torch.bfloat16, torch.float16, torch.float32)
+                or not t.is_contiguous() or t.numel() * t.element_size() % 16):
             raise ValueError(f"cannot register {t.numel()} x {t.dtype}")
         key = (t.data_ptr(), t.numel() * t.element_size())
         if key in self._regs:
@@ -149,6 +153,38 @@ class CustomAllReduce:
         _lib.check(self.lib.dlbb_car_allreduce_reg(self.h, rid, t.numel(), _lib.dt(t), nb,
                                                    _lib.stream(t.device)), "car_allreduce_reg")
         return t
+
+    def _direct(self, kind: int, t: torch.Tensor, rid: int, out: torch.Tensor, nbytes: int,
+                nblocks: Optional[int]) -> torch.Tensor:
+        if not out.is_contiguous() or out.dtype != t.dtype:
+            raise ValueError("direct collective: out must be contiguous, same dtype as input")
+        nb = nblocks or self.nblocks or int(min(256, max(8, nbytes // (256 << 10))))
+        _lib.check(self.lib.dlbb_car_direct_reg(self.h, rid, kind, nbytes, _lib.dt(t),
+                                                out.data_ptr(), nb, _lib.stream(t.device)),
+                   "car_direct_reg")
+        return out
+
+    def all_gather_registered(self, t: torch.Tensor, rid: int, out: torch.Tensor,
+                              nblocks: Optional[int] = None) -> torch.Tensor:
+        """out[p * n : (p + 1) * n] = t of rank p (t registered as ``rid``; out world x n)."""
+        if out.numel() != t.numel() * self.comm.world_size:
+            raise ValueError("all_gather_registered: out must hold world x input")
+        return self._direct(DIRECT_AG, t, rid, out, t.numel() * t.element_size(), nblocks)
+
+    def all_to_all_registered(self, t: torch.Tensor, rid: int, out: torch.Tensor,
+                              nblocks: Optional[int] = None) -> torch.Tensor:
+        """Equal splits: out chunk p = chunk ``rank`` of rank p's t (t, out: world x c)."""
+        W = self.comm.world_size
+        if out.numel() != t.numel() or t.numel() % W:
+            raise ValueError("all_to_all_registered: in/out of world x chunk elements")
+        return self._direct(DIRECT_A2A, t, rid, out, t.numel() // W * t.element_size(), nblocks)
+
+    def reduce_scatter_registered(self, t: torch.Tensor, rid: int, out: torch.Tensor,
+                                  nblocks: Optional[int] = None) -> torch.Tensor:
+        """out = shard ``rank`` of sum_p t_p (fp32 accumulation; out n / world)."""
+        if out.numel() * self.comm.world_size != t.numel():
+            raise ValueError("reduce_scatter_registered: out must hold input / world")
+        return self._direct(DIRECT_RS, t, rid, out, t.numel() * t.element_size(), nblocks)
 
     # ------------------------------------------------------------------ ops
     def all_reduce(self, inp: torch.Tensor, out: Optional[torch.Tensor] = None,

@@ -179,6 +179,39 @@ def test_custom_allreduce_registered_ranks_on_one_gpu(world):
             assert good and err == 0, (kind, nb, good, err)
 
 
+def _direct_worker(rank, world, n):
+    import torch
+
+    from distributed_llm_backend_benchmark_amd.parallel.collectives import make_data, make_op
+    from distributed_llm_backend_benchmark_amd.parallel.comm import init_distributed
+
+    comm = init_distributed("gloo", device="cuda")
+    res = []
+    for dt in (torch.bfloat16, torch.float32):
+        ins = [make_data((n,), dt, r, torch.device("cuda")) for r in range(world)]
+        for name in ("allgather", "reduce_scatter", "alltoall"):
+            for nb in (None, 3, 256):
+                op = make_op(name, comm, ins[rank], direct=True, nblocks=nb)
+                for _ in range(3):            # repeated calls on one registration
+                    op.reset()
+                    op.run()
+                torch.cuda.synchronize()
+                res.append((name, str(dt), nb, op.impl, op.check(ins)))
+    comm.barrier()
+    comm.destroy()
+    return res
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_direct_ipc_collectives_ranks_on_one_gpu(world):
+    """One-hop IPC all-gather / reduce-scatter / all-to-all (registered inputs, entry + exit
+    flag barriers) against closed forms, 2/4/8 ranks sharing one GPU, bf16 and fp32."""
+    res = run_multiprocess(_direct_worker, world, args=(world * 8 * 1000,), timeout=600)
+    for r in res:
+        for name, dt, nb, impl, ok in r:
+            assert impl == "custom" and ok, (name, dt, nb, impl, ok)
+
+
 def _ddp_custom_worker(rank, world):
     import torch
 
@@ -251,6 +284,10 @@ def test_bench_py_two_ranks_rehearsal():
     assert rec["n_gpus"] == 2 and rec["value"] > 0 and rec["vs_baseline"] is not None
     assert rec["config"]["impl"].split("/")[0] in ("custom", "custom_reg", "rccl")
     assert rec["p50_latency_us_512B"] > 0
+    coll = rec["collectives_same_message"]
+    for name in ("allgather", "reduce_scatter", "alltoall"):
+        assert set(coll[name]) == {"rccl", "direct_ipc"}, coll
+        assert all(v["busbw_GBps"] > 0 for v in coll[name].values()), coll
 
 
 def test_tp_forward_world1_matches_torch():
