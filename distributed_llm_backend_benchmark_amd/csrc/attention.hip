@@ -51,7 +51,31 @@ struct AttnArgs {
   int64_t ld, ldo;       // token row strides (elements)
   int B, T, H;
   float scale_log2;      // log2(e) / sqrt(D)
+  int xcd;               // 1: XCD-aware head-contiguous block order (head_block)
 };
+
+// Block -> (block-in-head, h, b) for a (blocks-per-head, H, B) grid. xcd = 1: XCD-aware
+// bijective remap (guide T1; blockIdx % 8 labels the blocks that share an L2) so each XCD's
+// eighth of the grid is a contiguous run of WHOLE heads — a head's K/V (forward, dQ) or Q/dO
+// (dK/dV) tiles are then fetched into one L2 instead of into all eight (the default dispatch
+// sends the consecutive blocks of one head to eight different XCDs). Order inside a head kept.
+__device__ __forceinline__ void head_block(int xcd_on, int& blk, int& h, int& b) {
+  const int nb = gridDim.x, H = gridDim.y;
+  if (!xcd_on) {
+    blk = blockIdx.x;
+    h = blockIdx.y;
+    b = blockIdx.z;
+    return;
+  }
+  const int nwg = nb * H * gridDim.z;
+  const int L = blockIdx.x + nb * (blockIdx.y + H * blockIdx.z);
+  const int x = L % 8, q = nwg / 8, r = nwg % 8;
+  const int wid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + L / 8;
+  blk = wid % nb;
+  const int hh = wid / nb;
+  h = hh % H;
+  b = hh / H;
+}
 
 // Stage keys [k0, k0 + 64) of head h: K (section 1 of the row) and V (section 2) tiles.
 // 64 rows x 128 B per image = 8 KiB = 8 wave-instructions; wave w issues rows [16w, 16w + 16)
@@ -75,8 +99,9 @@ __global__ void __launch_bounds__(kAttnThreads, 2) attn_fwd_d64_kernel(AttnArgs 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int nqb = (a.T + kQB - 1) / kQB;
-  const int qb = nqb - 1 - static_cast<int>(blockIdx.x);     // heaviest first
-  const int h = blockIdx.y, b = blockIdx.z;
+  int blk, h, b;
+  head_block(a.xcd, blk, h, b);
+  const int qb = nqb - 1 - blk;                   // heaviest first
   const int q0 = qb * kQB;
   const int qw = q0 + wave * 32;                  // this wave's first query
   const int r = lane & 31, hi = lane >> 5;
@@ -252,6 +277,7 @@ struct AttnBwdArgs {
   int B, T, H;
   float scale_log2;        // log2(e) / sqrt(D)
   float scale;             // 1 / sqrt(D)
+  int xcd;                 // see head_block
 };
 
 // delta[b, h, t] = sum_d dO[b, t, h, d] * O[b, t, h, d]; one thread per (b, t, h) row of 64
@@ -333,8 +359,9 @@ __global__ void __launch_bounds__(kAttnThreads, 2) attn_bwd_dkdv_d64_kernel(Attn
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int r = lane & 31, hi = lane >> 5;
-  const int h = blockIdx.y, b = blockIdx.z;
-  const int kb0 = blockIdx.x * kBwdKeys;            // block 0 = most query slices: first
+  int blk, h, b;
+  head_block(a.xcd, blk, h, b);
+  const int kb0 = blk * kBwdKeys;                   // block 0 = most query slices: first
   const int kw = kb0 + wave * 32;
   const int mykey = kw + r;
   const uint16_t* base_bt = a.qkv + static_cast<int64_t>(b) * a.T * a.ld;
@@ -478,8 +505,9 @@ __global__ void __launch_bounds__(kAttnThreads, 2) attn_bwd_dq_d64_kernel(AttnBw
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int nqb = (a.T + kQB - 1) / kQB;
-  const int qb = nqb - 1 - static_cast<int>(blockIdx.x);
-  const int h = blockIdx.y, b = blockIdx.z;
+  int blk, h, b;
+  head_block(a.xcd, blk, h, b);
+  const int qb = nqb - 1 - blk;
   const int q0 = qb * kQB;
   const int qw = q0 + wave * 32;
   const int r = lane & 31, hi = lane >> 5;
@@ -570,6 +598,10 @@ __global__ void __launch_bounds__(kAttnThreads, 2) attn_bwd_dq_d64_kernel(AttnBw
 
 using namespace dlbb;
 
+static int g_attn_xcd = 1;   // A/B switch for the XCD-aware block order (dlbb_attn_set_xcd)
+
+DLBB_API void dlbb_attn_set_xcd(int on) { g_attn_xcd = on ? 1 : 0; }
+
 // qkv: [B, T, 3, H, 64] bf16 (token row stride ld elements, 16-B aligned rows);
 // out: [B, T, H, 64] bf16 (row stride ldo); lse: [B, H, T] fp32 (may be null). Causal only.
 DLBB_API int dlbb_attn_fwd(const void* qkv, int64_t ld, void* out, int64_t ldo, float* lse,
@@ -581,7 +613,7 @@ DLBB_API int dlbb_attn_fwd(const void* qkv, int64_t ld, void* out, int64_t ldo, 
     return hipErrorInvalidValue;
   if (ld < 3 * H * D || ldo < H * D) return hipErrorInvalidValue;
   AttnArgs a{static_cast<const uint16_t*>(qkv), static_cast<uint16_t*>(out), lse, ld, ldo,
-             B, T, H, scale * 1.4426950408889634f};
+             B, T, H, scale * 1.4426950408889634f, g_attn_xcd};
   const dim3 grid((T + kQB - 1) / kQB, H, B);
   hipLaunchKernelGGL(attn_fwd_d64_kernel, grid, dim3(kAttnThreads), 4 * kTileKV, stream, a);
   return hipGetLastError();
@@ -603,7 +635,7 @@ DLBB_API int dlbb_attn_bwd(const void* qkv, int64_t ld, const void* out, const v
                      static_cast<const uint16_t*>(out), ldo, delta, B, T, H);
   AttnBwdArgs a{static_cast<const uint16_t*>(qkv), static_cast<const uint16_t*>(dout), lse, delta,
                 static_cast<uint16_t*>(dqkv), ld, ldo, B, T, H,
-                scale * 1.4426950408889634f, scale};
+                scale * 1.4426950408889634f, scale, g_attn_xcd};
   hipLaunchKernelGGL(attn_bwd_dkdv_d64_kernel, dim3((T + kBwdKeys - 1) / kBwdKeys, H, B),
                      dim3(kAttnThreads), 4 * kSliceImg, stream, a);
   hipLaunchKernelGGL(attn_bwd_dq_d64_kernel, dim3((T + kQB - 1) / kQB, H, B),
