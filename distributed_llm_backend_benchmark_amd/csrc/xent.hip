@@ -91,9 +91,104 @@ __global__ void __launch_bounds__(kXentThreads) xent_bwd_kernel(
   }
 }
 
+// Fused forward + backward for a loss whose upstream gradient is folded in later (the LM-head
+// linear + cross-entropy op scales dX / dW by it): one read of the row into registers (NV
+// 16-byte vectors per thread, kXentFusedThreads threads per row), block max, block sum-exp,
+// then dlogits = (exp(x - lse) - onehot(target)) * scale written IN PLACE over the logits and
+// the per-row loss. One HBM read + one write instead of read (fwd) + read + write (bwd).
+constexpr int kXentFusedThreads = 512;
+
+__device__ __forceinline__ float block_reduce(float v, bool is_max, float* sm) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float u = __shfl_xor(v, o, 64);
+    v = is_max ? fmaxf(v, u) : v + u;
+  }
+  const int w = threadIdx.x >> 6;
+  __syncthreads();                       // sm reuse across the two reductions
+  if ((threadIdx.x & 63) == 0) sm[w] = v;
+  __syncthreads();
+  float r = sm[0];
+#pragma unroll
+  for (int k = 1; k < kXentFusedThreads / 64; ++k) r = is_max ? fmaxf(r, sm[k]) : r + sm[k];
+  return r;
+}
+
+template <int NV>
+__global__ void __launch_bounds__(kXentFusedThreads) xent_fused_kernel(
+    uint16_t* __restrict__ logits, const int64_t* __restrict__ target, float* __restrict__ loss,
+    int64_t V, int64_t ld, const float* __restrict__ scale_ptr) {
+  __shared__ float sm[kXentFusedThreads / 64];
+  const int64_t row = blockIdx.x;
+  uint16_t* x = logits + row * ld;
+  const int nv = static_cast<int>(V / 8);
+  u16x8 r[NV];
+  float m = -FLT_MAX;
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    const int i = threadIdx.x + k * kXentFusedThreads;
+    if (i < nv) {
+      r[k] = reinterpret_cast<const u16x8*>(x)[i];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) m = fmaxf(m, bf16_to_f32(r[k][j]));
+    }
+  }
+  const float M = block_reduce(m, true, sm);
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    const int i = threadIdx.x + k * kXentFusedThreads;
+    if (i < nv) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s += __expf(bf16_to_f32(r[k][j]) - M);
+    }
+  }
+  const float S = block_reduce(s, false, sm);
+  const float lse = M + __logf(S);
+  const int64_t t = target[row];
+  const bool valid = t >= 0 && t < V;
+  const float sc = valid ? *scale_ptr : 0.f;
+  if (!valid && threadIdx.x == 0) loss[row] = 0.f;
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    const int i = threadIdx.x + k * kXentFusedThreads;
+    if (i < nv) {
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float xv = bf16_to_f32(r[k][j]);
+        const bool hit = static_cast<int64_t>(i) * 8 + j == t;
+        if (hit) loss[row] = lse - xv;
+        v[j] = (__expf(xv - lse) - (hit ? 1.f : 0.f)) * sc;
+      }
+      store8<DT_BF16>(x, i, v);
+    }
+  }
+}
+
 }  // namespace dlbb
 
 using namespace dlbb;
+
+// In place: logits [rows, V] bf16 (row stride ld, V % 8 == 0, V <= 8 * 512 * 16) become
+// dlogits * scale; loss[row] = lse - logit[target] (0 for target < 0).
+DLBB_API int dlbb_xent_fused(void* logits, const int64_t* target, float* loss, int64_t rows,
+                             int64_t V, int64_t ld, const float* scale, hipStream_t stream) {
+  if (rows <= 0) return hipSuccess;
+  if (V % 8 || ld % 8 || (reinterpret_cast<uintptr_t>(logits) & 15)) return hipErrorInvalidValue;
+  const int64_t per = (V / 8 + kXentFusedThreads - 1) / kXentFusedThreads;
+  uint16_t* lg = static_cast<uint16_t*>(logits);
+  const dim3 g(static_cast<unsigned>(rows)), b(kXentFusedThreads);
+#define XF_LAUNCH(NV) \
+  hipLaunchKernelGGL(xent_fused_kernel<NV>, g, b, 0, stream, lg, target, loss, V, ld, scale)
+  if (per <= 4) XF_LAUNCH(4);
+  else if (per <= 8) XF_LAUNCH(8);
+  else if (per <= 13) XF_LAUNCH(13);
+  else if (per <= 16) XF_LAUNCH(16);
+#undef XF_LAUNCH
+  else return hipErrorInvalidValue;
+  return hipGetLastError();
+}
 
 // logits [rows, V] bf16 with row stride ld (elements, multiple of 8); target int64 [rows].
 DLBB_API int dlbb_xent_fwd(const void* logits, const int64_t* target, float* loss, float* lse,

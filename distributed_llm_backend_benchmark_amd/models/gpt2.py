@@ -9,7 +9,8 @@ north star asks for, built from the same gfx950 kernels as the TP model:
 * QKV / attention-out / MLP / LM-head GEMMs on the MFMA kernel with fused bias and, for c_fc,
   fused tanh-GELU (pre-activation kept for backward),
 * causal attention: our gfx950 flash forward on the fused QKV (ops.causal_attention),
-* the LM-head loss as one fused bf16 softmax-cross-entropy kernel (``ops.cross_entropy``).
+* the LM head and its loss as one op (``ops.linear_cross_entropy``): the logits are turned
+  into per-row losses and dlogits in place by one fused kernel pass.
 
 All parameters are bf16 working copies (the trainer keeps fp32 masters); vocab is padded to a
 multiple of 128 (50257 → 50304) so the tied LM-head GEMM fits the MFMA tiling.
@@ -108,10 +109,10 @@ class GPT2(nn.Module):
             d, h = blk(y, h)
             nxt = self.blocks[i + 1].ln_1 if i + 1 < len(self.blocks) else self.ln_f
             y, h = nxt(d, residual=h)
-        logits = linear_train(y, self.wte)
         if targets is None:
-            return logits
-        return ops.cross_entropy(logits, targets)
+            return linear_train(y, self.wte)
+        # LM head + loss fused: one pass over the logits makes loss and dlogits together
+        return ops.linear_cross_entropy(y, self.wte, targets)
 
     def num_parameters(self) -> int:
         return sum(p.numel() for p in self.parameters())

@@ -5,7 +5,7 @@
 * :mod:`.gemm` — MFMA bf16 GEMM with fused bias / GELU / residual epilogues.
 * :mod:`.norm_act` — fused residual+LayerNorm and bias+GELU (fwd + bwd, autograd).
 * :mod:`.optim` — flat fused AdamW.
-* :mod:`.xent` — fused softmax cross-entropy on bf16 logits.
+* :mod:`.xent` — fused softmax cross-entropy on bf16 logits; LM-head-fused linear + loss.
 * :mod:`._lib` — loader; ``available()``, ``loaded_path()``.
 """
 
@@ -15,9 +15,9 @@ from .elementwise import reduce_sum, cast, pack_rows, ChunkTable, ScaleTable, fl
 from .gemm import linear
 from .norm_act import layernorm, bias_gelu
 from .optim import FlatAdamW
-from .xent import cross_entropy
+from .xent import cross_entropy, linear_cross_entropy
 from .attention import causal_attention
 
 __all__ = ["causal_attention", "available", "loaded_path", "KernelError", "reduce_sum", "cast", "pack_rows",
            "ChunkTable", "ScaleTable", "flatten_into", "linear", "layernorm", "bias_gelu",
-           "FlatAdamW", "cross_entropy"]
+           "FlatAdamW", "cross_entropy", "linear_cross_entropy"]

@@ -1,5 +1,10 @@
 """Fused softmax cross-entropy on bf16 logits (``csrc/xent.hip``), mean reduction over the
-non-ignored rows (``ignore_index`` = any negative target)."""
+non-ignored rows (``ignore_index`` = any negative target).
+
+``linear_cross_entropy(x, w, target)`` fuses the LM head with the loss: the forward GEMM writes
+the logits, ONE kernel pass turns them in place into ``dlogits / count`` and per-row losses
+(the loss forward and backward share a single read of the logits), and the backward only
+runs the two GEMMs, with the upstream gradient applied to their small outputs / inputs."""
 
 from __future__ import annotations
 
@@ -37,6 +42,55 @@ class _XentFn(torch.autograd.Function):
                                        dx.data_ptr(), rows, V, V, scale.data_ptr(),
                                        _lib.stream(x2.device)), "xent_bwd")
         return dx.view(ctx.shape), None
+
+
+class _LinearXentFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, target):
+        from .gemm import linear
+
+        K = x.shape[-1]
+        x2 = x.reshape(-1, K)
+        if not x2.is_contiguous():
+            x2 = x2.contiguous()
+        V = w.shape[0]
+        logits = linear(x2, w)                          # [rows, V] bf16 (autotuned GEMM)
+        t = target.reshape(-1).contiguous().to(torch.int64)
+        rows = x2.shape[0]
+        loss = torch.empty(rows, dtype=torch.float32, device=x2.device)
+        inv = (1.0 / (t >= 0).sum().clamp_min(1).float()).reshape(1).contiguous()
+        check(_lib.lib().dlbb_xent_fused(logits.data_ptr(), t.data_ptr(), loss.data_ptr(), rows,
+                                         V, V, inv.data_ptr(), _lib.stream(x2.device)),
+              "xent_fused")
+        ctx.save_for_backward(x2, w, logits)            # logits now hold dlogits / count
+        ctx.shape = x.shape
+        return loss.sum() * inv.reshape(())
+
+    @staticmethod
+    def backward(ctx, g):
+        from .gemm import wgrad
+
+        x2, w, dl = ctx.saved_tensors
+        gb = g.to(dl.dtype)                             # 1.0 in the usual loss.backward()
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.matmul(dl, w).mul_(gb).view(ctx.shape)
+        if ctx.needs_input_grad[1]:
+            dw = wgrad(dl, x2 * gb)
+        return dx, dw, None
+
+
+def linear_cross_entropy(x: torch.Tensor, w: torch.Tensor, target: torch.Tensor) -> torch.Tensor:
+    """``cross_entropy(x @ w.T, target)`` (mean over rows with target >= 0), LM-head fused."""
+    from .gemm import hip_supported
+
+    V = w.shape[0]
+    if (use_hip(x, w) and x.dtype == torch.bfloat16 and V % 8 == 0 and V <= 8 * 512 * 16
+            and hip_supported(x.reshape(-1, x.shape[-1]), w)):
+        return _LinearXentFn.apply(x, w, target)
+    from .linear_fn import linear_train
+
+    return cross_entropy(linear_train(x, w), target)
 
 
 def cross_entropy(logits: torch.Tensor, target: torch.Tensor) -> torch.Tensor:

@@ -296,6 +296,29 @@ def test_cross_entropy_fwd_bwd(V):
     torch.testing.assert_close(x.grad.float(), xf.grad, rtol=2e-2, atol=2e-5)
 
 
+@pytest.mark.parametrize("V,gscale", [(50304, 1.0), (1000, 3.0), (2048, 1.0)])
+def test_linear_cross_entropy_fused(V, gscale):
+    """LM head + loss fused (one in-place pass turns logits into loss and dlogits) against the
+    fp32 torch reference of linear + cross-entropy: loss, dX and dW, with ignore_index rows and
+    an upstream gradient != 1."""
+    from distributed_llm_backend_benchmark_amd.ops import linear_cross_entropy
+
+    rows, K = 512, 256
+    x = _randn(rows, K, seed=41, scale=1.0).requires_grad_(True)
+    w = _randn(V, K, seed=42, scale=0.05).requires_grad_(True)
+    t = torch.randint(0, V, (rows,), device=DEV, generator=torch.Generator(device=DEV).manual_seed(2))
+    t[::5] = -100
+    loss = linear_cross_entropy(x, w, t)
+    (loss * gscale).backward()
+    xf = x.detach().float().requires_grad_(True)
+    wf = w.detach().float().requires_grad_(True)
+    lf = F.cross_entropy(xf @ wf.t(), t, ignore_index=-100)
+    (lf * gscale).backward()
+    torch.testing.assert_close(loss.float(), lf, rtol=2e-3, atol=2e-3)
+    torch.testing.assert_close(x.grad.float(), xf.grad, rtol=3e-2, atol=3e-4 * gscale)
+    torch.testing.assert_close(w.grad.float(), wf.grad, rtol=3e-2, atol=3e-4 * gscale)
+
+
 @pytest.mark.parametrize("M,N,K", [(64, 128, 128), (16384, 768, 768), (4096, 2304, 768),
                                    (1024, 256, 3072), (320, 384, 256), (96, 128, 256)])
 @pytest.mark.parametrize("split", [None, 1, 3])
