@@ -249,8 +249,13 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(LnBwdArgs a) {
 // partial row, and each thread keeps 8 independent loads in flight (the naive
 // one-thread-per-column loop was latency-bound: 118 us for 512 x 768 partials).
 template <int DTO>
-__global__ void __launch_bounds__(256) col_reduce_kernel(const float* __restrict__ part,
-                                                         int nparts, int cols, void* out) {
+__global__ void __launch_bounds__(256) col_reduce_kernel(const float* __restrict__ part_g,
+                                                         const float* __restrict__ part_b,
+                                                         int nparts, int cols, void* out_g,
+                                                         void* out_b, int accumulate) {
+  // blockIdx.y: 0 = dgamma, 1 = dbeta (one launch for both)
+  const float* part = blockIdx.y ? part_b : part_g;
+  void* out = blockIdx.y ? out_b : out_g;
   __shared__ float red[8][33];
   const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
   const int c = blockIdx.x * 32 + tx;
@@ -272,7 +277,9 @@ __global__ void __launch_bounds__(256) col_reduce_kernel(const float* __restrict
     float t = 0.f;
 #pragma unroll
     for (int k = 0; k < 8; ++k) t += red[k][tx];
-    Elem<DTO>::st(static_cast<typename Elem<DTO>::T*>(out), c, t);
+    auto* o = static_cast<typename Elem<DTO>::T*>(out);
+    if (accumulate) t += Elem<DTO>::ld(o, c);     // into an existing gradient (grad sinks)
+    Elem<DTO>::st(o, c, t);
   }
 }
 
@@ -432,7 +439,7 @@ DLBB_API int dlbb_layernorm_bwd_grid(int64_t rows) {
 DLBB_API int dlbb_layernorm_bwd(const void* dy, const void* h, const void* gamma, int param_dtype,
                                 const float* mean, const float* rstd, const void* dres, void* dx,
                                 float* part_ws, void* dgamma, void* dbeta, int64_t rows,
-                                int cols, hipStream_t stream) {
+                                int cols, int accumulate, hipStream_t stream) {
   if (rows <= 0) return hipSuccess;
   if (cols % 256 != 0) return hipErrorInvalidValue;
   const int grid = dlbb_layernorm_bwd_grid(rows);
@@ -453,15 +460,12 @@ DLBB_API int dlbb_layernorm_bwd(const void* dy, const void* h, const void* gamma
   }
 #undef LB
   if (e != hipSuccess) return e;
-  const dim3 cg((cols + 31) / 32), cb(256);
-  if (param_dtype == DT_F32) {
-    hipLaunchKernelGGL((col_reduce_kernel<DT_F32>), cg, cb, 0, stream, pg, grid, cols, dgamma);
-    if (dbeta)
-      hipLaunchKernelGGL((col_reduce_kernel<DT_F32>), cg, cb, 0, stream, pb, grid, cols, dbeta);
-  } else {
-    hipLaunchKernelGGL((col_reduce_kernel<DT_BF16>), cg, cb, 0, stream, pg, grid, cols, dgamma);
-    if (dbeta)
-      hipLaunchKernelGGL((col_reduce_kernel<DT_BF16>), cg, cb, 0, stream, pb, grid, cols, dbeta);
-  }
+  const dim3 cg((cols + 31) / 32, dbeta ? 2 : 1), cb(256);
+  if (param_dtype == DT_F32)
+    hipLaunchKernelGGL((col_reduce_kernel<DT_F32>), cg, cb, 0, stream, pg, pb, grid, cols, dgamma,
+                       dbeta, accumulate);
+  else
+    hipLaunchKernelGGL((col_reduce_kernel<DT_BF16>), cg, cb, 0, stream, pg, pb, grid, cols,
+                       dgamma, dbeta, accumulate);
   return hipGetLastError();
 }

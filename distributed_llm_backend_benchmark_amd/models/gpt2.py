@@ -51,6 +51,7 @@ class LN(nn.Module):
         super().__init__()
         self.weight = nn.Parameter(torch.ones(d, device=device, dtype=torch.bfloat16))
         self.bias = nn.Parameter(torch.zeros(d, device=device, dtype=torch.bfloat16))
+        self.weight._dlbb_single_use = self.bias._dlbb_single_use = True   # see Block
 
     def forward(self, x, residual=None):
         y, h = ops.layernorm(x, self.weight, self.bias, 1e-5, residual=residual)

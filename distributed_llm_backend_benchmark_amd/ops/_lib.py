@@ -44,7 +44,7 @@ _SIGS = {
     "dlbb_layernorm_bwd_grid": (c_int, [c_int64]),
     "dlbb_layernorm_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p,
                                    c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64,
-                                   c_int, c_void_p]),
+                                   c_int, c_int, c_void_p]),
     "dlbb_bias_gelu_fwd": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int, c_int,
                                    c_void_p]),
     "dlbb_bias_gelu_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64,

@@ -43,6 +43,7 @@ class _FusedAddLayerNorm(torch.autograd.Function):
         ctx.save_for_backward(hin, weight, mean, rstd)
         ctx.has_res = residual is not None
         ctx.has_bias = bias is not None
+        ctx.params = (weight, bias)       # leaf parameters: only read for their grad sinks
         ctx.shape = shape
         if h is not None:
             return y.view(shape), h.view(shape)
@@ -60,13 +61,24 @@ class _FusedAddLayerNorm(torch.autograd.Function):
         grid = _lib.lib().dlbb_layernorm_bwd_grid(rows)
         ws = torch.empty((2 if ctx.has_bias else 1) * grid * cols, dtype=torch.float32,
                          device=hin.device)
-        dw = torch.empty_like(weight)
-        db = torch.empty_like(weight) if ctx.has_bias else None
+        # gradient sinks (ops.linear_fn): dγ/dβ accumulate straight into the trainer's views
+        from .linear_fn import _sink
+
+        w_p, b_p = ctx.params
+        w_sink, b_sink = _sink(w_p), (_sink(b_p) if ctx.has_bias else None)
+        direct = w_sink is not None and (not ctx.has_bias or b_sink is not None)
+        dw = w_p.grad if direct else torch.empty_like(weight)
+        db = (b_p.grad if direct else torch.empty_like(weight)) if ctx.has_bias else None
         check(_lib.lib().dlbb_layernorm_bwd(
             dy2.data_ptr(), hin.data_ptr(), weight.data_ptr(), dt(weight), mean.data_ptr(),
             rstd.data_ptr(), _lib.ptr(dh2), dx.data_ptr(), ws.data_ptr(), dw.data_ptr(),
-            _lib.ptr(db), rows, cols, _lib.stream(hin.device)), "layernorm_bwd")
+            _lib.ptr(db), rows, cols, int(direct), _lib.stream(hin.device)), "layernorm_bwd")
         dxv = dx.view(ctx.shape)
+        if direct:
+            w_sink(w_p)
+            if ctx.has_bias:
+                b_sink(b_p)
+            return dxv, (dxv if ctx.has_res else None), None, None, None
         return dxv, (dxv if ctx.has_res else None), dw, db, None
 
 

@@ -337,7 +337,7 @@ def test_gpt2_grad_sinks_match_autograd():
     ref(idx, idx).backward()
     m = GPT2(cfg, device=dev, seed=11)
     tr = FlatParamTrainer(m, None, lr=1e-3, bucket_mb=0.25)
-    assert sum(hasattr(p, "_dlbb_grad_sink") for p in m.parameters()) == 8 * cfg.n_layer
+    assert sum(hasattr(p, "_dlbb_grad_sink") for p in m.parameters()) == 12 * cfg.n_layer + 2
     for _ in range(2):                      # second pass: buffers reused, zeroed, re-counted
         tr.zero_grad()
         tr._reset()
