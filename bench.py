@@ -103,6 +103,10 @@ def main(argv=None) -> int:
             # in place on an IPC-registered buffer: no copy-in / staging pass
             cands += [(f"custom_reg/nb{nb}", "custom_reg", {"nblocks": nb})
                       for nb in (64, 128, 256)]
+            if car.push_healthy and flat.numel() * flat.element_size() <= car.capacity:
+                # same traffic as posted remote writes (peer staging + result pushes)
+                cands += [(f"custom_push/nb{nb}", "custom_reg", {"nblocks": nb, "push": True})
+                          for nb in (128, 256)]
         if args.impl == "custom" and not cands:
             raise SystemExit("custom all-reduce unavailable (setup or self-test failed)")
     trial = {}

@@ -322,6 +322,92 @@ __global__ void __launch_bounds__(kCarThreads) car_twoshot_reg_kernel(CarKernelA
   wait_peers(a, 2, e);
 }
 
+// Registered two-shot, PUSH form (in place): the same traffic per link as the pull form, but
+// every byte crosses xGMI as a posted remote WRITE instead of a read round trip.
+//   reduce-scatter push: shard p of my buffer -> slot `rank` of rank p's staging half (tmp[e&1])
+//   flag barrier 0 ; reduce the world slots of my staging half (local reads) and push the result
+//   into shard `rank` of every rank's buffer (mine included) ; flag barrier 1 (my buffer is
+//   complete once every peer's pushes into it have landed).
+// Staging halves alternate by epoch parity: a rank writes half e&1 of a peer in call e only
+// after passing barrier 1 of call e-1, i.e. after that peer finished reducing call e-2's half.
+// Requires nbytes <= cap (world slots of nbytes / world each).
+template <int DT, int W>
+__global__ void __launch_bounds__(kCarThreads) car_twoshot_push_kernel(CarKernelArgs a) {
+  constexpr int64_t kVecBytes = 8 * Elem<DT>::kBytes;
+  constexpr int kQ = kVecBytes / 16;
+  const uint32_t e = begin_epoch(a);
+  const int64_t half = (e & 1) * a.cap;
+  const int64_t shard_vec = a.nbytes / kVecBytes / a.world;
+  const int64_t shard_bytes = shard_vec * kVecBytes;
+  const int64_t per = (shard_vec + gridDim.x - 1) / gridDim.x;
+  const int64_t s0 = blockIdx.x * per;
+  const int64_t s1 = s0 + per < shard_vec ? s0 + per : shard_vec;
+  const char* mine = a.data[a.rank];
+  const int64_t my_slot = half + a.rank * shard_bytes;
+  if constexpr (W > 0) {
+    for (int64_t v = s0 + threadIdx.x; v < s1; v += blockDim.x) {
+      u16x8 t[W][kQ];
+#pragma unroll
+      for (int k = 0; k < W; ++k) {
+        const int p = (a.rank + k) & (W - 1);
+#pragma unroll
+        for (int q = 0; q < kQ; ++q)
+          t[k][q] = reinterpret_cast<const u16x8*>(mine + (p * shard_vec + v) * kVecBytes)[q];
+      }
+#pragma unroll
+      for (int k = 0; k < W; ++k) {
+        const int p = (a.rank + k) & (W - 1);
+#pragma unroll
+        for (int q = 0; q < kQ; ++q)
+          reinterpret_cast<u16x8*>(a.tmp[p] + my_slot + v * kVecBytes)[q] = t[k][q];
+      }
+    }
+  } else {
+    for (int k = 0; k < a.world; ++k) {
+      const int p = (a.rank + k) % a.world;
+      for (int64_t v = s0 + threadIdx.x; v < s1; v += blockDim.x)
+#pragma unroll
+        for (int q = 0; q < kQ; ++q)
+          reinterpret_cast<u16x8*>(a.tmp[p] + my_slot + v * kVecBytes)[q] =
+              reinterpret_cast<const u16x8*>(mine + (p * shard_vec + v) * kVecBytes)[q];
+    }
+  }
+  signal_peers(a, 0, e);
+  if (!wait_peers(a, 0, e)) return;
+  const char* stage = a.tmp[a.rank] + half;
+  const int64_t out_off = a.rank * shard_bytes;
+  for (int64_t v = s0 + threadIdx.x; v < s1; v += blockDim.x) {
+    float acc[8];
+    load8<DT>(stage, v, acc);
+    if constexpr (W > 0) {
+      float x[W - 1][8];
+#pragma unroll
+      for (int k = 1; k < W; ++k) load8<DT>(stage + k * shard_bytes, v, x[k - 1]);
+#pragma unroll
+      for (int k = 1; k < W; ++k)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[j] += x[k - 1][j];
+    } else {
+      for (int k = 1; k < a.world; ++k) {
+        float x[8];
+        load8<DT>(stage + k * shard_bytes, v, x);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[j] += x[j];
+      }
+    }
+    if constexpr (W > 0) {
+#pragma unroll
+      for (int k = 0; k < W; ++k)
+        store8<DT>(a.data[(a.rank + k) & (W - 1)] + out_off, v, acc);
+    } else {
+      for (int k = 0; k < a.world; ++k)
+        store8<DT>(a.data[(a.rank + k) % a.world] + out_off, v, acc);
+    }
+  }
+  signal_peers(a, 1, e);
+  wait_peers(a, 1, e);
+}
+
 // ---- direct (one-hop) collectives on registered inputs --------------------------------------
 // Every GPU reads its peers' registered input buffers over its own xGMI link to each of them, so
 // all 7 links of a GPU carry traffic at once (an RCCL ring uses one link in and one out per
@@ -396,6 +482,14 @@ void launch_direct(int kind, int dtype, dim3 g, dim3 b, hipStream_t st, const Ca
   else if (dtype == DT_BF16) hipLaunchKernelGGL((car_rs_kernel<DT_BF16, W>), g, b, 0, st, a);
   else if (dtype == DT_F16) hipLaunchKernelGGL((car_rs_kernel<DT_F16, W>), g, b, 0, st, a);
   else hipLaunchKernelGGL((car_rs_kernel<DT_F32, W>), g, b, 0, st, a);
+}
+
+template <int DT>
+void launch_push(int w, dim3 g, dim3 b, hipStream_t st, const CarKernelArgs& a) {
+  if (w == 2) hipLaunchKernelGGL((car_twoshot_push_kernel<DT, 2>), g, b, 0, st, a);
+  else if (w == 4) hipLaunchKernelGGL((car_twoshot_push_kernel<DT, 4>), g, b, 0, st, a);
+  else if (w == 8) hipLaunchKernelGGL((car_twoshot_push_kernel<DT, 8>), g, b, 0, st, a);
+  else hipLaunchKernelGGL((car_twoshot_push_kernel<DT, 0>), g, b, 0, st, a);
 }
 
 struct RegBuf {
@@ -663,6 +757,33 @@ DLBB_API int dlbb_car_allreduce_reg(void* h, int id, int64_t n, int dtype, int n
   else if (dtype == DT_F16) CAR_RW(DT_F16);
   else CAR_RW(DT_F32);
 #undef CAR_RW
+  return hipGetLastError();
+}
+
+// Push form of the registered two-shot (see car_twoshot_push_kernel); nbytes <= capacity.
+DLBB_API int dlbb_car_allreduce_reg_push(void* h, int id, int64_t n, int dtype, int nblocks,
+                                         hipStream_t stream) {
+  CarState* s = static_cast<CarState*>(h);
+  if (!s->opened || id < 0 || id >= static_cast<int>(s->regs.size())) return hipErrorInvalidValue;
+  const RegBuf& r = s->regs[id];
+  const int64_t esz = dtype == DT_F32 ? 4 : 2;
+  const int64_t nbytes = n * esz;
+  if (nbytes <= 0) return hipSuccess;
+  if (nbytes > r.bytes || nbytes > s->cap || nbytes % (8 * esz * s->world) != 0)
+    return hipErrorInvalidValue;
+  if (s->world == 1) return hipSuccess;
+  if (nblocks < 1) nblocks = 1;
+  if (nblocks > kMaxBlocks) nblocks = kMaxBlocks;
+  CarKernelArgs a = s->args;               // tmp[] = every rank's staging region
+  for (int p = 0; p < kMaxRanks; ++p) a.data[p] = r.ptr[p];
+  a.inp = r.ptr[s->rank];
+  a.out = r.ptr[s->rank];
+  a.nbytes = nbytes;
+  const dim3 g(nblocks), b(kCarThreads);
+  const int w = s->world == 2 || s->world == 4 || s->world == 8 ? s->world : 0;
+  if (dtype == DT_BF16) launch_push<DT_BF16>(w, g, b, stream, a);
+  else if (dtype == DT_F16) launch_push<DT_F16>(w, g, b, stream, a);
+  else launch_push<DT_F32>(w, g, b, stream, a);
   return hipGetLastError();
 }
 

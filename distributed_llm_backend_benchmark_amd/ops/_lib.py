@@ -99,6 +99,7 @@ _SIGS = {
     "dlbb_car_reg_open": (c_int, [c_void_p, c_void_p, c_int64, c_void_p,
                                   ctypes.POINTER(c_int64), ctypes.POINTER(c_int)]),
     "dlbb_car_allreduce_reg": (c_int, [c_void_p, c_int, c_int64, c_int, c_int, c_void_p]),
+    "dlbb_car_allreduce_reg_push": (c_int, [c_void_p, c_int, c_int64, c_int, c_int, c_void_p]),
     "dlbb_car_direct_reg": (c_int, [c_void_p, c_int, c_int, c_int64, c_int, c_void_p, c_int,
                                     c_void_p]),
     "dlbb_car_error": (c_int, [c_void_p]),

@@ -127,6 +127,7 @@ class AllReduce(CollectiveOp):
         impl = self.opts.get("impl", "rccl")
         self._custom = None
         self._reg_id = None
+        self._push = False
         self.nblocks = self.opts.get("nblocks")
         multi_gpu = self.comm.is_gpu and self.comm.world_size > 1
         if impl in ("custom", "custom_reg", "auto") and multi_gpu:
@@ -138,6 +139,11 @@ class AllReduce(CollectiveOp):
                 # every rank alike)
                 if car is None or not car.reg_healthy or not car.supports_registered(self.buf):
                     raise RuntimeError("registered custom all-reduce unavailable for "
+                                       f"{self.buf.numel()} x {self.buf.dtype}")
+                self._push = bool(self.opts.get("push"))
+                if self._push and (not car.push_healthy
+                                   or self.buf.numel() * self.buf.element_size() > car.capacity):
+                    raise RuntimeError("push-form registered all-reduce unavailable for "
                                        f"{self.buf.numel()} x {self.buf.dtype}")
                 self._reg_id = car.register(self.buf)
                 self._custom = car
@@ -159,7 +165,8 @@ class AllReduce(CollectiveOp):
 
     def run(self):
         if self._reg_id is not None:
-            self._custom.all_reduce_registered(self.buf, self._reg_id, nblocks=self.nblocks)
+            self._custom.all_reduce_registered(self.buf, self._reg_id, nblocks=self.nblocks,
+                                               push=self._push)
         elif self._custom is not None:
             self._custom.all_reduce_(self.buf, algo=self.algo, nblocks=self.nblocks)
         else:

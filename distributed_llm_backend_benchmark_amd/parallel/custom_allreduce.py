@@ -77,6 +77,7 @@ class CustomAllReduce:
         self.nblocks = nblocks
         self.healthy = False
         self.reg_healthy = False
+        self.push_healthy = False
         self._regs: Dict[tuple, int] = {}
         self._reg_keep = []
 
@@ -145,13 +146,16 @@ class CustomAllReduce:
         nbytes = t.numel() * t.element_size()
         return nbytes > 0 and nbytes % (8 * t.element_size() * self.comm.world_size) == 0
 
-    def all_reduce_registered(self, t: torch.Tensor, rid: int,
-                              nblocks: Optional[int] = None) -> torch.Tensor:
-        """In-place two-shot on registration ``rid`` (``t`` must be the registered tensor)."""
+    def all_reduce_registered(self, t: torch.Tensor, rid: int, nblocks: Optional[int] = None,
+                              push: bool = False) -> torch.Tensor:
+        """In-place two-shot on registration ``rid`` (``t`` must be the registered tensor).
+        ``push``: remote writes into the peers' staging halves + result pushes instead of
+        remote reads (needs ``t`` to fit the staging capacity)."""
         nbytes = t.numel() * t.element_size()
         nb = nblocks or self.nblocks or int(min(256, max(1, nbytes // (256 << 10))))
-        _lib.check(self.lib.dlbb_car_allreduce_reg(self.h, rid, t.numel(), _lib.dt(t), nb,
-                                                   _lib.stream(t.device)), "car_allreduce_reg")
+        fn = self.lib.dlbb_car_allreduce_reg_push if push else self.lib.dlbb_car_allreduce_reg
+        _lib.check(fn(self.h, rid, t.numel(), _lib.dt(t), nb, _lib.stream(t.device)),
+                   "car_allreduce_reg" + ("_push" if push else ""))
         return t
 
     def _direct(self, kind: int, t: torch.Tensor, rid: int, out: torch.Tensor, nbytes: int,
@@ -240,33 +244,39 @@ class CustomAllReduce:
         return self.healthy
 
     def _self_test_registered(self) -> None:
-        """Registered in-place two-shot vs RCCL (two calls: reuse of one registration);
-        ``reg_healthy`` only if it passes on every rank."""
+        """Registered in-place two-shot, pull and push forms, vs RCCL (two calls each: reuse of
+        one registration, both staging halves); ``reg_healthy`` / ``push_healthy`` only if the
+        form passes on every rank."""
         dev, W = self.comm.device, self.comm.world_size
-        ok = True
+        ok = {False: True, True: True}
         try:
             n = 1 << 20
             buf = torch.empty(n, device=dev, dtype=torch.bfloat16)
             rid = self.register(buf)
-            for it in range(2):
-                g = torch.Generator(device=dev)
-                g.manual_seed(777 + 31 * it + self.comm.rank)
-                x = torch.randn(n, generator=g, device=dev).to(torch.bfloat16)
-                ref = x.float().clone()
-                if W > 1:
-                    dist.all_reduce(ref)
-                buf.copy_(x)
-                self.all_reduce_registered(buf, rid)
-                torch.cuda.synchronize(dev)
-                ok = ok and bool(torch.allclose(buf.float(), ref, rtol=2e-2, atol=5e-2 * W))
-                ok = ok and self.check_error() == 0
-        except Exception:  # noqa: BLE001 - a failed registration/launch is a failed test
-            ok = False
-        flags = self.comm.all_gather_object(bool(ok))
-        self.reg_healthy = all(flags)
-        if not self.reg_healthy and self.comm.rank == 0:
-            print("[custom all-reduce] registered-buffer self-test failed on ranks "
-                  f"{[i for i, f in enumerate(flags) if not f]}", flush=True)
+            for push in (False, True):
+                for it in range(2):
+                    g = torch.Generator(device=dev)
+                    g.manual_seed(777 + 31 * it + 7 * push + self.comm.rank)
+                    x = torch.randn(n, generator=g, device=dev).to(torch.bfloat16)
+                    ref = x.float().clone()
+                    if W > 1:
+                        dist.all_reduce(ref)
+                    buf.copy_(x)
+                    try:
+                        self.all_reduce_registered(buf, rid, push=push)
+                        torch.cuda.synchronize(dev)
+                        good = bool(torch.allclose(buf.float(), ref, rtol=2e-2, atol=5e-2 * W))
+                        ok[push] = ok[push] and good and self.check_error() == 0
+                    except Exception:  # noqa: BLE001 - a failed launch is a failed test
+                        ok[push] = False
+        except Exception:  # noqa: BLE001 - a failed registration fails both forms
+            ok = {False: False, True: False}
+        flags = self.comm.all_gather_object((bool(ok[False]), bool(ok[True])))
+        self.reg_healthy = all(f[0] for f in flags)
+        self.push_healthy = self.reg_healthy and all(f[1] for f in flags)
+        if not self.push_healthy and self.comm.rank == 0:
+            print("[custom all-reduce] registered-buffer self-test failed (pull/push per rank): "
+                  f"{flags}", flush=True)
 
     def close(self) -> None:
         if getattr(self, "h", None):

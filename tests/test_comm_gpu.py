@@ -140,21 +140,22 @@ def _car_reg_worker(rank, world, n):
     comm = init_distributed("gloo", device="cuda")
     car = CustomAllReduce(comm, capacity_bytes=8 << 20)
     car.self_test()
-    ok = [("self_test", car.healthy, car.reg_healthy)]
+    ok = [("self_test", car.healthy, car.reg_healthy and car.push_healthy)]
     buf = torch.empty(n, device="cuda", dtype=torch.bfloat16)
     rid = car.register(buf)
     assert car.register(buf) == rid            # idempotent
     # interleave registered calls (grid sizes 1..256) with staging-buffer calls of other grid
     # sizes: the epoch (and buffer half) must stay consistent across workgroups and calls
     plan = [("reg", 256), ("copy2", 7), ("reg", 64), ("copy1", 3), ("reg", 1), ("copy2", 128),
-            ("reg", 200), ("reg", 256), ("copy1", 32), ("reg", 33)]
+            ("reg", 200), ("push", 256), ("push", 5), ("reg", 256), ("push", 128), ("copy1", 32),
+            ("push", 1), ("reg", 33), ("push", 64)]
     for it, (kind, nb) in enumerate(plan):
         xs = [torch.randn(n, generator=torch.Generator(device="cuda").manual_seed(
             1000 * r + it), device="cuda").to(torch.bfloat16) for r in range(world)]
         ref = sum(x.float() for x in xs)
-        if kind == "reg":
+        if kind in ("reg", "push"):
             buf.copy_(xs[rank])
-            out = car.all_reduce_registered(buf, rid, nblocks=nb)
+            out = car.all_reduce_registered(buf, rid, nblocks=nb, push=kind == "push")
         else:
             out = car.all_reduce(xs[rank].clone(), algo=ONESHOT if kind == "copy1" else TWOSHOT,
                                  nblocks=nb)
@@ -169,8 +170,9 @@ def _car_reg_worker(rank, world, n):
 
 @pytest.mark.parametrize("world", [2, 4, 8])
 def test_custom_allreduce_registered_ranks_on_one_gpu(world):
-    """Registered in-place two-shot (IPC-mapped user buffers, 3 flag phases) with 2/4/8 ranks
-    sharing one GPU, interleaved with staging-buffer calls of different grid sizes."""
+    """Registered in-place two-shot, pull form (IPC-mapped user buffers, 3 flag phases) and
+    push form (remote writes into peer staging halves), with 2/4/8 ranks sharing one GPU,
+    interleaved with staging-buffer calls of different grid sizes."""
     res = run_multiprocess(_car_reg_worker, world, args=(world * 8 * 4096 + world * 8 * 3,),
                            timeout=600)
     for r in res:
