@@ -188,7 +188,7 @@ class AllGather(CollectiveOp):
     def setup(self):
         self.form = self.opts.get("form", "tensor")
         n = self.data.numel()
-        self.impl, self._car = "rccl", None
+        self._car = None
         if self.form == "list":
             self.outs = [torch.empty_like(self.data) for _ in range(self.P)]
         else:
@@ -234,7 +234,7 @@ class ReduceScatter(CollectiveOp):
         self.inp = self.data.reshape(-1)[:n].contiguous()
         self.out = torch.empty(n // self.P, dtype=self.data.dtype, device=self.data.device)
         self._native = True
-        self.impl, self._car = "rccl", None
+        self._car = None
         if self.opts.get("direct"):
             self._car, self._rid = _direct_ipc(self.comm, self.inp,
                                                16 // self.inp.element_size() * self.P)
@@ -352,7 +352,7 @@ class AllToAll(CollectiveOp):
         n = self.data.numel() - self.data.numel() % self.P
         self.inp = self.data.reshape(-1)[:n].contiguous()
         self.out = torch.empty_like(self.inp)
-        self.impl, self._car = "rccl", None
+        self._car = None
         if self.opts.get("direct"):
             self._car, self._rid = _direct_ipc(self.comm, self.inp,
                                                16 // self.inp.element_size() * self.P)

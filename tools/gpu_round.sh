@@ -1,0 +1,28 @@
+#!/bin/bash
+# Round validation + evidence: full GPU test suite, smoke, bench (world 1), TP 7B forward,
+# GPT-2 DDP step, rocprofv3 kernel stats of the GPT-2 step. Each GPU step has its own limit;
+# the first failing step ends the call.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+R=$(pwd)
+mkdir -p gpurun_out
+export HSA_ENABLE_IPC_MODE_LEGACY=0
+python -c "import __graft_entry__ as g; g.build()" > gpurun_out/build.log 2>&1 || { cat gpurun_out/build.log; exit 1; }
+step() {  # step <name> <timeout> <cmd...>
+  local name=$1 t=$2; shift 2
+  echo "=== $name ($(date +%T))"
+  timeout -k 10 "$t" "$@" > "$R/gpurun_out/$name.log" 2>&1
+  local rc=$?
+  tail -3 "$R/gpurun_out/$name.log"
+  echo "=== $name rc=$rc"
+  [ $rc -ne 0 ] && exit $rc
+  return 0
+}
+step pytest_gpu 900 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 300
+step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
+step bench 600 python bench.py
+step tp7b 600 python -m distributed_llm_backend_benchmark_amd.cli.run_tp --config config/7b_config.yaml --backend rccl --output-dir gpurun_out/tp
+step gpt2 600 python -m distributed_llm_backend_benchmark_amd.cli.train_ddp --steps 30 --warmup 5 --output gpurun_out/gpt2.json
+cd /tmp && export TMPDIR=/tmp PYTHONPATH=$R
+step prof_gpt2 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/prof_gpt2" -o gpt2 -- python3 -m distributed_llm_backend_benchmark_amd.cli.train_ddp --steps 5 --warmup 2
+echo done
