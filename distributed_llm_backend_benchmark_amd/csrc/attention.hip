@@ -391,8 +391,21 @@ __global__ void __launch_bounds__(kAttnThreads, 2) attn_bwd_dkdv_d64_kernel(Attn
   const int ns = (a.T - kb0 + kSlice - 1) / kSlice;
   auto imgQ = [&](int c) { return smem + c * 2 * kSliceImg; };
   auto imgG = [&](int c) { return smem + c * 2 * kSliceImg + kSliceImg; };
+  // per-slice row constants (LSE, delta of the slice's 64 queries) ride the same LDS-DMA
+  // double buffer as the Q / dO images instead of being loaded from global memory right
+  // before use: waves 0 / 1 stage one 256-B row each (rows past T clamped, as for Q / dO)
+  auto rowv = [&](int c) { return reinterpret_cast<float*>(smem + 4 * kSliceImg + c * 512); };
+  auto stage_rows = [&](int q0, int c) {
+    if (wave < 2) {
+      int t = q0 + lane;
+      t = t < a.T ? t : a.T - 1;
+      __builtin_amdgcn_global_load_lds((wave == 0 ? lrow : drow) + t,
+                                       (lds_vptr_t)(rowv(c) + 64 * wave), 4, 0, 0);
+    }
+  };
   stage64(base_bt + hoff, a.ld, kb0, a.T, imgQ(0), wave, lane);
   stage64(dout_bt + hoff, a.ldo, kb0, a.T, imgG(0), wave, lane);
+  stage_rows(kb0, 0);
   for (int i = 0; i < ns; ++i) {
     const int cur = i & 1;
     const int qs = kb0 + i * kSlice;
@@ -401,36 +414,25 @@ __global__ void __launch_bounds__(kAttnThreads, 2) attn_bwd_dkdv_d64_kernel(Attn
     if (i + 1 < ns) {
       stage64(base_bt + hoff, a.ld, qs + kSlice, a.T, imgQ(cur ^ 1), wave, lane);
       stage64(dout_bt + hoff, a.ldo, qs + kSlice, a.T, imgG(cur ^ 1), wave, lane);
+      stage_rows(qs + kSlice, cur ^ 1);
     }
     const char* iq = imgQ(cur);
     const char* ig = imgG(cur);
+    const float* rv = rowv(cur);
 #pragma unroll
     for (int sub = 0; sub < 2; ++sub) {
       const int qsub = qs + 32 * sub;
       if (qsub + 31 < kw) continue;                 // wave-uniform: every query < every key
       const int rb = 32 * sub;                      // image row base of this 32-query block
-      // per-row constants for rows q = qsub + 8 g + 4 hi + u (register e = 4 g + u): 4 rows
-      // per float4 when the block is whole (a tail block clamps row by row)
+      // per-row constants for rows q = qsub + 8 g + 4 hi + u (register e = 4 g + u)
       float l2[16], dl[16];
-      if (qsub + 32 <= a.T && (a.T & 3) == 0) {
 #pragma unroll
-        for (int g4 = 0; g4 < 4; ++g4) {
-          const float4 lv = *reinterpret_cast<const float4*>(lrow + qsub + 8 * g4 + 4 * hi);
-          const float4 dv4 = *reinterpret_cast<const float4*>(drow + qsub + 8 * g4 + 4 * hi);
-          l2[4 * g4 + 0] = lv.x; l2[4 * g4 + 1] = lv.y; l2[4 * g4 + 2] = lv.z; l2[4 * g4 + 3] = lv.w;
-          dl[4 * g4 + 0] = dv4.x; dl[4 * g4 + 1] = dv4.y; dl[4 * g4 + 2] = dv4.z;
-          dl[4 * g4 + 3] = dv4.w;
-        }
-      } else {
-#pragma unroll
-        for (int g4 = 0; g4 < 4; ++g4)
-#pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            int q = qsub + 8 * g4 + 4 * hi + u;
-            q = q < a.T ? q : a.T - 1;
-            l2[4 * g4 + u] = lrow[q];
-            dl[4 * g4 + u] = drow[q];
-          }
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const float4 lv = *reinterpret_cast<const float4*>(rv + rb + 8 * g4 + 4 * hi);
+        const float4 dv4 = *reinterpret_cast<const float4*>(rv + 64 + rb + 8 * g4 + 4 * hi);
+        l2[4 * g4 + 0] = lv.x; l2[4 * g4 + 1] = lv.y; l2[4 * g4 + 2] = lv.z; l2[4 * g4 + 3] = lv.w;
+        dl[4 * g4 + 0] = dv4.x; dl[4 * g4 + 1] = dv4.y; dl[4 * g4 + 2] = dv4.z;
+        dl[4 * g4 + 3] = dv4.w;
       }
       f32x16 s, dp;
 #pragma unroll
@@ -637,7 +639,7 @@ DLBB_API int dlbb_attn_bwd(const void* qkv, int64_t ld, const void* out, const v
                 static_cast<uint16_t*>(dqkv), ld, ldo, B, T, H,
                 scale * 1.4426950408889634f, scale, g_attn_xcd};
   hipLaunchKernelGGL(attn_bwd_dkdv_d64_kernel, dim3((T + kBwdKeys - 1) / kBwdKeys, H, B),
-                     dim3(kAttnThreads), 4 * kSliceImg, stream, a);
+                     dim3(kAttnThreads), 4 * kSliceImg + 1024, stream, a);
   hipLaunchKernelGGL(attn_bwd_dq_d64_kernel, dim3((T + kQB - 1) / kQB, H, B),
                      dim3(kAttnThreads), 4 * kTileKV, stream, a);
   return hipGetLastError();
