@@ -13,6 +13,7 @@ parameter with ``_dlbb_grad_sink = callback`` (only for parameters used ONCE per
 model opts in with ``_dlbb_single_use``). The backward then accumulates dW / db straight into
 ``param.grad`` inside the weight-gradient kernel's reduce pass, calls ``callback(param)`` and
 returns no gradient for it — no separate gradient tensor and no AccumulateGrad add kernel.
+With ``_dlbb_grad_stream`` also set, that weight-gradient GEMM runs on the given side stream.
 """
 
 from __future__ import annotations
@@ -77,8 +78,20 @@ class _LinearFn(torch.autograd.Function):
         w_sink = _sink(ctx.weight) if ctx.needs_input_grad[1] else None
         b_sink = _sink(ctx.bias) if fuse_db else None
         if w_sink is not None and (not want_db or b_sink is not None):
-            wgrad(du, x2, out=ctx.weight.grad, accumulate=True,
-                  bias_out=ctx.bias.grad if want_db else None)
+            side = getattr(ctx.weight, "_dlbb_grad_stream", None)
+            if side is not None:
+                # dW is off the backward's critical path: run it on the trainer's side stream
+                # so it overlaps the next layer's dgrad / memory-bound kernels; the trainer
+                # orders its bucket reductions and the optimizer after that stream
+                side.wait_stream(torch.cuda.current_stream(du.device))
+                with torch.cuda.stream(side):
+                    wgrad(du, x2, out=ctx.weight.grad, accumulate=True,
+                          bias_out=ctx.bias.grad if want_db else None)
+                du.record_stream(side)
+                x2.record_stream(side)
+            else:
+                wgrad(du, x2, out=ctx.weight.grad, accumulate=True,
+                      bias_out=ctx.bias.grad if want_db else None)
             w_sink(ctx.weight)
             if want_db:
                 b_sink(ctx.bias)

@@ -20,6 +20,8 @@ optimizer memory drops by P.
 
 from __future__ import annotations
 
+import contextlib
+
 from typing import List, Tuple
 
 import torch
@@ -63,10 +65,17 @@ class ShardedTrainer(FlatParamTrainer):
         b.launched = True
         src, dst, n = self._chunks[b.idx]
         out = self.grad_shard[dst:dst + n]
-        if self.world == 1:
-            out.copy_(self.flat_grad[b.start:b.end])
-            return
-        b.work = dist.reduce_scatter_tensor(out, self.flat_grad[b.start:b.end], async_op=True)
+        ws = self._wgrad_stream
+        if ws is not None:
+            # bucket complete on main AND side stream (sink weight gradients): issue from the
+            # side stream after it joined the main one; finish() joins it back
+            ws.wait_stream(torch.cuda.current_stream(out.device))
+        with torch.cuda.stream(ws) if ws is not None else contextlib.nullcontext():
+            if self.world == 1:
+                out.copy_(self.flat_grad[b.start:b.end])
+                return
+            b.work = dist.reduce_scatter_tensor(out, self.flat_grad[b.start:b.end],
+                                                async_op=True)
 
     def _optimizer_step(self) -> None:
         self.opt.step(self.grad_shard, working_bf16=self.param_shard,
