@@ -26,6 +26,15 @@ ACTS = {None: 0, "none": 0, "gelu": EPI_GELU_ERF, "gelu_erf": EPI_GELU_ERF,
         "gelu_tanh": EPI_GELU_TANH}
 
 FALLBACKS = {"count": 0}
+TUNE_LOG = []         # (kind, key, {impl: median ms}, choice) per autotuned shape
+
+
+def _log_tune(kind, key, times, best) -> None:
+    TUNE_LOG.append((kind, key, times, best))
+    if os.environ.get("DLBB_TUNE_LOG") == "1":
+        import sys
+
+        print(f"[tune] {kind} {key} {times} -> {best}", file=sys.stderr, flush=True)
 
 
 def set_tile(tile: int) -> None:
@@ -135,7 +144,7 @@ def _autotune(key, args) -> str:
         return CHOICES[key]
     if torch.cuda.is_current_stream_capturing():
         return "mfma"
-    best, best_t = "mfma", float("inf")
+    best, best_t, times = "mfma", float("inf"), {}
     for name, fn in _IMPLS.items():
         for _ in range(2):
             fn(*args)
@@ -148,9 +157,11 @@ def _autotune(key, args) -> str:
             e.synchronize()
             ts.append(s.elapsed_time(e))
         t = sorted(ts)[len(ts) // 2]
+        times[name] = round(t, 4)
         if t < best_t:
             best, best_t = name, t
     CHOICES[key] = best
+    _log_tune("linear", key, times, best)
     return best
 
 
@@ -255,7 +266,7 @@ def _wgrad_choice(dy2, x2, out, bias_out=None) -> str:
         return "mfma"
     scratch = torch.empty_like(out)
     scratch_b = torch.empty_like(bias_out) if bias_out is not None else None
-    best, best_t = "mfma", float("inf")
+    best, best_t, times = "mfma", float("inf"), {}
     for name, fn in _WGRAD_IMPLS.items():
         for _ in range(2):
             fn(dy2, x2, scratch, False, None, scratch_b)
@@ -268,9 +279,11 @@ def _wgrad_choice(dy2, x2, out, bias_out=None) -> str:
             e0.synchronize()
             ts.append(s0.elapsed_time(e0))
         t = sorted(ts)[len(ts) // 2]
+        times[name] = round(t, 4)
         if t < best_t:
             best, best_t = name, t
     WGRAD_CHOICES[key] = best
+    _log_tune("wgrad", key, times, best)
     return best
 
 

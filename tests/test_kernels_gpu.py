@@ -319,6 +319,41 @@ def test_linear_cross_entropy_fused(V, gscale):
     torch.testing.assert_close(w.grad.float(), wf.grad, rtol=3e-2, atol=3e-4 * gscale)
 
 
+@pytest.mark.parametrize("variant", [1, 2])
+@pytest.mark.parametrize("V", [50304, 1000, 4096 * 8 + 8])
+def test_xent_fused_pass_elementwise(V, variant):
+    """The in-place fused loss pass itself: every dlogit against fp32 (softmax - onehot) * scale
+    and every row loss, with targets on the first / last column / a vector boundary and
+    ignore_index rows; both kernel variants (v2 default, v1 kept for A/B)."""
+    from distributed_llm_backend_benchmark_amd.ops import _lib as L
+
+    rows = 96
+    x = _randn(rows, V, seed=43, scale=4.0)
+    t = torch.randint(0, V, (rows,), device=DEV, generator=torch.Generator(device=DEV).manual_seed(3))
+    t[0], t[1], t[2], t[3] = 0, V - 1, 7, 8
+    t[5::9] = -100
+    sc = torch.full((1,), 0.37, device=DEV)
+    loss = torch.empty(rows, device=DEV)
+    buf = x.clone()
+    L.lib().dlbb_xent_set_variant(variant)
+    try:
+        L.check(L.lib().dlbb_xent_fused(buf.data_ptr(), t.data_ptr(), loss.data_ptr(), rows, V, V,
+                                        sc.data_ptr(), L.stream(buf.device)), "xent_fused")
+        torch.cuda.synchronize()
+    finally:
+        L.lib().dlbb_xent_set_variant(2)
+    xf = x.float()
+    valid = t >= 0
+    lse = torch.logsumexp(xf, dim=1)
+    ref_loss = torch.where(valid, lse - xf.gather(1, t.clamp_min(0)[:, None])[:, 0],
+                           torch.zeros_like(lse))
+    p = torch.softmax(xf, dim=1)
+    p[valid, t[valid]] -= 1.0
+    ref = p * 0.37 * valid[:, None].float()
+    torch.testing.assert_close(loss, ref_loss, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(buf.float(), ref, rtol=1.6e-2, atol=1e-6)
+
+
 @pytest.mark.parametrize("M,N,K", [(64, 128, 128), (16384, 768, 768), (4096, 2304, 768),
                                    (1024, 256, 3072), (320, 384, 256), (96, 128, 256)])
 @pytest.mark.parametrize("split", [None, 1, 3])

@@ -134,6 +134,31 @@ if "wgrad" in which:
         t_sum = t_med(lambda: dy.sum(0, dtype=torch.float32).to(torch.bfloat16), iters=30)
         out(kernel="wgrad", M=M, N=N, K=K, wgrad_us=t_w * 1e6, wgrad_fused_bias_us=t_wb * 1e6,
             torch_colsum_us=t_sum * 1e6, tflops=2 * M * N * K / t_w / 1e12)
+if "xent" in which:
+    # fused in-place LM-head loss pass (logits -> dlogits + per-row loss), v1 vs v2, at the
+    # GPT-2 step shape; the pass is in place, so each timed call first restores the logits
+    # from a copy and the copy's own time is subtracted
+    from distributed_llm_backend_benchmark_amd.ops import _lib as L
+    rows, V = 16384, 50304
+    src = (rnd(rows, V) * 2).to(torch.bfloat16)
+    buf = torch.empty_like(src)
+    tgt = torch.randint(0, V, (rows,), device="cuda")
+    loss = torch.empty(rows, device="cuda")
+    sc = torch.full((1,), 1.0 / rows, device="cuda")
+    t_copy = t_med(lambda: buf.copy_(src), iters=20)
+    res = {}
+    for var in (1, 2):
+        L.lib().dlbb_xent_set_variant(var)
+
+        def run():
+            buf.copy_(src)
+            L.check(L.lib().dlbb_xent_fused(buf.data_ptr(), tgt.data_ptr(), loss.data_ptr(), rows,
+                                            V, V, sc.data_ptr(), L.stream(buf.device)), "xent")
+        res[var] = t_med(run, iters=20) - t_copy
+    L.lib().dlbb_xent_set_variant(2)
+    nbytes = rows * V * 2 * 2
+    out(kernel="xent_fused", rows=rows, V=V, v1_us=res[1] * 1e6, v2_us=res[2] * 1e6,
+        v1_TBps=nbytes / res[1] / 1e12, v2_TBps=nbytes / res[2] / 1e12, copy_us=t_copy * 1e6)
 if "gelu" in which:
     a, bb, g = rnd(16384, 3072), rnd(3072), rnd(16384, 3072)
     from distributed_llm_backend_benchmark_amd.ops import _lib as L
