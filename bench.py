@@ -43,7 +43,65 @@ def parse(argv=None):
                          "the IPC xGMI kernel (if its self-test passed on every rank) during "
                          "warmup and run the fastest")
     ap.add_argument("--no-side", action="store_true", help="skip the 512 B / 8 MiB side runs")
+    ap.add_argument("--no-sweep", action="store_true", help="skip the all-reduce size sweep")
+    ap.add_argument("--sweep-max-mib", type=int, default=1024,
+                    help="largest message of the all-reduce size sweep (MiB per rank)")
     return ap.parse_args(argv)
+
+
+SWEEP_BYTES = [1 << 10, 8 << 10, 64 << 10, 512 << 10, 4 << 20, 32 << 20, 256 << 20, 1 << 30]
+
+
+def _allreduce_sweep(comm, max_mib: int):
+    """Mean time per call (back to back, rank max) of a bf16 SUM all-reduce per message size and
+    implementation; per size the fastest is reported with busBW / algBW. Candidates: RCCL via
+    torch, RCCL via our native engine, and (P > 1, self-test passed) the IPC xGMI kernel —
+    staged one-/two-shot within its staging capacity, and in place on a registered buffer."""
+    import torch
+
+    from distributed_llm_backend_benchmark_amd.parallel.collectives import make_data, make_op
+    from distributed_llm_backend_benchmark_amd.stats.bandwidth import algbw_gbps, busbw_gbps
+
+    P = comm.world_size
+    car = None
+    if P > 1 and comm.is_gpu:
+        from distributed_llm_backend_benchmark_amd.parallel.custom_allreduce import (
+            get_custom_allreduce)
+
+        car = get_custom_allreduce(comm)
+    out = []
+    for nbytes in SWEEP_BYTES:
+        if nbytes > max_mib << 20:
+            break
+        data = make_data((nbytes // 2,), torch.bfloat16, comm.rank, comm.device)
+        flat = data.reshape(-1)
+        cands = [("rccl", {"impl": "rccl"})]
+        if comm.is_gpu:
+            cands.append(("native", {"impl": "native"}))
+        if car is not None and car.healthy and car.supports(flat):
+            cands.append(("custom", {"impl": "custom"}))
+        if car is not None and car.reg_healthy and car.supports_registered(flat):
+            cands.append(("custom_reg", {"impl": "custom_reg", "nblocks": 256}))
+        iters = 50 if nbytes <= 4 << 20 else 20 if nbytes <= 32 << 20 else 8
+        res = {}
+        for label, opts in cands:
+            try:
+                op = make_op("allreduce", comm, data, **opts)
+            except RuntimeError:            # agreed on every rank (collective health flags)
+                continue
+            for _ in range(3):
+                op.run()
+            comm.sync()
+            res[label] = _timed_steps(comm, op, iters) / iters
+            del op
+        best = min(res, key=res.get)
+        t = res[best]
+        out.append({"bytes": nbytes, "impl": best, "us": round(t * 1e6, 2),
+                    "busbw_GBps": round(busbw_gbps("allreduce", nbytes, t, P), 3),
+                    "algbw_GBps": round(algbw_gbps("allreduce", nbytes, t, P), 3),
+                    "us_by_impl": {k: round(v * 1e6, 2) for k, v in res.items()}})
+        del data, flat
+    return out
 
 
 def _timed_steps(comm, op, steps: int) -> float:
@@ -177,6 +235,14 @@ def main(argv=None) -> int:
                 "ref_busbw_GBps_8MiB": REF_BUSBW_8MIB,
             }
 
+    # the BASELINE.json metric is busBW + latency *vs message size*: a 1 KiB .. 1 GiB all-reduce
+    # sweep (bf16) in the same run, best implementation per size (every rank builds the same
+    # candidate list; health flags are agreed collectively), so each N of the driver's scaling
+    # runs carries the whole curve
+    sweep = []
+    if not args.no_side and not args.no_sweep:
+        sweep = _allreduce_sweep(comm, args.sweep_max_mib)
+
     # BASELINE configs 3/4 on the same [B,S,H] message at P > 1: all-gather, reduce-scatter and
     # all-to-all through RCCL and through the direct one-hop IPC kernels (side measurements)
     coll = {}
@@ -233,6 +299,8 @@ def main(argv=None) -> int:
         }
         if coll:
             rec["collectives_same_message"] = coll
+        if sweep:
+            rec["allreduce_sweep"] = sweep
         print(json.dumps(rec), flush=True)
     comm.barrier()
     comm.destroy()

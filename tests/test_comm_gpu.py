@@ -269,6 +269,10 @@ def test_bench_py_world1():
     rec = json.loads(line)
     assert rec["n_gpus"] == 1 and rec["steps"] == 5 and rec["unit"] == "GB/s"
     assert rec["ms_per_step"] > 0
+    sweep = rec["allreduce_sweep"]
+    assert [e["bytes"] for e in sweep] == [1 << 10, 8 << 10, 64 << 10, 512 << 10, 4 << 20,
+                                           32 << 20, 256 << 20, 1 << 30]
+    assert all(e["us"] > 0 and e["impl"] in e["us_by_impl"] for e in sweep), sweep
 
 
 def test_bench_py_two_ranks_rehearsal():
@@ -279,7 +283,8 @@ def test_bench_py_two_ranks_rehearsal():
     env = dict(os.environ, DLBB_BENCH_BACKEND="gloo", HSA_ENABLE_IPC_MODE_LEGACY="0")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
-           os.path.join(REPO, "bench.py"), "--gpus", "2", "--steps", "5", "--warmup", "2"]
+           os.path.join(REPO, "bench.py"), "--gpus", "2", "--steps", "5", "--warmup", "2",
+           "--sweep-max-mib", "32"]
     out = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=REPO, env=env)
     assert out.returncode == 0, out.stderr[-3000:]
     rec = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][-1])
@@ -290,6 +295,11 @@ def test_bench_py_two_ranks_rehearsal():
     for name in ("allgather", "reduce_scatter", "alltoall"):
         assert set(coll[name]) == {"rccl", "direct_ipc"}, coll
         assert all(v["busbw_GBps"] > 0 for v in coll[name].values()), coll
+    sweep = rec["allreduce_sweep"]
+    assert [e["bytes"] for e in sweep][-1] == 32 << 20
+    # the IPC kernel (staged and registered) is a candidate at every size on 2 ranks
+    assert all({"custom", "custom_reg"} <= set(e["us_by_impl"]) for e in sweep), sweep
+    assert all(e["busbw_GBps"] > 0 for e in sweep), sweep
 
 
 def test_tp_forward_world1_matches_torch():

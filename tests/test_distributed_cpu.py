@@ -310,3 +310,31 @@ def test_flatten_mode_matches_view_mode_over_steps():
     """Regression: flatten mode must pick up each step's freshly allocated .grad tensors."""
     for d in run_multiprocess(_mode_worker, 2, timeout=300):
         assert d < 1e-6, d
+
+
+def test_bench_py_gloo_world2_contract():
+    """bench.py under torchrun on the CPU (gloo, world 2, small message): the driver's JSON
+    contract — one line, the BASELINE metric, busBW > 0 at P = 2, vs_baseline set, the
+    all-reduce size sweep present."""
+    import json
+    import subprocess
+    import sys
+
+    from conftest import free_port
+
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
+           os.path.join(repo, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "1",
+           "--shape", "1,64,256", "--sweep-max-mib", "1"]
+    env = {k: v for k, v in os.environ.items() if k not in ("CUDA_VISIBLE_DEVICES",)}
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=repo, env=env)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    rec = json.loads(lines[0])
+    assert rec["metric"] == "all-reduce bus BW (GB/s)" and rec["n_gpus"] == 2
+    assert rec["value"] > 0 and rec["vs_baseline"] is not None and rec["steps"] == 3
+    assert rec["higher_is_better"] is True and rec["scaling"] == "weak"
+    assert [e["bytes"] for e in rec["allreduce_sweep"]] == [1 << 10, 8 << 10, 64 << 10, 512 << 10]
+    assert all(e["impl"] == "rccl" and e["busbw_GBps"] > 0 for e in rec["allreduce_sweep"])
