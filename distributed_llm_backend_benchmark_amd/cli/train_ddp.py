@@ -34,6 +34,10 @@ def parse_args(argv=None):
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--lr", type=float, default=3e-4)
+    ap.add_argument("--lr-warmup", type=int, default=10,
+                    help="linear learning-rate warmup over the first N optimizer steps (Adam "
+                         "without warmup can spike on this synthetic data); under --graph the "
+                         "rate is the one in effect at capture")
     ap.add_argument("--bucket-mb", type=float, default=64.0)
     ap.add_argument("--mode", choices=["view", "flatten"], default="view")
     ap.add_argument("--allreduce", choices=["rccl", "custom", "native"], default="rccl",
@@ -80,10 +84,21 @@ def run(args, comm, overlap: bool):
                                  device=comm.device)
     if args.resume_from:
         tr.load_checkpoint(args.resume_from)
-    for _ in range(args.warmup):
+
+    def set_lr():   # host-side scalar: one attribute per step, no device work
+        tr.opt.lr = args.lr * min(1.0, (tr.step_count + 1) / max(1, args.lr_warmup))
+
+    first_loss = None
+    for i in range(args.warmup):
         x, y = data.get_batch()
-        tr.step(x, y, sync_loss=False)
-    step_fn = lambda x, y: tr.step(x, y, sync_loss=False)  # noqa: E731
+        set_lr()
+        out = tr.step(x, y, sync_loss=(i == 0))
+        if i == 0:
+            first_loss = out
+
+    def step_fn(x, y):
+        set_lr()
+        return tr.step(x, y, sync_loss=False)
     if args.graph:
         x, y = data.get_batch()
         step_fn = tr.capture_step(x, y)
@@ -100,6 +115,7 @@ def run(args, comm, overlap: bool):
         "ms_per_step": dt / args.steps * 1e3,
         "tokens_per_s": comm.world_size * args.batch * args.seq * args.steps / dt,
         "loss": float(loss.item()) if loss is not None else None,
+        "loss_first_step": first_loss,
         "params": model.num_parameters(),
         "buckets": len(tr.buckets),
         "hip_graph": bool(args.graph),
