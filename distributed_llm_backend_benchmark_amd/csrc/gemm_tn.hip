@@ -23,9 +23,8 @@ namespace dlbb {
 
 namespace tn {
 
-constexpr int BN = 128, BKO = 128, BM = 32;       // output rows (N), output cols (K), reduction
-constexpr int kThreads = 256;
-constexpr int kTile = BM * 128 * 2;               // 16 KiB per operand tile
+constexpr int BKO = 128, BM = 32;                 // output cols (K) per tile, reduction rows/stage
+constexpr int kTile = BM * 128 * 2;               // 8 KiB per [BM][128] image
 
 typedef short i16x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) void* lds_vptr_t;
@@ -42,21 +41,6 @@ struct Args {
   int m_per_split;
   int nsplit;          // fused db partials (BIAS) at ws + nsplit * N * K (tk == 0 blocks)
 };
-
-// Stage rows [m0, m0 + BM) x cols [c0, c0 + 128) of a row-major matrix into a swizzled image.
-// One wave-instruction = 4 rows x 256 B; wave w issues rows [BM/4 w, BM/4 (w + 1)).
-__device__ __forceinline__ void stage(const uint16_t* X, int64_t ld, int m0, int c0, char* img,
-                                      int wave, int lane) {
-  const int rq = lane >> 4, slot = lane & 15;
-#pragma unroll
-  for (int i = 0; i < BM / 16; ++i) {
-    const int row = wave * (BM / 4) + i * 4 + rq;
-    const int chunk = slot ^ swz(row);
-    const uint16_t* src = X + static_cast<int64_t>(m0 + row) * ld + c0 + chunk * 8;
-    __builtin_amdgcn_global_load_lds(src, (lds_vptr_t)(img + (wave * (BM / 4) + i * 4) * 256),
-                                     16, 0, 0);
-  }
-}
 
 // MFMA 16x16x32 operand from a [64 m][128 col] image: lane l gets column colbase + (l & 15),
 // rows kbase + 8 (l >> 4) + j, j = 0..7 (two transposed reads of 4 rows each).
@@ -76,12 +60,42 @@ __device__ __forceinline__ bf16x8 frag(const char* img, int kbase, int colbase, 
   return f;
 }
 
-// BIAS: a separate instantiation (two extra accumulators + the ones operand: 112 -> 122 VGPRs,
-// still 4 waves/SIMD). NB: LDS ring depth (stages) — NB - 1 stages of DMA in flight while one
-// is consumed (NB = 2: 32 KiB, 3 workgroups/CU; 3: 48 KiB, 3/CU; 4: 64 KiB, 2/CU).
-template <bool BIAS, int NB>
-__global__ void __launch_bounds__(kThreads, 3) wgrad_kernel(Args a) {
+// One stage = BM rows of m of the NA = WM / 2 A sub-images ([BM][128 cols of dY] each) and the B
+// image ([BM][128 cols of X]); every 4-row x 256-B wave-instruction of the stage is one slot
+// j = wave * per + q of NIMG * BM / 4, spread evenly over the workgroup's waves.
+template <int WM>
+__device__ __forceinline__ void stage_all(const Args& a, int m0, int n0, int k0, char* buf,
+                                          int wave, int lane) {
+  constexpr int NA = WM / 2, NIMG = NA + 1, RG = BM / 4, NW = 2 * WM;
+  constexpr int PER = NIMG * RG / NW;
+  static_assert(NIMG * RG % NW == 0, "stage slots must divide evenly over the waves");
+  const int rq = lane >> 4, slot = lane & 15;
+#pragma unroll
+  for (int q = 0; q < PER; ++q) {
+    const int j = wave * PER + q;
+    const int img = j / RG, rg = j % RG;
+    const int row = rg * 4 + rq;
+    const int chunk = slot ^ swz(row);
+    const bool is_a = img < NA;
+    const uint16_t* X = is_a ? a.A : a.B;
+    const int64_t ld = is_a ? a.lda : a.ldb;
+    const int c0 = is_a ? n0 + img * 128 : k0;
+    const uint16_t* src = X + static_cast<int64_t>(m0 + row) * ld + c0 + chunk * 8;
+    __builtin_amdgcn_global_load_lds(src, (lds_vptr_t)(buf + img * kTile + rg * 4 * 256), 16, 0,
+                                     0);
+  }
+}
+
+// BIAS: a separate instantiation (two extra accumulators + the ones operand). NB: LDS ring
+// depth (stages) — NB - 1 stages of DMA in flight while one is consumed. WM: output rows (N) per
+// workgroup in 64-row wave blocks — 2: 128 x 128 tile, 4 waves, three workgroups per CU;
+// 4: 256 x 128 tile, 8 waves, two per CU: 1.33x the MFMA work per byte staged through L2 (the
+// 128 x 128 tile needs ~64 FLOP per L2 byte, more than the L2 delivers at the MFMA rate).
+template <bool BIAS, int NB, int WM>
+__global__ void __launch_bounds__(128 * WM, WM == 2 ? 3 : 2) wgrad_kernel(Args a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int NIMG = WM / 2 + 1;
+  constexpr int kStage = NIMG * kTile;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = wave >> 1, wn = wave & 1;
@@ -92,12 +106,12 @@ __global__ void __launch_bounds__(kThreads, 3) wgrad_kernel(Args a) {
   // instead of from the Infinity Cache / HBM (the default round-robin puts neighbours on
   // different XCDs, so every workgroup fetched its panels from beyond L2).
   const int tiles_k = a.K / BKO;
-  const int tiles = (a.N / BN) * tiles_k;
+  const int tiles = (a.N / (64 * WM)) * tiles_k;
   const int nwg = gridDim.x, xcd = blockIdx.x % 8, q = nwg / 8, r = nwg % 8;
   const int wid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + blockIdx.x / 8;
   const int split = wid / tiles, t = wid % tiles;
   const int tn = t / tiles_k, tk = t % tiles_k;
-  const int n0 = tn * BN, k0 = tk * BKO;
+  const int n0 = tn * 64 * WM, k0 = tk * BKO;
   const int mb = split * a.m_per_split;
   const int me = mb + a.m_per_split < a.M ? mb + a.m_per_split : a.M;
   const int nsteps = (me - mb) / BM;
@@ -114,15 +128,13 @@ __global__ void __launch_bounds__(kThreads, 3) wgrad_kernel(Args a) {
 #pragma unroll
   for (int u = 0; u < 8; ++u) ones[u] = static_cast<short>(0x3F80);
 
-  auto imgA = [&](int c) { return smem + c * 2 * kTile; };
-  auto imgB = [&](int c) { return smem + c * 2 * kTile + kTile; };
-  constexpr int kLoadsPerStage = 2 * (BM / 16);   // global_load_lds per wave per stage
+  auto stg = [&](int c) { return smem + c * kStage; };
+  // this wave's A sub-image (128 dY columns) and the row offset of its 64 inside it
+  const int asub = (wm * 64) / 128, acol = (wm * 64) % 128;
+  constexpr int kLoadsPerStage = NIMG * (BM / 4) / (2 * WM);   // global_load_lds per wave
 #pragma unroll
   for (int p = 0; p < NB - 1; ++p)
-    if (p < nsteps) {
-      stage(a.A, a.lda, mb + p * BM, n0, imgA(p), wave, lane);
-      stage(a.B, a.ldb, mb + p * BM, k0, imgB(p), wave, lane);
-    }
+    if (p < nsteps) stage_all<WM>(a, mb + p * BM, n0, k0, stg(p), wave, lane);
   for (int s = 0; s < nsteps; ++s) {
     const int cur = s % NB;
     // stage s landed: later stages (up to NB - 2 of them) may still be in flight
@@ -136,18 +148,15 @@ __global__ void __launch_bounds__(kThreads, 3) wgrad_kernel(Args a) {
     // one barrier per stage: it publishes stage s (every wave's DMA of it retired) and frees
     // the buffer of stage s - 1 (every wave finished it), which stage s + NB - 1 now refills
     __builtin_amdgcn_s_barrier();
-    if (s + NB - 1 < nsteps) {
-      const int nxt = (s + NB - 1) % NB;
-      stage(a.A, a.lda, mb + (s + NB - 1) * BM, n0, imgA(nxt), wave, lane);
-      stage(a.B, a.ldb, mb + (s + NB - 1) * BM, k0, imgB(nxt), wave, lane);
-    }
-    const char* ia = imgA(cur);
-    const char* ib = imgB(cur);
+    if (s + NB - 1 < nsteps)
+      stage_all<WM>(a, mb + (s + NB - 1) * BM, n0, k0, stg((s + NB - 1) % NB), wave, lane);
+    const char* ia = stg(cur) + asub * kTile;
+    const char* ib = stg(cur) + (NIMG - 1) * kTile;
 #pragma unroll
     for (int ks = 0; ks < BM / 32; ++ks) {
       bf16x8 af[4], bfr[4];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) af[i] = frag(ia, 32 * ks, wm * 64 + i * 16, lane);
+      for (int i = 0; i < 4; ++i) af[i] = frag(ia, 32 * ks, acol + i * 16, lane);
 #pragma unroll
       for (int j = 0; j < 4; ++j) bfr[j] = frag(ib, 32 * ks, wn * 64 + j * 16, lane);
       __builtin_amdgcn_s_setprio(1);
@@ -236,15 +245,17 @@ static int g_wgrad_stages = 2;
 DLBB_API void dlbb_gemm_wgrad_set_stages(int nb) { g_wgrad_stages = nb >= 2 && nb <= 4 ? nb : 2; }
 
 // dW[N][K] = A^T B with A = [M][lda] (N columns used), B = [M][ldb] (K columns used), bf16.
-// Requires M % 32 == 0, N % 128 == 0, K % 128 == 0, lda/ldb % 8 == 0, 16-B aligned bases.
-// ws: fp32 workspace of split * (N * K + N) floats. out: bf16 (dt_out 1) or fp32 (0), dense
-// [N][K]. out_bias (optional, same dtype as out, N elements): fused db = column sums of A.
-DLBB_API int dlbb_gemm_wgrad(const void* A, int64_t lda, const void* B, int64_t ldb, void* out,
-                             int dt_out, int accumulate, float* ws, int M, int N, int K,
-                             int split, void* out_bias, hipStream_t stream) {
+// Requires M % 32 == 0, N % bn == 0, K % 128 == 0, lda/ldb % 8 == 0, 16-B aligned bases;
+// bn = 128 (128 x 128 tiles) or 256 (256 x 128 tiles). ws: fp32 workspace of
+// split * (N * K + N) floats. out: bf16 (dt_out 1) or fp32 (0), dense [N][K]. out_bias
+// (optional, same dtype as out, N elements): fused db = column sums of A.
+DLBB_API int dlbb_gemm_wgrad_tile(const void* A, int64_t lda, const void* B, int64_t ldb,
+                                  void* out, int dt_out, int accumulate, float* ws, int M, int N,
+                                  int K, int split, void* out_bias, int bn, hipStream_t stream) {
   using namespace dlbb::tn;
   if (M <= 0 || N <= 0 || K <= 0) return hipSuccess;
-  if (M % BM || N % BN || K % BKO || lda % 8 || ldb % 8 || split < 1) return hipErrorInvalidValue;
+  if (bn != 128 && bn != 256) return hipErrorInvalidValue;
+  if (M % BM || N % bn || K % BKO || lda % 8 || ldb % 8 || split < 1) return hipErrorInvalidValue;
   if ((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(B) |
        reinterpret_cast<uintptr_t>(ws)) & 15)
     return hipErrorInvalidValue;
@@ -253,19 +264,21 @@ DLBB_API int dlbb_gemm_wgrad(const void* A, int64_t lda, const void* B, int64_t 
   split = (M + per - 1) / per;
   Args a{static_cast<const uint16_t*>(A), static_cast<const uint16_t*>(B), ws, lda, ldb, M, N, K,
          per, split};
-  const dim3 grid((N / BN) * (K / BKO) * split);
-#define WG_LAUNCH(BIASV, NBV)                                                               \
-  hipLaunchKernelGGL((wgrad_kernel<BIASV, NBV>), grid, dim3(kThreads), NBV * 2 * kTile, stream, a)
+  const dim3 grid((N / bn) * (K / BKO) * split);
   const int stages = g_wgrad_stages;
-  if (out_bias) {
-    if (stages == 4) WG_LAUNCH(true, 4);
-    else if (stages == 3) WG_LAUNCH(true, 3);
-    else WG_LAUNCH(true, 2);
+#define WG_LAUNCH(BIASV, NBV, WMV)                                                          \
+  hipLaunchKernelGGL((wgrad_kernel<BIASV, NBV, WMV>), grid, dim3(128 * (WMV)),             \
+                     NBV * ((WMV) / 2 + 1) * kTile, stream, a)
+#define WG_STAGES(BIASV, WMV)                \
+  if (stages == 4) WG_LAUNCH(BIASV, 4, WMV); \
+  else if (stages == 3) WG_LAUNCH(BIASV, 3, WMV); \
+  else WG_LAUNCH(BIASV, 2, WMV)
+  if (bn == 256) {
+    if (out_bias) { WG_STAGES(true, 4); } else { WG_STAGES(false, 4); }
   } else {
-    if (stages == 4) WG_LAUNCH(false, 4);
-    else if (stages == 3) WG_LAUNCH(false, 3);
-    else WG_LAUNCH(false, 2);
+    if (out_bias) { WG_STAGES(true, 2); } else { WG_STAGES(false, 2); }
   }
+#undef WG_STAGES
 #undef WG_LAUNCH
   const int64_t n = static_cast<int64_t>(N) * K;
   const int64_t nb = out_bias ? N : 0;
@@ -277,4 +290,11 @@ DLBB_API int dlbb_gemm_wgrad(const void* A, int64_t lda, const void* B, int64_t 
     hipLaunchKernelGGL(split_reduce_kernel<DT_F32>, dim3(g), dim3(256), 0, stream, ws, out, n,
                        out_bias, nb, split, accumulate);
   return hipGetLastError();
+}
+
+DLBB_API int dlbb_gemm_wgrad(const void* A, int64_t lda, const void* B, int64_t ldb, void* out,
+                             int dt_out, int accumulate, float* ws, int M, int N, int K,
+                             int split, void* out_bias, hipStream_t stream) {
+  return dlbb_gemm_wgrad_tile(A, lda, B, ldb, out, dt_out, accumulate, ws, M, N, K, split,
+                              out_bias, 128, stream);
 }

@@ -72,6 +72,9 @@ _SIGS = {
                               c_void_p, c_void_p]),
     "dlbb_gemm_wgrad": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int, c_int,
                                 c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p]),
+    "dlbb_gemm_wgrad_tile": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int,
+                                     c_int, c_void_p, c_int, c_int, c_int, c_int, c_void_p,
+                                     c_int, c_void_p]),
     "dlbb_attn_fwd": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int, c_int,
                               c_int, c_int, c_float, c_void_p]),
     "dlbb_attn_bwd": (c_int, [c_void_p, c_int64, c_void_p, c_void_p, c_int64, c_void_p,

@@ -221,19 +221,28 @@ def wgrad_supported(dy2: torch.Tensor, x2: torch.Tensor) -> bool:
             and dy2.data_ptr() % 16 == 0 and x2.data_ptr() % 16 == 0)
 
 
-def _wgrad_hip(dy2, x2, out, accumulate, split=None, bias_out=None):
+def _wgrad_hip(dy2, x2, out, accumulate, split=None, bias_out=None, bn=128):
     M, N = dy2.shape
     K = x2.shape[1]
-    tiles = (N // 128) * (K // 128)
+    tiles = (N // bn) * (K // 128)
     if split is None:
-        # about one resident wave of workgroups (3 per CU x 256 CUs): measured best with the
-        # XCD-aware tile order (profiles/r01_gpt2/wgrad_split_xcd.jsonl)
-        split = max(1, min(M // 256, -(-768 // tiles)))
+        # about one resident wave of workgroups (3 per CU x 256 CUs for 128 x 128 tiles, 2 per
+        # CU for 256 x 128): measured best with the XCD-aware tile order
+        # (profiles/r01_gpt2/wgrad_split_xcd.jsonl)
+        # (256 x 128 tiles: at most the 512 resident slots — a 2nd partial round costs a
+        # whole workgroup time)
+        split = max(1, min(M // 256, (-(-768 // tiles)) if bn == 128 else 512 // tiles))
     ws = torch.empty(split * (N * K + N), dtype=torch.float32, device=dy2.device)
-    check(_lib.lib().dlbb_gemm_wgrad(dy2.data_ptr(), dy2.stride(0), x2.data_ptr(), x2.stride(0),
-                                     out.data_ptr(), _lib.dt(out), int(accumulate), ws.data_ptr(),
-                                     M, N, K, split, _lib.ptr(bias_out),
-                                     _lib.stream(dy2.device)), "gemm_wgrad")
+    check(_lib.lib().dlbb_gemm_wgrad_tile(dy2.data_ptr(), dy2.stride(0), x2.data_ptr(),
+                                          x2.stride(0), out.data_ptr(), _lib.dt(out),
+                                          int(accumulate), ws.data_ptr(), M, N, K, split,
+                                          _lib.ptr(bias_out), int(bn), _lib.stream(dy2.device)),
+          "gemm_wgrad")
+
+
+def _wgrad_hip256(dy2, x2, out, accumulate, split=None, bias_out=None):
+    """256 x 128 output tiles (8 waves): 1.33x the MFMA work per L2 byte of the 128^2 tile."""
+    _wgrad_hip(dy2, x2, out, accumulate, split, bias_out, bn=256)
 
 
 def _wgrad_blas(dy2, x2, out, accumulate, split=None, bias_out=None):
@@ -251,14 +260,14 @@ def _wgrad_blas(dy2, x2, out, accumulate, split=None, bias_out=None):
             bias_out.copy_(db)
 
 
-WGRAD_CHOICES = {}    # (M, N, K, out dtype, fused bias) -> "mfma" | "blas"
-_WGRAD_IMPLS = {"mfma": _wgrad_hip, "blas": _wgrad_blas}
+WGRAD_CHOICES = {}    # (M, N, K, out dtype, fused bias) -> "mfma" | "mfma256" | "blas"
+_WGRAD_IMPLS = {"mfma": _wgrad_hip, "mfma256": _wgrad_hip256, "blas": _wgrad_blas}
 
 
 def _wgrad_choice(dy2, x2, out, bias_out=None) -> str:
     mode = os.environ.get("DLBB_GEMM", "auto").lower()
     if mode in _WGRAD_IMPLS:
-        return mode
+        return "mfma" if mode == "mfma256" and dy2.shape[1] % 256 else mode
     key = (dy2.shape[0], dy2.shape[1], x2.shape[1], out.dtype, bias_out is not None)
     if key in WGRAD_CHOICES:
         return WGRAD_CHOICES[key]
@@ -268,6 +277,8 @@ def _wgrad_choice(dy2, x2, out, bias_out=None) -> str:
     scratch_b = torch.empty_like(bias_out) if bias_out is not None else None
     best, best_t, times = "mfma", float("inf"), {}
     for name, fn in _WGRAD_IMPLS.items():
+        if name == "mfma256" and (dy2.shape[1] % 256 or os.environ.get("DLBB_WGRAD256") == "0"):
+            continue
         for _ in range(2):
             fn(dy2, x2, scratch, False, None, scratch_b)
         ts = []

@@ -382,6 +382,49 @@ def test_wgrad_matches_fp32(M, N, K, split):
     torch.testing.assert_close(b32, refb + 1, rtol=2e-3, atol=2e-3 * (M ** 0.5))
 
 
+@pytest.mark.parametrize("M,N,K", [(16384, 768, 768), (4096, 2304, 768), (1024, 256, 3072),
+                                   (512, 3072, 768), (96, 512, 128)])
+@pytest.mark.parametrize("split", [None, 1, 3])
+def test_wgrad_256_tile_matches_fp32(M, N, K, split):
+    """The 256 x 128 output tile (8 waves, two A sub-images per stage): dW, accumulate and the
+    fused bias gradient against fp32."""
+    from distributed_llm_backend_benchmark_amd.ops.gemm import _wgrad_hip256
+
+    dy = _randn(M, N, seed=51, scale=0.5)
+    x = _randn(M, K, seed=52, scale=0.5)
+    ref = dy.float().t() @ x.float()
+    refb = dy.float().sum(0)
+    tol = dict(rtol=2e-3, atol=2e-3 * (M ** 0.5))
+    w32, b32 = torch.empty(N, K, device=DEV), torch.empty(N, device=DEV)
+    _wgrad_hip256(dy, x, w32, False, split, None)
+    torch.testing.assert_close(w32, ref, **tol)
+    _wgrad_hip256(dy, x, w32, False, split, b32)
+    torch.testing.assert_close(w32, ref, **tol)
+    torch.testing.assert_close(b32, refb, **tol)
+    w32.fill_(1.0)
+    b32.fill_(1.0)
+    _wgrad_hip256(dy, x, w32, True, split, b32)
+    torch.testing.assert_close(w32, ref + 1, **tol)
+    torch.testing.assert_close(b32, refb + 1, **tol)
+    wb = torch.empty(N, K, device=DEV, dtype=torch.bfloat16)
+    _wgrad_hip256(dy, x, wb, False, split, None)
+    torch.testing.assert_close(wb.float(), ref, rtol=2e-2, atol=2e-2 * (M ** 0.5))
+
+
+def test_wgrad_256_tile_asymmetric():
+    """One-hot dY columns through the 256-row tile: every dW row must be the right X row."""
+    from distributed_llm_backend_benchmark_amd.ops.gemm import _wgrad_hip256
+
+    M, N, K = 256, 512, 256
+    dy = torch.zeros(M, N, device=DEV)
+    dy[torch.arange(M), (torch.arange(M) * 7) % N] = 1.0
+    x = (torch.arange(M * K, device=DEV, dtype=torch.float32).view(M, K) % 13)
+    dy, x = dy.to(torch.bfloat16), x.to(torch.bfloat16)
+    out = torch.empty(N, K, dtype=torch.float32, device=DEV)
+    _wgrad_hip256(dy, x, out, False, None, None)
+    torch.testing.assert_close(out, dy.float().t() @ x.float(), rtol=0, atol=0)
+
+
 def test_wgrad_asymmetric():
     """dY = one-hot columns: dW rows must be the right X rows (catches swapped maps)."""
     from distributed_llm_backend_benchmark_amd.ops.gemm import wgrad

@@ -134,6 +134,23 @@ if "wgrad" in which:
         t_sum = t_med(lambda: dy.sum(0, dtype=torch.float32).to(torch.bfloat16), iters=30)
         out(kernel="wgrad", M=M, N=N, K=K, wgrad_us=t_w * 1e6, wgrad_fused_bias_us=t_wb * 1e6,
             torch_colsum_us=t_sum * 1e6, tflops=2 * M * N * K / t_w / 1e12)
+if "wgrad256" in which:
+    # weight-gradient GEMM at the GPT-2 shapes: 128 x 128 vs 256 x 128 output tiles vs library
+    from distributed_llm_backend_benchmark_amd.ops.gemm import _wgrad_blas, _wgrad_hip, _wgrad_hip256
+    for N, K in ((2304, 768), (768, 768), (3072, 768), (768, 3072)):
+        M = 16384
+        dy, x = rnd(M, N), rnd(M, K)
+        w_out, b_out = torch.empty(N, K, device="cuda", dtype=torch.bfloat16), \
+            torch.empty(N, device="cuda", dtype=torch.bfloat16)
+        res = {}
+        for name, fn in (("t128", _wgrad_hip), ("t256", _wgrad_hip256), ("blas", _wgrad_blas)):
+            res[name] = t_med(lambda: fn(dy, x, w_out, True, None, b_out), iters=30) * 1e6
+        if N % 256 == 0:
+            for sp in (6, 7, 8, 9):
+                res[f"t256_split{sp}"] = t_med(
+                    lambda: _wgrad_hip256(dy, x, w_out, True, sp, b_out), iters=30) * 1e6
+        out(kernel="wgrad_tiles", M=M, N=N, K=K, us=res,
+            tflops={k: round(2 * M * N * K / v / 1e6, 1) for k, v in res.items()})
 if "xent" in which:
     # fused in-place LM-head loss pass (logits -> dlogits + per-row loss), v1 vs v2, at the
     # GPT-2 step shape; the pass is in place, so each timed call first restores the logits
