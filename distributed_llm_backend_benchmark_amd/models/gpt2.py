@@ -20,11 +20,11 @@ Weights: N(0, 0.02), residual projections scaled by 1/sqrt(2*n_layer) (GPT-2 ini
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass
 
 import torch
 import torch.nn as nn
-import torch.nn.functional as F
 
 from .. import ops
 from ..ops.linear_fn import linear_train
@@ -99,12 +99,21 @@ class GPT2(nn.Module):
         gen.manual_seed(seed)
         self.wte = _param((cfg.vocab_size, cfg.n_embd), 0.02, device, gen)
         self.wpe = _param((cfg.block_size, cfg.n_embd), 0.01, device, gen)
+        # gradient sinks (trainer opt-in): wpe is used once per step; wte twice (input
+        # embedding + tied LM head), both uses accumulate into its .grad in-kernel
+        self._fused_embedding = os.environ.get("DLBB_EMB", "1") != "0"   # A/B switch
+        if self._fused_embedding:
+            self.wpe._dlbb_single_use = True
+            self.wte._dlbb_sink_uses = 2
         self.blocks = nn.ModuleList([Block(cfg, device, gen) for _ in range(cfg.n_layer)])
         self.ln_f = LN(cfg.n_embd, device)
 
     def forward(self, idx, targets=None):
         B, T = idx.shape
-        x = F.embedding(idx, self.wte) + self.wpe[:T]
+        if self._fused_embedding:
+            x = ops.embedding(idx, self.wte, self.wpe)
+        else:
+            x = torch.nn.functional.embedding(idx, self.wte) + self.wpe[:T]
         y, h = self.blocks[0].ln_1(x)
         for i, blk in enumerate(self.blocks):
             d, h = blk(y, h)

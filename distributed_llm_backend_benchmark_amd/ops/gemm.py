@@ -246,7 +246,9 @@ def _wgrad_hip256(dy2, x2, out, accumulate, split=None, bias_out=None):
 
 
 def _wgrad_blas(dy2, x2, out, accumulate, split=None, bias_out=None):
-    if accumulate:
+    if accumulate and out.dtype == dy2.dtype:
+        out.addmm_(dy2.t(), x2)             # the library GEMM accumulates (beta = 1): no add pass
+    elif accumulate:
         out.add_(torch.matmul(dy2.t(), x2).to(out.dtype))
     elif out.dtype == dy2.dtype:
         torch.matmul(dy2.t(), x2, out=out)

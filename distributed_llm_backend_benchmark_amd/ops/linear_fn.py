@@ -92,9 +92,9 @@ class _LinearFn(torch.autograd.Function):
             else:
                 wgrad(du, x2, out=ctx.weight.grad, accumulate=True,
                       bias_out=ctx.bias.grad if want_db else None)
-            w_sink(ctx.weight)
+            sink_used(ctx.weight)
             if want_db:
-                b_sink(ctx.bias)
+                sink_used(ctx.bias)
             if dx is not None:
                 dx = dx.view(*ctx.lead, K)
             return dx, None, None, None
@@ -117,6 +117,19 @@ def _sink(p: Optional[torch.Tensor]):
     if g is None or g.dtype != p.dtype or g.shape != p.shape or not g.is_contiguous():
         return None
     return cb
+
+
+def sink_used(p: torch.Tensor) -> None:
+    """Record one in-kernel accumulation into a sink parameter's ``.grad``; the sink callback
+    fires after the parameter's last use of the step (``_dlbb_sink_uses``, default 1 — e.g. 2
+    for a tied embedding / LM-head weight), so the trainer sees the gradient complete."""
+    uses = getattr(p, "_dlbb_sink_uses", 1)
+    n = getattr(p, "_dlbb_sink_count", 0) + 1
+    if n >= uses:
+        p._dlbb_sink_count = 0
+        p._dlbb_grad_sink(p)
+    else:
+        p._dlbb_sink_count = n
 
 
 def linear_train(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor] = None,

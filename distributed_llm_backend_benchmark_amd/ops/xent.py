@@ -64,11 +64,14 @@ class _LinearXentFn(torch.autograd.Function):
               "xent_fused")
         ctx.save_for_backward(x2, w, logits)            # logits now hold dlogits / count
         ctx.shape = x.shape
+        ctx.weight = w                                  # leaf parameter: read for its grad sink
         return loss.sum() * inv.reshape(())
 
     @staticmethod
     def backward(ctx, g):
         from .gemm import wgrad
+
+        from .linear_fn import _sink, sink_used
 
         x2, w, dl = ctx.saved_tensors
         gb = g.to(dl.dtype)                             # 1.0 in the usual loss.backward()
@@ -76,7 +79,12 @@ class _LinearXentFn(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dx = torch.matmul(dl, w).mul_(gb).view(ctx.shape)
         if ctx.needs_input_grad[1]:
-            dw = wgrad(dl, x2 * gb)
+            if _sink(ctx.weight) is not None:
+                # gradient sink (e.g. the tied embedding): accumulate into .grad in the GEMM
+                wgrad(dl, x2 * gb, out=ctx.weight.grad, accumulate=True)
+                sink_used(ctx.weight)
+            else:
+                dw = wgrad(dl, x2 * gb)
         return dx, dw, None
 
 

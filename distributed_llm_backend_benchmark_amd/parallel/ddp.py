@@ -113,7 +113,10 @@ class FlatParamTrainer:
                 p.grad = self.flat_grad[o:o + p.numel()].view_as(p)
                 # single-use params (model opt-in): backward accumulates into the bucket view
                 # in-kernel and reports readiness itself (ops.linear_fn gradient sinks)
-                if getattr(p, "_dlbb_single_use", False) and _GRAD_SINKS:
+                # (a param used n > 1 times per step opts in with _dlbb_sink_uses = n, e.g. a
+                # tied embedding / LM head: ready after its last use, ops.linear_fn.sink_used)
+                if (getattr(p, "_dlbb_single_use", False)
+                        or getattr(p, "_dlbb_sink_uses", 0) > 0) and _GRAD_SINKS:
                     p._dlbb_grad_sink = self._on_grad
                     if self._wgrad_stream is not None:
                         p._dlbb_grad_stream = self._wgrad_stream
@@ -166,6 +169,9 @@ class FlatParamTrainer:
             b.ready, b.launched, b.work = 0, False, None
         self._next = 0
         self._seen.clear()
+        for p in self._params:          # per-step use counters of multi-use gradient sinks
+            if getattr(p, "_dlbb_sink_count", 0):
+                p._dlbb_sink_count = 0
 
     def _on_grad(self, p: torch.nn.Parameter) -> None:
         # a param is counted once per step: a gradient-sink param reports itself from inside its
@@ -379,6 +385,6 @@ class FlatParamTrainer:
         for h in self._hooks:
             h.remove()
         for p in self._params:
-            for attr in ("_dlbb_grad_sink", "_dlbb_grad_stream"):
+            for attr in ("_dlbb_grad_sink", "_dlbb_grad_stream", "_dlbb_sink_count"):
                 if hasattr(p, attr):
                     delattr(p, attr)

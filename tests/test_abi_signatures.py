@@ -1,0 +1,59 @@
+"""Static checks of the ctypes ABI (CPU only).
+
+Every ``_lib.lib().dlbb_*`` call in the package must have an entry in ``_lib._SIGS``: without
+``argtypes`` ctypes passes Python ints as 32-bit C ints, silently truncating device pointers
+(the kernel then faults on the GPU). Every signature must name a ``DLBB_API`` function of the
+HIP sources, and the built library (when present) must export it.
+"""
+
+import os
+import re
+import shutil
+import subprocess
+
+import pytest
+
+PKG = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                   "distributed_llm_backend_benchmark_amd")
+
+
+def _sigs():
+    from distributed_llm_backend_benchmark_amd.ops import _lib
+
+    return set(_lib._SIGS)
+
+
+def test_every_called_symbol_has_a_signature():
+    used = set()
+    for root, _, files in os.walk(PKG):
+        for f in files:
+            if f.endswith(".py"):
+                with open(os.path.join(root, f)) as fh:
+                    used |= set(re.findall(r"lib\(\)\.(dlbb_[a-z0-9_]+)", fh.read()))
+    assert used, "no library calls found"
+    missing = sorted(used - _sigs())
+    assert not missing, f"called without a ctypes signature: {missing}"
+
+
+def test_every_signature_is_a_c_api_function():
+    api = set()
+    csrc = os.path.join(PKG, "csrc")
+    for f in os.listdir(csrc):
+        if f.endswith(".hip"):
+            with open(os.path.join(csrc, f)) as fh:
+                api |= set(re.findall(r"DLBB_API\s+[\w\s\*]+?\b(dlbb_[a-z0-9_]+)\s*\(", fh.read()))
+    missing = sorted(_sigs() - api)
+    assert not missing, f"signatures without a DLBB_API definition: {missing}"
+
+
+@pytest.mark.skipif(shutil.which("nm") is None, reason="needs nm")
+def test_built_library_exports_every_signature():
+    from distributed_llm_backend_benchmark_amd.ops.build import LIB_PATH
+
+    if not os.path.exists(LIB_PATH):
+        pytest.skip("library not built")
+    out = subprocess.run(["nm", "-D", "--defined-only", LIB_PATH], capture_output=True,
+                         text=True).stdout
+    exported = set(re.findall(r"\b(dlbb_[a-z0-9_]+)\b", out))
+    missing = sorted(_sigs() - exported)
+    assert not missing, f"not exported by {LIB_PATH}: {missing}"

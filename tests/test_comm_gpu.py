@@ -335,8 +335,9 @@ def test_gpt2_ddp_step_world1():
 
 
 def test_gpt2_grad_sinks_match_autograd():
-    """Gradient sinks: block linears accumulate dW/db in-kernel into the trainer's flat buckets
-    (no AccumulateGrad); every other param goes through autograd. The flat gradients must
+    """Gradient sinks: block linears, LayerNorms, the position embedding and the tied token
+    embedding / LM head (two uses per step) accumulate in-kernel into the trainer's flat buckets
+    (no AccumulateGrad); the flat gradients must
     equal a plain autograd backward of the same model, and every bucket must be counted
     complete exactly once during backward."""
     from distributed_llm_backend_benchmark_amd.models.gpt2 import GPT2, GPT2Config
@@ -349,7 +350,7 @@ def test_gpt2_grad_sinks_match_autograd():
     ref(idx, idx).backward()
     m = GPT2(cfg, device=dev, seed=11)
     tr = FlatParamTrainer(m, None, lr=1e-3, bucket_mb=0.25)
-    assert sum(hasattr(p, "_dlbb_grad_sink") for p in m.parameters()) == 12 * cfg.n_layer + 2
+    assert sum(hasattr(p, "_dlbb_grad_sink") for p in m.parameters()) == 12 * cfg.n_layer + 4
     for _ in range(2):                      # second pass: buffers reused, zeroed, re-counted
         tr.zero_grad()
         tr._reset()
