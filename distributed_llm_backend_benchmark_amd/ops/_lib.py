@@ -57,6 +57,7 @@ _SIGS = {
     "dlbb_gemm_get_stagger": (c_int, []),
     "dlbb_gemm_wgrad_set_stages": (None, [c_int]),
     "dlbb_attn_set_xcd": (None, [c_int]),
+    "dlbb_attn_set_concurrent": (None, [c_int]),
     "dlbb_xent_set_variant": (None, [c_int]),
     "dlbb_xent_fused": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int64,
                                 c_void_p, c_void_p]),

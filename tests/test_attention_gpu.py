@@ -96,3 +96,36 @@ def test_attn_bwd_matches_fp32_reference(B, T, H):
         err = float((got - want).abs().max())
         scale = float(want.abs().max())
         assert err <= 0.03 * scale + 0.02, (name, err, scale)
+
+
+def test_attn_bwd_concurrent_matches_sequential():
+    """The opt-in concurrent backward (dQ on a forked side stream, joined back) gives bitwise the
+    same dQKV as the sequential launch, eagerly and inside a captured HIP graph."""
+    from distributed_llm_backend_benchmark_amd.ops import _lib
+    from distributed_llm_backend_benchmark_amd.ops.attention import attn_bwd, attn_fwd
+
+    B, T, H = 2, 384, 4
+    g = torch.Generator(device="cuda").manual_seed(9)
+    qkv = torch.randn(B, T, 3 * H * 64, device="cuda", generator=g).to(torch.bfloat16)
+    gout = torch.randn(B, T, H * 64, device="cuda", generator=g).to(torch.bfloat16)
+    out, lse = attn_fwd(qkv, H)
+    try:
+        _lib.lib().dlbb_attn_set_concurrent(0)
+        ref = attn_bwd(qkv, out, lse, gout, H)
+        _lib.lib().dlbb_attn_set_concurrent(1)
+        got = attn_bwd(qkv, out, lse, gout, H)
+        torch.cuda.synchronize()
+        assert torch.equal(got, ref)
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            attn_bwd(qkv, out, lse, gout, H)        # warm allocations off the capture
+        torch.cuda.current_stream().wait_stream(side)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            static = attn_bwd(qkv, out, lse, gout, H)
+        graph.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(static, ref)
+    finally:
+        _lib.lib().dlbb_attn_set_concurrent(0)
