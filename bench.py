@@ -54,10 +54,12 @@ SWEEP_BYTES = [1 << 10, 8 << 10, 64 << 10, 512 << 10, 4 << 20, 32 << 20, 256 << 
 
 def _allreduce_sweep(comm, max_mib: int):
     """Mean time per call (back to back, rank max) of a bf16 SUM all-reduce per message size and
-    implementation; per size the fastest is reported with busBW / algBW. Candidates: RCCL via
+    implementation; per size the fastest VALIDATED one (one extra call on fresh data checked
+    against an fp32 reference sum on every rank) is reported with busBW / algBW. Candidates: RCCL via
     torch, RCCL via our native engine, and (P > 1, self-test passed) the IPC xGMI kernel —
     staged one-/two-shot within its staging capacity, and in place on a registered buffer."""
     import torch
+    import torch.distributed as dist
 
     from distributed_llm_backend_benchmark_amd.parallel.collectives import make_data, make_op
     from distributed_llm_backend_benchmark_amd.stats.bandwidth import algbw_gbps, busbw_gbps
@@ -83,7 +85,10 @@ def _allreduce_sweep(comm, max_mib: int):
         if car is not None and car.reg_healthy and car.supports_registered(flat):
             cands.append(("custom_reg", {"impl": "custom_reg", "nblocks": 256}))
         iters = 50 if nbytes <= 4 << 20 else 20 if nbytes <= 32 << 20 else 8
-        res = {}
+        ref = data.float()                  # fp32 reference sum through the process group
+        if P > 1:
+            dist.all_reduce(ref)
+        res, invalid = {}, []
         for label, opts in cands:
             try:
                 op = make_op("allreduce", comm, data, **opts)
@@ -92,16 +97,37 @@ def _allreduce_sweep(comm, max_mib: int):
             for _ in range(3):
                 op.run()
             comm.sync()
-            res[label] = _timed_steps(comm, op, iters) / iters
+            t = _timed_steps(comm, op, iters) / iters
+            if _checked(comm, op, ref):
+                res[label] = t
+            else:
+                invalid.append(label)
             del op
+        if not res:
+            out.append({"bytes": nbytes, "impl": None, "invalid": invalid})
+            continue
         best = min(res, key=res.get)
         t = res[best]
         out.append({"bytes": nbytes, "impl": best, "us": round(t * 1e6, 2),
                     "busbw_GBps": round(busbw_gbps("allreduce", nbytes, t, P), 3),
                     "algbw_GBps": round(algbw_gbps("allreduce", nbytes, t, P), 3),
-                    "us_by_impl": {k: round(v * 1e6, 2) for k, v in res.items()}})
+                    "us_by_impl": {k: round(v * 1e6, 2) for k, v in res.items()},
+                    **({"invalid": invalid} if invalid else {})})
         del data, flat
     return out
+
+
+def _checked(comm, op, ref) -> bool:
+    """One all-reduce on fresh data compared with the fp32 reference sum ``ref``; collective:
+    True only if it matched on every rank (a candidate that fails is never reported)."""
+    import torch
+
+    op.reset()
+    op.run()
+    comm.sync()
+    ok = bool(torch.allclose(op.result().float(), ref, rtol=2e-2,
+                             atol=5e-2 * comm.world_size))
+    return all(comm.all_gather_object(ok))
 
 
 def _timed_steps(comm, op, steps: int) -> float:
@@ -167,8 +193,13 @@ def main(argv=None) -> int:
                           for nb in (128, 256)]
         if args.impl == "custom" and not cands:
             raise SystemExit("custom all-reduce unavailable (setup or self-test failed)")
-    trial = {}
+    trial, invalid = {}, []
     op, op_label = None, None
+    ref = data.float()                  # fp32 reference sum: every candidate is checked once
+    if P > 1:
+        import torch.distributed as dist
+
+        dist.all_reduce(ref)
     for label, impl, opts in cands:
         try:
             cand = make_op("allreduce", comm, data, impl=impl, **opts)
@@ -178,12 +209,19 @@ def main(argv=None) -> int:
             if comm.rank == 0:
                 print(f"note: {label} all-reduce unavailable: {e}", file=sys.stderr)
             continue
+        if not _checked(comm, cand, ref):
+            invalid.append(label)
+            if comm.rank == 0:
+                print(f"note: {label} all-reduce gave a wrong sum; not used", file=sys.stderr)
+            continue
         for _ in range(max(1, args.warmup)):
             cand.run()
         comm.sync()
         trial[label] = _timed_steps(comm, cand, 10) / 10 if len(cands) > 1 else 0.0
         if op is None or trial[label] < trial[op_label]:
             op, op_label = cand, label
+    if op is None:
+        raise SystemExit(f"no all-reduce implementation passed its check: {invalid}")
     nbytes = op.message_bytes
     for _ in range(args.warmup):
         op.run()
@@ -290,6 +328,7 @@ def main(argv=None) -> int:
                 "parallelism": f"{'rccl' if comm.backend == 'nccl' else comm.backend}_world{P}",
                 "impl": op_label,
                 "impl_trial_ms": {k: v * 1e3 for k, v in trial.items()} if len(trial) > 1 else None,
+                "impl_invalid": invalid or None,
             },
             "algbw_GBps": alg,
             "baseline_busbw_GBps": REF_BUSBW_GBPS,
