@@ -151,6 +151,24 @@ if "wgrad256" in which:
                     lambda: _wgrad_hip256(dy, x, w_out, True, sp, b_out), iters=30) * 1e6
         out(kernel="wgrad_tiles", M=M, N=N, K=K, us=res,
             tflops={k: round(2 * M * N * K / v / 1e6, 1) for k, v in res.items()})
+if "wgradsplit" in which:
+    # total weight-gradient time (split-K GEMM + partial reduce, accumulate + fused bias) by
+    # split, both tiles: the split heuristic targets the GEMM alone
+    from distributed_llm_backend_benchmark_amd.ops.gemm import _wgrad_hip, _wgrad_hip256
+    for N, K in ((2304, 768), (768, 768), (3072, 768), (768, 3072)):
+        M = 16384
+        dy, x = rnd(M, N), rnd(M, K)
+        w_out, b_out = torch.empty(N, K, device="cuda", dtype=torch.bfloat16), \
+            torch.empty(N, device="cuda", dtype=torch.bfloat16)
+        res = {}
+        for sp in (None, 1, 2, 3, 4, 6, 8, 12, 16, 24):
+            res[f"t128_s{sp}"] = round(t_med(lambda: _wgrad_hip(dy, x, w_out, True, sp, b_out),
+                                             iters=30) * 1e6, 1)
+            if N % 256 == 0:
+                res[f"t256_s{sp}"] = round(t_med(
+                    lambda: _wgrad_hip256(dy, x, w_out, True, sp, b_out), iters=30) * 1e6, 1)
+        best = min(res, key=res.get)
+        out(kernel="wgrad_split_total", M=M, N=N, K=K, best=best, us=res)
 if "xent" in which:
     # fused in-place LM-head loss pass (logits -> dlogits + per-row loss), v1 vs v2, at the
     # GPT-2 step shape; the pass is in place, so each timed call first restores the logits
