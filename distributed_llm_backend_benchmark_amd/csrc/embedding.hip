@@ -27,7 +27,7 @@ __global__ void __launch_bounds__(kEmbThreads) emb_fwd_kernel(
   const int64_t row = blockIdx.x;                 // b * T + t
   const int t = static_cast<int>(row % T);
   int64_t id = idx[row];
-  id = id < 0 ? 0 : (id >= V ? V - 1 : id);        // host validated; clamp keeps reads in bounds
+  id = id < 0 ? 0 : (id >= V ? V - 1 : id);        // invalid ids: clamped reads stay in bounds
   const uint16_t* e = wte + id * C;
   const uint16_t* p = wpe + static_cast<int64_t>(t) * C;
   uint16_t* o = out + row * C;
@@ -46,13 +46,14 @@ template <int DTG>
 __global__ void __launch_bounds__(kEmbThreads) emb_bwd_kernel(
     const int64_t* __restrict__ sorted_ids, const int64_t* __restrict__ order,
     const uint16_t* __restrict__ dx, void* __restrict__ wte_grad, void* __restrict__ wpe_grad,
-    int64_t N, int T, int C) {
+    int64_t N, int T, int C, int64_t V) {
   const int64_t blk = blockIdx.x;
   const int nv = C / 8;
   if (blk < N) {
     if (wte_grad == nullptr) return;
     const int64_t id = sorted_ids[blk];
     if (blk > 0 && sorted_ids[blk - 1] == id) return;     // not the start of this id's run
+    if (id < 0 || id >= V) return;                        // invalid ids contribute nothing
     int64_t end = blk + 1;
     while (end < N && sorted_ids[end] == id) ++end;
     for (int v = threadIdx.x; v < nv; v += kEmbThreads) {
@@ -103,11 +104,12 @@ DLBB_API int dlbb_embedding_fwd(const int64_t* idx, const void* wte, const void*
 }
 
 // Accumulate the embedding gradients: wte_grad[sorted_ids[i]] += dx[order[i]] (runs of equal ids
-// summed in order), wpe_grad[t] += sum_b dx[b, t]. Either grad pointer may be null (skipped).
+// summed in order; ids outside [0, V) are skipped), wpe_grad[t] += sum_b dx[b, t]. Either grad
+// pointer may be null (skipped).
 // dt_grad: 1 bf16, 0 fp32 (both grads). dx bf16 [N = B*T, C].
 DLBB_API int dlbb_embedding_bwd(const int64_t* sorted_ids, const int64_t* order, const void* dx,
                                 void* wte_grad, void* wpe_grad, int dt_grad, int64_t N, int T,
-                                int C, hipStream_t stream) {
+                                int C, int64_t V, hipStream_t stream) {
   if (N <= 0) return hipSuccess;
   if (C % 8 || T <= 0 || N % T) return hipErrorInvalidValue;
   auto mis = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) != 0; };
@@ -116,10 +118,10 @@ DLBB_API int dlbb_embedding_bwd(const int64_t* sorted_ids, const int64_t* order,
   const auto* d = static_cast<const uint16_t*>(dx);
   if (dt_grad == DT_BF16)
     hipLaunchKernelGGL(emb_bwd_kernel<DT_BF16>, g, dim3(kEmbThreads), 0, stream, sorted_ids,
-                       order, d, wte_grad, wpe_grad, N, T, C);
+                       order, d, wte_grad, wpe_grad, N, T, C, V);
   else if (dt_grad == DT_F32)
     hipLaunchKernelGGL(emb_bwd_kernel<DT_F32>, g, dim3(kEmbThreads), 0, stream, sorted_ids,
-                       order, d, wte_grad, wpe_grad, N, T, C);
+                       order, d, wte_grad, wpe_grad, N, T, C, V);
   else
     return hipErrorInvalidValue;
   return hipGetLastError();

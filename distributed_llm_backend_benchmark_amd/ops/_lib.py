@@ -79,7 +79,7 @@ _SIGS = {
     "dlbb_embedding_fwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int, c_int,
                                    c_int64, c_void_p]),
     "dlbb_embedding_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
-                                   c_int64, c_int, c_int, c_void_p]),
+                                   c_int64, c_int, c_int, c_int64, c_void_p]),
     "dlbb_attn_fwd": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int, c_int,
                               c_int, c_int, c_float, c_void_p]),
     "dlbb_attn_bwd": (c_int, [c_void_p, c_int64, c_void_p, c_void_p, c_int64, c_void_p,

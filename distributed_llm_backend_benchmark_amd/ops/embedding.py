@@ -70,7 +70,7 @@ class _EmbeddingFn(torch.autograd.Function):
             check(_lib.lib().dlbb_embedding_bwd(
                 _lib.ptr(sorted_ids) if e is not None else None,
                 _lib.ptr(order) if e is not None else None, d2.data_ptr(), _lib.ptr(e),
-                _lib.ptr(p), _lib._DT[g_dt], N, T, C,
+                _lib.ptr(p), _lib._DT[g_dt], N, T, C, wte.shape[0],
                 _lib.stream(d2.device)), "embedding_bwd")
         out_e = out_p = None
         if need_e:

@@ -57,3 +57,23 @@ def test_built_library_exports_every_signature():
     exported = set(re.findall(r"\b(dlbb_[a-z0-9_]+)\b", out))
     missing = sorted(_sigs() - exported)
     assert not missing, f"not exported by {LIB_PATH}: {missing}"
+
+
+def test_signature_argument_counts_match_the_c_api():
+    """argtypes must have exactly as many entries as the C function has parameters (a missing
+    one shifts every later argument — e.g. the stream — into the wrong register)."""
+    from distributed_llm_backend_benchmark_amd.ops import _lib
+
+    csrc = os.path.join(PKG, "csrc")
+    nargs = {}
+    for f in os.listdir(csrc):
+        if f.endswith(".hip"):
+            with open(os.path.join(csrc, f)) as fh:
+                src = fh.read()
+            for m in re.finditer(r"DLBB_API\s+[\w\s\*]+?\b(dlbb_[a-z0-9_]+)\s*\(([^)]*)\)", src):
+                params = m.group(2).strip()
+                nargs[m.group(1)] = 0 if params in ("", "void") else params.count(",") + 1
+    assert len(nargs) > 30, f"parsed only {len(nargs)} C API functions"
+    bad = {name: (len(args), nargs.get(name)) for name, (_, args) in _lib._SIGS.items()
+           if nargs.get(name) is not None and len(args) != nargs[name]}
+    assert not bad, f"argtypes count != C parameter count (argtypes, C): {bad}"
