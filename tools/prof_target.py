@@ -1,5 +1,5 @@
 """Tiny driver for PMC-counter profiling: runs ONE op a few times (no timing logic).
-usage: prof_target.py gemm256|gemm128|blas|reduce8|ln|xent"""
+usage: prof_target.py gemm256|gemm128|blas|reduce8|ln|xent|xentfused|embbwd"""
 import os
 import sys
 
@@ -32,6 +32,27 @@ elif what == "xent":
     x = torch.randn(16384, 50304, device=dev, generator=g).to(torch.bfloat16)
     t = torch.randint(0, 50304, (16384,), device=dev)
     fn = lambda: ops.cross_entropy(x, t)  # noqa: E731
+elif what == "xentfused":       # the in-place LM-head loss pass (v2), GPT-2 step shape
+    from distributed_llm_backend_benchmark_amd.ops import _lib as L
+
+    x = torch.randn(16384, 50304, device=dev, generator=g).to(torch.bfloat16)
+    t = torch.randint(0, 50304, (16384,), device=dev)
+    loss = torch.empty(16384, device=dev)
+    sc = torch.full((1,), 1.0 / 16384, device=dev)
+    fn = lambda: L.check(L.lib().dlbb_xent_fused(  # noqa: E731
+        x.data_ptr(), t.data_ptr(), loss.data_ptr(), 16384, 50304, 50304, sc.data_ptr(),
+        L.stream(x.device)), "xent_fused")
+elif what == "embbwd":          # embedding backward into bf16 gradient buffers, GPT-2 shape
+    from distributed_llm_backend_benchmark_amd.ops import _lib as L
+
+    ids = torch.randint(0, 50304, (16384,), device=dev)
+    s_ids, order = torch.sort(ids, stable=True)
+    dx = torch.randn(16384, 768, device=dev, generator=g).to(torch.bfloat16)
+    ge = torch.zeros(50304, 768, device=dev, dtype=torch.bfloat16)
+    gp = torch.zeros(1024, 768, device=dev, dtype=torch.bfloat16)
+    fn = lambda: L.check(L.lib().dlbb_embedding_bwd(  # noqa: E731
+        s_ids.data_ptr(), order.data_ptr(), dx.data_ptr(), ge.data_ptr(), gp.data_ptr(),
+        L.DT_BF16, 16384, 1024, 768, 50304, L.stream(dx.device)), "embedding_bwd")
 else:
     raise SystemExit(f"unknown target {what}")
 for _ in range(5):
