@@ -62,7 +62,7 @@ class _FusedAddLayerNorm(torch.autograd.Function):
         ws = torch.empty((2 if ctx.has_bias else 1) * grid * cols, dtype=torch.float32,
                          device=hin.device)
         # gradient sinks (ops.linear_fn): dγ/dβ accumulate straight into the trainer's views
-        from .linear_fn import _sink
+        from .linear_fn import _sink, sink_used
 
         w_p, b_p = ctx.params
         w_sink, b_sink = _sink(w_p), (_sink(b_p) if ctx.has_bias else None)
@@ -75,9 +75,9 @@ class _FusedAddLayerNorm(torch.autograd.Function):
             _lib.ptr(db), rows, cols, int(direct), _lib.stream(hin.device)), "layernorm_bwd")
         dxv = dx.view(ctx.shape)
         if direct:
-            w_sink(w_p)
+            sink_used(w_p)
             if ctx.has_bias:
-                b_sink(b_p)
+                sink_used(b_p)
             return dxv, (dxv if ctx.has_res else None), None, None, None
         return dxv, (dxv if ctx.has_res else None), dw, db, None
 
