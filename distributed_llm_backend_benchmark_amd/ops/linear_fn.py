@@ -119,10 +119,17 @@ def _sink(p: Optional[torch.Tensor]):
     return cb
 
 
+def sink_fresh(p: torch.Tensor) -> bool:
+    """True if the sink parameter's ``.grad`` is still the zeros the trainer wrote this step (no
+    write since ``zero_grad``): a writer may then store instead of accumulate."""
+    return bool(getattr(p, "_dlbb_grad_fresh", False))
+
+
 def sink_used(p: torch.Tensor) -> None:
     """Record one in-kernel accumulation into a sink parameter's ``.grad``; the sink callback
     fires after the parameter's last use of the step (``_dlbb_sink_uses``, default 1 — e.g. 2
     for a tied embedding / LM-head weight), so the trainer sees the gradient complete."""
+    p._dlbb_grad_fresh = False          # the buffer now holds this step's partial gradient
     uses = getattr(p, "_dlbb_sink_uses", 1)
     n = getattr(p, "_dlbb_sink_count", 0) + 1
     if n >= uses:

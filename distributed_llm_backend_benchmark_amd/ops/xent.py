@@ -71,7 +71,7 @@ class _LinearXentFn(torch.autograd.Function):
     def backward(ctx, g):
         from .gemm import wgrad
 
-        from .linear_fn import _sink, sink_used
+        from .linear_fn import _sink, sink_fresh, sink_used
 
         x2, w, dl = ctx.saved_tensors
         gb = g.to(dl.dtype)                             # 1.0 in the usual loss.backward()
@@ -80,8 +80,10 @@ class _LinearXentFn(torch.autograd.Function):
             dx = torch.matmul(dl, w).mul_(gb).view(ctx.shape)
         if ctx.needs_input_grad[1]:
             if _sink(ctx.weight) is not None:
-                # gradient sink (e.g. the tied embedding): accumulate into .grad in the GEMM
-                wgrad(dl, x2 * gb, out=ctx.weight.grad, accumulate=True)
+                # gradient sink (e.g. the tied embedding): accumulate into .grad in the GEMM —
+                # or store, when this is the first write since zero_grad (the LM head is the
+                # first op of the backward: a beta = 0 GEMM, no read of the 77 MB buffer)
+                wgrad(dl, x2 * gb, out=ctx.weight.grad, accumulate=not sink_fresh(ctx.weight))
                 sink_used(ctx.weight)
             else:
                 dw = wgrad(dl, x2 * gb)

@@ -261,6 +261,9 @@ class FlatParamTrainer:
     def zero_grad(self) -> None:
         if self.mode == "view":
             self.flat_grad.zero_()
+            for p in self._params:      # sink writers may store instead of accumulate once
+                if hasattr(p, "_dlbb_grad_sink"):
+                    p._dlbb_grad_fresh = True
         else:
             for p in self._params:
                 p.grad = None
@@ -385,6 +388,7 @@ class FlatParamTrainer:
         for h in self._hooks:
             h.remove()
         for p in self._params:
-            for attr in ("_dlbb_grad_sink", "_dlbb_grad_stream", "_dlbb_sink_count"):
+            for attr in ("_dlbb_grad_sink", "_dlbb_grad_stream", "_dlbb_sink_count",
+                         "_dlbb_grad_fresh"):
                 if hasattr(p, attr):
                     delattr(p, attr)
