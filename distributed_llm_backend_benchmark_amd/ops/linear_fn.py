@@ -78,6 +78,8 @@ class _LinearFn(torch.autograd.Function):
         w_sink = _sink(ctx.weight) if ctx.needs_input_grad[1] else None
         b_sink = _sink(ctx.bias) if fuse_db else None
         if w_sink is not None and (not want_db or b_sink is not None):
+            # store instead of accumulate while the buffers are still this step's zeros
+            acc = not (sink_fresh(ctx.weight) and (not want_db or sink_fresh(ctx.bias)))
             side = getattr(ctx.weight, "_dlbb_grad_stream", None)
             if side is not None:
                 # dW is off the backward's critical path: run it on the trainer's side stream
@@ -85,12 +87,12 @@ class _LinearFn(torch.autograd.Function):
                 # orders its bucket reductions and the optimizer after that stream
                 side.wait_stream(torch.cuda.current_stream(du.device))
                 with torch.cuda.stream(side):
-                    wgrad(du, x2, out=ctx.weight.grad, accumulate=True,
+                    wgrad(du, x2, out=ctx.weight.grad, accumulate=acc,
                           bias_out=ctx.bias.grad if want_db else None)
                 du.record_stream(side)
                 x2.record_stream(side)
             else:
-                wgrad(du, x2, out=ctx.weight.grad, accumulate=True,
+                wgrad(du, x2, out=ctx.weight.grad, accumulate=acc,
                       bias_out=ctx.bias.grad if want_db else None)
             sink_used(ctx.weight)
             if want_db:

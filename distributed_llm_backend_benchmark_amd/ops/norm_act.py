@@ -62,7 +62,7 @@ class _FusedAddLayerNorm(torch.autograd.Function):
         ws = torch.empty((2 if ctx.has_bias else 1) * grid * cols, dtype=torch.float32,
                          device=hin.device)
         # gradient sinks (ops.linear_fn): dγ/dβ accumulate straight into the trainer's views
-        from .linear_fn import _sink, sink_used
+        from .linear_fn import _sink, sink_fresh, sink_used
 
         w_p, b_p = ctx.params
         w_sink, b_sink = _sink(w_p), (_sink(b_p) if ctx.has_bias else None)
@@ -72,7 +72,9 @@ class _FusedAddLayerNorm(torch.autograd.Function):
         check(_lib.lib().dlbb_layernorm_bwd(
             dy2.data_ptr(), hin.data_ptr(), weight.data_ptr(), dt(weight), mean.data_ptr(),
             rstd.data_ptr(), _lib.ptr(dh2), dx.data_ptr(), ws.data_ptr(), dw.data_ptr(),
-            _lib.ptr(db), rows, cols, int(direct), _lib.stream(hin.device)), "layernorm_bwd")
+            _lib.ptr(db), rows, cols,
+            int(direct and not (sink_fresh(w_p) and (not ctx.has_bias or sink_fresh(b_p)))),
+            _lib.stream(hin.device)), "layernorm_bwd")
         dxv = dx.view(ctx.shape)
         if direct:
             sink_used(w_p)
