@@ -27,6 +27,11 @@ import os
 import sys
 import time
 
+# RCCL / HIP IPC on this pool support only the dmabuf path: set before torch initialises HIP
+# (every launcher exports it too; the driver's scaling run starts bench.py directly)
+os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+
+HBM_PEAK_GBPS = 8000.0         # MI355X HBM3E: no all-reduce can report algBW above this
 REF_BUSBW_GBPS = 5.46          # best 3D all-reduce busBW (P=8, 64 MiB bf16)
 REF_LAT_512B_US = {2: 22.9, 8: 32.0}
 REF_BUSBW_8MIB = 7.53
@@ -77,9 +82,14 @@ def _allreduce_sweep(comm, max_mib: int):
             break
         data = make_data((nbytes // 2,), torch.bfloat16, comm.rank, comm.device)
         flat = data.reshape(-1)
-        cands = [("rccl", {"impl": "rccl"})]
-        if comm.is_gpu:
-            cands.append(("native", {"impl": "native"}))
+        if P == 1 and comm.is_gpu:
+            # one rank: an in-place all-reduce enqueues no GPU work; time the out-of-place form
+            # (the identity all-reduce = a real device copy of the message)
+            cands = [("native_oop", {"impl": "native", "out_of_place": True})]
+        else:
+            cands = [("rccl", {"impl": "rccl"})]
+            if comm.is_gpu:
+                cands.append(("native", {"impl": "native"}))
         if car is not None and car.healthy and car.supports(flat):
             cands.append(("custom", {"impl": "custom"}))
         if car is not None and car.reg_healthy and car.supports_registered(flat):
@@ -103,6 +113,13 @@ def _allreduce_sweep(comm, max_mib: int):
             else:
                 invalid.append(label)
             del op
+        if not res:
+            out.append({"bytes": nbytes, "impl": None, "invalid": invalid})
+            continue
+        for k in [k for k, v in res.items() if algbw_gbps("allreduce", nbytes, v, P)
+                  > HBM_PEAK_GBPS]:
+            invalid.append(f"{k}:above_hbm_roofline")   # an empty call, not a measurement
+            del res[k]
         if not res:
             out.append({"bytes": nbytes, "impl": None, "invalid": invalid})
             continue
@@ -171,10 +188,15 @@ def main(argv=None) -> int:
     # candidates: (label, impl, opts); every rank builds the same list (the custom kernel's
     # health flags are agreed collectively), so trial construction stays collective-safe
     cands = []
-    if args.impl in ("best", "rccl"):
-        cands.append(("rccl", "rccl", {}))
-    if args.impl in ("best", "native") and comm.is_gpu:
-        cands.append(("native", "native", {}))
+    if P == 1 and comm.is_gpu:
+        # one rank: in-place all-reduces (RCCL or native) enqueue no GPU work, so the only
+        # candidate is the out-of-place identity all-reduce, a real HBM copy of the message
+        cands.append(("native_oop", "native", {"out_of_place": True}))
+    else:
+        if args.impl in ("best", "rccl"):
+            cands.append(("rccl", "rccl", {}))
+        if args.impl in ("best", "native") and comm.is_gpu:
+            cands.append(("native", "native", {}))
     if args.impl in ("best", "custom") and P > 1 and comm.is_gpu:
         from distributed_llm_backend_benchmark_amd.parallel.custom_allreduce import (
             get_custom_allreduce)
@@ -230,11 +252,16 @@ def main(argv=None) -> int:
     per_step = total / args.steps
     bus = busbw_gbps("allreduce", nbytes, per_step, P)
     alg = algbw_gbps("allreduce", nbytes, per_step, P)
+    if alg > HBM_PEAK_GBPS:
+        raise SystemExit(f"algBW {alg:.0f} GB/s is above the HBM roofline: {op_label} timed an "
+                         "empty call, refusing to report it")
 
     side = {}
     if not args.no_side:
+        small_opts = ({"impl": "native", "out_of_place": True} if P == 1 and comm.is_gpu
+                      else {"impl": "auto"})
         small = make_op("allreduce", comm, make_data((256,), torch.bfloat16, comm.rank,
-                                                     comm.device), impl="auto")
+                                                     comm.device), **small_opts)
         tr = time_per_iteration(comm, small, iters=100, warmup=10)
         allt = comm.gather_floats(tr.timings)
         lat_native = None
@@ -244,14 +271,16 @@ def main(argv=None) -> int:
 
                 eng = get_native(comm)
                 sb = make_data((256,), torch.bfloat16, comm.rank, comm.device)
+                rb = torch.empty_like(sb) if P == 1 else sb   # one rank: out of place (a copy)
                 # per-iteration loop in C++: device barrier, event, all-reduce, event
-                lat_native = comm.gather_floats(eng.time_iters("allreduce", sb, sb, 256,
+                lat_native = comm.gather_floats(eng.time_iters("allreduce", sb, rb, 256,
                                                                iters=100, warmup=10))
             except RuntimeError as e:
                 if comm.rank == 0:
                     print(f"note: native 512 B timing unavailable: {e}", file=sys.stderr)
         mid = make_op("allreduce", comm, make_data((4 * 1024 * 1024,), torch.bfloat16,
-                                                   comm.rank, comm.device), impl=op.impl)
+                                                   comm.rank, comm.device),
+                      **(small_opts if P == 1 else {"impl": op.impl}))
         for _ in range(5):
             mid.run()
         mid_t = _timed_steps(comm, mid, 20) / 20
@@ -305,6 +334,19 @@ def main(argv=None) -> int:
                 del cop
             coll[name] = res
 
+    # one GPU: the IPC collective kernels measured with W virtual ranks in this process
+    # (parallel/virtual_ranks.py) — protocol latency and in-place two-shot time on one HBM,
+    # validated against an fp32 sum first; NOT inter-GPU numbers (never used for "value")
+    emulation = None
+    if P == 1 and comm.is_gpu and not args.no_side:
+        try:
+            from distributed_llm_backend_benchmark_amd.parallel.virtual_ranks import (
+                emulation_summary)
+
+            emulation = emulation_summary(big_bytes=nbytes)
+        except Exception as e:  # noqa: BLE001 - side measurement only
+            emulation = {"error": repr(e)}
+
     if comm.rank == 0:
         rec = {
             "metric": "all-reduce bus BW (GB/s)",
@@ -333,13 +375,23 @@ def main(argv=None) -> int:
             "algbw_GBps": alg,
             "baseline_busbw_GBps": REF_BUSBW_GBPS,
             "note": ("busBW = bytes/t*2(P-1)/P (nccl-tests); identically 0 at P=1, where "
-                     "vs_baseline is null (reference has no single-rank data)"),
+                     "vs_baseline is null (reference has no single-rank data)" +
+                     ("; P=1 step = out-of-place identity all-reduce (a device copy of the "
+                      "message: real GPU work, algBW = copy throughput); in-place candidates "
+                      "enqueue nothing at one rank and are excluded" if P == 1 else "")),
             **side,
         }
         if coll:
             rec["collectives_same_message"] = coll
         if sweep:
             rec["allreduce_sweep"] = sweep
+        if emulation is not None:
+            rec["virtual_rank_emulation"] = {
+                "what": ("IPC all-reduce kernels, W ranks emulated on ONE GPU (one fused launch "
+                         "of the production device code; all traffic through one HBM, not "
+                         "xGMI): one-shot 512 B latency and registered two-shot on the headline "
+                         "message, us per call back to back"),
+                **emulation}
         print(json.dumps(rec), flush=True)
     comm.barrier()
     comm.destroy()

@@ -67,23 +67,32 @@ struct CarKernelArgs {
   int world;
 };
 
-__device__ __forceinline__ void signal_peers(const CarKernelArgs& a, int phase, uint32_t e) {
+// Every kernel body takes its workgroup index `bid` and workgroup count `nb` explicitly instead of
+// reading blockIdx / gridDim, so the same device code runs in two launch forms:
+//   * per rank (production): one grid of nb workgroups per GPU, bid = blockIdx.x;
+//   * virtual ranks (single-GPU harness, dlbb_car_vr_launch): ONE grid of world x nb workgroups
+//     on one GPU, workgroup g plays rank g / nb with bid = g % nb against the sibling ranks'
+//     buffers in the same HBM. Same loads, stores, flags and fences as production; only the
+//     transport differs (local HBM instead of xGMI).
+__device__ __forceinline__ void signal_peers(const CarKernelArgs& a, int phase, uint32_t e,
+                                             unsigned bid) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x < static_cast<unsigned>(a.world)) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __hip_atomic_store(&a.sig[threadIdx.x]->flags[phase][blockIdx.x][a.rank], e,
+    __hip_atomic_store(&a.sig[threadIdx.x]->flags[phase][bid][a.rank], e,
                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
 
-__device__ __forceinline__ bool wait_peers(const CarKernelArgs& a, int phase, uint32_t e) {
+__device__ __forceinline__ bool wait_peers(const CarKernelArgs& a, int phase, uint32_t e,
+                                           unsigned bid) {
   __shared__ int timed_out;
   if (threadIdx.x == 0) timed_out = 0;
   __syncthreads();
   if (threadIdx.x < static_cast<unsigned>(a.world)) {
-    uint32_t* f = &a.sig[a.rank]->flags[phase][blockIdx.x][threadIdx.x];
+    uint32_t* f = &a.sig[a.rank]->flags[phase][bid][threadIdx.x];
     unsigned spins = 0;
     while (static_cast<int32_t>(
                __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - e) < 0) {
@@ -101,15 +110,15 @@ __device__ __forceinline__ bool wait_peers(const CarKernelArgs& a, int phase, ui
   return timed_out == 0;
 }
 
-// Advance this call's epoch (see header): each workgroup bumps its own slot, block 0 also the
-// slots no workgroup of this grid owns. Returns the epoch of the calling workgroup.
-__device__ __forceinline__ uint32_t begin_epoch(const CarKernelArgs& a) {
+// Advance this call's epoch (see header): each workgroup bumps its own slot, workgroup 0 also the
+// slots no workgroup of this call owns. Returns the epoch of the calling workgroup.
+__device__ __forceinline__ uint32_t begin_epoch(const CarKernelArgs& a, unsigned bid,
+                                                unsigned nb) {
   __shared__ uint32_t s_epoch;
   Signal* s = a.sig[a.rank];
-  if (threadIdx.x == 0) s_epoch = ++s->epoch[blockIdx.x];
-  if (blockIdx.x == 0)
-    for (unsigned b = gridDim.x + threadIdx.x; b < static_cast<unsigned>(kMaxBlocks);
-         b += blockDim.x)
+  if (threadIdx.x == 0) s_epoch = ++s->epoch[bid];
+  if (bid == 0)
+    for (unsigned b = nb + threadIdx.x; b < static_cast<unsigned>(kMaxBlocks); b += blockDim.x)
       ++s->epoch[b];
   __syncthreads();
   return s_epoch;
@@ -146,15 +155,21 @@ __device__ __forceinline__ void sum_vec(const CarKernelArgs& a, int64_t half, in
   }
 }
 
+// Sub-range [r0, r1) of n items owned by workgroup bid of nb.
+__device__ __forceinline__ void split_range(int64_t n, unsigned bid, unsigned nb, int64_t& r0,
+                                            int64_t& r1) {
+  const int64_t per = (n + nb - 1) / nb;
+  r0 = bid * per;
+  r1 = r0 + per < n ? r0 + per : n;
+}
+
 template <int DT, int W>
-__global__ void __launch_bounds__(kCarThreads) car_oneshot_kernel(CarKernelArgs a) {
+__device__ __forceinline__ void oneshot_body(const CarKernelArgs& a, unsigned bid, unsigned nb) {
   constexpr int64_t kVecBytes = 8 * Elem<DT>::kBytes;
-  const uint32_t e = begin_epoch(a);
+  const uint32_t e = begin_epoch(a, bid, nb);
   const int64_t half = (e & 1) * a.cap;
-  const int64_t nvec = a.nbytes / kVecBytes;
-  const int64_t per = (nvec + gridDim.x - 1) / gridDim.x;
-  const int64_t v0 = blockIdx.x * per;
-  const int64_t v1 = v0 + per < nvec ? v0 + per : nvec;
+  int64_t v0, v1;
+  split_range(a.nbytes / kVecBytes, bid, nb, v0, v1);
   char* mine = a.data[a.rank] + half;
   for (int64_t v = v0 + threadIdx.x; v < v1; v += blockDim.x) {
 #pragma unroll
@@ -162,8 +177,8 @@ __global__ void __launch_bounds__(kCarThreads) car_oneshot_kernel(CarKernelArgs 
       reinterpret_cast<u16x8*>(mine + v * kVecBytes)[q] =
           reinterpret_cast<const u16x8*>(static_cast<const char*>(a.inp) + v * kVecBytes)[q];
   }
-  signal_peers(a, 0, e);
-  if (!wait_peers(a, 0, e)) return;
+  signal_peers(a, 0, e, bid);
+  if (!wait_peers(a, 0, e, bid)) return;
   for (int64_t v = v0 + threadIdx.x; v < v1; v += blockDim.x) {
     float acc[8];
     sum_vec<DT, W>(a, half, v * kVecBytes, acc);
@@ -172,14 +187,13 @@ __global__ void __launch_bounds__(kCarThreads) car_oneshot_kernel(CarKernelArgs 
 }
 
 template <int DT, int W>
-__global__ void __launch_bounds__(kCarThreads) car_twoshot_kernel(CarKernelArgs a) {
+__device__ __forceinline__ void twoshot_body(const CarKernelArgs& a, unsigned bid, unsigned nb) {
   constexpr int64_t kVecBytes = 8 * Elem<DT>::kBytes;
-  const uint32_t e = begin_epoch(a);
+  const uint32_t e = begin_epoch(a, bid, nb);
   const int64_t half = (e & 1) * a.cap;
   const int64_t shard_vec = a.nbytes / kVecBytes / a.world;      // vectors per shard
-  const int64_t per = (shard_vec + gridDim.x - 1) / gridDim.x;
-  const int64_t s0 = blockIdx.x * per;
-  const int64_t s1 = s0 + per < shard_vec ? s0 + per : shard_vec;
+  int64_t s0, s1;
+  split_range(shard_vec, bid, nb, s0, s1);
   char* mine = a.data[a.rank] + half;
   constexpr int kQ = kVecBytes / 16;
   // publish sub-range [s0, s1) of every shard (W > 0: all W loads in flight per thread)
@@ -210,8 +224,8 @@ __global__ void __launch_bounds__(kCarThreads) car_twoshot_kernel(CarKernelArgs 
       }
     }
   }
-  signal_peers(a, 0, e);
-  if (!wait_peers(a, 0, e)) return;
+  signal_peers(a, 0, e, bid);
+  if (!wait_peers(a, 0, e, bid)) return;
   // reduce-scatter: my shard, sub-range b
   char* my_tmp = a.tmp[a.rank] + half;
   const int64_t mybase = a.rank * shard_vec;
@@ -221,8 +235,8 @@ __global__ void __launch_bounds__(kCarThreads) car_twoshot_kernel(CarKernelArgs 
     store8<DT>(my_tmp, mybase + v, acc);
     store8<DT>(a.out, mybase + v, acc);
   }
-  signal_peers(a, 1, e);
-  if (!wait_peers(a, 1, e)) return;
+  signal_peers(a, 1, e, bid);
+  if (!wait_peers(a, 1, e, bid)) return;
   // all-gather: every other shard's sub-range b from its owner's tmp. W > 0: the W-1 remote
   // loads of a thread are all in flight before its stores (one per xGMI link), instead of one
   // peer at a time.
@@ -268,25 +282,25 @@ __global__ void __launch_bounds__(kCarThreads) car_twoshot_kernel(CarKernelArgs 
 // and peers only read shard `rank` of it. Workgroup b of every rank owns sub-range b of every
 // shard, so the per-workgroup flags order exactly the producer/consumer pairs.
 template <int DT, int W>
-__global__ void __launch_bounds__(kCarThreads) car_twoshot_reg_kernel(CarKernelArgs a) {
+__device__ __forceinline__ void twoshot_reg_body(const CarKernelArgs& a, unsigned bid,
+                                                 unsigned nb) {
   constexpr int64_t kVecBytes = 8 * Elem<DT>::kBytes;
   constexpr int kQ = kVecBytes / 16;
-  const uint32_t e = begin_epoch(a);
+  const uint32_t e = begin_epoch(a, bid, nb);
   const int64_t shard_vec = a.nbytes / kVecBytes / a.world;
-  const int64_t per = (shard_vec + gridDim.x - 1) / gridDim.x;
-  const int64_t s0 = blockIdx.x * per;
-  const int64_t s1 = s0 + per < shard_vec ? s0 + per : shard_vec;
+  int64_t s0, s1;
+  split_range(shard_vec, bid, nb, s0, s1);
   char* mine = a.data[a.rank];
-  signal_peers(a, 0, e);                       // my input is complete (stream order)
-  if (!wait_peers(a, 0, e)) return;
+  signal_peers(a, 0, e, bid);                  // my input is complete (stream order)
+  if (!wait_peers(a, 0, e, bid)) return;
   const int64_t mybase = a.rank * shard_vec;
   for (int64_t v = s0 + threadIdx.x; v < s1; v += blockDim.x) {
     float acc[8];
     sum_vec<DT, W>(a, 0, (mybase + v) * kVecBytes, acc);
     store8<DT>(mine, mybase + v, acc);
   }
-  signal_peers(a, 1, e);
-  if (!wait_peers(a, 1, e)) return;
+  signal_peers(a, 1, e, bid);
+  if (!wait_peers(a, 1, e, bid)) return;
   if constexpr (W > 0) {
     for (int64_t v = s0 + threadIdx.x; v < s1; v += blockDim.x) {
       u16x8 t[W - 1][kQ];
@@ -318,8 +332,8 @@ __global__ void __launch_bounds__(kCarThreads) car_twoshot_reg_kernel(CarKernelA
       }
     }
   }
-  signal_peers(a, 2, e);                       // done reading every peer's buffer
-  wait_peers(a, 2, e);
+  signal_peers(a, 2, e, bid);                  // done reading every peer's buffer
+  wait_peers(a, 2, e, bid);
 }
 
 // Registered two-shot, PUSH form (in place): the same traffic per link as the pull form, but
@@ -332,16 +346,16 @@ __global__ void __launch_bounds__(kCarThreads) car_twoshot_reg_kernel(CarKernelA
 // after passing barrier 1 of call e-1, i.e. after that peer finished reducing call e-2's half.
 // Requires nbytes <= cap (world slots of nbytes / world each).
 template <int DT, int W>
-__global__ void __launch_bounds__(kCarThreads) car_twoshot_push_kernel(CarKernelArgs a) {
+__device__ __forceinline__ void twoshot_push_body(const CarKernelArgs& a, unsigned bid,
+                                                  unsigned nb) {
   constexpr int64_t kVecBytes = 8 * Elem<DT>::kBytes;
   constexpr int kQ = kVecBytes / 16;
-  const uint32_t e = begin_epoch(a);
+  const uint32_t e = begin_epoch(a, bid, nb);
   const int64_t half = (e & 1) * a.cap;
   const int64_t shard_vec = a.nbytes / kVecBytes / a.world;
   const int64_t shard_bytes = shard_vec * kVecBytes;
-  const int64_t per = (shard_vec + gridDim.x - 1) / gridDim.x;
-  const int64_t s0 = blockIdx.x * per;
-  const int64_t s1 = s0 + per < shard_vec ? s0 + per : shard_vec;
+  int64_t s0, s1;
+  split_range(shard_vec, bid, nb, s0, s1);
   const char* mine = a.data[a.rank];
   const int64_t my_slot = half + a.rank * shard_bytes;
   if constexpr (W > 0) {
@@ -372,8 +386,8 @@ __global__ void __launch_bounds__(kCarThreads) car_twoshot_push_kernel(CarKernel
               reinterpret_cast<const u16x8*>(mine + (p * shard_vec + v) * kVecBytes)[q];
     }
   }
-  signal_peers(a, 0, e);
-  if (!wait_peers(a, 0, e)) return;
+  signal_peers(a, 0, e, bid);
+  if (!wait_peers(a, 0, e, bid)) return;
   const char* stage = a.tmp[a.rank] + half;
   const int64_t out_off = a.rank * shard_bytes;
   for (int64_t v = s0 + threadIdx.x; v < s1; v += blockDim.x) {
@@ -404,8 +418,8 @@ __global__ void __launch_bounds__(kCarThreads) car_twoshot_push_kernel(CarKernel
         store8<DT>(a.data[(a.rank + k) % a.world] + out_off, v, acc);
     }
   }
-  signal_peers(a, 1, e);
-  wait_peers(a, 1, e);
+  signal_peers(a, 1, e, bid);
+  wait_peers(a, 1, e, bid);
 }
 
 // ---- direct (one-hop) collectives on registered inputs --------------------------------------
@@ -417,17 +431,15 @@ __global__ void __launch_bounds__(kCarThreads) car_twoshot_push_kernel(CarKernel
 //   all-gather : out[p * chunk .. ] = in_p[0 .. chunk)
 //   all-to-all : out[p * chunk .. ] = in_p[rank * chunk .. ]   (equal splits)
 template <int W, bool A2A>
-__global__ void __launch_bounds__(kCarThreads) car_pull_kernel(CarKernelArgs a) {
-  const uint32_t e = begin_epoch(a);
+__device__ __forceinline__ void pull_body(const CarKernelArgs& a, unsigned bid, unsigned nb) {
+  const uint32_t e = begin_epoch(a, bid, nb);
   const int64_t chunk = a.nbytes;                    // bytes per peer chunk, multiple of 16
-  const int64_t nvec = chunk / 16;
-  const int64_t per = (nvec + gridDim.x - 1) / gridDim.x;
-  const int64_t v0 = blockIdx.x * per;
-  const int64_t v1 = v0 + per < nvec ? v0 + per : nvec;
+  int64_t v0, v1;
+  split_range(chunk / 16, bid, nb, v0, v1);
   const int64_t src_off = A2A ? a.rank * chunk : 0;
   char* out = static_cast<char*>(a.out);
-  signal_peers(a, 0, e);
-  if (!wait_peers(a, 0, e)) return;
+  signal_peers(a, 0, e, bid);
+  if (!wait_peers(a, 0, e, bid)) return;
   if constexpr (W > 0) {
     for (int64_t v = v0 + threadIdx.x; v < v1; v += blockDim.x) {
       u16x8 t[W];
@@ -450,57 +462,120 @@ __global__ void __launch_bounds__(kCarThreads) car_pull_kernel(CarKernelArgs a) 
             reinterpret_cast<const u16x8*>(a.data[p] + src_off)[v];
     }
   }
-  signal_peers(a, 2, e);
-  wait_peers(a, 2, e);
+  signal_peers(a, 2, e, bid);
+  wait_peers(a, 2, e, bid);
+}
+
+template <int DT, int W>
+__device__ __forceinline__ void ag_body(const CarKernelArgs& a, unsigned bid, unsigned nb) {
+  pull_body<W, false>(a, bid, nb);
+}
+template <int DT, int W>
+__device__ __forceinline__ void a2a_body(const CarKernelArgs& a, unsigned bid, unsigned nb) {
+  pull_body<W, true>(a, bid, nb);
 }
 
 //   reduce-scatter : out[0 .. n/P) = sum_p in_p[rank * n/P .. ]   (fp32 accumulation)
 template <int DT, int W>
-__global__ void __launch_bounds__(kCarThreads) car_rs_kernel(CarKernelArgs a) {
+__device__ __forceinline__ void rs_body(const CarKernelArgs& a, unsigned bid, unsigned nb) {
   constexpr int64_t kVecBytes = 8 * Elem<DT>::kBytes;
-  const uint32_t e = begin_epoch(a);
+  const uint32_t e = begin_epoch(a, bid, nb);
   const int64_t shard_vec = a.nbytes / kVecBytes / a.world;
-  const int64_t per = (shard_vec + gridDim.x - 1) / gridDim.x;
-  const int64_t s0 = blockIdx.x * per;
-  const int64_t s1 = s0 + per < shard_vec ? s0 + per : shard_vec;
-  signal_peers(a, 0, e);
-  if (!wait_peers(a, 0, e)) return;
+  int64_t s0, s1;
+  split_range(shard_vec, bid, nb, s0, s1);
+  signal_peers(a, 0, e, bid);
+  if (!wait_peers(a, 0, e, bid)) return;
   const int64_t mybase = a.rank * shard_vec;
   for (int64_t v = s0 + threadIdx.x; v < s1; v += blockDim.x) {
     float acc[8];
     sum_vec<DT, W>(a, 0, (mybase + v) * kVecBytes, acc);
     store8<DT>(a.out, v, acc);
   }
-  signal_peers(a, 2, e);
-  wait_peers(a, 2, e);
+  signal_peers(a, 2, e, bid);
+  wait_peers(a, 2, e, bid);
 }
 
-template <int W>
-void launch_direct(int kind, int dtype, dim3 g, dim3 b, hipStream_t st, const CarKernelArgs& a) {
-  if (kind == 0) hipLaunchKernelGGL((car_pull_kernel<W, false>), g, b, 0, st, a);
-  else if (kind == 1) hipLaunchKernelGGL((car_pull_kernel<W, true>), g, b, 0, st, a);
-  else if (dtype == DT_BF16) hipLaunchKernelGGL((car_rs_kernel<DT_BF16, W>), g, b, 0, st, a);
-  else if (dtype == DT_F16) hipLaunchKernelGGL((car_rs_kernel<DT_F16, W>), g, b, 0, st, a);
-  else hipLaunchKernelGGL((car_rs_kernel<DT_F32, W>), g, b, 0, st, a);
+// Kernel-argument block of the virtual-rank launch: every rank's own argument block.
+struct CarVirtArgs {
+  CarKernelArgs r[kMaxRanks];
+};
+
+// NAME<DT, W>: production per-rank grid. NAME##_vr<DT, W>: world x nb workgroups on one GPU,
+// workgroup g runs rank g / nb (wave-uniform, so the argument block is read with scalar loads).
+#define DLBB_CAR_KERNELS(NAME, BODY)                                                          \
+  template <int DT, int W>                                                                    \
+  __global__ void __launch_bounds__(kCarThreads) NAME(CarKernelArgs a) {                     \
+    BODY<DT, W>(a, blockIdx.x, gridDim.x);                                                    \
+  }                                                                                           \
+  template <int DT, int W>                                                                    \
+  __global__ void __launch_bounds__(kCarThreads) NAME##_vr(CarVirtArgs v, unsigned nb) {     \
+    const unsigned r = blockIdx.x / nb;                                                       \
+    BODY<DT, W>(v.r[r], blockIdx.x - r * nb, nb);                                             \
+  }
+
+DLBB_CAR_KERNELS(car_oneshot_kernel, oneshot_body)
+DLBB_CAR_KERNELS(car_twoshot_kernel, twoshot_body)
+DLBB_CAR_KERNELS(car_twoshot_reg_kernel, twoshot_reg_body)
+DLBB_CAR_KERNELS(car_twoshot_push_kernel, twoshot_push_body)
+DLBB_CAR_KERNELS(car_ag_kernel, ag_body)
+DLBB_CAR_KERNELS(car_a2a_kernel, a2a_body)
+DLBB_CAR_KERNELS(car_rs_kernel, rs_body)
+#undef DLBB_CAR_KERNELS
+
+enum CarKind : int {
+  K_ONESHOT = 1, K_TWOSHOT = 2, K_REG = 3, K_PUSH = 4, K_AG = 5, K_A2A = 6, K_RS = 7
+};
+
+// Resolves (kind, DT, W) to the kernel symbol: per-rank form (VR = false) or virtual form.
+template <int DT, int W, bool VR>
+const void* car_kernel_ptr(int kind) {
+#define DLBB_CAR_PTR(NAME)                                                        \
+  (VR ? reinterpret_cast<const void*>(&NAME##_vr<DT, W>)                          \
+      : reinterpret_cast<const void*>(&NAME<DT, W>))
+  switch (kind) {
+    case K_ONESHOT: return DLBB_CAR_PTR(car_oneshot_kernel);
+    case K_TWOSHOT: return DLBB_CAR_PTR(car_twoshot_kernel);
+    case K_REG: return DLBB_CAR_PTR(car_twoshot_reg_kernel);
+    case K_PUSH: return DLBB_CAR_PTR(car_twoshot_push_kernel);
+    case K_RS: return DLBB_CAR_PTR(car_rs_kernel);
+    default: break;
+  }
+  if constexpr (DT == DT_BF16) {     // byte movers: one instantiation (dtype-free)
+    if (kind == K_AG) return DLBB_CAR_PTR(car_ag_kernel);
+    if (kind == K_A2A) return DLBB_CAR_PTR(car_a2a_kernel);
+  }
+#undef DLBB_CAR_PTR
+  return nullptr;
 }
 
-template <int DT>
-void launch_push(int w, dim3 g, dim3 b, hipStream_t st, const CarKernelArgs& a) {
-  if (w == 2) hipLaunchKernelGGL((car_twoshot_push_kernel<DT, 2>), g, b, 0, st, a);
-  else if (w == 4) hipLaunchKernelGGL((car_twoshot_push_kernel<DT, 4>), g, b, 0, st, a);
-  else if (w == 8) hipLaunchKernelGGL((car_twoshot_push_kernel<DT, 8>), g, b, 0, st, a);
-  else hipLaunchKernelGGL((car_twoshot_push_kernel<DT, 0>), g, b, 0, st, a);
+template <bool VR>
+const void* car_kernel(int kind, int dtype, int world) {
+  if (kind == K_AG || kind == K_A2A) dtype = DT_BF16;
+  const int w = world == 2 || world == 4 || world == 8 ? world : 0;
+#define DLBB_CAR_W(D)                                        \
+  switch (w) {                                               \
+    case 2: return car_kernel_ptr<D, 2, VR>(kind);           \
+    case 4: return car_kernel_ptr<D, 4, VR>(kind);           \
+    case 8: return car_kernel_ptr<D, 8, VR>(kind);           \
+    default: return car_kernel_ptr<D, 0, VR>(kind);          \
+  }
+  if (dtype == DT_BF16) DLBB_CAR_W(DT_BF16)
+  if (dtype == DT_F16) DLBB_CAR_W(DT_F16)
+  DLBB_CAR_W(DT_F32)
+#undef DLBB_CAR_W
 }
 
 struct RegBuf {
   char* ptr[kMaxRanks] = {};    // every rank's registered buffer (mine at [rank])
-  int64_t bytes = 0;
+  char* map[kMaxRanks] = {};    // base of the opened peer mapping it lives in (null: own / local)
+  int64_t bytes = 0;            // 0: released (dlbb_car_reg_close); ids are never reused
 };
 
 struct OpenedMap {               // one hipIpcOpenMemHandle per (peer, allocation)
   int peer;
   hipIpcMemHandle_t handle;
   char* base;
+  int refs;                      // live registrations inside this mapping
 };
 
 struct CarState {
@@ -510,6 +585,7 @@ struct CarState {
   char* tmp = nullptr;        // 2 * cap
   Signal* sig = nullptr;      // uncached, IPC
   bool opened = false;
+  bool local = false;         // virtual rank: peers are sibling states in this process (no IPC)
   CarKernelArgs args{};
   char* peer_data[kMaxRanks] = {};
   char* peer_tmp[kMaxRanks] = {};
@@ -578,6 +654,18 @@ DLBB_API int dlbb_car_ipc_handles(void* h, void* out_handles) {
 
 DLBB_API int dlbb_car_handle_bytes() { return 3 * 64; }
 
+static void car_finish_open(CarState* s) {
+  for (int p = 0; p < kMaxRanks; ++p) {
+    s->args.data[p] = s->peer_data[p];
+    s->args.tmp[p] = s->peer_tmp[p];
+    s->args.sig[p] = s->peer_sig[p];
+  }
+  s->args.rank = s->rank;
+  s->args.world = s->world;
+  s->args.cap = s->cap;
+  s->opened = true;
+}
+
 // all_handles: world x 192 bytes in rank order; peer_devices: each rank's device ordinal
 // (used to decide whether peer access must be enabled; same device -> plain IPC mapping).
 DLBB_API int dlbb_car_open(void* h, const void* all_handles, const int* peer_devices) {
@@ -614,64 +702,118 @@ DLBB_API int dlbb_car_open(void* h, const void* all_handles, const int* peer_dev
     CAR_CHECK(hipMemcpy(&magic, &s->peer_sig[p]->pad[0], sizeof(magic), hipMemcpyDeviceToHost));
     if (magic != (kMagic | static_cast<uint32_t>(p))) return hipErrorInvalidHandle;
   }
-  for (int p = 0; p < kMaxRanks; ++p) {
-    s->args.data[p] = s->peer_data[p];
-    s->args.tmp[p] = s->peer_tmp[p];
-    s->args.sig[p] = s->peer_sig[p];
+  car_finish_open(s);
+  return hipSuccess;
+}
+
+// Virtual ranks (single-GPU harness): states[r] was created with dlbb_car_create(r, world, ...)
+// in THIS process on the same device; every state's peers become its siblings' own allocations
+// (no IPC handles). The kernels then run unchanged against buffers in one HBM.
+DLBB_API int dlbb_car_open_local(void* const* states, int world) {
+  if (world < 1 || world > kMaxRanks) return hipErrorInvalidValue;
+  for (int r = 0; r < world; ++r) {
+    const CarState* s = static_cast<const CarState*>(states[r]);
+    if (!s || s->rank != r || s->world != world || s->opened ||
+        s->cap != static_cast<const CarState*>(states[0])->cap ||
+        s->device != static_cast<const CarState*>(states[0])->device)
+      return hipErrorInvalidValue;
   }
-  s->args.rank = s->rank;
-  s->args.world = s->world;
-  s->args.cap = s->cap;
-  s->opened = true;
+  for (int r = 0; r < world; ++r) {
+    CarState* s = static_cast<CarState*>(states[r]);
+    for (int p = 0; p < world; ++p) {
+      const CarState* q = static_cast<const CarState*>(states[p]);
+      s->peer_data[p] = q->data;
+      s->peer_tmp[p] = q->tmp;
+      s->peer_sig[p] = q->sig;
+    }
+    s->local = true;
+    car_finish_open(s);
+  }
   return hipSuccess;
 }
 
 DLBB_API int64_t dlbb_car_capacity(void* h) { return static_cast<CarState*>(h)->cap; }
 
-// algo: 1 = one-shot, 2 = two-shot. nblocks <= 128. dtype: bf16 | f16 | f32.
+static const RegBuf* car_reg(const CarState* s, int id) {
+  if (id < 0 || id >= static_cast<int>(s->regs.size()) || s->regs[id].bytes <= 0) return nullptr;
+  return &s->regs[id];
+}
+
+// Validates one rank's call and fills its kernel-argument block. `count` is in elements for the
+// all-reduce kinds and in bytes for the direct kinds (as the public entry points take them).
+// *noop: nothing to launch (empty message, or a registered all-reduce at world 1).
+static int car_prepare(const CarState* s, int kind, const void* inp, void* out, int64_t count,
+                       int dtype, int id, CarKernelArgs* a, bool* noop) {
+  *noop = false;
+  if (!s->opened) return hipErrorNotInitialized;
+  if (dtype != DT_BF16 && dtype != DT_F16 && dtype != DT_F32) return hipErrorInvalidValue;
+  const int64_t esz = dtype == DT_F32 ? 4 : 2;
+  const int64_t vec = 8 * esz;
+  const int64_t W = s->world;
+  *a = s->args;
+  if (kind == K_ONESHOT || kind == K_TWOSHOT) {
+    const int64_t nbytes = count * esz;
+    if (nbytes < 0 || nbytes > s->cap || nbytes % vec != 0) return hipErrorInvalidValue;
+    if (kind == K_TWOSHOT && nbytes % (vec * W) != 0) return hipErrorInvalidValue;
+    a->inp = inp;
+    a->out = out;
+    a->nbytes = nbytes;
+    *noop = nbytes == 0 || W == 1;
+    return hipSuccess;
+  }
+  const RegBuf* r = car_reg(s, id);
+  if (!r) return hipErrorInvalidValue;
+  for (int p = 0; p < kMaxRanks; ++p) a->data[p] = r->ptr[p];
+  a->inp = r->ptr[s->rank];
+  if (kind == K_REG || kind == K_PUSH) {
+    const int64_t nbytes = count * esz;
+    if (nbytes < 0 || nbytes > r->bytes || nbytes % (vec * W) != 0) return hipErrorInvalidValue;
+    if (kind == K_PUSH && nbytes > s->cap) return hipErrorInvalidValue;
+    a->out = r->ptr[s->rank];
+    a->nbytes = nbytes;
+    *noop = nbytes == 0 || W == 1;
+    return hipSuccess;
+  }
+  if (!out || count < 0) return hipErrorInvalidValue;
+  if (kind == K_AG && (count % 16 || count > r->bytes)) return hipErrorInvalidValue;
+  if (kind == K_A2A && (count % 16 || count * W > r->bytes)) return hipErrorInvalidValue;
+  if (kind == K_RS && (count % (vec * W) || count > r->bytes)) return hipErrorInvalidValue;
+  if (kind != K_AG && kind != K_A2A && kind != K_RS) return hipErrorInvalidValue;
+  a->out = out;
+  a->nbytes = count;
+  *noop = count == 0;
+  return hipSuccess;
+}
+
+static int clamp_blocks(int nblocks) {
+  return nblocks < 1 ? 1 : nblocks > kMaxBlocks ? kMaxBlocks : nblocks;
+}
+
+static int car_launch_rank(CarState* s, int kind, const void* inp, void* out, int64_t count,
+                           int dtype, int id, int nblocks, hipStream_t stream) {
+  CarKernelArgs a;
+  bool noop = false;
+  const int rc = car_prepare(s, kind, inp, out, count, dtype, id, &a, &noop);
+  if (rc != hipSuccess) return rc;
+  if (noop) {
+    if ((kind == K_ONESHOT || kind == K_TWOSHOT) && a.nbytes > 0 && out != inp)
+      CAR_CHECK(hipMemcpyAsync(out, inp, a.nbytes, hipMemcpyDeviceToDevice, stream));
+    return hipSuccess;
+  }
+  const void* fn = car_kernel<false>(kind, dtype, s->world);
+  if (!fn) return hipErrorInvalidValue;
+  void* args[] = {&a};
+  CAR_CHECK(hipLaunchKernel(fn, dim3(clamp_blocks(nblocks)), dim3(kCarThreads), args, 0, stream));
+  return hipSuccess;
+}
+
+// algo: 1 = one-shot, 2 = two-shot. nblocks <= 256. dtype: bf16 | f16 | f32.
 // Requirements (checked): nbytes <= cap; nbytes % 16 == 0 (one-shot) or
 // nbytes % (vec_bytes * world) == 0 (two-shot).
 DLBB_API int dlbb_car_allreduce(void* h, const void* inp, void* out, int64_t n, int dtype,
                                 int algo, int nblocks, hipStream_t stream) {
-  CarState* s = static_cast<CarState*>(h);
-  if (!s->opened) return hipErrorNotInitialized;
-  const int64_t esz = dtype == DT_F32 ? 4 : 2;
-  const int64_t vec = 8 * esz;
-  const int64_t nbytes = n * esz;
-  if (nbytes <= 0) return hipSuccess;
-  if (nbytes > s->cap || nbytes % vec != 0) return hipErrorInvalidValue;
-  if (algo == 2 && nbytes % (vec * s->world) != 0) return hipErrorInvalidValue;
-  if (nblocks < 1) nblocks = 1;
-  if (nblocks > kMaxBlocks) nblocks = kMaxBlocks;
-  if (s->world == 1) {
-    if (out != inp) CAR_CHECK(hipMemcpyAsync(out, inp, nbytes, hipMemcpyDeviceToDevice, stream));
-    return hipSuccess;
-  }
-  CarKernelArgs a = s->args;
-  a.inp = inp;
-  a.out = out;
-  a.nbytes = nbytes;
-  const dim3 g(nblocks), b(kCarThreads);
-#define CAR_W(KERN, D)                                                                  \
-  do {                                                                                  \
-    if (s->world == 2) hipLaunchKernelGGL((KERN<D, 2>), g, b, 0, stream, a);            \
-    else if (s->world == 4) hipLaunchKernelGGL((KERN<D, 4>), g, b, 0, stream, a);       \
-    else if (s->world == 8) hipLaunchKernelGGL((KERN<D, 8>), g, b, 0, stream, a);       \
-    else hipLaunchKernelGGL((KERN<D, 0>), g, b, 0, stream, a);                          \
-  } while (0)
-#define CAR_L(KERN, D) CAR_W(KERN, D)
-  if (algo == 2) {
-    if (dtype == DT_BF16) CAR_L(car_twoshot_kernel, DT_BF16);
-    else if (dtype == DT_F16) CAR_L(car_twoshot_kernel, DT_F16);
-    else CAR_L(car_twoshot_kernel, DT_F32);
-  } else {
-    if (dtype == DT_BF16) CAR_L(car_oneshot_kernel, DT_BF16);
-    else if (dtype == DT_F16) CAR_L(car_oneshot_kernel, DT_F16);
-    else CAR_L(car_oneshot_kernel, DT_F32);
-  }
-#undef CAR_W
-#undef CAR_L
-  return hipGetLastError();
+  return car_launch_rank(static_cast<CarState*>(h), algo == 2 ? K_TWOSHOT : K_ONESHOT, inp, out,
+                         n, dtype, -1, nblocks, stream);
 }
 
 // ---- registered buffers -----------------------------------------------------------------------
@@ -690,12 +832,12 @@ DLBB_API int dlbb_car_reg_export(void* h, const void* ptr, void* out_handle, int
 }
 
 // Map every peer's exported buffer (all_handles: world x 64 bytes, offsets: world) and record
-// the registration; *out_id indexes it for dlbb_car_allreduce_reg. A peer allocation already
-// mapped by an earlier registration is reused (one open per allocation and peer).
+// the registration; *out_id indexes it for the registered launches. A peer allocation already
+// mapped by a live registration is reused (one open per allocation and peer, reference counted).
 DLBB_API int dlbb_car_reg_open(void* h, const void* ptr, int64_t nbytes, const void* all_handles,
                                const int64_t* offsets, int* out_id) {
   CarState* s = static_cast<CarState*>(h);
-  if (!s->opened) return hipErrorNotInitialized;
+  if (!s->opened || s->local || nbytes <= 0) return hipErrorInvalidValue;
   RegBuf r;
   r.bytes = nbytes;
   const char* hs = static_cast<const char*>(all_handles);
@@ -706,23 +848,87 @@ DLBB_API int dlbb_car_reg_open(void* h, const void* ptr, int64_t nbytes, const v
     }
     hipIpcMemHandle_t hd;
     memcpy(&hd, hs + p * 64, 64);
-    char* base = nullptr;
-    for (const OpenedMap& m : s->opened_maps)
-      if (m.peer == p && memcmp(&m.handle, &hd, sizeof(hd)) == 0) base = m.base;
-    if (!base) {
+    OpenedMap* m = nullptr;
+    for (OpenedMap& o : s->opened_maps)
+      if (o.peer == p && memcmp(&o.handle, &hd, sizeof(hd)) == 0) m = &o;
+    if (!m) {
       void* pd = nullptr;
       CAR_CHECK(hipIpcOpenMemHandle(&pd, hd, hipIpcMemLazyEnablePeerAccess));
-      base = static_cast<char*>(pd);
-      s->opened_maps.push_back(OpenedMap{p, hd, base});
+      s->opened_maps.push_back(OpenedMap{p, hd, static_cast<char*>(pd), 0});
+      m = &s->opened_maps.back();
     }
-    r.ptr[p] = base + offsets[p];
+    r.ptr[p] = m->base + offsets[p];
+    r.map[p] = m->base;
     // copy-engine read of the first and last byte: a bad mapping fails here, not in a kernel
     char probe[2];
-    CAR_CHECK(hipMemcpy(&probe[0], r.ptr[p], 1, hipMemcpyDeviceToHost));
-    CAR_CHECK(hipMemcpy(&probe[1], r.ptr[p] + nbytes - 1, 1, hipMemcpyDeviceToHost));
+    hipError_t e = hipMemcpy(&probe[0], r.ptr[p], 1, hipMemcpyDeviceToHost);
+    if (e == hipSuccess) e = hipMemcpy(&probe[1], r.ptr[p] + nbytes - 1, 1, hipMemcpyDeviceToHost);
+    if (e != hipSuccess) {
+      if (m->refs == 0) {          // drop the mapping this call opened
+        (void)hipIpcCloseMemHandle(m->base);
+        s->opened_maps.pop_back();
+      }
+      for (int q = 0; q < p; ++q)  // and the references taken for the earlier peers
+        for (OpenedMap& o : s->opened_maps)
+          if (r.map[q] && o.peer == q && o.base == r.map[q]) --o.refs;
+      return (int)e;
+    }
+    ++m->refs;
   }
   s->regs.push_back(r);
   *out_id = static_cast<int>(s->regs.size()) - 1;
+  return hipSuccess;
+}
+
+// Virtual ranks: register ptrs[r] (one buffer per virtual rank, nbytes each) in every sibling
+// state under the same id.
+DLBB_API int dlbb_car_reg_local(void* const* states, int world, void* const* ptrs, int64_t nbytes,
+                                int* out_id) {
+  if (world < 1 || world > kMaxRanks || nbytes <= 0) return hipErrorInvalidValue;
+  const size_t id = static_cast<CarState*>(states[0])->regs.size();
+  for (int r = 0; r < world; ++r) {
+    const CarState* s = static_cast<const CarState*>(states[r]);
+    if (!s->local || s->world != world || s->regs.size() != id || !ptrs[r])
+      return hipErrorInvalidValue;
+  }
+  RegBuf reg;
+  reg.bytes = nbytes;
+  for (int p = 0; p < world; ++p) reg.ptr[p] = static_cast<char*>(ptrs[p]);
+  for (int r = 0; r < world; ++r) static_cast<CarState*>(states[r])->regs.push_back(reg);
+  *out_id = static_cast<int>(id);
+  return hipSuccess;
+}
+
+// Release registration `id`: peer mappings no other live registration uses are closed. The caller
+// guarantees that no launch on it is in flight on ANY rank (synchronize + barrier first).
+DLBB_API int dlbb_car_reg_close(void* h, int id) {
+  CarState* s = static_cast<CarState*>(h);
+  if (id < 0 || id >= static_cast<int>(s->regs.size()) || s->regs[id].bytes <= 0)
+    return hipErrorInvalidValue;
+  RegBuf& r = s->regs[id];
+  for (int p = 0; p < s->world; ++p) {
+    if (!r.map[p]) continue;
+    for (size_t i = 0; i < s->opened_maps.size(); ++i) {
+      OpenedMap& m = s->opened_maps[i];
+      if (m.peer != p || m.base != r.map[p]) continue;
+      if (--m.refs <= 0) {
+        CAR_CHECK(hipIpcCloseMemHandle(m.base));
+        s->opened_maps.erase(s->opened_maps.begin() + i);
+      }
+      break;
+    }
+  }
+  r = RegBuf();
+  return hipSuccess;
+}
+
+// Live registrations and opened peer mappings (lifecycle tests).
+DLBB_API int dlbb_car_reg_counts(void* h, int* live_regs, int* open_maps) {
+  const CarState* s = static_cast<const CarState*>(h);
+  int live = 0;
+  for (const RegBuf& r : s->regs) live += r.bytes > 0;
+  *live_regs = live;
+  *open_maps = static_cast<int>(s->opened_maps.size());
   return hipSuccess;
 }
 
@@ -730,92 +936,72 @@ DLBB_API int dlbb_car_reg_open(void* h, const void* ptr, int64_t nbytes, const v
 // multiple of 16 * world and at most the registered size).
 DLBB_API int dlbb_car_allreduce_reg(void* h, int id, int64_t n, int dtype, int nblocks,
                                     hipStream_t stream) {
-  CarState* s = static_cast<CarState*>(h);
-  if (!s->opened || id < 0 || id >= static_cast<int>(s->regs.size())) return hipErrorInvalidValue;
-  const RegBuf& r = s->regs[id];
-  const int64_t esz = dtype == DT_F32 ? 4 : 2;
-  const int64_t nbytes = n * esz;
-  if (nbytes <= 0) return hipSuccess;
-  if (nbytes > r.bytes || nbytes % (8 * esz * s->world) != 0) return hipErrorInvalidValue;
-  if (s->world == 1) return hipSuccess;
-  if (nblocks < 1) nblocks = 1;
-  if (nblocks > kMaxBlocks) nblocks = kMaxBlocks;
-  CarKernelArgs a = s->args;
-  for (int p = 0; p < kMaxRanks; ++p) a.data[p] = r.ptr[p];
-  a.inp = r.ptr[s->rank];
-  a.out = r.ptr[s->rank];
-  a.nbytes = nbytes;
-  const dim3 g(nblocks), b(kCarThreads);
-#define CAR_RW(D)                                                                            \
-  do {                                                                                       \
-    if (s->world == 2) hipLaunchKernelGGL((car_twoshot_reg_kernel<D, 2>), g, b, 0, stream, a); \
-    else if (s->world == 4) hipLaunchKernelGGL((car_twoshot_reg_kernel<D, 4>), g, b, 0, stream, a); \
-    else if (s->world == 8) hipLaunchKernelGGL((car_twoshot_reg_kernel<D, 8>), g, b, 0, stream, a); \
-    else hipLaunchKernelGGL((car_twoshot_reg_kernel<D, 0>), g, b, 0, stream, a);            \
-  } while (0)
-  if (dtype == DT_BF16) CAR_RW(DT_BF16);
-  else if (dtype == DT_F16) CAR_RW(DT_F16);
-  else CAR_RW(DT_F32);
-#undef CAR_RW
-  return hipGetLastError();
+  return car_launch_rank(static_cast<CarState*>(h), K_REG, nullptr, nullptr, n, dtype, id,
+                         nblocks, stream);
 }
 
-// Push form of the registered two-shot (see car_twoshot_push_kernel); nbytes <= capacity.
+// Push form of the registered two-shot (see twoshot_push_body); nbytes <= capacity.
 DLBB_API int dlbb_car_allreduce_reg_push(void* h, int id, int64_t n, int dtype, int nblocks,
                                          hipStream_t stream) {
-  CarState* s = static_cast<CarState*>(h);
-  if (!s->opened || id < 0 || id >= static_cast<int>(s->regs.size())) return hipErrorInvalidValue;
-  const RegBuf& r = s->regs[id];
-  const int64_t esz = dtype == DT_F32 ? 4 : 2;
-  const int64_t nbytes = n * esz;
-  if (nbytes <= 0) return hipSuccess;
-  if (nbytes > r.bytes || nbytes > s->cap || nbytes % (8 * esz * s->world) != 0)
-    return hipErrorInvalidValue;
-  if (s->world == 1) return hipSuccess;
-  if (nblocks < 1) nblocks = 1;
-  if (nblocks > kMaxBlocks) nblocks = kMaxBlocks;
-  CarKernelArgs a = s->args;               // tmp[] = every rank's staging region
-  for (int p = 0; p < kMaxRanks; ++p) a.data[p] = r.ptr[p];
-  a.inp = r.ptr[s->rank];
-  a.out = r.ptr[s->rank];
-  a.nbytes = nbytes;
-  const dim3 g(nblocks), b(kCarThreads);
-  const int w = s->world == 2 || s->world == 4 || s->world == 8 ? s->world : 0;
-  if (dtype == DT_BF16) launch_push<DT_BF16>(w, g, b, stream, a);
-  else if (dtype == DT_F16) launch_push<DT_F16>(w, g, b, stream, a);
-  else launch_push<DT_F32>(w, g, b, stream, a);
-  return hipGetLastError();
+  return car_launch_rank(static_cast<CarState*>(h), K_PUSH, nullptr, nullptr, n, dtype, id,
+                         nblocks, stream);
 }
 
 // Direct collectives on registration `id` (this rank's registered input; out is local).
 //   kind 0 = all-gather  : bytes = chunk bytes per rank (<= registered), out = world x chunk
 //   kind 1 = all-to-all  : bytes = chunk bytes per peer (world x chunk <= registered)
-//   kind 2 = reduce-scatter (dtype): bytes = whole input (multiple of 16 x world), out = bytes/world
+//   kind 2 = reduce-scatter (dtype): bytes = whole input (multiple of vec x world), out = bytes/world
 DLBB_API int dlbb_car_direct_reg(void* h, int id, int kind, int64_t bytes, int dtype, void* out,
                                  int nblocks, hipStream_t stream) {
-  CarState* s = static_cast<CarState*>(h);
-  if (!s->opened || id < 0 || id >= static_cast<int>(s->regs.size()) || !out)
-    return hipErrorInvalidValue;
-  const RegBuf& r = s->regs[id];
-  if (bytes <= 0) return hipSuccess;
-  if (kind == 0 && (bytes % 16 || bytes > r.bytes)) return hipErrorInvalidValue;
-  if (kind == 1 && (bytes % 16 || bytes * s->world > r.bytes)) return hipErrorInvalidValue;
-  if (kind == 2 && (bytes % (16 * s->world) || bytes > r.bytes)) return hipErrorInvalidValue;
   if (kind < 0 || kind > 2) return hipErrorInvalidValue;
-  if (nblocks < 1) nblocks = 1;
-  if (nblocks > kMaxBlocks) nblocks = kMaxBlocks;
-  CarKernelArgs a = s->args;
-  for (int p = 0; p < kMaxRanks; ++p) a.data[p] = r.ptr[p];
-  a.inp = r.ptr[s->rank];
-  a.out = out;
-  a.nbytes = bytes;
-  const dim3 g(nblocks), b(kCarThreads);
-  const int w = s->world == 2 || s->world == 4 || s->world == 8 ? s->world : 0;
-  if (w == 2) launch_direct<2>(kind, dtype, g, b, stream, a);
-  else if (w == 4) launch_direct<4>(kind, dtype, g, b, stream, a);
-  else if (w == 8) launch_direct<8>(kind, dtype, g, b, stream, a);
-  else launch_direct<0>(kind, dtype, g, b, stream, a);
-  return hipGetLastError();
+  static const int kKinds[3] = {K_AG, K_A2A, K_RS};
+  return car_launch_rank(static_cast<CarState*>(h), kKinds[kind], nullptr, out, bytes, dtype, id,
+                         nblocks, stream);
+}
+
+// ---- virtual-rank launch (single-GPU harness) -------------------------------------------------
+// Resident workgroups of the virtual form of (kind, dtype, world) on this device: one launch of
+// world x nblocks workgroups must fit entirely (every rank's workgroups spin on the others'), so
+// dlbb_car_vr_launch refuses a larger grid instead of letting it wait for its spin limit.
+DLBB_API int dlbb_car_vr_max_blocks(int kind, int dtype, int world) {
+  const void* fn = car_kernel<true>(kind, dtype, world);
+  if (!fn) return -1;
+  int dev = 0, per_cu = 0, cus = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return -1;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kCarThreads, 0) != hipSuccess)
+    return -1;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    return -1;
+  return per_cu * cus;
+}
+
+// One launch of world x nblocks workgroups: every virtual rank r of the states opened with
+// dlbb_car_open_local runs its part of collective `kind` (1 one-shot, 2 two-shot, 3 registered
+// pull, 4 registered push, 5 all-gather, 6 all-to-all, 7 reduce-scatter) with inputs inp[r] /
+// outputs out[r] (all-reduce kinds; direct kinds read registration `id` and write out[r]).
+DLBB_API int dlbb_car_vr_launch(void* const* states, int world, int kind, const void* const* inp,
+                                void* const* out, int64_t count, int dtype, int id, int nblocks,
+                                hipStream_t stream) {
+  if (world < 2 || world > kMaxRanks) return hipErrorInvalidValue;
+  const int nb = clamp_blocks(nblocks);
+  const int cap = dlbb_car_vr_max_blocks(kind, dtype, world);
+  if (cap < 0) return hipErrorInvalidValue;
+  if (nb * world > cap) return hipErrorInvalidConfiguration;
+  CarVirtArgs v;
+  bool noop = false;
+  for (int r = 0; r < world; ++r) {
+    const CarState* s = static_cast<const CarState*>(states[r]);
+    if (!s || !s->local || s->rank != r || s->world != world) return hipErrorInvalidValue;
+    const int rc = car_prepare(s, kind, inp ? inp[r] : nullptr, out ? out[r] : nullptr, count,
+                               dtype, id, &v.r[r], &noop);
+    if (rc != hipSuccess) return rc;
+    if (noop) return hipSuccess;
+  }
+  const void* fn = car_kernel<true>(kind, dtype, world);
+  unsigned nbu = static_cast<unsigned>(nb);
+  void* args[] = {&v, &nbu};
+  CAR_CHECK(hipLaunchKernel(fn, dim3(nb * world), dim3(kCarThreads), args, 0, stream));
+  return hipSuccess;
 }
 
 // Reads (and clears) the device-side timeout flag. Synchronous: call outside timed regions.
@@ -835,7 +1021,7 @@ DLBB_API int dlbb_car_destroy(void* h) {
   if (!s) return hipSuccess;
   (void)hipDeviceSynchronize();
   for (int p = 0; p < s->world; ++p) {
-    if (p == s->rank || !s->opened) continue;
+    if (p == s->rank || !s->opened || s->local) continue;
     if (s->peer_data[p]) (void)hipIpcCloseMemHandle(s->peer_data[p]);
     if (s->peer_tmp[p]) (void)hipIpcCloseMemHandle(s->peer_tmp[p]);
     if (s->peer_sig[p]) (void)hipIpcCloseMemHandle(s->peer_sig[p]);

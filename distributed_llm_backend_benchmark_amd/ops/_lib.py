@@ -111,6 +111,15 @@ _SIGS = {
     "dlbb_car_allreduce_reg_push": (c_int, [c_void_p, c_int, c_int64, c_int, c_int, c_void_p]),
     "dlbb_car_direct_reg": (c_int, [c_void_p, c_int, c_int, c_int64, c_int, c_void_p, c_int,
                                     c_void_p]),
+    "dlbb_car_reg_close": (c_int, [c_void_p, c_int]),
+    "dlbb_car_reg_counts": (c_int, [c_void_p, ctypes.POINTER(c_int), ctypes.POINTER(c_int)]),
+    "dlbb_car_open_local": (c_int, [ctypes.POINTER(c_void_p), c_int]),
+    "dlbb_car_reg_local": (c_int, [ctypes.POINTER(c_void_p), c_int, ctypes.POINTER(c_void_p),
+                                   c_int64, ctypes.POINTER(c_int)]),
+    "dlbb_car_vr_max_blocks": (c_int, [c_int, c_int, c_int]),
+    "dlbb_car_vr_launch": (c_int, [ctypes.POINTER(c_void_p), c_int, c_int,
+                                   ctypes.POINTER(c_void_p), ctypes.POINTER(c_void_p), c_int64,
+                                   c_int, c_int, c_int, c_void_p]),
     "dlbb_car_error": (c_int, [c_void_p]),
     "dlbb_car_destroy": (c_int, [c_void_p]),
 }

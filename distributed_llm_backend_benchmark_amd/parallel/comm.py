@@ -153,7 +153,14 @@ def init_distributed(backend: str = "auto", timeout_s: float = 600.0,
         if not torch.cuda.is_available():
             raise RuntimeError("backend rccl requested but no HIP device is visible")
         ndev = torch.cuda.device_count()
-        dev_index = local_rank % ndev
+        if local_rank >= ndev:
+            # RCCL refuses two ranks on one GPU only late (duplicate-device error at the first
+            # collective); fail at init with the reason instead
+            raise RuntimeError(
+                f"LOCAL_RANK {local_rank} but only {ndev} visible HIP device(s): RCCL needs one "
+                f"GPU per rank (launch at most {ndev} ranks per node, or use backend gloo with "
+                f"device='cuda' to share a GPU for rehearsals)")
+        dev_index = local_rank
         torch.cuda.set_device(dev_index)
         dev = torch.device("cuda", dev_index)
     else:

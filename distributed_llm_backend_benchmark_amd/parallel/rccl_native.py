@@ -167,9 +167,15 @@ class NativeAllReduce(_Native, C.AllReduce):
         self.buf = self.data.clone()
         self.engine = self._engine()
         self.algo = None
+        # out_of_place: result into a separate buffer (at one rank the collective is then a real
+        # device copy instead of an empty call)
+        self.out = torch.empty_like(self.buf) if self.opts.get("out_of_place") else self.buf
 
     def native_args(self):
-        return self.buf, self.buf, self.buf.numel(), 0
+        return self.buf, self.out, self.buf.numel(), 0
+
+    def result(self):
+        return self.out
 
 
 class NativeAllGather(_Native, C.AllGather):

@@ -22,7 +22,7 @@ def _run(expect_devices):
                                         "halt_on_error=1",
                LSAN_OPTIONS=f"suppressions={supp}:print_suppressions=0",
                UBSAN_OPTIONS="print_stacktrace=1:halt_on_error=1")
-    r = subprocess.run([exe], capture_output=True, text=True, timeout=300, env=env)
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=150, env=env)
     out = r.stdout + r.stderr
     assert r.returncode == 0, out[-4000:]
     assert "ERROR: AddressSanitizer" not in out and "ERROR: LeakSanitizer" not in out, out[-4000:]

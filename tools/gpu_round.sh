@@ -18,11 +18,13 @@ step() {  # step <name> <timeout> <cmd...>
   [ $rc -ne 0 ] && exit $rc
   return 0
 }
-step pytest_gpu 900 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 300
+step pytest_gpu 900 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 200 --timeout-method thread --deselect tests/test_native_host_asan.py::test_host_asan_with_device
 step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 step bench 600 python bench.py
 step tp7b 600 python -m distributed_llm_backend_benchmark_amd.cli.run_tp --config config/7b_config.yaml --backend rccl --output-dir gpurun_out/tp
 step gpt2 600 python -m distributed_llm_backend_benchmark_amd.cli.train_ddp --steps 30 --warmup 5 --output gpurun_out/gpt2.json
 cd /tmp && export TMPDIR=/tmp PYTHONPATH=$R
+step prof_tp7b 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/prof_tp7b" -o tp7b -- python3 -m distributed_llm_backend_benchmark_amd.cli.run_tp --config "$R/config/7b_config.yaml" --backend rccl --output-dir "$R/gpurun_out/tp_prof"
 step prof_gpt2 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/prof_gpt2" -o gpt2 -- python3 -m distributed_llm_backend_benchmark_amd.cli.train_ddp --steps 5 --warmup 2
+step asan_probe 200 bash -c "cd $R && ASAN_OPTIONS=detect_leaks=1:verify_asan_link_order=0 LSAN_OPTIONS=suppressions=$R/tests/native/lsan.supp timeout -k 5 150 build/asan/host_checks"
 echo done
