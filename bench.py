@@ -112,6 +112,7 @@ def _allreduce_sweep(comm, max_mib: int):
                 res[label] = t
             else:
                 invalid.append(label)
+            op.close()                      # releases its IPC registration (collective)
             del op
         if not res:
             out.append({"bytes": nbytes, "impl": None, "invalid": invalid})
@@ -235,13 +236,18 @@ def main(argv=None) -> int:
             invalid.append(label)
             if comm.rank == 0:
                 print(f"note: {label} all-reduce gave a wrong sum; not used", file=sys.stderr)
+            cand.close()
             continue
         for _ in range(max(1, args.warmup)):
             cand.run()
         comm.sync()
         trial[label] = _timed_steps(comm, cand, 10) / 10 if len(cands) > 1 else 0.0
         if op is None or trial[label] < trial[op_label]:
+            if op is not None:
+                op.close()                  # trial times are rank-max: same choice everywhere
             op, op_label = cand, label
+        else:
+            cand.close()
     if op is None:
         raise SystemExit(f"no all-reduce implementation passed its check: {invalid}")
     nbytes = op.message_bytes
@@ -250,6 +256,8 @@ def main(argv=None) -> int:
     comm.sync()
     total = _timed_steps(comm, op, args.steps)
     per_step = total / args.steps
+    if op.ipc_kernel() is not None:     # collective: raise everywhere after an IPC timeout
+        op.ipc_kernel().raise_if_error()
     bus = busbw_gbps("allreduce", nbytes, per_step, P)
     alg = algbw_gbps("allreduce", nbytes, per_step, P)
     if alg > HBM_PEAK_GBPS:
@@ -331,6 +339,7 @@ def main(argv=None) -> int:
                 t = _timed_steps(comm, cop, 10) / 10
                 res[label] = {"busbw_GBps": busbw_gbps(name, cop.message_bytes, t, P),
                               "ms": t * 1e3}
+                cop.close()
                 del cop
             coll[name] = res
 

@@ -72,6 +72,9 @@ def _bench_one(comm: Comm, op_name: str, data: torch.Tensor, warmup: int, iters:
 
         out["batched_method"] = ("hip_graph" if (graph and comm.is_gpu and graph_safe(op))
                                  else "back_to_back")
+    if op.ipc_kernel() is not None:     # a timed-out IPC kernel must not pass silently
+        op.ipc_kernel().raise_if_error()
+    op.close()          # collective: releases IPC registrations (direct / registered ops)
     del op
     return out
 

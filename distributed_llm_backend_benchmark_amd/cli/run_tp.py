@@ -188,6 +188,9 @@ def main(argv=None) -> int:
         if gpu:
             ev.append(s.elapsed_time(e) * 1e-3)
     prof.__exit__(None, None, None)
+    car = getattr(model, "ipc_allreduce", lambda: None)()
+    if car is not None:                 # a timed-out IPC all-reduce must not pass silently
+        car.raise_if_error()
     ar_bytes = fwd_bytes
     if ev:
         metrics.metrics["forward_device_times"] = ev
@@ -208,6 +211,8 @@ def main(argv=None) -> int:
             "hip_graph": use_graph,
             "gemm_fallbacks": __import__(
                 "distributed_llm_backend_benchmark_amd.ops.gemm", fromlist=["x"]).FALLBACKS["count"],
+            "gemm_kernel_mix": __import__(
+                "distributed_llm_backend_benchmark_amd.ops.gemm", fromlist=["x"]).kernel_mix(),
         }
         results = {
             "experiment": config["experiment"]["name"],

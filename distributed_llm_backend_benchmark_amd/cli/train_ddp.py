@@ -111,6 +111,9 @@ def run(args, comm, overlap: bool):
         loss = step_fn(x, y)
     comm.sync()
     dt = comm.allreduce_max(time.perf_counter() - t0)
+    tr.check_comm_errors()              # collective; raises on every rank after an IPC timeout
+    from ..ops import gemm as _gemm
+
     res = {
         "ms_per_step": dt / args.steps * 1e3,
         "tokens_per_s": comm.world_size * args.batch * args.seq * args.steps / dt,
@@ -121,6 +124,7 @@ def run(args, comm, overlap: bool):
         "hip_graph": bool(args.graph),
         "tflops_per_gpu": model.flops_per_token(args.seq) * args.batch * args.seq
         * args.steps / dt / 1e12,
+        "gemm_kernel_mix": _gemm.kernel_mix(),
     }
     if args.save_checkpoint:
         tr.save_checkpoint(args.save_checkpoint)

@@ -116,6 +116,14 @@ class LLM(nn.Module):
         self.ln_final = LayerNormParams(hidden_size, comm.device)
 
     @torch.inference_mode()
+    def ipc_allreduce(self):
+        """The IPC all-reduce instance the row-parallel layers may use (None: RCCL only)."""
+        for m in self.modules():
+            car = getattr(m, "_car", None)
+            if car is not None:
+                return car
+        return None
+
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         y, h = self.layers[0].ln1(x, kernels=self.kernels) if self.layers else (x, x)
         for i, layer in enumerate(self.layers):

@@ -19,7 +19,7 @@ from typing import Optional
 
 import torch
 
-from .build import LIB_PATH
+from .build import LIB_PATH, source_id
 
 DT_F32, DT_BF16, DT_F16 = 0, 1, 2
 _DT = {torch.float32: DT_F32, torch.bfloat16: DT_BF16, torch.float16: DT_F16}
@@ -142,6 +142,7 @@ def _load() -> ctypes.CDLL:
                     f"{LIB_PATH} not built; run `python -m "
                     f"distributed_llm_backend_benchmark_amd.ops.build`")
             lib = ctypes.CDLL(LIB_PATH)
+            check_build_id(lib, source_id())
             for name, (res, args) in _SIGS.items():
                 fn = getattr(lib, name)
                 fn.restype = res
@@ -151,6 +152,23 @@ def _load() -> ctypes.CDLL:
         except BaseException as e:  # remember and re-raise loudly on every use
             _load_error = e
             raise KernelError(f"HIP kernel library unavailable: {e}") from e
+
+
+def check_build_id(lib, expected: str) -> str:
+    """Raise unless the loaded library was built from exactly the csrc/ sources on disk (its
+    ``dlbb_build_id()`` equals :func:`.build.source_id`): a stale binary must never be what a
+    test or benchmark measures."""
+    fn = getattr(lib, "dlbb_build_id", None)
+    if fn is None:
+        raise KernelError(f"{LIB_PATH} has no dlbb_build_id(): rebuild it")
+    fn.restype = ctypes.c_char_p
+    fn.argtypes = []
+    got = fn().decode()
+    if got != expected:
+        raise KernelError(f"{LIB_PATH} was built from other sources (build id {got}, csrc/ on "
+                          f"disk is {expected}): run `python -m "
+                          "distributed_llm_backend_benchmark_amd.ops.build`")
+    return got
 
 
 def lib() -> ctypes.CDLL:

@@ -324,3 +324,20 @@ def wgrad(dy2: torch.Tensor, x2: torch.Tensor, out: Optional[torch.Tensor] = Non
         return out
     _wgrad_blas(dy2, x2, out, accumulate, None, bias_out)
     return out
+
+
+def kernel_mix() -> dict:
+    """Which implementation each autotuned GEMM shape runs, for result JSONs (the
+    kernel choice must be visible next to the throughput it produced). Per kind: shape count by
+    choice plus every shape's measured median ms per candidate."""
+    out = {}
+    for kind, table in (("linear", CHOICES), ("wgrad", WGRAD_CHOICES)):
+        counts = {}
+        for v in table.values():
+            counts[v] = counts.get(v, 0) + 1
+        out[kind] = {"shapes_by_choice": counts,
+                     "tuned": [{"key": [str(k) for k in key], "ms": times, "choice": best}
+                               for knd, key, times, best in TUNE_LOG if knd == kind]}
+    out["forced"] = os.environ.get("DLBB_GEMM", "auto")
+    out["contract_fallbacks"] = FALLBACKS["count"]
+    return out

@@ -93,6 +93,18 @@ class CollectiveOp:
     def run(self) -> None:
         raise NotImplementedError
 
+    def ipc_kernel(self):
+        """The IPC collective instance this op launches (None: RCCL / gloo only)."""
+        return getattr(self, "_custom", None) or getattr(self, "_car", None)
+
+    def close(self) -> None:
+        """Collective teardown: release IPC registrations this op made (every rank, same
+        order). Safe to call twice; the op must not run afterwards."""
+        car, rid = getattr(self, "_reg_owner", (None, None))
+        if car is not None:
+            self._reg_owner = (None, None)
+            car.deregister(rid)
+
     # ---- accounting
     @property
     def message_bytes(self) -> int:
@@ -146,6 +158,7 @@ class AllReduce(CollectiveOp):
                     raise RuntimeError("push-form registered all-reduce unavailable for "
                                        f"{self.buf.numel()} x {self.buf.dtype}")
                 self._reg_id = car.register(self.buf)
+                self._reg_owner = (car, self._reg_id)
                 self._custom = car
             elif impl == "custom":
                 if car is None or not car.healthy:
@@ -198,6 +211,7 @@ class AllGather(CollectiveOp):
             if self.opts.get("direct"):     # direct one-hop pulls over xGMI
                 self._car, self._rid = _direct_ipc(self.comm, self.flat,
                                                    16 // self.data.element_size())
+                self._reg_owner = (self._car, self._rid)
                 self.impl = "custom"
 
     def run(self):
@@ -238,6 +252,7 @@ class ReduceScatter(CollectiveOp):
         if self.opts.get("direct"):
             self._car, self._rid = _direct_ipc(self.comm, self.inp,
                                                16 // self.inp.element_size() * self.P)
+            self._reg_owner = (self._car, self._rid)
             self.impl = "custom"
 
     @property
@@ -356,6 +371,7 @@ class AllToAll(CollectiveOp):
         if self.opts.get("direct"):
             self._car, self._rid = _direct_ipc(self.comm, self.inp,
                                                16 // self.inp.element_size() * self.P)
+            self._reg_owner = (self._car, self._rid)
             self.impl = "custom"
 
     @property

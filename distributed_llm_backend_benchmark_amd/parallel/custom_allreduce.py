@@ -21,7 +21,7 @@ from __future__ import annotations
 
 import ctypes
 import os
-from typing import Dict, Optional
+from typing import Dict, Optional, Tuple
 
 import torch
 import torch.distributed as dist
@@ -35,9 +35,27 @@ DIRECT_AG, DIRECT_A2A, DIRECT_RS = 0, 1, 2
 _INSTANCES: Dict[int, "CustomAllReduce"] = {}
 
 
+# Crossovers. Measured with the single-GPU virtual-rank harness (tools/car_harness.py, one fused
+# launch of the production kernels for W ranks; profiles/r02_car_harness/SUMMARY.md, "crossover"):
+#   * one-shot vs staged two-shot: equal within noise up to 512 KiB at W = 2 / 4 / 8 (e.g. W=8:
+#     13.7 vs 13.7 us at 256 KiB, 13.5 vs 13.7 us at 512 KiB); from 1 MiB two-shot is ahead at
+#     W = 8 (16.2 vs 16.6 us, 2 MiB 23.3 vs 23.5 us, 8 MiB 68 vs 83 us). On real xGMI each link
+#     carries n bytes per one-shot call but only 2n/W per two-shot call, which moves the
+#     crossover further down, never up: ONESHOT_MAX = 256 KiB.
+#   * the registered in-place two-shot (no copy-in, no staging) is the fastest form at every
+#     size measured (W=8: 10.0 us at 64 KiB, 31 us at 8 MiB vs 68 us staged), so long-lived
+#     buffers (DDP buckets, benchmark messages) are registered once and use it.
+#   * custom vs RCCL (AUTO_MAX = 8 MiB) cannot be measured on one GPU (RCCL needs one GPU per
+#     rank); bench.py times every candidate per size on the driver's multi-GPU node and keeps
+#     the fastest validated one, which is what its JSON reports.
+ONESHOT_MAX_BYTES = 256 << 10
+AUTO_MAX_BYTES = 8 << 20
+
+
 class CustomAllReduce:
     def __init__(self, comm: Comm, capacity_bytes: int = 64 << 20,
-                 oneshot_max_bytes: int = 256 << 10, auto_max_bytes: int = 8 << 20,
+                 oneshot_max_bytes: int = ONESHOT_MAX_BYTES,
+                 auto_max_bytes: int = AUTO_MAX_BYTES,
                  nblocks: Optional[int] = None):
         if not comm.is_gpu:
             raise RuntimeError("custom all-reduce needs HIP devices")
@@ -79,7 +97,8 @@ class CustomAllReduce:
         self.reg_healthy = False
         self.push_healthy = False
         self._regs: Dict[tuple, int] = {}
-        self._reg_keep = []
+        self._reg_keep: Dict[int, torch.Tensor] = {}   # rid -> registered tensor (kept alive)
+        self._reg_refs: Dict[int, int] = {}            # rid -> register() calls not released
 
     # ------------------------------------------------------------------ policy
     def supports(self, t: torch.Tensor) -> bool:
@@ -109,12 +128,14 @@ class CustomAllReduce:
     def register(self, t: torch.Tensor) -> int:
         """Collective: IPC-map tensor ``t`` of every rank (same numel / dtype everywhere) for
         :meth:`all_reduce_registered`. Every local failure is agreed on by all ranks (then
-        every rank raises). Registered tensors are kept alive by this object."""
+        every rank raises). Registered tensors are kept alive by this object until
+        :meth:`deregister`."""
         if (t.dtype not in (torch.bfloat16, torch.float16, torch.float32)
                 or not t.is_contiguous() or t.numel() * t.element_size() % 16):
             raise ValueError(f"cannot register {t.numel()} x {t.dtype}")
         key = (t.data_ptr(), t.numel() * t.element_size())
-        if key in self._regs:
+        if key in self._regs:                 # same tensor again: one more reference
+            self._reg_refs[self._regs[key]] += 1
             return self._regs[key]
         mine, err = None, None
         try:
@@ -137,8 +158,39 @@ class CustomAllReduce:
         if any(r != 0 for r in oks):
             raise RuntimeError(f"custom all-reduce registration open failed (hip rc: {oks})")
         self._regs[key] = int(rid.value)
-        self._reg_keep.append(t)
+        self._reg_keep[int(rid.value)] = t
+        self._reg_refs[int(rid.value)] = 1
         return int(rid.value)
+
+    def deregister(self, rid: int) -> None:
+        """Collective: drop one reference to registration ``rid``; at the last one release it on
+        every rank — the peer IPC mappings no
+        other live registration uses are closed and the tensor is no longer kept alive. Every
+        rank first drains its stream and meets the others at a barrier, so no kernel on any rank
+        still reads or writes the buffers being unmapped."""
+        if rid not in self._reg_keep:
+            raise KeyError(f"registration {rid} is not live")
+        self._reg_refs[rid] -= 1             # (identical on every rank: same call sequence)
+        if self._reg_refs[rid] > 0:
+            return
+        del self._reg_refs[rid]
+        torch.cuda.synchronize(self.comm.device)
+        self.comm.barrier()
+        rc = self.lib.dlbb_car_reg_close(self.h, int(rid))
+        oks = self.comm.all_gather_object(rc)
+        t = self._reg_keep.pop(rid)
+        self._regs.pop((t.data_ptr(), t.numel() * t.element_size()), None)
+        # every rank unmapped before any rank lets its buffer go back to the allocator
+        self.comm.barrier()
+        if any(r != 0 for r in oks):
+            raise RuntimeError(f"custom all-reduce deregistration failed (hip rc: {oks})")
+
+    def reg_counts(self) -> Tuple[int, int]:
+        """(live registrations, opened peer IPC mappings) of this rank."""
+        live, maps = ctypes.c_int(), ctypes.c_int()
+        _lib.check(self.lib.dlbb_car_reg_counts(self.h, ctypes.byref(live), ctypes.byref(maps)),
+                   "car_reg_counts")
+        return int(live.value), int(maps.value)
 
     def supports_registered(self, t: torch.Tensor) -> bool:
         if t.dtype not in (torch.bfloat16, torch.float16, torch.float32) or not t.is_contiguous():
@@ -208,7 +260,18 @@ class CustomAllReduce:
         return self.all_reduce(t, t, algo, nblocks)
 
     def check_error(self) -> int:
+        """This rank's device-side timeout flag (read and cleared; synchronous)."""
         return int(self.lib.dlbb_car_error(self.h))
+
+    def raise_if_error(self) -> None:
+        """Collective: if any rank's IPC kernel timed out in a spin wait since the last check
+        (its result is partial and the double-buffer reuse guarantee is void), raise on EVERY
+        rank. Call outside timed regions: one synchronous 4-byte read + one object all-gather."""
+        flags = self.comm.all_gather_object(self.check_error())
+        if any(flags):
+            bad = [i for i, f in enumerate(flags) if f]
+            raise RuntimeError(f"custom all-reduce timed out on ranks {bad}: results since the "
+                               "last check are partial; restart the job")
 
     def self_test(self) -> bool:
         """Compare one-shot and two-shot against RCCL on small/medium messages; all ranks must
@@ -244,36 +307,44 @@ class CustomAllReduce:
         return self.healthy
 
     def _self_test_registered(self) -> None:
-        """Registered in-place two-shot, pull and push forms, vs RCCL (two calls each: reuse of
-        one registration, both staging halves); ``reg_healthy`` / ``push_healthy`` only if the
-        form passes on every rank."""
+        """Registered in-place two-shot, pull and push forms, vs RCCL: six calls alternating the
+        forms, each followed by a staged two-shot call on other data, so both staging halves are
+        re-read after local writes of the other form. ``reg_healthy`` /
+        ``push_healthy`` only if the form passes on every rank. The test buffer is released."""
         dev, W = self.comm.device, self.comm.world_size
         ok = {False: True, True: True}
+        rid = None
         try:
             n = 1 << 20
             buf = torch.empty(n, device=dev, dtype=torch.bfloat16)
             rid = self.register(buf)
-            for push in (False, True):
-                for it in range(2):
-                    g = torch.Generator(device=dev)
-                    g.manual_seed(777 + 31 * it + 7 * push + self.comm.rank)
-                    x = torch.randn(n, generator=g, device=dev).to(torch.bfloat16)
-                    ref = x.float().clone()
-                    if W > 1:
-                        dist.all_reduce(ref)
-                    buf.copy_(x)
-                    try:
-                        self.all_reduce_registered(buf, rid, push=push)
-                        torch.cuda.synchronize(dev)
-                        good = bool(torch.allclose(buf.float(), ref, rtol=2e-2, atol=5e-2 * W))
-                        ok[push] = ok[push] and good and self.check_error() == 0
-                    except Exception:  # noqa: BLE001 - a failed launch is a failed test
-                        ok[push] = False
+            for it in range(6):
+                push = bool(it % 2)
+                g = torch.Generator(device=dev)
+                g.manual_seed(777 + 31 * it + self.comm.rank)
+                x = torch.randn(n, generator=g, device=dev).to(torch.bfloat16)
+                y = torch.randn(n // 4, generator=g, device=dev).to(torch.bfloat16)
+                ref, ref_y = x.float().clone(), y.float().clone()
+                if W > 1:
+                    dist.all_reduce(ref)
+                    dist.all_reduce(ref_y)
+                buf.copy_(x)
+                try:
+                    self.all_reduce_registered(buf, rid, push=push)
+                    self.all_reduce(y, algo=TWOSHOT)
+                    torch.cuda.synchronize(dev)
+                    good = bool(torch.allclose(buf.float(), ref, rtol=2e-2, atol=5e-2 * W))
+                    good_y = bool(torch.allclose(y.float(), ref_y, rtol=2e-2, atol=5e-2 * W))
+                    ok[push] = ok[push] and good and good_y and self.check_error() == 0
+                except Exception:  # noqa: BLE001 - a failed launch is a failed test
+                    ok[push] = False
         except Exception:  # noqa: BLE001 - a failed registration fails both forms
             ok = {False: False, True: False}
-        flags = self.comm.all_gather_object((bool(ok[False]), bool(ok[True])))
+        flags = self.comm.all_gather_object((bool(ok[False]), bool(ok[True]), rid is not None))
         self.reg_healthy = all(f[0] for f in flags)
         self.push_healthy = self.reg_healthy and all(f[1] for f in flags)
+        if all(f[2] for f in flags):
+            self.deregister(rid)
         if not self.push_healthy and self.comm.rank == 0:
             print("[custom all-reduce] registered-buffer self-test failed (pull/push per rank): "
                   f"{flags}", flush=True)

@@ -35,7 +35,7 @@ import torch
 import torch.distributed as dist
 
 from ..ops import FlatAdamW
-from ..ops.elementwise import ChunkTable
+from ..ops.elementwise import ChunkTable, ScaleTable
 from ..utils import tracing
 from .comm import Comm
 
@@ -62,6 +62,10 @@ class FlatParamTrainer:
                  betas=(0.9, 0.95), weight_decay: float = 0.0, bucket_mb: float = 64.0,
                  overlap: bool = True, mode: str = "view", allreduce: str = "rccl",
                  grad_dtype: torch.dtype = torch.bfloat16):
+        if mode == "view" and grad_dtype != torch.bfloat16:
+            raise ValueError("grad_dtype must be the parameter dtype (bf16) in mode='view': "
+                             "autograd accumulates straight into the bucket views; use "
+                             "mode='flatten' for fp32 gradient buckets")
         self.model = model
         self.comm = comm
         self.world = comm.world_size if comm is not None else 1
@@ -203,7 +207,9 @@ class FlatParamTrainer:
                 pairs = [(p.grad.reshape(-1), self.flat_grad[self._offsets[id(p)]:
                                                               self._offsets[id(p)] + p.numel()])
                          for p in b.params]
-                b.table = ChunkTable(pairs)
+                # fp32 buckets (mode="flatten", grad_dtype=fp32): the flatten pass also casts
+                b.table = (ChunkTable(pairs) if self.flat_grad.dtype == b.params[0].grad.dtype
+                           else ScaleTable(pairs, 1.0))
                 b.table_key = key
             b.table.run()
         if self.world == 1:
@@ -256,6 +262,14 @@ class FlatParamTrainer:
                 b.work.wait()
         if self._wgrad_stream is not None:      # side-stream weight gradients (and copies)
             torch.cuda.current_stream(self.flat_grad.device).wait_stream(self._wgrad_stream)
+
+    def check_comm_errors(self) -> None:
+        """Collective: raise on every rank if an IPC all-reduce of any rank timed out since the
+        last check (its spin wait gave up: the reduced gradients are partial). One small
+        synchronous read per rank + one object all-gather: call it every few steps and at the
+        end of a run, outside timed regions (a timeout must never pass silently)."""
+        if self._car is not None:
+            self._car.raise_if_error()
 
     # ------------------------------------------------------------------ step
     def zero_grad(self) -> None:
@@ -378,6 +392,8 @@ class FlatParamTrainer:
             for k, t in self.state_tensors().items():
                 t.copy_(f.get_tensor(k).to(t.device))
         self.opt.t = int(meta["adam_t"])
+        if self.opt.t_dev is not None:         # HIP-graph mode reads the device counter
+            self.opt.t_dev.fill_(self.opt.t)
         self.step_count = int(meta["step"])
         self._refresh_params()
 

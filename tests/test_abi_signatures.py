@@ -77,3 +77,40 @@ def test_signature_argument_counts_match_the_c_api():
     bad = {name: (len(args), nargs.get(name)) for name, (_, args) in _lib._SIGS.items()
            if nargs.get(name) is not None and len(args) != nargs[name]}
     assert not bad, f"argtypes count != C parameter count (argtypes, C): {bad}"
+
+
+def test_build_id_detects_source_change(tmp_path, monkeypatch):
+    """The library's dlbb_build_id() must equal the hash of csrc/ on disk; editing any source
+    makes a previously built library refuse to load."""
+    import shutil as _sh
+
+    from distributed_llm_backend_benchmark_amd.ops import _lib, build
+
+    csrc = tmp_path / "csrc"
+    _sh.copytree(build.CSRC, csrc)
+    monkeypatch.setattr(build, "CSRC", str(csrc))
+    before = build.source_id()
+    hip = csrc / "reduce.hip"
+    hip.write_text(hip.read_text() + "\n// touched\n")
+    after = build.source_id()
+    assert before != after
+
+    def fake_lib(bid):
+        class L:
+            pass
+        lib = L()
+        lib.dlbb_build_id = lambda: bid.encode()
+        return lib
+
+    assert _lib.check_build_id(fake_lib(after), after) == after
+    with pytest.raises(_lib.KernelError, match="built from other sources"):
+        _lib.check_build_id(fake_lib(before), after)
+
+
+def test_built_library_matches_tree():
+    from distributed_llm_backend_benchmark_amd.ops import _lib, build
+
+    if not os.path.exists(build.LIB_PATH):
+        pytest.skip("library not built")
+    lib = _lib.lib()            # raises if stale
+    assert _lib.check_build_id(lib, build.source_id()) == build.source_id()

@@ -338,3 +338,76 @@ def test_bench_py_gloo_world2_contract():
     assert rec["higher_is_better"] is True and rec["scaling"] == "weak"
     assert [e["bytes"] for e in rec["allreduce_sweep"]] == [1 << 10, 8 << 10, 64 << 10, 512 << 10]
     assert all(e["impl"] == "rccl" and e["busbw_GBps"] > 0 for e in rec["allreduce_sweep"])
+
+
+def _precision_worker(rank, world, grad_dtype_name):
+    """Reduction error of the DDP gradient all-reduce alone: flatten-mode buckets (bf16 or fp32)
+    reduced through the process group vs the exact fp64 mean of every rank's local bf16
+    gradient (all-gathered)."""
+    from distributed_llm_backend_benchmark_amd.models.gpt2 import GPT2, GPT2Config
+    from distributed_llm_backend_benchmark_amd.parallel.comm import init_distributed
+    from distributed_llm_backend_benchmark_amd.parallel.ddp import FlatParamTrainer
+
+    gd = {"bf16": torch.bfloat16, "fp32": torch.float32}[grad_dtype_name]
+    comm = init_distributed("gloo")
+    cfg = GPT2Config(vocab_size=256, block_size=32, n_layer=2, n_head=2, n_embd=64)
+    g = torch.Generator().manual_seed(21)
+    data = torch.randint(0, 256, (world * 2, 33), generator=g)
+    local = data[rank * 2:(rank + 1) * 2]
+    m = GPT2(cfg, seed=4)
+    tr = FlatParamTrainer(m, comm, lr=1e-3, bucket_mb=0.05, mode="flatten", grad_dtype=gd)
+    assert tr.flat_grad.dtype == gd
+    tr.zero_grad()
+    tr._reset()
+    m(local[:, :-1], local[:, 1:]).backward()
+    tr.finish()
+    worst = 0.0
+    for p in tr._params:
+        mine = p.grad.double().reshape(-1)
+        every = [torch.empty_like(mine) for _ in range(world)]
+        torch.distributed.all_gather(every, mine)
+        exact = torch.stack(every).mean(0)
+        o = tr._offsets[id(p)]
+        got = tr.flat_grad[o:o + p.numel()].double() / world
+        scale = float(exact.abs().max()) or 1.0
+        worst = max(worst, float((got - exact).abs().max()) / scale)
+    comm.destroy()
+    return worst
+
+
+def test_ddp_reduction_precision_world8():
+    """P = 8 (the driver's scaling node): bf16 gradient buckets are summed in bf16 by the
+    collective, fp32 buckets (mode='flatten', grad_dtype=fp32) in fp32. Pins the max error of
+    the averaged gradient relative to each tensor's largest entry."""
+    bf = run_multiprocess(_precision_worker, 8, args=("bf16",), timeout=600)
+    fp = run_multiprocess(_precision_worker, 8, args=("fp32",), timeout=600)
+    worst_bf, worst_fp = max(bf), max(fp)         # per-rank worst errors
+    print(f"P=8 averaged-gradient max rel error: bf16 buckets {worst_bf:.3e}, "
+          f"fp32 buckets {worst_fp:.3e}")
+    assert worst_fp < 1e-6, worst_fp          # fp32 sum of bf16 values (measured 3.0e-8)
+    assert worst_bf < 3e-2, worst_bf          # 8-way bf16 sum: a few bf16 ulps (measured 8.2e-3)
+    assert worst_fp < worst_bf
+
+
+def test_view_mode_rejects_non_param_grad_dtype():
+    from distributed_llm_backend_benchmark_amd.models.gpt2 import GPT2, GPT2Config
+    from distributed_llm_backend_benchmark_amd.parallel.ddp import FlatParamTrainer
+
+    m = GPT2(GPT2Config(vocab_size=64, block_size=8, n_layer=1, n_head=1, n_embd=32), seed=1)
+    with pytest.raises(ValueError, match="mode='flatten'"):
+        FlatParamTrainer(m, None, mode="view", grad_dtype=torch.float32)
+
+
+def test_rccl_init_refuses_more_ranks_than_gpus(monkeypatch):
+    """RCCL needs one GPU per rank: a LOCAL_RANK beyond the visible devices fails at init with
+    the reason (instead of a late duplicate-device error from RCCL)."""
+    from distributed_llm_backend_benchmark_amd.parallel import comm as C
+
+    monkeypatch.setattr(C.torch.cuda, "is_available", lambda: True)
+    monkeypatch.setattr(C.torch.cuda, "device_count", lambda: 1)
+    monkeypatch.setenv("LOCAL_RANK", "3")
+    monkeypatch.setenv("RANK", "3")
+    monkeypatch.setenv("WORLD_SIZE", "4")
+    monkeypatch.setenv("MASTER_PORT", "1")
+    with pytest.raises(RuntimeError, match="one GPU per rank"):
+        C.init_distributed("rccl")

@@ -6,6 +6,7 @@ sum of the W rank inputs before it is timed; a configuration that fails is recor
 ``"valid": false`` and never timed):
 
 * ``latency``    one-shot all-reduce, 512 B .. 256 KiB, workgroups per rank swept
+* ``crossover``  one-shot vs staged two-shot vs registered two-shot, 64 KiB .. 8 MiB
 * ``throughput`` staged two-shot, registered in-place two-shot (pull) and push form,
                  1 MiB .. 128 MiB, workgroups per rank swept
 * ``direct``     one-hop all-gather / reduce-scatter / all-to-all on registered inputs
@@ -13,9 +14,10 @@ sum of the W rank inputs before it is timed; a configuration that fails is recor
 
 Times: ``us_b2b`` = mean per call of ``iters`` back-to-back launches between two events (the
 nccl-tests convention); ``us_p50`` = median of per-call event pairs. ``hbm_GBps`` = the bytes the
-W ranks together read + write in HBM per call (model in ``_hbm_bytes``) / time: on one GPU every
-byte a real rank would move over xGMI goes through this HBM, so large messages are bounded by
-the HBM roofline (~8 TB/s), not by xGMI; small messages give the protocol's latency floor.
+W ranks together load + store per call (model in ``_hbm_bytes``) / time: on one GPU every byte a
+real rank would move over xGMI goes through this GPU's memory system, so large messages are
+bounded by the HBM roofline (~8 TB/s; messages that fit L2 / the 256 MB MALL can exceed it), not
+by xGMI; small messages give the protocol's latency floor.
 
 usage: python tools/car_harness.py --out profiles/r02_car_harness/car_harness.jsonl [--quick]
 """
@@ -228,7 +230,7 @@ def main(argv=None) -> int:
     ap.add_argument("--out", required=True)
     ap.add_argument("--quick", action="store_true", help="fewer sizes / block counts")
     ap.add_argument("--worlds", default="2,4,8")
-    ap.add_argument("--sections", default="latency,throughput,direct,streams")
+    ap.add_argument("--sections", default="latency,crossover,throughput,direct,streams")
     args = ap.parse_args(argv)
     os.makedirs(os.path.dirname(os.path.abspath(args.out)), exist_ok=True)
     worlds = [int(w) for w in args.worlds.split(",")]
@@ -246,6 +248,13 @@ def main(argv=None) -> int:
                     for n in lat_sizes:
                         H.allreduce("latency", V, vr.K_ONESHOT, n, [1, 2, 4, 8, 16, 32],
                                     iters=200)
+                if "crossover" in sections:
+                    # one-shot vs staged two-shot vs registered two-shot around the crossovers
+                    for n in [64 << 10, 256 << 10, 512 << 10, 1 << 20, 2 << 20, 4 << 20,
+                              8 << 20]:
+                        for kind in (vr.K_ONESHOT, vr.K_TWOSHOT, vr.K_REG):
+                            H.allreduce("crossover", V, kind, n, [4, 8, 16, 32, 64, 128],
+                                        iters=100)
                 if "throughput" in sections:
                     for n in big:
                         for kind in (vr.K_TWOSHOT, vr.K_REG, vr.K_PUSH):
