@@ -44,6 +44,13 @@ def parse_args(argv=None):
                     help="bucket all-reduce: torch ProcessGroupNCCL, IPC xGMI kernel, or our "
                          "C++ RCCL engine on a dedicated stream")
     ap.add_argument("--no-overlap", action="store_true")
+    ap.add_argument("--comm-blocks", type=int, default=None,
+                    help="CU budget: workgroups per bucket-reduction launch (IPC kernel / "
+                         "emulation); default = the kernel's size heuristic")
+    ap.add_argument("--emulate-comm", action="store_true",
+                    help="world 1: run a bucket-sized stand-in reduction (one rank's all-reduce "
+                         "HBM traffic) on the comm stream at every bucket-ready hook, to measure "
+                         "what overlapped gradient reduction costs the backward pass")
     ap.add_argument("--zero", action="store_true",
                     help="ZeRO-2-style: reduce-scatter grads, sharded AdamW, all-gather params")
     ap.add_argument("--compare-overlap", action="store_true")
@@ -79,7 +86,8 @@ def run(args, comm, overlap: bool):
     else:
         tr = FlatParamTrainer(model, comm if comm.world_size > 1 else None, lr=args.lr,
                               bucket_mb=args.bucket_mb, overlap=overlap, mode=args.mode,
-                              allreduce=args.allreduce)
+                              allreduce=args.allreduce, comm_blocks=args.comm_blocks,
+                              emulate_comm=args.emulate_comm)
     data = SyntheticTokenDataset(args.batch, args.seq, cfg.vocab_size, rank=comm.rank,
                                  device=comm.device)
     if args.resume_from:
@@ -152,7 +160,8 @@ def main(argv=None) -> int:
            "n_gpus": comm.world_size, "overlap": not args.no_overlap, **main_res,
            "config": {k: getattr(args, k) for k in ("n_layer", "n_head", "n_embd", "vocab",
                                                     "batch", "seq", "bucket_mb", "mode",
-                                                    "allreduce", "zero")}}
+                                                    "allreduce", "zero", "comm_blocks",
+                                                    "emulate_comm")}}
     if args.compare_overlap:
         alt = run(args, comm, overlap=args.no_overlap)
         out["other_overlap_setting"] = alt

@@ -53,9 +53,9 @@ __global__ void __launch_bounds__(256) reduce_sum_kernel(ReduceArgs a) {
 }
 
 template <int DTI, int DTO>
-static hipError_t launch_reduce(const ReduceArgs& a, hipStream_t s) {
+static hipError_t launch_reduce(const ReduceArgs& a, int nblocks, hipStream_t s) {
   const int block = 256;
-  const int grid = stream_grid((a.n + 7) / 8, block);
+  const int grid = nblocks > 0 ? nblocks : stream_grid((a.n + 7) / 8, block);
   hipLaunchKernelGGL((reduce_sum_kernel<DTI, DTO>), dim3(grid), dim3(block), 0, s, a);
   return hipGetLastError();
 }
@@ -65,8 +65,11 @@ static hipError_t launch_reduce(const ReduceArgs& a, hipStream_t s) {
 using namespace dlbb;
 
 // srcs: host array of nsrc device pointers (passed by value in the kernel argument block).
-DLBB_API int dlbb_reduce_sum(const void* const* srcs, int nsrc, void* dst, int64_t n,
-                             int dtype_in, int dtype_out, float scale, hipStream_t stream) {
+// nblocks > 0 caps the grid (a CU budget, e.g. for a reduction running beside compute);
+// 0 = enough workgroups to fill the chip.
+DLBB_API int dlbb_reduce_sum_grid(const void* const* srcs, int nsrc, void* dst, int64_t n,
+                                  int dtype_in, int dtype_out, float scale, int nblocks,
+                                  hipStream_t stream) {
   if (nsrc < 1 || nsrc > kMaxSrc || n < 0) return hipErrorInvalidValue;
   if (n == 0) return hipSuccess;
   ReduceArgs a{};
@@ -75,10 +78,16 @@ DLBB_API int dlbb_reduce_sum(const void* const* srcs, int nsrc, void* dst, int64
   a.n = n;
   a.nsrc = nsrc;
   a.scale = scale;
-#define DLBB_R(I, O) if (dtype_in == I && dtype_out == O) return launch_reduce<I, O>(a, stream);
+#define DLBB_R(I, O) \
+  if (dtype_in == I && dtype_out == O) return launch_reduce<I, O>(a, nblocks, stream);
   DLBB_R(DT_BF16, DT_BF16) DLBB_R(DT_BF16, DT_F32) DLBB_R(DT_F16, DT_F16)
   DLBB_R(DT_F16, DT_F32) DLBB_R(DT_F32, DT_F32) DLBB_R(DT_F32, DT_BF16)
   DLBB_R(DT_F32, DT_F16)
 #undef DLBB_R
   return hipErrorInvalidValue;
+}
+
+DLBB_API int dlbb_reduce_sum(const void* const* srcs, int nsrc, void* dst, int64_t n,
+                             int dtype_in, int dtype_out, float scale, hipStream_t stream) {
+  return dlbb_reduce_sum_grid(srcs, nsrc, dst, n, dtype_in, dtype_out, scale, 0, stream);
 }

@@ -33,6 +33,8 @@ c_void_p, c_int, c_int64, c_float = ctypes.c_void_p, ctypes.c_int, ctypes.c_int6
 _SIGS = {
     "dlbb_reduce_sum": (c_int, [ctypes.POINTER(c_void_p), c_int, c_void_p, c_int64, c_int, c_int,
                                 c_float, c_void_p]),
+    "dlbb_reduce_sum_grid": (c_int, [ctypes.POINTER(c_void_p), c_int, c_void_p, c_int64, c_int,
+                                     c_int, c_float, c_int, c_void_p]),
     "dlbb_cast": (c_int, [c_void_p, c_int, c_void_p, c_int, c_int64, c_void_p]),
     "dlbb_pack_rows": (c_int, [c_void_p, c_int, c_int64, c_void_p, c_int, c_int64, c_int64,
                                c_int64, c_void_p]),

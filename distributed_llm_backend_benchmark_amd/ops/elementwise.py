@@ -19,8 +19,10 @@ MAX_REDUCE_SRCS = 16
 
 
 def reduce_sum(srcs: Sequence[torch.Tensor], out: Optional[torch.Tensor] = None,
-               out_dtype: Optional[torch.dtype] = None, scale: float = 1.0) -> torch.Tensor:
-    """``out = scale * sum(srcs)`` with fp32 accumulation (the local SUM of an all-reduce)."""
+               out_dtype: Optional[torch.dtype] = None, scale: float = 1.0,
+               nblocks: Optional[int] = None) -> torch.Tensor:
+    """``out = scale * sum(srcs)`` with fp32 accumulation (the local SUM of an all-reduce).
+    ``nblocks`` caps the kernel's grid (a CU budget when it runs beside compute)."""
     if not srcs:
         raise ValueError("reduce_sum needs at least one source")
     n = srcs[0].numel()
@@ -36,8 +38,9 @@ def reduce_sum(srcs: Sequence[torch.Tensor], out: Optional[torch.Tensor] = None,
             return reduce_sum([part.to(srcs[0].dtype)] + list(srcs[MAX_REDUCE_SRCS:]), out,
                               scale=scale)
         arr = (ctypes.c_void_p * len(srcs))(*[s.data_ptr() for s in srcs])
-        check(_lib.lib().dlbb_reduce_sum(arr, len(srcs), out.data_ptr(), n, dt(srcs[0]), dt(out),
-                                         float(scale), stream(out.device)), "reduce_sum")
+        check(_lib.lib().dlbb_reduce_sum_grid(arr, len(srcs), out.data_ptr(), n, dt(srcs[0]),
+                                              dt(out), float(scale), int(nblocks or 0),
+                                              stream(out.device)), "reduce_sum")
         return out
     acc = torch.zeros(srcs[0].shape, dtype=torch.float32, device=srcs[0].device)
     for s in srcs:

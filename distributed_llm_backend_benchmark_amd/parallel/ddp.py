@@ -15,14 +15,17 @@ the MI355X-native replacement used by the GPT-2 DDP microbenchmark:
   buckets amortise RCCL launch/protocol cost; still several buckets so the first all-reduce
   starts early in backward).
 * **Overlap**: a post-accumulate-grad hook counts ready params; a full bucket is all-reduced
-  asynchronously (RCCL runs on ProcessGroupNCCL's own high-priority stream, ordered after the
+  asynchronously (RCCL runs on ProcessGroupNCCL's own stream, ordered after the
   producing kernels by an event), strictly in bucket order on every rank (identical collective
   order — RCCL would hang otherwise). ``finish()`` waits the works; the optimizer consumes the
   reduced flat gradient with the 1/world average fused into the AdamW kernel.
 * ``allreduce="custom"`` routes buckets through the IPC xGMI kernel (in place on the
   IPC-registered bucket when the registered self-test passed, else via its staging buffer), and
   ``allreduce="native"`` through our own RCCL communicator (``rccl_native``), both on a
-  dedicated high-priority comm stream instead of ProcessGroupNCCL's.
+  dedicated comm stream instead of ProcessGroupNCCL's. That stream has NORMAL priority: at high
+  priority its workgroups took CU slots ahead of the backward's hipBLASLt Stream-K GEMMs, whose
+  persistent grids then stalled (+69 % step time in 4 of 15 settings;
+  profiles/r02_overlap/SUMMARY.md). ``comm_blocks`` is the reductions' CU budget.
 """
 
 from __future__ import annotations
@@ -35,7 +38,7 @@ import torch
 import torch.distributed as dist
 
 from ..ops import FlatAdamW
-from ..ops.elementwise import ChunkTable, ScaleTable
+from ..ops.elementwise import ChunkTable, ScaleTable, reduce_sum
 from ..utils import tracing
 from .comm import Comm
 
@@ -43,6 +46,9 @@ _GRAD_SINKS = os.environ.get("DLBB_GRAD_SINKS", "1") != "0"   # A/B switch for t
 # opt-in: sink dW GEMMs on a side stream. Measured +4 % step time on GPT-2 (the concurrent
 # GEMMs take CUs from the critical-path dgrad chain), so off by default
 _WGRAD_STREAM = os.environ.get("DLBB_WGRAD_STREAM", "0") == "1"
+# priority of the dedicated bucket-reduction stream: 0 = normal (default, measured), -1 = high
+# (A/B knob; see the module docstring and profiles/r02_overlap/SUMMARY.md)
+_COMM_PRIORITY = int(os.environ.get("DLBB_COMM_STREAM_PRIORITY", "0"))
 _ALIGN = 64  # elements: keeps every param view 128-B aligned (16-B MFMA/glds rows)
 
 
@@ -61,7 +67,8 @@ class FlatParamTrainer:
     def __init__(self, model: torch.nn.Module, comm: Optional[Comm], lr: float = 3e-4,
                  betas=(0.9, 0.95), weight_decay: float = 0.0, bucket_mb: float = 64.0,
                  overlap: bool = True, mode: str = "view", allreduce: str = "rccl",
-                 grad_dtype: torch.dtype = torch.bfloat16):
+                 grad_dtype: torch.dtype = torch.bfloat16, comm_blocks: Optional[int] = None,
+                 emulate_comm: bool = False):
         if mode == "view" and grad_dtype != torch.bfloat16:
             raise ValueError("grad_dtype must be the parameter dtype (bf16) in mode='view': "
                              "autograd accumulates straight into the bucket views; use "
@@ -135,7 +142,7 @@ class FlatParamTrainer:
             from .custom_allreduce import get_custom_allreduce
 
             self._car = get_custom_allreduce(comm)
-            self._comm_stream = torch.cuda.Stream(dev, priority=-1)
+            self._comm_stream = torch.cuda.Stream(dev, priority=_COMM_PRIORITY)
             # buckets are fixed slices of flat_grad: IPC-map them once, then every bucket
             # all-reduce is the in-place two-shot (no staging copy, no capacity limit)
             if self._car is not None and self._car.reg_healthy:
@@ -147,7 +154,21 @@ class FlatParamTrainer:
             from .rccl_native import get_native
 
             self._native = get_native(comm)
-            self._comm_stream = torch.cuda.Stream(dev, priority=-1)
+            self._comm_stream = torch.cuda.Stream(dev, priority=_COMM_PRIORITY)
+        # CU budget of the bucket reductions that run beside backward: workgroups per IPC /
+        # emulated reduction launch (None = the kernel's own size heuristic)
+        self.comm_blocks = comm_blocks
+        # world 1 only: every ready bucket runs a stand-in reduction on the comm
+        # stream — the local HBM traffic of one rank's all-reduce (read 2n, write n: bucket +
+        # zeros -> bucket, so gradients are unchanged) — to measure what overlapped bucket
+        # reductions cost the backward pass on one GPU (tools/ddp_overlap.py)
+        self._emu_zero = None
+        if emulate_comm:
+            if self.world != 1 or dev.type != "cuda":
+                raise ValueError("emulate_comm is a single-GPU measurement (world 1, HIP device)")
+            self._comm_stream = torch.cuda.Stream(dev, priority=_COMM_PRIORITY)
+            self._emu_zero = torch.zeros(max(b.end - b.start for b in self.buckets),
+                                         dtype=grad_dtype, device=dev)
         self.step_count = 0
 
     # ------------------------------------------------------------------ hooks for subclasses
@@ -212,6 +233,15 @@ class FlatParamTrainer:
                            else ScaleTable(pairs, 1.0))
                 b.table_key = key
             b.table.run()
+        if self._emu_zero is not None:
+            buf = self.flat_grad[b.start:b.end]
+            cs = self._comm_stream
+            cs.wait_stream(torch.cuda.current_stream(buf.device))
+            with torch.cuda.stream(cs):
+                reduce_sum([buf, self._emu_zero[:buf.numel()]], out=buf,
+                           nblocks=self.comm_blocks)
+            b.work = "stream"
+            return
         if self.world == 1:
             return
         buf = self.flat_grad[b.start:b.end]
@@ -222,7 +252,8 @@ class FlatParamTrainer:
             if ws is not None:
                 cs.wait_stream(ws)
             with torch.cuda.stream(cs):
-                self._car.all_reduce_registered(buf, self._bucket_reg[b.idx])
+                self._car.all_reduce_registered(buf, self._bucket_reg[b.idx],
+                                                nblocks=self.comm_blocks)
             b.work = "stream"
         elif self._car is not None and self._car.healthy and self._car.supports(buf):
             cs = self._comm_stream
@@ -230,10 +261,10 @@ class FlatParamTrainer:
             if ws is not None:
                 cs.wait_stream(ws)
             with torch.cuda.stream(cs):
-                self._car.all_reduce_(buf)
+                self._car.all_reduce_(buf, nblocks=self.comm_blocks)
             b.work = "stream"
         elif self._native is not None:
-            # our RCCL communicator on a dedicated high-priority stream, ordered after the
+            # our RCCL communicator on the dedicated comm stream, ordered after the
             # producing backward kernels; finish() joins the stream
             cs = self._comm_stream
             cs.wait_stream(torch.cuda.current_stream(buf.device))

@@ -473,3 +473,29 @@ def test_gpt2_training_step_hip_graph_matches_eager():
     for a, b in zip(eager[2:], graphed):
         assert abs(a - b) < 2e-2, (eager[2:], graphed)
     assert float((ea.master - gr.master).abs().max()) < 5e-3
+
+
+def test_ddp_emulated_comm_is_numerically_transparent():
+    """The single-GPU overlap measurement (bucket + zeros -> bucket on the comm stream at each
+    bucket-ready hook, CU budget comm_blocks) must not change training: same losses and masters
+    bit for bit as the plain world-1 step."""
+    from distributed_llm_backend_benchmark_amd.models.gpt2 import GPT2, GPT2Config
+    from distributed_llm_backend_benchmark_amd.ops.elementwise import reduce_sum
+    from distributed_llm_backend_benchmark_amd.parallel.ddp import FlatParamTrainer
+
+    dev = torch.device("cuda", 0)
+    x = [torch.randn(1 << 16, device=dev).to(torch.bfloat16) for _ in range(2)]
+    assert torch.equal(reduce_sum(x, nblocks=3), reduce_sum(x))
+    cfg = GPT2Config(vocab_size=512, block_size=64, n_layer=2, n_head=4, n_embd=256)
+    idx = torch.randint(0, cfg.vocab_size, (4, 65), device=dev)
+    out = []
+    for emulate in (False, True):
+        tr = FlatParamTrainer(GPT2(cfg, device=dev, seed=5), None, lr=1e-3, bucket_mb=0.1,
+                              emulate_comm=emulate, comm_blocks=8 if emulate else None)
+        assert len(tr.buckets) > 1
+        losses = [tr.step(idx[:, :-1], idx[:, 1:]) for _ in range(3)]
+        torch.cuda.synchronize()
+        out.append((losses, tr.master.clone()))
+        tr.close()
+    assert out[0][0] == out[1][0]
+    assert torch.equal(out[0][1], out[1][1])
