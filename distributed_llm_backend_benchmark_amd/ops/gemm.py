@@ -133,6 +133,7 @@ def _blas_linear(x2, w, bias, act, r2, out, preact):
 
 
 CHOICES = {}          # (M, N, K, epi-signature) -> "mfma" | "blas"
+CALLS = {}            # ("linear" | "wgrad", key) -> calls since import (kernel-mix accounting)
 _IMPLS = {"mfma": _mfma_linear, "blas": _blas_linear}
 
 
@@ -207,6 +208,7 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
                preact is not None)
         args = (x2, w, bias, act, r2, o2, preact)
         _IMPLS[_autotune(key, args)](*args)
+        CALLS[("linear", key)] = CALLS.get(("linear", key), 0) + 1
         return out
     y = _torch_linear(x2, w, bias, act, residual, out_dtype, preact)
     return y.reshape(*lead, N) if out is None else out.copy_(y.reshape(out.shape))
@@ -321,9 +323,19 @@ def wgrad(dy2: torch.Tensor, x2: torch.Tensor, out: Optional[torch.Tensor] = Non
             and out.dtype in (torch.bfloat16, torch.float32)):
         choice = "mfma" if split is not None else _wgrad_choice(dy2, x2, out, bias_out)
         _WGRAD_IMPLS[choice](dy2, x2, out, accumulate, split, bias_out)
+        if split is None:
+            k = (dy2.shape[0], dy2.shape[1], x2.shape[1], out.dtype, bias_out is not None)
+            CALLS[("wgrad", k)] = CALLS.get(("wgrad", k), 0) + 1
         return out
     _wgrad_blas(dy2, x2, out, accumulate, None, bias_out)
     return out
+
+
+def dgrad(dy2: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    """``dX = dY @ W`` (NN: the reduction runs along W's rows, which our NT kernels cannot
+    stream without a transposed copy of W) — a plain library GEMM, counted for the kernel mix."""
+    CALLS[("dgrad", "library")] = CALLS.get(("dgrad", "library"), 0) + 1
+    return torch.matmul(dy2, w)
 
 
 def kernel_mix() -> dict:
@@ -331,13 +343,24 @@ def kernel_mix() -> dict:
     kernel choice must be visible next to the throughput it produced). Per kind: shape count by
     choice plus every shape's measured median ms per candidate."""
     out = {}
+    ours = total = 0.0
     for kind, table in (("linear", CHOICES), ("wgrad", WGRAD_CHOICES)):
         counts = {}
         for v in table.values():
             counts[v] = counts.get(v, 0) + 1
-        out[kind] = {"shapes_by_choice": counts,
-                     "tuned": [{"key": [str(k) for k in key], "ms": times, "choice": best}
-                               for knd, key, times, best in TUNE_LOG if knd == kind]}
+        tuned = []
+        for knd, key, times, best in TUNE_LOG:
+            if knd != kind:
+                continue
+            n = CALLS.get((kind, key), 0)
+            tuned.append({"key": [str(k) for k in key], "ms": times, "choice": best, "calls": n})
+            total += n * times[best]
+            ours += n * times[best] if best != "blas" else 0.0
+        out[kind] = {"shapes_by_choice": counts, "tuned": tuned}
+    # share of the autotuned GEMM time (calls x measured ms of the chosen implementation) that
+    # runs on the hand-written kernels; the rest is hipBLASLt
+    out["hand_written_time_fraction"] = round(ours / total, 4) if total else None
+    out["dgrad_library_calls"] = CALLS.get(("dgrad", "library"), 0)   # not in the fraction
     out["forced"] = os.environ.get("DLBB_GEMM", "auto")
     out["contract_fallbacks"] = FALLBACKS["count"]
     return out

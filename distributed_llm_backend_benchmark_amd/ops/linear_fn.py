@@ -24,6 +24,7 @@ import torch
 import torch.nn.functional as F
 
 from . import _lib
+from . import gemm as _gemm
 from ._lib import check, use_hip
 from .gemm import hip_supported, linear as _linear, wgrad
 
@@ -73,7 +74,7 @@ class _LinearFn(torch.autograd.Function):
             du = dy2
             if want_db and not fuse_db:
                 db = du.sum(0, dtype=torch.float32).to(w.dtype)
-        dx = torch.matmul(du, w) if ctx.needs_input_grad[0] else None
+        dx = _gemm.dgrad(du, w) if ctx.needs_input_grad[0] else None
         dw = None
         w_sink = _sink(ctx.weight) if ctx.needs_input_grad[1] else None
         b_sink = _sink(ctx.bias) if fuse_db else None

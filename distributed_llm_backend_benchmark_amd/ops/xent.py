@@ -12,6 +12,7 @@ import torch
 import torch.nn.functional as F
 
 from . import _lib
+from . import gemm as _gemm
 from ._lib import check, use_hip
 
 
@@ -77,7 +78,7 @@ class _LinearXentFn(torch.autograd.Function):
         gb = g.to(dl.dtype)                             # 1.0 in the usual loss.backward()
         dx = dw = None
         if ctx.needs_input_grad[0]:
-            dx = torch.matmul(dl, w).mul_(gb).view(ctx.shape)
+            dx = _gemm.dgrad(dl, w).mul_(gb).view(ctx.shape)
         if ctx.needs_input_grad[1]:
             if _sink(ctx.weight) is not None:
                 # gradient sink (e.g. the tied embedding): accumulate into .grad in the GEMM —

@@ -326,6 +326,14 @@ def test_bench_py_world1():
     assert [e["bytes"] for e in sweep] == [1 << 10, 8 << 10, 64 << 10, 512 << 10, 4 << 20,
                                            32 << 20, 256 << 20, 1 << 30]
     assert all(e["us"] > 0 and e["impl"] in e["us_by_impl"] for e in sweep), sweep
+    # one rank: the timed step is real GPU work (out-of-place copy), never an empty in-place call
+    # (algBW above the HBM peak), and the IPC kernels' emulation rides along
+    assert rec["config"]["impl"] == "native_oop"
+    assert 0 < rec["algbw_GBps"] <= 8000.0, rec["algbw_GBps"]
+    assert all(e["impl"] == "native_oop" and e["algbw_GBps"] <= 8000.0 for e in sweep), sweep
+    emu = rec["virtual_rank_emulation"]
+    for w in ("W2", "W8"):
+        assert all(v["valid"] and v["us"] > 0 for v in emu[w].values()), emu
 
 
 def test_bench_py_two_ranks_rehearsal():
