@@ -166,14 +166,30 @@ __device__ __forceinline__ void split_range(int64_t n, unsigned bid, unsigned nb
 template <int DT, int W>
 __device__ __forceinline__ void oneshot_body(const CarKernelArgs& a, unsigned bid, unsigned nb) {
   constexpr int64_t kVecBytes = 8 * Elem<DT>::kBytes;
-  const uint32_t e = begin_epoch(a, bid, nb);
-  const int64_t half = (e & 1) * a.cap;
+  constexpr int kQ = kVecBytes / 16;
   int64_t v0, v1;
   split_range(a.nbytes / kVecBytes, bid, nb, v0, v1);
-  char* mine = a.data[a.rank] + half;
-  for (int64_t v = v0 + threadIdx.x; v < v1; v += blockDim.x) {
+  // the thread's first input vector is loaded BEFORE the epoch read-modify-write (uncached
+  // signal page), so the two memory round trips overlap instead of running back to back — the
+  // latency floor of a small message (one vector per thread)
+  const int64_t vf = v0 + threadIdx.x;
+  u16x8 first[kQ];
+  if (vf < v1) {
 #pragma unroll
-    for (int q = 0; q < kVecBytes / 16; ++q)
+    for (int q = 0; q < kQ; ++q)
+      first[q] = reinterpret_cast<const u16x8*>(static_cast<const char*>(a.inp) +
+                                                vf * kVecBytes)[q];
+  }
+  const uint32_t e = begin_epoch(a, bid, nb);
+  const int64_t half = (e & 1) * a.cap;
+  char* mine = a.data[a.rank] + half;
+  if (vf < v1) {
+#pragma unroll
+    for (int q = 0; q < kQ; ++q) reinterpret_cast<u16x8*>(mine + vf * kVecBytes)[q] = first[q];
+  }
+  for (int64_t v = vf + blockDim.x; v < v1; v += blockDim.x) {
+#pragma unroll
+    for (int q = 0; q < kQ; ++q)
       reinterpret_cast<u16x8*>(mine + v * kVecBytes)[q] =
           reinterpret_cast<const u16x8*>(static_cast<const char*>(a.inp) + v * kVecBytes)[q];
   }
