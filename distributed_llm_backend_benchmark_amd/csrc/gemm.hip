@@ -649,13 +649,188 @@ __global__ void __launch_bounds__(kThreads2, 1) gemm_bf16_nt_256_persistent(Gemm
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// Row clamping is per 8-row group and wave-uniform (host contract: M % 8 == 0, N % 64 == 0),
+// so each load is buffer_load_dwordx4 ... lds with the tile's operand base in a buffer
+// resource (SGPRs), the group's row + k offset in soffset (SGPR) and one per-lane 32-bit
+// offset (aoff / boff: the lane's row within the group and its swizzled k-chunk) — two VGPRs
+// of addressing for all sixteen loads, nothing 64-bit per load for hipcc to hoist into VGPRs.
+// perm_brow(trow + r) == perm_brow(trow) | perm_brow(r) for trow % 8 == 0 (the bits it swaps
+// are split between the two), and a 64-row block of B is wholly in or out. Every access is in
+// bounds by construction (clamped rows), so the resource carries no range limit.
+__device__ __forceinline__ void bldsx4(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff,
+                                       char* lds_base_wave_uniform) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_ptr_t)(lds_base_wave_uniform), 16, voff, soff,
+                                           0, 0);
+}
+
+// Ping-pong with all 160 KiB of LDS (set_stagger(6)): A double-buffered (2 x 32 KiB), B triple-
+// buffered (3 x 32 KiB), and each A buffer refilled in halves as soon as the wave row that reads
+// that half is done with it. The A rows [0,128) are read only by wave row 0 (intervals 2u) and
+// rows [128,256) only by wave row 1 (intervals 2u+1), so every load gets 3-4 intervals to land
+// instead of 2:
+//   interval 2u   (row 0 reads tile u):  row 0 issues A-hi(u+1) and B(u+2)
+//   interval 2u+1 (row 1 reads tile u):  row 1 issues A-lo(u+2)
+// Waits (counted, oldest first): row 0 ends interval 2u with A-hi(u) retired (row 1 reads it
+// next) and interval 2u+1 with B(u+1) retired; row 1 ends 2u+1 with A-lo(u+1) retired.
+// WAR: A-hi(u+1) replaces A-hi(u-1) (last read by row 1 in 2u-1), B(u+2) replaces B(u-1)
+// (2u-1), A-lo(u+2) replaces A-lo(u) (row 0, 2u) — each behind the barrier that closes the read.
+constexpr int kPP6Lds = 2 * kTile2Bytes + 3 * kTile2Bytes;  // 160 KiB
+
+__device__ __forceinline__ void stage_a_half(__amdgpu_buffer_rsrc_t ra, uint32_t lda2, int rows_a,
+                                             uint32_t k2, char* abuf, int half, int w4,
+                                             uint32_t aoff) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {            // 16 groups of 8 rows, 4 per wave
+    const int trow = half * 128 + (i * 4 + w4) * 8;
+    const int g = trow < rows_a - 8 ? trow : rows_a - 8;
+    bldsx4(ra, aoff, static_cast<uint32_t>(g) * lda2 + k2, abuf + trow * (BK * 2));
+  }
+}
+
+__device__ __forceinline__ void stage_b(__amdgpu_buffer_rsrc_t rb, uint32_t ldb2, int rows_b,
+                                        uint32_t k2, char* bbuf, int w4, uint32_t boff) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int trow = (i * 4 + w4) * 8;
+    const int g = (trow & ~63) < rows_b ? perm_brow(trow) : (perm_brow(trow) & 63);
+    bldsx4(rb, boff, static_cast<uint32_t>(g) * ldb2 + k2, bbuf + trow * (BK * 2));
+  }
+}
+
+__device__ __forceinline__ void read_split(const char* abuf, const char* bbuf, int wr, int wc,
+                                           int fr, int fq, bf16x8 (&af)[2][8],
+                                           bf16x8 (&bf)[2][4]) {
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) af[ks][i] = read_frag(abuf, wr * 128 + i * 16 + fr, ks * 4 + fq);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bf[ks][j] = read_frag(bbuf, wc * 64 + j * 16 + fr, ks * 4 + fq);
+  }
+}
+
+// all 64 MFMAs of one wave's 128 x 64 outputs for one K-tile (k outer, so the two MFMAs into
+// one accumulator are 32 instructions apart)
+__device__ __forceinline__ void mfma_full(f32x4 (&acc)[8][4], const bf16x8 (&af)[2][8],
+                                          const bf16x8 (&bf)[2][4]) {
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[ks][j], af[ks][i], acc[i][j], 0,
+                                                            0, 0);
+}
+
+__global__ void __launch_bounds__(kThreads2, 1) gemm_bf16_nt_256_pingpong3(GemmArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = wave >> 2, wc = wave & 3;
+  const int fr = lane & 15, fq = lane >> 4;
+  const Tile256 tl = tile_of(a, static_cast<int>(blockIdx.x));
+  const int64_t m0 = tl.m0, n0 = tl.n0;
+  const int nk = static_cast<int>(a.K / BK);
+  char* const abuf0 = smem;
+  char* const bbuf0 = smem + 2 * kTile2Bytes;
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 af[2][8], bf[2][4];
+  const int r_in = lane >> 3, chunk = (lane & 7) ^ (lane >> 3);
+  const uint32_t lda2 = static_cast<uint32_t>(a.lda) * 2, ldb2 = static_cast<uint32_t>(a.ldb) * 2;
+  const uint32_t aoff = static_cast<uint32_t>(r_in) * lda2 + chunk * 16;
+  const uint32_t boff = static_cast<uint32_t>(perm_brow(r_in)) * ldb2 + chunk * 16;
+  const int rows_a = static_cast<int>(a.M - m0), rows_b = static_cast<int>(a.N - n0);
+  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint16_t*>(a.A + m0 * a.lda), 0, 0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint16_t*>(a.B + n0 * a.ldb), 0, 0x7fffffff, 0x00020000);
+  constexpr uint32_t kStep = BK * 2;
+
+  if (wr == 0) {
+    // prologue, row 0: A-lo(0), B(0), B(1); retire the first two
+    stage_a_half(ra, lda2, rows_a, 0, abuf0, 0, wc, aoff);
+    stage_b(rb, ldb2, rows_b, 0, bbuf0, wc, boff);
+    if (nk > 1) {
+      stage_b(rb, ldb2, rows_b, kStep, bbuf0 + kTile2Bytes, wc, boff);
+      DLBB_WAIT_VM(8);
+    } else {
+      DLBB_WAIT_VM(0);
+    }
+    __builtin_amdgcn_s_barrier();
+    int cb = 0;                                       // B buffer of tile u
+    for (int u = 0; u < nk; ++u) {
+      const char* ab = abuf0 + (u & 1) * kTile2Bytes;
+      read_split(ab, bbuf0 + cb * kTile2Bytes, 0, wc, fr, fq, af, bf);
+      const bool h1 = u + 1 < nk, b2 = u + 2 < nk;
+      if (h1)
+        stage_a_half(ra, lda2, rows_a, (u + 1) * kStep, abuf0 + ((u + 1) & 1) * kTile2Bytes, 1,
+                     wc, aoff);
+      if (b2) {
+        const int cb2 = cb == 0 ? 2 : cb - 1;         // (u + 2) % 3
+        stage_b(rb, ldb2, rows_b, (u + 2) * kStep, bbuf0 + cb2 * kTile2Bytes, wc, boff);
+      }
+      // retire A-hi(u) (issued two intervals ago; tile 0's came from row 1)
+      if (b2) DLBB_WAIT_VM(20);
+      else if (h1) DLBB_WAIT_VM(12);
+      else DLBB_WAIT_VM(0);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();                   // end of interval 2u
+      __builtin_amdgcn_sched_barrier(0);
+      mfma_full(acc, af, bf);
+      __builtin_amdgcn_sched_barrier(0);
+      if (h1) {                                       // retire B(u+1)
+        if (b2) DLBB_WAIT_VM(12);
+        else DLBB_WAIT_VM(4);
+      }
+      __builtin_amdgcn_s_barrier();                   // end of interval 2u+1
+      cb = cb == 2 ? 0 : cb + 1;
+    }
+  } else {
+    // prologue, row 1: A-hi(0), A-lo(1)
+    stage_a_half(ra, lda2, rows_a, 0, abuf0, 1, wc, aoff);
+    if (nk > 1) stage_a_half(ra, lda2, rows_a, kStep, abuf0 + kTile2Bytes, 0, wc, aoff);
+    __builtin_amdgcn_s_barrier();                     // prologue barrier
+    if (nk > 1) DLBB_WAIT_VM(4); else DLBB_WAIT_VM(0);  // A-hi(0)
+    __builtin_amdgcn_s_barrier();                     // end of interval 0
+    int cb = 0;
+    for (int u = 0; u < nk; ++u) {
+      const char* ab = abuf0 + (u & 1) * kTile2Bytes;
+      read_split(ab, bbuf0 + cb * kTile2Bytes, 1, wc, fr, fq, af, bf);
+      const bool l2 = u + 2 < nk;
+      if (l2) stage_a_half(ra, lda2, rows_a, (u + 2) * kStep, abuf0 + (u & 1) * kTile2Bytes, 0,
+                           wc, aoff);
+      if (u + 1 < nk) {                               // retire A-lo(u+1)
+        if (l2) DLBB_WAIT_VM(4);
+        else DLBB_WAIT_VM(0);
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();                   // end of interval 2u+1
+      __builtin_amdgcn_sched_barrier(0);
+      mfma_full(acc, af, bf);
+      __builtin_amdgcn_sched_barrier(0);
+      if (u + 1 < nk) __builtin_amdgcn_s_barrier();   // end of interval 2u+2
+      cb = cb == 2 ? 0 : cb + 1;
+    }
+  }
+  store_tile_256(a, acc, m0, n0, wave, lane);
+}
+
 }  // namespace dlbb
 
 using namespace dlbb;
 
 static int dlbb_gemm_force_tile = 0;   // 0 = heuristic, 128 or 256 = force (A/B testing)
 
-static int dlbb_gemm_stagger = 3;      // 256^2 schedule (set_stagger): 3 = deep restaging, measured fastest
+static int dlbb_gemm_stagger = 6;      // 256^2 schedule (set_stagger): 6 = ping-pong, 160 KiB LDS, measured fastest
 
 DLBB_API void dlbb_gemm_set_tile(int tile) { dlbb_gemm_force_tile = tile; }
 DLBB_API void dlbb_gemm_set_stagger(int on) { dlbb_gemm_stagger = on; }
@@ -685,7 +860,14 @@ DLBB_API int dlbb_gemm_bf16_nt(const void* A, int64_t lda, const void* B, int64_
   const int force = dlbb_gemm_force_tile;
   if (force == 256 || (force != 128 && tiles256 >= 192)) {
     const dim3 g(static_cast<unsigned>(tiles256)), b(kThreads2);
-    if (dlbb_gemm_stagger == 4) {
+    int mode = dlbb_gemm_stagger;
+    // ping-pong contract: 8-row A groups and 64-row B blocks wholly in or out (uniform clamps),
+    // 32-bit buffer offsets within a 256-row panel
+    if (mode == 6 && !(M % 8 == 0 && N % 64 == 0 && M >= 8 && lda * 2 * 256 + K * 2 < (1LL << 31) &&
+                       ldb * 2 * 256 + K * 2 < (1LL << 31)))
+      mode = 3;
+    if (mode == 5 || mode > 6) mode = 3;
+    if (mode == 4) {
       static int ncu[64] = {0};
       int dev = 0;
       (void)hipGetDevice(&dev);
@@ -700,11 +882,13 @@ DLBB_API int dlbb_gemm_bf16_nt(const void* A, int64_t lda, const void* B, int64_
       const int64_t grid = tiles256 < ncu[dev] ? tiles256 : ncu[dev];
       hipLaunchKernelGGL(gemm_bf16_nt_256_persistent, dim3(static_cast<unsigned>(grid)), b,
                          2 * kBuf2Bytes, stream, a);
-    } else if (dlbb_gemm_stagger == 3)
+    } else if (mode == 6)
+      hipLaunchKernelGGL(gemm_bf16_nt_256_pingpong3, g, b, kPP6Lds, stream, a);
+    else if (mode == 3)
       hipLaunchKernelGGL(gemm_bf16_nt_256_kernel<3>, g, b, 2 * kBuf2Bytes, stream, a);
-    else if (dlbb_gemm_stagger == 2)
+    else if (mode == 2)
       hipLaunchKernelGGL(gemm_bf16_nt_256_kernel<2>, g, b, 2 * kBuf2Bytes, stream, a);
-    else if (dlbb_gemm_stagger == 1)
+    else if (mode == 1)
       hipLaunchKernelGGL(gemm_bf16_nt_256_kernel<1>, g, b, 2 * kBuf2Bytes, stream, a);
     else
       hipLaunchKernelGGL(gemm_bf16_nt_256_kernel<0>, g, b, 2 * kBuf2Bytes, stream, a);

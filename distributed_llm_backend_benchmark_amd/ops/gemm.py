@@ -45,8 +45,10 @@ def set_tile(tile: int) -> None:
 def set_stagger(mode: int) -> None:
     """256^2 kernel schedule: 0 lock-step, 1 staggered wave rows, 2 staggered + next tile
     issued at phase 1, 3 staggered + deep restaging (one K-tile in flight), 4 = 3 as a
-    persistent kernel (next tile's prologue overlaps this tile's epilogue). For A/B
-    benchmarking; the library default is the measured fastest (profiles/)."""
+    persistent kernel (next tile's prologue overlaps this tile's epilogue), 6 ping-pong (the
+    two waves of each SIMD alternate whole-K-tile MFMA clusters and fragment loads, 160 KiB of
+    LDS; M % 8 == 0 and N % 64 == 0, else 3 — the default). For A/B benchmarking; the library
+    default is the measured fastest (profiles/r02_gemm)."""
     _lib.lib().dlbb_gemm_set_stagger(int(mode))
 
 

@@ -90,9 +90,11 @@ def test_chunk_copy_and_scale():
 
 
 @pytest.fixture(params=[("mfma", 0, 1), ("mfma", 128, 1), ("mfma", 256, 1), ("mfma", 256, 0),
-                        ("mfma", 256, 2), ("mfma", 256, 3), ("mfma", 256, 4), ("blas", 0, 1)],
+                        ("mfma", 256, 2), ("mfma", 256, 3), ("mfma", 256, 4), ("mfma", 256, 6),
+                        ("blas", 0, 1)],
                 ids=["mfma_auto", "mfma_t128", "mfma_t256", "mfma_t256_lockstep",
-                     "mfma_t256_early", "mfma_t256_deep", "mfma_t256_persistent", "blas"])
+                     "mfma_t256_early", "mfma_t256_deep", "mfma_t256_persistent",
+                     "mfma_t256_pingpong", "blas"])
 def gemm_tile(request, monkeypatch):
     from distributed_llm_backend_benchmark_amd.ops.gemm import get_stagger, set_stagger, set_tile
 

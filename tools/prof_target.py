@@ -1,5 +1,5 @@
 """Tiny driver for PMC-counter profiling: runs ONE op a few times (no timing logic).
-usage: prof_target.py gemm256|gemm128|blas|reduce8|ln|xent|xentfused|embbwd"""
+usage: prof_target.py gemm256|gemm256s6|gemm128|blas|reduce8|ln|xent|xentfused|embbwd"""
 import os
 import sys
 
@@ -17,8 +17,13 @@ if what.startswith("gemm") or what == "blas":
     x = torch.randn(M, K, device=dev, generator=g).to(torch.bfloat16)
     w = torch.randn(N, K, device=dev, generator=g).to(torch.bfloat16)
     os.environ["DLBB_GEMM"] = "blas" if what == "blas" else "mfma"
-    if what != "blas":
-        set_tile(int(what[4:]))
+    if what != "blas":             # gemm<tile>[s<schedule>], e.g. gemm256s6
+        tile, _, sched = what[4:].partition("s")
+        set_tile(int(tile))
+        if sched:
+            from distributed_llm_backend_benchmark_amd.ops.gemm import set_stagger
+
+            set_stagger(int(sched))
     fn = lambda: ops.linear(x, w)  # noqa: E731
 elif what == "reduce8":
     srcs = [torch.randn(1 << 25, device=dev, generator=g).to(torch.bfloat16) for _ in range(8)]
