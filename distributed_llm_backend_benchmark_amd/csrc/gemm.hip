@@ -290,10 +290,13 @@ __device__ __forceinline__ void deep_mainloop(const GemmArgs& a, f32x4 (&acc)[8]
 // Epilogue of one 256^2 tile (global stores from registers; no LDS, no barriers).
 // Epilogue of one wave's MI*16 x 64 output block at (row0, col0) — global stores from
 // registers (no LDS, no barriers). Requires the swapped-operand MFMA + perm_brow B staging.
-template <int MI>
+// JSWAP (NN kernel, transposed-read B image): lanes with fq odd hold column (j ^ 1)*4 + r in
+// acc[i][j][r] (see read_b_nn), so the 4-column groups are swapped pairwise back into order.
+template <int MI, bool JSWAP = false>
 __device__ __forceinline__ void store_tile(const GemmArgs& a, const f32x4 (&acc)[MI][4],
                                            int64_t row0, int64_t col0, int lane) {
   const int fr = lane & 15, fq = lane >> 4;
+  const bool odd = JSWAP && (fq & 1);
   // epilogue. Lane (fr, fq) holds output row rbase + i*16 + fr, columns cbase .. cbase+15
   // (acc[i][j][r] = column j*4 + r, see perm_brow).
   const int epi = a.epi;
@@ -329,7 +332,8 @@ __device__ __forceinline__ void store_tile(const GemmArgs& a, const f32x4 (&acc)
 #pragma unroll
     for (int j = 0; j < 4; ++j)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) v[j * 4 + r] = acc[i][j][r] + bias[j * 4 + r];
+      for (int r = 0; r < 4; ++r)
+        v[j * 4 + r] = (odd ? acc[i][j ^ 1][r] : acc[i][j][r]) + bias[j * 4 + r];
     const int oc = i * 16 * ldc, orr = i * 16 * ldr;
     if (vec) {
       if (pb) {
@@ -374,9 +378,10 @@ __device__ __forceinline__ void store_tile(const GemmArgs& a, const f32x4 (&acc)
     }
   }
 }
+template <bool JSWAP = false>
 __device__ __forceinline__ void store_tile_256(const GemmArgs& a, const f32x4 (&acc)[8][4],
                                                int64_t m0, int64_t n0, int wave, int lane) {
-  store_tile<8>(a, acc, m0 + (wave >> 2) * 128, n0 + (wave & 3) * 64, lane);
+  store_tile<8, JSWAP>(a, acc, m0 + (wave >> 2) * 128, n0 + (wave & 3) * 64, lane);
 }
 
 // 128 x 128 x 64 tile, 4 waves (2 x 2, 64 x 64 each), two LDS buffers, 2 workgroups per CU:
@@ -724,8 +729,87 @@ __device__ __forceinline__ void mfma_full(f32x4 (&acc)[8][4], const bf16x8 (&af)
                                                             0, 0);
 }
 
-__global__ void __launch_bounds__(kThreads2, 1) gemm_bf16_nt_256_pingpong3(GemmArgs a) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
+// ---------------------------------------------------------------------------------------
+// NN operand B (dgrad: dX[M, N] = dY[M, K] · W[K, N], W stored [K][N] row-major — the reduction
+// runs along W's ROWS). One K-tile of B = 64 k-rows x 256 columns, staged as two [64][128]
+// images (256-B rows, 16 KiB each: image c holds tile columns [128c, 128c + 128)) by the same
+// buffer_load ... lds DMA (one instruction = 4 k-rows x 256 B), and read as MFMA fragments with
+// ds_read_b64_tr_b16 (CDNA guide T10), so no transposed copy of W is ever made.
+// Fragment (ks, j) of wave column wc, lane (fq, fr = 4q + p): k-rows ks*32 + 8 fq + 4h + q,
+// columns (wc & 1)*64 + 16 p + 4 (j ^ (p & 1)) + 0..3 — the perm_brow column order (each lane
+// ends with 16 consecutive output columns), with the 4-column groups of odd p swapped pairwise
+// so the 32 lanes of a half read both 8-B halves of the 16-B slots (JSWAP epilogue undoes it).
+// Image swizzle: 16-B chunk c of k-row r lives in slot c ^ nnf(r), nnf(r) = (r & 3) | ((r >> 3)
+// & 1) << 3: with the half-slot alternation every 32-lane half of a transposed read hits 32
+// distinct (slot, half) bank pairs — conflict-free (the bank of byte a is (a/4) mod 64).
+__device__ __forceinline__ int nnf(int row) { return (row & 3) | (((row >> 3) & 1) << 3); }
+
+// rows [64u, 64u + 64) of the B panel (columns n0 .. n0 + 255): 32 wave-instructions, 8 per
+// wave of the staging wave row (w4 = its wave column). Instruction s = 4i + w4: image s >> 4,
+// row group rg = s & 15; nnf's bit 3 for its rows is (rg >> 1) & 1 = (w4 >> 1) & 1, fixed per
+// wave, so one per-lane offset (boff) serves all eight loads.
+__device__ __forceinline__ void stage_b_nn(__amdgpu_buffer_rsrc_t rb, uint32_t ldb2, int u,
+                                           char* bbuf, int w4, uint32_t boff) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int s = i * 4 + w4, img = s >> 4, rg = s & 15;
+    bldsx4(rb, boff, static_cast<uint32_t>(u * BK + rg * 4) * ldb2 + img * 256,
+           bbuf + img * (kTile2Bytes / 2) + rg * 1024);
+  }
+}
+
+typedef short i16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) i16x4* lds_i16x4_ptr;
+
+__device__ __forceinline__ void read_b_nn(const char* bbuf, int wc, int fr, int fq,
+                                          bf16x8 (&bf)[2][4]) {
+  const int q = fr >> 2, p = fr & 3;
+  const char* img = bbuf + (wc >> 1) * (kTile2Bytes / 2);
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int row = ks * 32 + 8 * fq + 4 * h + q;
+        const int col = (wc & 1) * 64 + 16 * p + 4 * (j ^ (p & 1));
+        const int off = row * 256 + (((col >> 3) ^ nnf(row)) << 4) + (col & 7) * 2;
+        const i16x4 t = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4_ptr)(img + off));
+#pragma unroll
+        for (int e = 0; e < 4; ++e) bf[ks][j][4 * h + e] = t[e];
+      }
+}
+
+template <bool NN>
+__device__ __forceinline__ void stage_b_any(__amdgpu_buffer_rsrc_t rb, uint32_t ldb2, int rows_b,
+                                            int u, char* bbuf, int w4, uint32_t boff) {
+  if constexpr (NN)
+    stage_b_nn(rb, ldb2, u, bbuf, w4, boff);
+  else
+    stage_b(rb, ldb2, rows_b, static_cast<uint32_t>(u) * (BK * 2), bbuf, w4, boff);
+}
+
+template <bool NN>
+__device__ __forceinline__ void read_split_any(const char* abuf, const char* bbuf, int wr, int wc,
+                                               int fr, int fq, bf16x8 (&af)[2][8],
+                                               bf16x8 (&bf)[2][4]) {
+  if constexpr (NN) {
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        af[ks][i] = read_frag(abuf, wr * 128 + i * 16 + fr, ks * 4 + fq);
+    read_b_nn(bbuf, wc, fr, fq, bf);
+  } else {
+    read_split(abuf, bbuf, wr, wc, fr, fq, af, bf);
+  }
+}
+
+// The ping-pong schedule, for B stored [N][K] (NT: forward, C = A · B^T) or [K][N] (NN: dgrad).
+// Both B layouts stage 32 wave-instructions per K-tile from wave row 0, so the counted waits
+// are identical.
+template <bool NN>
+__device__ __forceinline__ void pingpong_body(const GemmArgs& a, char* smem) {
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wr = wave >> 2, wc = wave & 3;
@@ -745,20 +829,27 @@ __global__ void __launch_bounds__(kThreads2, 1) gemm_bf16_nt_256_pingpong3(GemmA
   const int r_in = lane >> 3, chunk = (lane & 7) ^ (lane >> 3);
   const uint32_t lda2 = static_cast<uint32_t>(a.lda) * 2, ldb2 = static_cast<uint32_t>(a.ldb) * 2;
   const uint32_t aoff = static_cast<uint32_t>(r_in) * lda2 + chunk * 16;
-  const uint32_t boff = static_cast<uint32_t>(perm_brow(r_in)) * ldb2 + chunk * 16;
+  uint32_t boff;
+  if constexpr (NN) {
+    const int rq = lane >> 4, slot = lane & 15;
+    boff = static_cast<uint32_t>(rq) * ldb2 +
+           static_cast<uint32_t>(slot ^ rq ^ (((wc >> 1) & 1) << 3)) * 16;
+  } else {
+    boff = static_cast<uint32_t>(perm_brow(r_in)) * ldb2 + chunk * 16;
+  }
   const int rows_a = static_cast<int>(a.M - m0), rows_b = static_cast<int>(a.N - n0);
   const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<uint16_t*>(a.A + m0 * a.lda), 0, 0x7fffffff, 0x00020000);
   const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<uint16_t*>(a.B + n0 * a.ldb), 0, 0x7fffffff, 0x00020000);
+      const_cast<uint16_t*>(NN ? a.B + n0 : a.B + n0 * a.ldb), 0, 0x7fffffff, 0x00020000);
   constexpr uint32_t kStep = BK * 2;
 
   if (wr == 0) {
     // prologue, row 0: A-lo(0), B(0), B(1); retire the first two
     stage_a_half(ra, lda2, rows_a, 0, abuf0, 0, wc, aoff);
-    stage_b(rb, ldb2, rows_b, 0, bbuf0, wc, boff);
+    stage_b_any<NN>(rb, ldb2, rows_b, 0, bbuf0, wc, boff);
     if (nk > 1) {
-      stage_b(rb, ldb2, rows_b, kStep, bbuf0 + kTile2Bytes, wc, boff);
+      stage_b_any<NN>(rb, ldb2, rows_b, 1, bbuf0 + kTile2Bytes, wc, boff);
       DLBB_WAIT_VM(8);
     } else {
       DLBB_WAIT_VM(0);
@@ -767,14 +858,14 @@ __global__ void __launch_bounds__(kThreads2, 1) gemm_bf16_nt_256_pingpong3(GemmA
     int cb = 0;                                       // B buffer of tile u
     for (int u = 0; u < nk; ++u) {
       const char* ab = abuf0 + (u & 1) * kTile2Bytes;
-      read_split(ab, bbuf0 + cb * kTile2Bytes, 0, wc, fr, fq, af, bf);
+      read_split_any<NN>(ab, bbuf0 + cb * kTile2Bytes, 0, wc, fr, fq, af, bf);
       const bool h1 = u + 1 < nk, b2 = u + 2 < nk;
       if (h1)
         stage_a_half(ra, lda2, rows_a, (u + 1) * kStep, abuf0 + ((u + 1) & 1) * kTile2Bytes, 1,
                      wc, aoff);
       if (b2) {
         const int cb2 = cb == 0 ? 2 : cb - 1;         // (u + 2) % 3
-        stage_b(rb, ldb2, rows_b, (u + 2) * kStep, bbuf0 + cb2 * kTile2Bytes, wc, boff);
+        stage_b_any<NN>(rb, ldb2, rows_b, u + 2, bbuf0 + cb2 * kTile2Bytes, wc, boff);
       }
       // retire A-hi(u) (issued two intervals ago; tile 0's came from row 1)
       if (b2) DLBB_WAIT_VM(20);
@@ -803,7 +894,7 @@ __global__ void __launch_bounds__(kThreads2, 1) gemm_bf16_nt_256_pingpong3(GemmA
     int cb = 0;
     for (int u = 0; u < nk; ++u) {
       const char* ab = abuf0 + (u & 1) * kTile2Bytes;
-      read_split(ab, bbuf0 + cb * kTile2Bytes, 1, wc, fr, fq, af, bf);
+      read_split_any<NN>(ab, bbuf0 + cb * kTile2Bytes, 1, wc, fr, fq, af, bf);
       const bool l2 = u + 2 < nk;
       if (l2) stage_a_half(ra, lda2, rows_a, (u + 2) * kStep, abuf0 + (u & 1) * kTile2Bytes, 0,
                            wc, aoff);
@@ -821,7 +912,19 @@ __global__ void __launch_bounds__(kThreads2, 1) gemm_bf16_nt_256_pingpong3(GemmA
       cb = cb == 2 ? 0 : cb + 1;
     }
   }
-  store_tile_256(a, acc, m0, n0, wave, lane);
+  store_tile_256<NN>(a, acc, m0, n0, wave, lane);
+}
+
+__global__ void __launch_bounds__(kThreads2, 1) gemm_bf16_nt_256_pingpong3(GemmArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  pingpong_body<false>(a, smem);
+}
+
+// dgrad: C[M, N] = A[M, K] · B[K, N] (B row-major over the reduction); host contract
+// N % 256 == 0, M % 8 == 0, K % 64 == 0.
+__global__ void __launch_bounds__(kThreads2, 1) gemm_bf16_nn_256_pingpong3(GemmArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  pingpong_body<true>(a, smem);
 }
 
 }  // namespace dlbb
@@ -897,5 +1000,35 @@ DLBB_API int dlbb_gemm_bf16_nt(const void* A, int64_t lda, const void* B, int64_
   const int64_t tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
   hipLaunchKernelGGL(gemm_bf16_nt_kernel, dim3(static_cast<unsigned>(tiles)), dim3(kThreads),
                      4 * kTileBytes, stream, a);
+  return hipGetLastError();
+}
+
+// dgrad GEMM: C[M, N] = epilogue(A[M, K] · B[K, N]), B row-major [K][N] (a Linear weight
+// [out, in] is exactly this for dX = dY · W). Ping-pong 256^2 schedule with transposed-read B.
+DLBB_API int dlbb_gemm_bf16_nn(const void* A, int64_t lda, const void* B, int64_t ldb, void* C,
+                               int64_t ldc, int64_t M, int64_t N, int64_t K, const void* bias,
+                               const void* residual, int64_t ldr, void* preact, int epi,
+                               int out_f32, hipStream_t stream) {
+  if (M <= 0 || N <= 0) return hipSuccess;
+  if (K <= 0 || K % BK != 0 || N % BN2 != 0 || M % 8 != 0) return hipErrorInvalidValue;
+  if (lda % 8 || ldb % 8 || ldb < N || lda < K) return hipErrorInvalidValue;
+  if ((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(B)) & 15)
+    return hipErrorInvalidValue;
+  // 32-bit buffer offsets: a 256-row panel of A, all K rows of B
+  if (lda * 2 * 256 + K * 2 >= (1LL << 31) || K * ldb * 2 >= (1LL << 31))
+    return hipErrorInvalidValue;
+  if ((epi & EPI_BIAS) && !bias) return hipErrorInvalidValue;
+  if ((epi & EPI_RESIDUAL) && !residual) return hipErrorInvalidValue;
+  auto al16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+  const int vec_ok = (ldc % 8 == 0) && al16(C) && (!preact || al16(preact)) &&
+                     (!(epi & EPI_RESIDUAL) || (ldr % 8 == 0 && al16(residual))) &&
+                     (!(epi & EPI_BIAS) || al16(bias));
+  GemmArgs a{static_cast<const uint16_t*>(A), static_cast<const uint16_t*>(B), C,
+             static_cast<const uint16_t*>(bias), static_cast<const uint16_t*>(residual),
+             static_cast<uint16_t*>(preact), M, N, K, lda, ldb, ldc, ldr, epi, out_f32,
+             vec_ok};
+  const int64_t tiles256 = ((M + BM2 - 1) / BM2) * (N / BN2);
+  hipLaunchKernelGGL(gemm_bf16_nn_256_pingpong3, dim3(static_cast<unsigned>(tiles256)),
+                     dim3(kThreads2), kPP6Lds, stream, a);
   return hipGetLastError();
 }

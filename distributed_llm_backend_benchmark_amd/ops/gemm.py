@@ -333,11 +333,88 @@ def wgrad(dy2: torch.Tensor, x2: torch.Tensor, out: Optional[torch.Tensor] = Non
     return out
 
 
-def dgrad(dy2: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
-    """``dX = dY @ W`` (NN: the reduction runs along W's rows, which our NT kernels cannot
-    stream without a transposed copy of W) — a plain library GEMM, counted for the kernel mix."""
+def dgrad_supported(dy2: torch.Tensor, w: torch.Tensor) -> bool:
+    """Contract of the NN kernel (``dlbb_gemm_bf16_nn``): reduction K % 64, output N % 256,
+    M % 8, 16-byte aligned rows, 32-bit buffer offsets over all of W."""
+    M, K = dy2.shape
+    N = w.shape[1]
+    return (dy2.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and w.shape[0] == K
+            and K % 64 == 0 and N % 256 == 0 and M % 8 == 0 and M >= 8
+            and dy2.stride(1) == 1 and w.stride(1) == 1 and dy2.stride(0) % 8 == 0
+            and w.stride(0) % 8 == 0 and dy2.data_ptr() % 16 == 0 and w.data_ptr() % 16 == 0
+            and K * w.stride(0) * 2 < (1 << 31) and dy2.stride(0) * 512 + K * 2 < (1 << 31))
+
+
+def _dgrad_hip(dy2, w, out):
+    M, K = dy2.shape
+    N = w.shape[1]
+    check(_lib.lib().dlbb_gemm_bf16_nn(
+        dy2.data_ptr(), dy2.stride(0), w.data_ptr(), w.stride(0), out.data_ptr(), N, M, N, K,
+        None, None, 0, None, 0, 0, _lib.stream(dy2.device)), "gemm_bf16_nn")
+    return out
+
+
+def _dgrad_blas(dy2, w, out):
+    return torch.matmul(dy2, w, out=out)
+
+
+DGRAD_CHOICES = {}    # (M, N, K, lda) -> "mfma" | "blas"
+_DGRAD_IMPLS = {"mfma": _dgrad_hip, "blas": _dgrad_blas}
+
+
+def _dgrad_choice(dy2, w, out) -> str:
+    mode = os.environ.get("DLBB_GEMM", "auto").lower()
+    if mode in ("mfma", "blas"):
+        return mode
+    key = (dy2.shape[0], w.shape[1], dy2.shape[1], dy2.stride(0))
+    if key in DGRAD_CHOICES:
+        return DGRAD_CHOICES[key]
+    if torch.cuda.is_current_stream_capturing():
+        return "mfma"
+    best, best_t, times = "mfma", float("inf"), {}
+    scratch = torch.empty_like(out)
+    for name, fn in _DGRAD_IMPLS.items():
+        for _ in range(2):
+            fn(dy2, w, scratch)
+        ts = []
+        for _ in range(5):
+            s0, e0 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s0.record()
+            fn(dy2, w, scratch)
+            e0.record()
+            e0.synchronize()
+            ts.append(s0.elapsed_time(e0))
+        t = sorted(ts)[len(ts) // 2]
+        times[name] = round(t, 4)
+        if t < best_t:
+            best, best_t = name, t
+    DGRAD_CHOICES[key] = best
+    _log_tune("dgrad", key, times, best)
+    return best
+
+
+def dgrad(dy2: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Input gradient ``dX = dY @ W`` for ``dy2 [M, K]`` and a Linear weight ``w [K, N]``
+    (``[out_features, in_features]``): an NN GEMM — the reduction runs along W's rows.
+
+    HIP path (``csrc/gemm.hip`` ``gemm_bf16_nn_256_pingpong3``): the forward's ping-pong 256^2
+    schedule with W's [64 k][256 n] tiles staged as-is by LDS-DMA and read as MFMA fragments
+    with ``ds_read_b64_tr_b16`` — no transposed copy of W. Per shape the faster of this kernel
+    and the library GEMM is measured once (:data:`DGRAD_CHOICES`; ``DLBB_GEMM`` forces);
+    shapes outside the contract go to the library and are counted as ``dgrad_library_calls``."""
+    M, K = dy2.shape
+    N = w.shape[1]
+    if use_hip(dy2, w) and dgrad_supported(dy2, w) and (out is None or (
+            out.is_contiguous() and out.dtype == torch.bfloat16)):
+        if out is None:
+            out = torch.empty(M, N, dtype=dy2.dtype, device=dy2.device)
+        choice = _dgrad_choice(dy2, w, out)
+        _DGRAD_IMPLS[choice](dy2, w, out)
+        key = (M, N, K, dy2.stride(0))
+        CALLS[("dgrad", key)] = CALLS.get(("dgrad", key), 0) + 1
+        return out
     CALLS[("dgrad", "library")] = CALLS.get(("dgrad", "library"), 0) + 1
-    return torch.matmul(dy2, w)
+    return torch.matmul(dy2, w) if out is None else torch.matmul(dy2, w, out=out)
 
 
 def kernel_mix() -> dict:
@@ -346,7 +423,7 @@ def kernel_mix() -> dict:
     choice plus every shape's measured median ms per candidate."""
     out = {}
     ours = total = 0.0
-    for kind, table in (("linear", CHOICES), ("wgrad", WGRAD_CHOICES)):
+    for kind, table in (("linear", CHOICES), ("wgrad", WGRAD_CHOICES), ("dgrad", DGRAD_CHOICES)):
         counts = {}
         for v in table.values():
             counts[v] = counts.get(v, 0) + 1

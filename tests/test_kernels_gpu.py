@@ -170,6 +170,54 @@ def test_gemm_strided_A_view():
                                a.float() @ w.float().t(), rtol=2e-3, atol=2e-2)
 
 
+@pytest.mark.parametrize("M,N,K", [(256, 256, 64), (16384, 768, 2304), (520, 512, 192),
+                                   (8, 256, 64), (1000, 3072, 768), (2048, 768, 50304),
+                                   (4096, 4096, 4096)])
+def test_dgrad_nn_matches_fp32(M, N, K):
+    """NN kernel (transposed-read W): dX = dY @ W against an fp32 reference; ragged M, one
+    K-tile, LM-head-sized reduction."""
+    from distributed_llm_backend_benchmark_amd.ops import gemm
+
+    dy = _randn(M, K, seed=21, scale=0.5)
+    w = _randn(K, N, seed=22, scale=0.5)
+    assert gemm.dgrad_supported(dy, w)
+    out = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+    gemm._dgrad_hip(dy, w, out)
+    ref = dy.float() @ w.float()
+    torch.testing.assert_close(out.float(), ref, rtol=2e-2, atol=2e-2 * (K ** 0.5))
+
+
+def test_dgrad_nn_asymmetric_identity_and_strided():
+    """A = I with an asymmetric W catches any column permutation (the JSWAP epilogue) or a
+    transposed write; a strided dY view (lda > K) checks the A panel addressing."""
+    from distributed_llm_backend_benchmark_amd.ops import gemm
+
+    n = 512
+    eye = torch.eye(n, device=DEV, dtype=torch.bfloat16)
+    w = (torch.arange(n * n, device=DEV, dtype=torch.float32).view(n, n) % 61).to(torch.bfloat16)
+    out = torch.empty(n, n, dtype=torch.bfloat16, device=DEV)
+    gemm._dgrad_hip(eye, w, out)
+    torch.testing.assert_close(out.float(), w.float(), rtol=0, atol=0)
+    big = _randn(768, 3 * 256, seed=23, scale=0.5)
+    dy = big[:, :256]
+    w2 = _randn(256, 1024, seed=24, scale=0.5)
+    out2 = torch.empty(768, 1024, dtype=torch.bfloat16, device=DEV)
+    gemm._dgrad_hip(dy, w2, out2)
+    torch.testing.assert_close(out2.float(), dy.float() @ w2.float(), rtol=2e-2, atol=2e-2 * 16)
+
+
+def test_dgrad_dispatch_counts_hand_written():
+    from distributed_llm_backend_benchmark_amd.ops import gemm
+
+    dy = _randn(4096, 1024, seed=25, scale=0.5)
+    w = _randn(1024, 768, seed=26, scale=0.5)
+    y = gemm.dgrad(dy, w)
+    torch.testing.assert_close(y.float(), dy.float() @ w.float(), rtol=2e-2, atol=2e-2 * 32)
+    assert (4096, 768, 1024, 1024) in gemm.DGRAD_CHOICES
+    mix = gemm.kernel_mix()
+    assert "dgrad" in mix and mix["dgrad"]["tuned"]
+
+
 @pytest.mark.parametrize("cols", [256, 768, 2048, 4096, 5120, 8192, 100])
 @pytest.mark.parametrize("with_res", [False, True])
 def test_layernorm_fwd(cols, with_res):
