@@ -49,6 +49,8 @@ struct GemmArgs {
   int epi;
   int out_f32;
   int vec_ok;              // 16-B aligned C / residual / preact / bias rows (vector epilogue)
+  int kt_split;            // NN split-K (gridDim.y > 1): K-tiles per split; split s writes fp32
+                           // partials to C + s * M * ldc
 };
 
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
@@ -809,7 +811,15 @@ __device__ __forceinline__ void read_split_any(const char* abuf, const char* bbu
 // Both B layouts stage 32 wave-instructions per K-tile from wave row 0, so the counted waits
 // are identical.
 template <bool NN>
-__device__ __forceinline__ void pingpong_body(const GemmArgs& a, char* smem) {
+__device__ __forceinline__ void pingpong_body(GemmArgs a, char* smem) {
+  if (NN && gridDim.y > 1) {         // split-K slice blockIdx.y (wave-uniform, SGPR math)
+    const int s = blockIdx.y, nkt = static_cast<int>(a.K / BK);
+    const int kt0 = s * a.kt_split, kt1 = kt0 + a.kt_split < nkt ? kt0 + a.kt_split : nkt;
+    a.A += static_cast<int64_t>(kt0) * BK;
+    a.B += static_cast<int64_t>(kt0) * BK * a.ldb;
+    a.K = static_cast<int64_t>(kt1 - kt0) * BK;
+    a.C = static_cast<float*>(a.C) + static_cast<int64_t>(s) * a.M * a.ldc;
+  }
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wr = wave >> 2, wc = wave & 3;
@@ -957,7 +967,7 @@ DLBB_API int dlbb_gemm_bf16_nt(const void* A, int64_t lda, const void* B, int64_
   GemmArgs a{static_cast<const uint16_t*>(A), static_cast<const uint16_t*>(B), C,
              static_cast<const uint16_t*>(bias), static_cast<const uint16_t*>(residual),
              static_cast<uint16_t*>(preact), M, N, K, lda, ldb, ldc, ldr, epi, out_f32,
-             vec_ok};
+             vec_ok, 0};
   const int64_t tiles256 = ((M + BM2 - 1) / BM2) * ((N + BN2 - 1) / BN2);
   // the 256^2 schedule needs >= ~1 workgroup per CU to fill the chip; otherwise 128^2 tiles
   const int force = dlbb_gemm_force_tile;
@@ -1003,12 +1013,16 @@ DLBB_API int dlbb_gemm_bf16_nt(const void* A, int64_t lda, const void* B, int64_
   return hipGetLastError();
 }
 
+// split-K partial reduce + cast (csrc/gemm_tn.hip): out[i] = sum_s ws[s * n + i]
+int dlbb_split_reduce_launch(const float* ws, void* out, int dt_f32, int64_t n, int split,
+                             hipStream_t stream);
+
 // dgrad GEMM: C[M, N] = epilogue(A[M, K] · B[K, N]), B row-major [K][N] (a Linear weight
 // [out, in] is exactly this for dX = dY · W). Ping-pong 256^2 schedule with transposed-read B.
 DLBB_API int dlbb_gemm_bf16_nn(const void* A, int64_t lda, const void* B, int64_t ldb, void* C,
                                int64_t ldc, int64_t M, int64_t N, int64_t K, const void* bias,
                                const void* residual, int64_t ldr, void* preact, int epi,
-                               int out_f32, hipStream_t stream) {
+                               int out_f32, int split, float* ws, hipStream_t stream) {
   if (M <= 0 || N <= 0) return hipSuccess;
   if (K <= 0 || K % BK != 0 || N % BN2 != 0 || M % 8 != 0) return hipErrorInvalidValue;
   if (lda % 8 || ldb % 8 || ldb < N || lda < K) return hipErrorInvalidValue;
@@ -1026,8 +1040,23 @@ DLBB_API int dlbb_gemm_bf16_nn(const void* A, int64_t lda, const void* B, int64_
   GemmArgs a{static_cast<const uint16_t*>(A), static_cast<const uint16_t*>(B), C,
              static_cast<const uint16_t*>(bias), static_cast<const uint16_t*>(residual),
              static_cast<uint16_t*>(preact), M, N, K, lda, ldb, ldc, ldr, epi, out_f32,
-             vec_ok};
+             vec_ok, 0};
   const int64_t tiles256 = ((M + BM2 - 1) / BM2) * (N / BN2);
+  const int nkt = static_cast<int>(K / BK);
+  if (split > 1) {
+    // split-K for grids below one workgroup per CU (the LM-head dX: 192 tiles, 786 K-tiles):
+    // fp32 partials [split][M][N] in ws, then one reduce + bf16 cast pass. Plain product only.
+    if (!ws || epi != 0 || out_f32 || ldc != N || split > nkt) return hipErrorInvalidValue;
+    a.kt_split = (nkt + split - 1) / split;
+    a.C = ws;
+    a.out_f32 = 1;
+    a.vec_ok = (reinterpret_cast<uintptr_t>(ws) & 15) == 0 && N % 8 == 0;
+    hipLaunchKernelGGL(gemm_bf16_nn_256_pingpong3, dim3(static_cast<unsigned>(tiles256), split),
+                       dim3(kThreads2), kPP6Lds, stream, a);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    return dlbb_split_reduce_launch(ws, C, 0, M * N, split, stream);
+  }
   hipLaunchKernelGGL(gemm_bf16_nn_256_pingpong3, dim3(static_cast<unsigned>(tiles256)),
                      dim3(kThreads2), kPP6Lds, stream, a);
   return hipGetLastError();

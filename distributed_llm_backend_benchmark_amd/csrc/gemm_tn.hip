@@ -292,6 +292,21 @@ DLBB_API int dlbb_gemm_wgrad_tile(const void* A, int64_t lda, const void* B, int
   return hipGetLastError();
 }
 
+// out (bf16, or fp32 when dt_f32) = sum over `split` fp32 slices of n elements (n % 8 == 0);
+// used by the NN dgrad's split-K (csrc/gemm.hip).
+int dlbb_split_reduce_launch(const float* ws, void* out, int dt_f32, int64_t n, int split,
+                             hipStream_t stream) {
+  if (n % 8 != 0) return hipErrorInvalidValue;
+  const int g = stream_grid(n / 8, 256);
+  if (dt_f32)
+    hipLaunchKernelGGL(tn::split_reduce_kernel<DT_F32>, dim3(g), dim3(256), 0, stream, ws, out,
+                       n, nullptr, int64_t{0}, split, 0);
+  else
+    hipLaunchKernelGGL(tn::split_reduce_kernel<DT_BF16>, dim3(g), dim3(256), 0, stream, ws, out,
+                       n, nullptr, int64_t{0}, split, 0);
+  return hipGetLastError();
+}
+
 DLBB_API int dlbb_gemm_wgrad(const void* A, int64_t lda, const void* B, int64_t ldb, void* out,
                              int dt_out, int accumulate, float* ws, int M, int N, int K,
                              int split, void* out_bias, hipStream_t stream) {

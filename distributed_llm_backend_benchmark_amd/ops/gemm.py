@@ -345,12 +345,29 @@ def dgrad_supported(dy2: torch.Tensor, w: torch.Tensor) -> bool:
             and K * w.stride(0) * 2 < (1 << 31) and dy2.stride(0) * 512 + K * 2 < (1 << 31))
 
 
-def _dgrad_hip(dy2, w, out):
+def dgrad_split(M: int, N: int, K: int) -> int:
+    """Split-K factor of the NN kernel: 1 unless the 256^2 grid is below one workgroup per CU
+    and K is long (the LM-head dX: 192 tiles x 786 K-tiles), then the smallest split that
+    fills whole rounds of the 256 CUs with >= 16 K-tiles per slice."""
+    tiles = -(-M // 256) * (N // 256)
+    if tiles >= 256 or K < 64 * 64:
+        return 1
+    for s in range(2, 9):
+        if (tiles * s) % 256 == 0 and K // 64 >= 16 * s:
+            return s
+    return 1
+
+
+def _dgrad_hip(dy2, w, out, split=None):
     M, K = dy2.shape
     N = w.shape[1]
+    if split is None:
+        split = dgrad_split(M, N, K)
+    ws = torch.empty(split * M * N, dtype=torch.float32, device=dy2.device) if split > 1 else None
     check(_lib.lib().dlbb_gemm_bf16_nn(
         dy2.data_ptr(), dy2.stride(0), w.data_ptr(), w.stride(0), out.data_ptr(), N, M, N, K,
-        None, None, 0, None, 0, 0, _lib.stream(dy2.device)), "gemm_bf16_nn")
+        None, None, 0, None, 0, 0, int(split), _lib.ptr(ws), _lib.stream(dy2.device)),
+        "gemm_bf16_nn")
     return out
 
 

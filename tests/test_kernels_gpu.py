@@ -187,6 +187,21 @@ def test_dgrad_nn_matches_fp32(M, N, K):
     torch.testing.assert_close(out.float(), ref, rtol=2e-2, atol=2e-2 * (K ** 0.5))
 
 
+@pytest.mark.parametrize("M,N,K,split", [(2048, 768, 50304, 4), (520, 512, 64 * 7, 3),
+                                         (1024, 256, 4096, 2)])
+def test_dgrad_nn_split_k(M, N, K, split):
+    """Split-K NN (uneven last slice for 786 / 4 and 7 / 3 K-tiles): fp32 partials + reduce."""
+    from distributed_llm_backend_benchmark_amd.ops import gemm
+
+    dy = _randn(M, K, seed=27, scale=0.5)
+    w = _randn(K, N, seed=28, scale=0.5)
+    out = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+    gemm._dgrad_hip(dy, w, out, split=split)
+    ref = dy.float() @ w.float()
+    torch.testing.assert_close(out.float(), ref, rtol=2e-2, atol=2e-2 * (K ** 0.5))
+    assert gemm.dgrad_split(16384, 768, 50304) == 4 and gemm.dgrad_split(16384, 768, 3072) == 1
+
+
 def test_dgrad_nn_asymmetric_identity_and_strided():
     """A = I with an asymmetric W catches any column permutation (the JSWAP epilogue) or a
     transposed write; a strided dY view (lda > K) checks the A panel addressing."""
