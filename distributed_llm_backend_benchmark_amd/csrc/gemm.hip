@@ -35,7 +35,18 @@ enum Epi : int {
   EPI_GELU_ERF = 2,
   EPI_GELU_TANH = 4,
   EPI_RESIDUAL = 8,
+  // dgrad through a GELU: C = (A · B) * gelu'(u), u = the forward pre-activation [M, N] passed
+  // in `residual` / ldr (the GELU backward fused into the producing GEMM's epilogue)
+  EPI_DGELU_ERF = 16,
+  EPI_DGELU_TANH = 32,
 };
+constexpr int EPI_READS_R = EPI_RESIDUAL | EPI_DGELU_ERF | EPI_DGELU_TANH;
+
+__device__ __forceinline__ float apply_r(float v, float r, int epi) {
+  if (epi & EPI_DGELU_TANH) return v * gelu_tanh_grad(r);
+  if (epi & EPI_DGELU_ERF) return v * gelu_erf_grad(r);
+  return v + r;
+}
 
 struct GemmArgs {
   const uint16_t* A;
@@ -326,7 +337,7 @@ __device__ __forceinline__ void store_tile(const GemmArgs& a, const f32x4 (&acc)
   float* cf = static_cast<float*>(a.C) + rbase * a.ldc + cbase;
   uint16_t* cb = static_cast<uint16_t*>(a.C) + rbase * a.ldc + cbase;
   uint16_t* pb = a.preact ? a.preact + rbase * a.ldc + cbase : nullptr;
-  const uint16_t* rb = (epi & EPI_RESIDUAL) ? a.residual + rbase * a.ldr + cbase : nullptr;
+  const uint16_t* rb = (epi & EPI_READS_R) ? a.residual + rbase * a.ldr + cbase : nullptr;
 #pragma unroll
   for (int i = 0; i < MI; ++i) {
     if (i * 16 >= rows_left) break;
@@ -353,7 +364,10 @@ __device__ __forceinline__ void store_tile(const GemmArgs& a, const f32x4 (&acc)
         const u16x8 r0 = reinterpret_cast<const u16x8*>(rb + orr)[0];
         const u16x8 r1 = reinterpret_cast<const u16x8*>(rb + orr)[1];
 #pragma unroll
-        for (int c = 0; c < 8; ++c) { v[c] += bf16_to_f32(r0[c]); v[8 + c] += bf16_to_f32(r1[c]); }
+        for (int c = 0; c < 8; ++c) {
+          v[c] = apply_r(v[c], bf16_to_f32(r0[c]), epi);
+          v[8 + c] = apply_r(v[8 + c], bf16_to_f32(r1[c]), epi);
+        }
       }
       if (a.out_f32) {
         float4* o = reinterpret_cast<float4*>(cf + oc);
@@ -374,7 +388,7 @@ __device__ __forceinline__ void store_tile(const GemmArgs& a, const f32x4 (&acc)
         float x = v[c];
         if (pb) pb[oc + c] = f32_to_bf16(x);
         x = apply_act(x, epi);
-        if (rb) x += bf16_to_f32(rb[orr + c]);
+        if (rb) x = apply_r(x, bf16_to_f32(rb[orr + c]), epi);
         if (a.out_f32) cf[oc + c] = x; else cb[oc + c] = f32_to_bf16(x);
       }
     }
@@ -959,10 +973,10 @@ DLBB_API int dlbb_gemm_bf16_nt(const void* A, int64_t lda, const void* B, int64_
   if ((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(B)) & 15)
     return hipErrorInvalidValue;
   if ((epi & EPI_BIAS) && !bias) return hipErrorInvalidValue;
-  if ((epi & EPI_RESIDUAL) && !residual) return hipErrorInvalidValue;
+  if ((epi & EPI_READS_R) && !residual) return hipErrorInvalidValue;
   auto al16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
   const int vec_ok = (ldc % 8 == 0) && al16(C) && (!preact || al16(preact)) &&
-                     (!(epi & EPI_RESIDUAL) || (ldr % 8 == 0 && al16(residual))) &&
+                     (!(epi & EPI_READS_R) || (ldr % 8 == 0 && al16(residual))) &&
                      (!(epi & EPI_BIAS) || al16(bias));
   GemmArgs a{static_cast<const uint16_t*>(A), static_cast<const uint16_t*>(B), C,
              static_cast<const uint16_t*>(bias), static_cast<const uint16_t*>(residual),
@@ -1032,10 +1046,10 @@ DLBB_API int dlbb_gemm_bf16_nn(const void* A, int64_t lda, const void* B, int64_
   if (lda * 2 * 256 + K * 2 >= (1LL << 31) || K * ldb * 2 >= (1LL << 31))
     return hipErrorInvalidValue;
   if ((epi & EPI_BIAS) && !bias) return hipErrorInvalidValue;
-  if ((epi & EPI_RESIDUAL) && !residual) return hipErrorInvalidValue;
+  if ((epi & EPI_READS_R) && !residual) return hipErrorInvalidValue;
   auto al16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
   const int vec_ok = (ldc % 8 == 0) && al16(C) && (!preact || al16(preact)) &&
-                     (!(epi & EPI_RESIDUAL) || (ldr % 8 == 0 && al16(residual))) &&
+                     (!(epi & EPI_READS_R) || (ldr % 8 == 0 && al16(residual))) &&
                      (!(epi & EPI_BIAS) || al16(bias));
   GemmArgs a{static_cast<const uint16_t*>(A), static_cast<const uint16_t*>(B), C,
              static_cast<const uint16_t*>(bias), static_cast<const uint16_t*>(residual),

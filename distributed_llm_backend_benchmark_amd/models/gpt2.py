@@ -27,7 +27,7 @@ import torch
 import torch.nn as nn
 
 from .. import ops
-from ..ops.linear_fn import linear_train
+from ..ops.linear_fn import linear_train, mlp_train
 
 
 @dataclass
@@ -86,8 +86,9 @@ class Block(nn.Module):
         att = ops.causal_attention(qkv, self.n_head)
         a = linear_train(att, self.attn_proj_w, self.attn_proj_b)
         y2, h = self.ln_2(a, residual=h)
-        g = linear_train(y2, self.fc_w, self.fc_b, act="gelu_tanh")
-        d = linear_train(g, self.mlp_proj_w, self.mlp_proj_b)
+        # fc -> GELU -> proj as one op: the GELU backward rides in the proj dgrad's epilogue
+        d = mlp_train(y2, self.fc_w, self.fc_b, self.mlp_proj_w, self.mlp_proj_b,
+                      act="gelu_tanh")
         return d, h
 
 

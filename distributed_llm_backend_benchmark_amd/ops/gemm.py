@@ -22,6 +22,7 @@ from . import _lib
 from ._lib import check, use_hip
 
 EPI_BIAS, EPI_GELU_ERF, EPI_GELU_TANH, EPI_RESIDUAL = 1, 2, 4, 8
+EPI_DGELU = {"gelu": 16, "gelu_erf": 16, "gelu_tanh": 32}   # dgrad epilogue: * act'(u)
 ACTS = {None: 0, "none": 0, "gelu": EPI_GELU_ERF, "gelu_erf": EPI_GELU_ERF,
         "gelu_tanh": EPI_GELU_TANH}
 
@@ -358,32 +359,48 @@ def dgrad_split(M: int, N: int, K: int) -> int:
     return 1
 
 
-def _dgrad_hip(dy2, w, out, split=None):
+def _dgrad_hip(dy2, w, out, split=None, dgelu=None):
     M, K = dy2.shape
     N = w.shape[1]
+    epi, u = 0, None
+    if dgelu is not None:
+        u, act = dgelu
+        epi = EPI_DGELU[act]
+        split = 1
     if split is None:
         split = dgrad_split(M, N, K)
     ws = torch.empty(split * M * N, dtype=torch.float32, device=dy2.device) if split > 1 else None
     check(_lib.lib().dlbb_gemm_bf16_nn(
         dy2.data_ptr(), dy2.stride(0), w.data_ptr(), w.stride(0), out.data_ptr(), N, M, N, K,
-        None, None, 0, None, 0, 0, int(split), _lib.ptr(ws), _lib.stream(dy2.device)),
-        "gemm_bf16_nn")
+        None, _lib.ptr(u), u.stride(0) if u is not None else 0, None, epi, 0, int(split),
+        _lib.ptr(ws), _lib.stream(dy2.device)), "gemm_bf16_nn")
     return out
 
 
-def _dgrad_blas(dy2, w, out):
-    return torch.matmul(dy2, w, out=out)
+_GELU_APPROX = {"gelu": 0, "gelu_erf": 0, "gelu_tanh": 1}
+
+
+def _dgrad_blas(dy2, w, out, split=None, dgelu=None):
+    if dgelu is None:
+        return torch.matmul(dy2, w, out=out)
+    u, act = dgelu
+    dg = torch.matmul(dy2, w)
+    check(_lib.lib().dlbb_bias_gelu_bwd(dg.data_ptr(), u.data_ptr(), None, out.data_ptr(), None,
+                                        out.shape[0], out.shape[1], _GELU_APPROX[act],
+                                        _lib.stream(dy2.device)), "bias_gelu_bwd")
+    return out
 
 
 DGRAD_CHOICES = {}    # (M, N, K, lda) -> "mfma" | "blas"
 _DGRAD_IMPLS = {"mfma": _dgrad_hip, "blas": _dgrad_blas}
 
 
-def _dgrad_choice(dy2, w, out) -> str:
+def _dgrad_choice(dy2, w, out, dgelu=None) -> str:
     mode = os.environ.get("DLBB_GEMM", "auto").lower()
     if mode in ("mfma", "blas"):
         return mode
-    key = (dy2.shape[0], w.shape[1], dy2.shape[1], dy2.stride(0))
+    key = (dy2.shape[0], w.shape[1], dy2.shape[1], dy2.stride(0),
+           dgelu[1] if dgelu is not None else None)
     if key in DGRAD_CHOICES:
         return DGRAD_CHOICES[key]
     if torch.cuda.is_current_stream_capturing():
@@ -392,12 +409,12 @@ def _dgrad_choice(dy2, w, out) -> str:
     scratch = torch.empty_like(out)
     for name, fn in _DGRAD_IMPLS.items():
         for _ in range(2):
-            fn(dy2, w, scratch)
+            fn(dy2, w, scratch, dgelu=dgelu)
         ts = []
         for _ in range(5):
             s0, e0 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             s0.record()
-            fn(dy2, w, scratch)
+            fn(dy2, w, scratch, dgelu=dgelu)
             e0.record()
             e0.synchronize()
             ts.append(s0.elapsed_time(e0))
@@ -410,7 +427,8 @@ def _dgrad_choice(dy2, w, out) -> str:
     return best
 
 
-def dgrad(dy2: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+def dgrad(dy2: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None,
+          dgelu=None) -> torch.Tensor:
     """Input gradient ``dX = dY @ W`` for ``dy2 [M, K]`` and a Linear weight ``w [K, N]``
     (``[out_features, in_features]``): an NN GEMM — the reduction runs along W's rows.
 
@@ -418,19 +436,39 @@ def dgrad(dy2: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None
     schedule with W's [64 k][256 n] tiles staged as-is by LDS-DMA and read as MFMA fragments
     with ``ds_read_b64_tr_b16`` — no transposed copy of W. Per shape the faster of this kernel
     and the library GEMM is measured once (:data:`DGRAD_CHOICES`; ``DLBB_GEMM`` forces);
-    shapes outside the contract go to the library and are counted as ``dgrad_library_calls``."""
+    shapes outside the contract go to the library and are counted as ``dgrad_library_calls``.
+
+    ``dgelu=(u, act)``: the input of this GEMM was ``act(u)`` (GELU), and the result is the
+    gradient w.r.t. ``u``: ``(dY @ W) * act'(u)`` — the GELU backward fused into the epilogue
+    (``u`` [M, N] bf16, the forward's stored pre-activation)."""
     M, K = dy2.shape
     N = w.shape[1]
-    if use_hip(dy2, w) and dgrad_supported(dy2, w) and (out is None or (
+    u_ok = dgelu is None or (dgelu[0].dtype == torch.bfloat16 and dgelu[0].stride(1) == 1
+                             and dgelu[0].stride(0) % 8 == 0 and dgelu[0].data_ptr() % 16 == 0
+                             and tuple(dgelu[0].shape) == (M, N))
+    if use_hip(dy2, w) and dgrad_supported(dy2, w) and u_ok and (out is None or (
             out.is_contiguous() and out.dtype == torch.bfloat16)):
         if out is None:
             out = torch.empty(M, N, dtype=dy2.dtype, device=dy2.device)
-        choice = _dgrad_choice(dy2, w, out)
-        _DGRAD_IMPLS[choice](dy2, w, out)
-        key = (M, N, K, dy2.stride(0))
+        choice = _dgrad_choice(dy2, w, out, dgelu)
+        _DGRAD_IMPLS[choice](dy2, w, out, dgelu=dgelu)
+        key = (M, N, K, dy2.stride(0), dgelu[1] if dgelu is not None else None)
         CALLS[("dgrad", key)] = CALLS.get(("dgrad", key), 0) + 1
         return out
     CALLS[("dgrad", "library")] = CALLS.get(("dgrad", "library"), 0) + 1
+    if dgelu is not None:
+        u, act = dgelu
+        dg = torch.matmul(dy2.float(), w.float())
+        uf = u.float()
+        if act == "gelu_tanh":
+            k0, k1 = 0.7978845608028654, 0.044715
+            t = torch.tanh(k0 * (uf + k1 * uf ** 3))
+            gp = 0.5 * (1 + t) + 0.5 * uf * (1 - t * t) * k0 * (1 + 3 * k1 * uf * uf)
+        else:
+            gp = 0.5 * (1 + torch.erf(uf * 0.7071067811865476)) + \
+                uf * 0.3989422804014327 * torch.exp(-0.5 * uf * uf)
+        r = (dg * gp).to(dy2.dtype)
+        return r if out is None else out.copy_(r)
     return torch.matmul(dy2, w) if out is None else torch.matmul(dy2, w, out=out)
 
 

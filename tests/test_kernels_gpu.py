@@ -228,7 +228,7 @@ def test_dgrad_dispatch_counts_hand_written():
     w = _randn(1024, 768, seed=26, scale=0.5)
     y = gemm.dgrad(dy, w)
     torch.testing.assert_close(y.float(), dy.float() @ w.float(), rtol=2e-2, atol=2e-2 * 32)
-    assert (4096, 768, 1024, 1024) in gemm.DGRAD_CHOICES
+    assert (4096, 768, 1024, 1024, None) in gemm.DGRAD_CHOICES
     mix = gemm.kernel_mix()
     assert "dgrad" in mix and mix["dgrad"]["tuned"]
 
@@ -323,6 +323,57 @@ def test_linear_train_grads(act):
     torch.testing.assert_close(x.grad.float(), xf.grad, rtol=3e-2, atol=0.2)
     torch.testing.assert_close(w.grad.float(), wf.grad, rtol=3e-2, atol=0.5)
     torch.testing.assert_close(b.grad.float(), bf.grad, rtol=3e-2, atol=0.5)
+
+
+@pytest.mark.parametrize("act", ["gelu_tanh", "gelu"])
+@pytest.mark.parametrize("impl", ["mfma", "blas"])
+def test_dgrad_fused_gelu_backward(act, impl, monkeypatch):
+    """dgrad epilogue (dY @ W) * act'(u) vs fp32, through both dispatch paths."""
+    from distributed_llm_backend_benchmark_amd.ops import gemm
+
+    monkeypatch.setenv("DLBB_GEMM", impl)
+    M, N, K = 1024, 3072, 768
+    dy = _randn(M, K, seed=31, scale=0.5)
+    w = _randn(K, N, seed=32, scale=0.05)
+    u = _randn(M, N, seed=33, scale=2.0)
+    out = gemm.dgrad(dy, w, dgelu=(u, act))
+    uf = u.float().requires_grad_(True)
+    g = F.gelu(uf, approximate="tanh" if act == "gelu_tanh" else "none")
+    g.backward(dy.float() @ w.float())
+    torch.testing.assert_close(out.float(), uf.grad, rtol=2e-2, atol=3e-2)
+
+
+@pytest.mark.parametrize("sinks", [False, True])
+def test_mlp_train_grads(sinks):
+    """Fused MLP op (GELU backward in the dgrad epilogue) vs an fp32 autograd reference; with
+    gradient sinks the weight gradients land in the parameters' .grad buffers in-kernel."""
+    from distributed_llm_backend_benchmark_amd.ops.linear_fn import mlp_train
+
+    M, C, H = 512, 256, 1024
+    x = _randn(M, C, seed=34, scale=0.5).requires_grad_(True)
+    w1 = _randn(H, C, seed=35, scale=0.05).requires_grad_(True)
+    b1 = _randn(H, seed=36, scale=0.1).requires_grad_(True)
+    w2 = _randn(C, H, seed=37, scale=0.05).requires_grad_(True)
+    b2 = _randn(C, seed=38, scale=0.1).requires_grad_(True)
+    params = (w1, b1, w2, b2)
+    fired = []
+    if sinks:
+        for p in params:
+            p.grad = torch.zeros_like(p)
+            p._dlbb_grad_fresh = True
+            p._dlbb_grad_sink = fired.append
+    dy = _randn(M, C, seed=39)
+    y = mlp_train(x, w1, b1, w2, b2, act="gelu_tanh")
+    (y.float() * dy.float()).sum().backward()
+    xf, w1f, b1f, w2f, b2f = (t.detach().float().requires_grad_(True) for t in (x, *params))
+    yf = F.gelu(xf @ w1f.t() + b1f, approximate="tanh") @ w2f.t() + b2f
+    (yf * dy.float()).sum().backward()
+    torch.testing.assert_close(y.float(), yf, rtol=2e-2, atol=5e-2)
+    torch.testing.assert_close(x.grad.float(), xf.grad, rtol=3e-2, atol=0.1)
+    for p, pf in zip(params, (w1f, b1f, w2f, b2f)):
+        torch.testing.assert_close(p.grad.float(), pf.grad, rtol=3e-2, atol=0.3)
+    if sinks:
+        assert len(fired) == 4
 
 
 @pytest.mark.parametrize("gdt", [torch.bfloat16, torch.float32])
