@@ -45,7 +45,9 @@ namespace dlbb {
 constexpr int kMaxRanks = 8;
 constexpr int kMaxBlocks = 256;
 constexpr int kCarThreads = 512;
-constexpr unsigned kSpinLimit = 1u << 26;   // ~ seconds of polling, then give up
+// Every wait is bounded in WALL time (s_memrealtime, the 100 MHz constant clock), not in polls:
+// a poll of a peer's flag over xGMI costs ~1 us, so a poll count would stretch to a minute.
+constexpr uint64_t kRealtimeHz = 100000000ull;
 constexpr uint32_t kMagic = 0xD1BB0000u;
 
 struct Signal {
@@ -65,6 +67,7 @@ struct CarKernelArgs {
   int64_t cap;                  // capacity per buffer half
   int rank;
   int world;
+  uint64_t timeout_ticks;       // wait bound, s_memrealtime ticks (dlbb_car_set_timeout_ms)
 };
 
 // Every kernel body takes its workgroup index `bid` and workgroup count `nb` explicitly instead of
@@ -93,15 +96,22 @@ __device__ __forceinline__ bool wait_peers(const CarKernelArgs& a, int phase, ui
   __syncthreads();
   if (threadIdx.x < static_cast<unsigned>(a.world)) {
     uint32_t* f = &a.sig[a.rank]->flags[phase][bid][threadIdx.x];
-    unsigned spins = 0;
-    while (static_cast<int32_t>(
-               __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - e) < 0) {
-      __builtin_amdgcn_s_sleep(1);
-      if (++spins > kSpinLimit) {
-        timed_out = 1;
-        __hip_atomic_store(&a.sig[a.rank]->error, 1u, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_SYSTEM);
-        break;
+    // fail fast: after one timed-out wait on this rank the instance is dead (raise_if_error
+    // raises on every rank); later calls skip their waits instead of each waiting out the bound
+    if (__hip_atomic_load(&a.sig[a.rank]->error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) {
+      timed_out = 1;
+    } else {
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      unsigned spins = 0;
+      while (static_cast<int32_t>(
+                 __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - e) < 0) {
+        __builtin_amdgcn_s_sleep(1);
+        if ((++spins & 63) == 0 && __builtin_amdgcn_s_memrealtime() - t0 > a.timeout_ticks) {
+          timed_out = 1;
+          __hip_atomic_store(&a.sig[a.rank]->error, 1u, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_SYSTEM);
+          break;
+        }
       }
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
@@ -758,6 +768,16 @@ static const RegBuf* car_reg(const CarState* s, int id) {
 // Validates one rank's call and fills its kernel-argument block. `count` is in elements for the
 // all-reduce kinds and in bytes for the direct kinds (as the public entry points take them).
 // *noop: nothing to launch (empty message, or a registered all-reduce at world 1).
+// wait bound of every IPC kernel launched from now on. Default 60 s: ranks can enter a
+// collective seconds apart (a peer still autotuning its first GEMMs; 8 processes time-sliced on
+// one GPU in the rehearsal tests measured > 5 s), and a wrong timeout kills the instance; with
+// fail-fast a dead peer costs one bound per rank, not one per call.
+static uint64_t g_car_timeout_ticks = 60 * kRealtimeHz;
+
+DLBB_API void dlbb_car_set_timeout_ms(int ms) {
+  g_car_timeout_ticks = static_cast<uint64_t>(ms < 1 ? 1 : ms) * (kRealtimeHz / 1000);
+}
+
 static int car_prepare(const CarState* s, int kind, const void* inp, void* out, int64_t count,
                        int dtype, int id, CarKernelArgs* a, bool* noop) {
   *noop = false;
@@ -767,6 +787,7 @@ static int car_prepare(const CarState* s, int kind, const void* inp, void* out, 
   const int64_t vec = 8 * esz;
   const int64_t W = s->world;
   *a = s->args;
+  a->timeout_ticks = g_car_timeout_ticks;
   if (kind == K_ONESHOT || kind == K_TWOSHOT) {
     const int64_t nbytes = count * esz;
     if (nbytes < 0 || nbytes > s->cap || nbytes % vec != 0) return hipErrorInvalidValue;
@@ -978,7 +999,7 @@ DLBB_API int dlbb_car_direct_reg(void* h, int id, int kind, int64_t bytes, int d
 // ---- virtual-rank launch (single-GPU harness) -------------------------------------------------
 // Resident workgroups of the virtual form of (kind, dtype, world) on this device: one launch of
 // world x nblocks workgroups must fit entirely (every rank's workgroups spin on the others'), so
-// dlbb_car_vr_launch refuses a larger grid instead of letting it wait for its spin limit.
+// dlbb_car_vr_launch refuses a larger grid instead of letting it wait out its timeout.
 DLBB_API int dlbb_car_vr_max_blocks(int kind, int dtype, int world) {
   const void* fn = car_kernel<true>(kind, dtype, world);
   if (!fn) return -1;

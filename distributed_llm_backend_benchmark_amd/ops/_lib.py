@@ -126,6 +126,7 @@ _SIGS = {
                                    ctypes.POINTER(c_void_p), ctypes.POINTER(c_void_p), c_int64,
                                    c_int, c_int, c_int, c_void_p]),
     "dlbb_car_error": (c_int, [c_void_p]),
+    "dlbb_car_set_timeout_ms": (None, [c_int]),
     "dlbb_car_destroy": (c_int, [c_void_p]),
 }
 

@@ -361,6 +361,14 @@ class CustomAllReduce:
             pass
 
 
+def set_timeout_ms(ms: int) -> None:
+    """Wall-clock bound of every IPC kernel's wait for its peers, for launches from now on
+    (default 60000 ms; ``DLBB_CUSTOM_AR_TIMEOUT_MS``). A wait that exceeds it flags the error,
+    later calls on that rank skip their waits (fail fast), and :meth:`CustomAllReduce.
+    raise_if_error` raises on every rank."""
+    _lib.lib().dlbb_car_set_timeout_ms(int(ms))
+
+
 def get_custom_allreduce(comm: Comm, self_test: bool = True) -> Optional[CustomAllReduce]:
     """Process-wide instance (created collectively on first use). Returns None when disabled
     (``DLBB_CUSTOM_AR=0``) or unavailable."""
@@ -369,6 +377,8 @@ def get_custom_allreduce(comm: Comm, self_test: bool = True) -> Optional[CustomA
     key = id(comm)
     if key not in _INSTANCES:
         cap = int(os.environ.get("DLBB_CUSTOM_AR_CAP", str(128 << 20)))
+        if os.environ.get("DLBB_CUSTOM_AR_TIMEOUT_MS"):
+            set_timeout_ms(int(os.environ["DLBB_CUSTOM_AR_TIMEOUT_MS"]))
         try:
             inst = CustomAllReduce(comm, capacity_bytes=cap)
             if self_test:

@@ -14,8 +14,8 @@ Two launch forms, both executing the production device code:
 * ``streams``: the per-rank production launch (``dlbb_car_allreduce`` etc.) of every rank on its
   own HIP stream, i.e. W concurrent kernels exactly as W processes would enqueue them. Needs
   ``W <= GPU_MAX_HW_QUEUES`` (4 here) distinct hardware queues: two ranks on one queue serialize,
-  the first spins until its bounded spin limit and flags the timeout, which :meth:`errors`
-  reports — never a hang.
+  the first waits out its wall-clock bound (``custom_allreduce.set_timeout_ms``) and flags the
+  timeout, which :meth:`errors` reports — never a hang.
 
 What the numbers mean: every byte a real rank would move over xGMI moves through the one
 GPU's HBM here, so the harness measures the kernels' protocol cost (flag round trip, epoch and
