@@ -1,0 +1,63 @@
+"""CPU checks of the GEMM dispatch layer (ops/gemm.py, ops/linear_fn.py) that need no GPU: the
+dgrad fallbacks (plain and through a GELU), the NN kernel's split-K heuristic and contract
+predicate, and the fused MLP op's CPU path against a float64 autograd reference."""
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from distributed_llm_backend_benchmark_amd.ops import gemm
+from distributed_llm_backend_benchmark_amd.ops.linear_fn import mlp_train
+
+
+def test_dgrad_cpu_fallback_plain():
+    g = torch.Generator().manual_seed(0)
+    dy = torch.randn(64, 96, generator=g).to(torch.bfloat16)
+    w = torch.randn(96, 128, generator=g).to(torch.bfloat16)
+    out = gemm.dgrad(dy, w)
+    torch.testing.assert_close(out.float(), dy.float() @ w.float(), rtol=2e-2, atol=5e-2)
+
+
+@pytest.mark.parametrize("act,approx", [("gelu_tanh", "tanh"), ("gelu", "none")])
+def test_dgrad_cpu_fallback_through_gelu(act, approx):
+    """dgelu=(u, act) returns (dY @ W) * act'(u): the gradient w.r.t. the pre-activation."""
+    g = torch.Generator().manual_seed(1)
+    dy = torch.randn(32, 64, generator=g).to(torch.bfloat16)
+    w = torch.randn(64, 256, generator=g).to(torch.bfloat16)
+    u = (2 * torch.randn(32, 256, generator=g)).to(torch.bfloat16)
+    out = gemm.dgrad(dy, w, dgelu=(u, act))
+    uf = u.double().requires_grad_(True)
+    F.gelu(uf, approximate=approx).backward(dy.double() @ w.double())
+    torch.testing.assert_close(out.double(), uf.grad, rtol=2e-2, atol=5e-2)
+
+
+def test_dgrad_split_heuristic_and_contract():
+    # LM-head dX: 192 tiles of 256^2, 786 K-tiles -> split 4 (768 workgroups = 3 rounds)
+    assert gemm.dgrad_split(16384, 768, 50304) == 4
+    # a full grid or a short reduction: no split
+    assert gemm.dgrad_split(16384, 3072, 768) == 1
+    assert gemm.dgrad_split(16384, 768, 3072) == 1
+    assert gemm.dgrad_split(4096, 4096, 16384) == 1
+    bf = torch.bfloat16
+    assert gemm.dgrad_supported(torch.empty(64, 128, dtype=bf), torch.empty(128, 256, dtype=bf))
+    assert not gemm.dgrad_supported(torch.empty(64, 128, dtype=bf), torch.empty(128, 200, dtype=bf))
+    assert not gemm.dgrad_supported(torch.empty(60, 128, dtype=bf), torch.empty(128, 256, dtype=bf))
+    assert not gemm.dgrad_supported(torch.empty(64, 100, dtype=bf), torch.empty(100, 256, dtype=bf))
+
+
+def test_mlp_train_cpu_matches_autograd():
+    g = torch.Generator().manual_seed(2)
+    x = torch.randn(4, 8, 32, generator=g, dtype=torch.float64, requires_grad=True)
+    w1 = (0.1 * torch.randn(128, 32, generator=g, dtype=torch.float64)).requires_grad_(True)
+    b1 = (0.1 * torch.randn(128, generator=g, dtype=torch.float64)).requires_grad_(True)
+    w2 = (0.1 * torch.randn(32, 128, generator=g, dtype=torch.float64)).requires_grad_(True)
+    b2 = (0.1 * torch.randn(32, generator=g, dtype=torch.float64)).requires_grad_(True)
+    params = (x, w1, b1, w2, b2)
+    y = mlp_train(x, w1, b1, w2, b2, act="gelu_tanh")
+    dy = torch.randn(y.shape, generator=g, dtype=torch.float64)
+    grads = torch.autograd.grad((y * dy).sum(), params)
+    ref = F.linear(F.gelu(F.linear(x, w1, b1), approximate="tanh"), w2, b2)
+    ref_grads = torch.autograd.grad((ref * dy).sum(), params)
+    torch.testing.assert_close(y, ref)
+    for a, b in zip(grads, ref_grads):
+        torch.testing.assert_close(a, b)
