@@ -709,10 +709,13 @@ __device__ __forceinline__ void stage_a_half(__amdgpu_buffer_rsrc_t ra, uint32_t
   }
 }
 
+// I0 / I1: the slice [I0, I1) of the 8 instructions (0..3 = tile rows [0, 128), 4..7 = rows
+// [128, 256)) — the balanced ping-pong splits a B tile between the two wave rows
+template <int I0 = 0, int I1 = 8>
 __device__ __forceinline__ void stage_b(__amdgpu_buffer_rsrc_t rb, uint32_t ldb2, int rows_b,
                                         uint32_t k2, char* bbuf, int w4, uint32_t boff) {
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
+  for (int i = I0; i < I1; ++i) {
     const int trow = (i * 4 + w4) * 8;
     const int g = (trow & ~63) < rows_b ? perm_brow(trow) : (perm_brow(trow) & 63);
     bldsx4(rb, boff, static_cast<uint32_t>(g) * ldb2 + k2, bbuf + trow * (BK * 2));
@@ -764,10 +767,11 @@ __device__ __forceinline__ int nnf(int row) { return (row & 3) | (((row >> 3) & 
 // wave of the staging wave row (w4 = its wave column). Instruction s = 4i + w4: image s >> 4,
 // row group rg = s & 15; nnf's bit 3 for its rows is (rg >> 1) & 1 = (w4 >> 1) & 1, fixed per
 // wave, so one per-lane offset (boff) serves all eight loads.
+template <int I0 = 0, int I1 = 8>
 __device__ __forceinline__ void stage_b_nn(__amdgpu_buffer_rsrc_t rb, uint32_t ldb2, int u,
                                            char* bbuf, int w4, uint32_t boff) {
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
+  for (int i = I0; i < I1; ++i) {
     const int s = i * 4 + w4, img = s >> 4, rg = s & 15;
     bldsx4(rb, boff, static_cast<uint32_t>(u * BK + rg * 4) * ldb2 + img * 256,
            bbuf + img * (kTile2Bytes / 2) + rg * 1024);
@@ -796,13 +800,13 @@ __device__ __forceinline__ void read_b_nn(const char* bbuf, int wc, int fr, int 
       }
 }
 
-template <bool NN>
+template <bool NN, int I0 = 0, int I1 = 8>
 __device__ __forceinline__ void stage_b_any(__amdgpu_buffer_rsrc_t rb, uint32_t ldb2, int rows_b,
                                             int u, char* bbuf, int w4, uint32_t boff) {
   if constexpr (NN)
-    stage_b_nn(rb, ldb2, u, bbuf, w4, boff);
+    stage_b_nn<I0, I1>(rb, ldb2, u, bbuf, w4, boff);
   else
-    stage_b(rb, ldb2, rows_b, static_cast<uint32_t>(u) * (BK * 2), bbuf, w4, boff);
+    stage_b<I0, I1>(rb, ldb2, rows_b, static_cast<uint32_t>(u) * (BK * 2), bbuf, w4, boff);
 }
 
 template <bool NN>
@@ -824,7 +828,16 @@ __device__ __forceinline__ void read_split_any(const char* abuf, const char* bbu
 // The ping-pong schedule, for B stored [N][K] (NT: forward, C = A · B^T) or [K][N] (NN: dgrad).
 // Both B layouts stage 32 wave-instructions per K-tile from wave row 0, so the counted waits
 // are identical.
-template <bool NN>
+// BAL (balanced DMA issue): LDS-DMA instructions are expensive to ISSUE (~60-185 cycles each
+// beside a phase's ds_reads, MI355X_MICROARCH.md), and the plain schedule has wave row 0 issue
+// 12 of the 16 per K-tile (A-hi + all of B) in its memory interval against row 1's 4 (A-lo).
+// BAL moves the second half of every B tile from tile 2 on (rows [128, 256) / the second
+// image) to wave row 1, issued in interval 2u+1 next to A-lo(u+2) — 8 per row per K-tile:
+//   interval 2u   (row 0): A-hi(u+1), B0(u+2)    interval 2u+1 (row 1): A-lo(u+2), B1(u+2)
+// B1(u+2) replaces B(u-1), last read by row 1 in interval 2u-1; row 1 retires A-lo(u+1) and
+// B1(u+1) together before the barrier ending 2u+1 (row 0 reads tile u+1 in 2u+2). B(1) stays
+// whole in row 0's prologue, so the counted waits below also hold for u = 0.
+template <bool NN, bool BAL = false>
 __device__ __forceinline__ void pingpong_body(GemmArgs a, char* smem) {
   if (NN && gridDim.y > 1) {         // split-K slice blockIdx.y (wave-uniform, SGPR math)
     const int s = blockIdx.y, nkt = static_cast<int>(a.K / BK);
@@ -889,20 +902,29 @@ __device__ __forceinline__ void pingpong_body(GemmArgs a, char* smem) {
                      wc, aoff);
       if (b2) {
         const int cb2 = cb == 0 ? 2 : cb - 1;         // (u + 2) % 3
-        stage_b_any<NN>(rb, ldb2, rows_b, u + 2, bbuf0 + cb2 * kTile2Bytes, wc, boff);
+        if (BAL)
+          stage_b_any<NN, 0, 4>(rb, ldb2, rows_b, u + 2, bbuf0 + cb2 * kTile2Bytes, wc, boff);
+        else
+          stage_b_any<NN>(rb, ldb2, rows_b, u + 2, bbuf0 + cb2 * kTile2Bytes, wc, boff);
       }
       // retire A-hi(u) (issued two intervals ago; tile 0's came from row 1)
-      if (b2) DLBB_WAIT_VM(20);
-      else if (h1) DLBB_WAIT_VM(12);
-      else DLBB_WAIT_VM(0);
+      if (BAL) {
+        if (b2) DLBB_WAIT_VM(12);
+        else if (h1) DLBB_WAIT_VM(8);
+        else DLBB_WAIT_VM(0);
+      } else {
+        if (b2) DLBB_WAIT_VM(20);
+        else if (h1) DLBB_WAIT_VM(12);
+        else DLBB_WAIT_VM(0);
+      }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
       __builtin_amdgcn_s_barrier();                   // end of interval 2u
       __builtin_amdgcn_sched_barrier(0);
       mfma_full(acc, af, bf);
       __builtin_amdgcn_sched_barrier(0);
-      if (h1) {                                       // retire B(u+1)
-        if (b2) DLBB_WAIT_VM(12);
+      if (h1) {                                       // retire B(u+1) (BAL: its first half)
+        if (b2) { if (BAL) DLBB_WAIT_VM(8); else DLBB_WAIT_VM(12); }
         else DLBB_WAIT_VM(4);
       }
       __builtin_amdgcn_s_barrier();                   // end of interval 2u+1
@@ -922,8 +944,12 @@ __device__ __forceinline__ void pingpong_body(GemmArgs a, char* smem) {
       const bool l2 = u + 2 < nk;
       if (l2) stage_a_half(ra, lda2, rows_a, (u + 2) * kStep, abuf0 + (u & 1) * kTile2Bytes, 0,
                            wc, aoff);
-      if (u + 1 < nk) {                               // retire A-lo(u+1)
-        if (l2) DLBB_WAIT_VM(4);
+      if (BAL && l2) {
+        const int cb2 = cb == 0 ? 2 : cb - 1;         // (u + 2) % 3
+        stage_b_any<NN, 4, 8>(rb, ldb2, rows_b, u + 2, bbuf0 + cb2 * kTile2Bytes, wc, boff);
+      }
+      if (u + 1 < nk) {                               // retire A-lo(u+1) (BAL: and B1(u+1))
+        if (l2) { if (BAL) DLBB_WAIT_VM(8); else DLBB_WAIT_VM(4); }
         else DLBB_WAIT_VM(0);
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -944,11 +970,21 @@ __global__ void __launch_bounds__(kThreads2, 1) gemm_bf16_nt_256_pingpong3(GemmA
   pingpong_body<false>(a, smem);
 }
 
+// A/B variant (set_stagger(7)): the balanced DMA issue (BAL above).
+__global__ void __launch_bounds__(kThreads2, 1) gemm_bf16_nt_256_pingpong3_bal(GemmArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  pingpong_body<false, true>(a, smem);
+}
+
 // dgrad: C[M, N] = A[M, K] · B[K, N] (B row-major over the reduction); host contract
 // N % 256 == 0, M % 8 == 0, K % 64 == 0.
 __global__ void __launch_bounds__(kThreads2, 1) gemm_bf16_nn_256_pingpong3(GemmArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   pingpong_body<true>(a, smem);
+}
+__global__ void __launch_bounds__(kThreads2, 1) gemm_bf16_nn_256_pingpong3_bal(GemmArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  pingpong_body<true, true>(a, smem);
 }
 
 }  // namespace dlbb
@@ -958,10 +994,20 @@ using namespace dlbb;
 static int dlbb_gemm_force_tile = 0;   // 0 = heuristic, 128 or 256 = force (A/B testing)
 
 static int dlbb_gemm_stagger = 6;      // 256^2 schedule (set_stagger): 6 = ping-pong, 160 KiB LDS, measured fastest
+// Balanced DMA issue (BAL) for the ping-pong kernels: 0 never, 1 always, 2 (default) = always
+// for NN (dgrad: +1-5 % on every measured shape, K 768 .. 50304) and for NT when the reduction
+// has >= kBalMinKTiles K-tiles (NT: +1-5 % at K >= 2048, -1.5 % at K = 768)
+// (profiles/r02_gemm/gemm_ab_pingpong_bal.jsonl, dgrad_ab_nn_bal.jsonl)
+static int dlbb_gemm_bal = 2;
+constexpr int64_t kBalMinKTiles = 32;
+static bool use_bal(int64_t k_tiles, bool nn) {
+  return dlbb_gemm_bal == 1 || (dlbb_gemm_bal == 2 && (nn || k_tiles >= kBalMinKTiles));
+}
 
 DLBB_API void dlbb_gemm_set_tile(int tile) { dlbb_gemm_force_tile = tile; }
 DLBB_API void dlbb_gemm_set_stagger(int on) { dlbb_gemm_stagger = on; }
 DLBB_API int dlbb_gemm_get_stagger() { return dlbb_gemm_stagger; }
+DLBB_API void dlbb_gemm_set_bal(int mode) { dlbb_gemm_bal = mode >= 0 && mode <= 2 ? mode : 2; }
 
 DLBB_API int dlbb_gemm_bf16_nt(const void* A, int64_t lda, const void* B, int64_t ldb, void* C,
                                int64_t ldc, int64_t M, int64_t N, int64_t K, const void* bias,
@@ -990,10 +1036,10 @@ DLBB_API int dlbb_gemm_bf16_nt(const void* A, int64_t lda, const void* B, int64_
     int mode = dlbb_gemm_stagger;
     // ping-pong contract: 8-row A groups and 64-row B blocks wholly in or out (uniform clamps),
     // 32-bit buffer offsets within a 256-row panel
-    if (mode == 6 && !(M % 8 == 0 && N % 64 == 0 && M >= 8 && lda * 2 * 256 + K * 2 < (1LL << 31) &&
+    if ((mode == 6 || mode == 7) && !(M % 8 == 0 && N % 64 == 0 && M >= 8 && lda * 2 * 256 + K * 2 < (1LL << 31) &&
                        ldb * 2 * 256 + K * 2 < (1LL << 31)))
       mode = 3;
-    if (mode == 5 || mode > 6) mode = 3;
+    if (mode == 5 || mode > 7) mode = 3;
     if (mode == 4) {
       static int ncu[64] = {0};
       int dev = 0;
@@ -1009,7 +1055,9 @@ DLBB_API int dlbb_gemm_bf16_nt(const void* A, int64_t lda, const void* B, int64_
       const int64_t grid = tiles256 < ncu[dev] ? tiles256 : ncu[dev];
       hipLaunchKernelGGL(gemm_bf16_nt_256_persistent, dim3(static_cast<unsigned>(grid)), b,
                          2 * kBuf2Bytes, stream, a);
-    } else if (mode == 6)
+    } else if (mode == 7 || (mode == 6 && use_bal(K / BK, false)))
+      hipLaunchKernelGGL(gemm_bf16_nt_256_pingpong3_bal, g, b, kPP6Lds, stream, a);
+    else if (mode == 6)
       hipLaunchKernelGGL(gemm_bf16_nt_256_pingpong3, g, b, kPP6Lds, stream, a);
     else if (mode == 3)
       hipLaunchKernelGGL(gemm_bf16_nt_256_kernel<3>, g, b, 2 * kBuf2Bytes, stream, a);
@@ -1065,13 +1113,22 @@ DLBB_API int dlbb_gemm_bf16_nn(const void* A, int64_t lda, const void* B, int64_
     a.C = ws;
     a.out_f32 = 1;
     a.vec_ok = (reinterpret_cast<uintptr_t>(ws) & 15) == 0 && N % 8 == 0;
-    hipLaunchKernelGGL(gemm_bf16_nn_256_pingpong3, dim3(static_cast<unsigned>(tiles256), split),
-                       dim3(kThreads2), kPP6Lds, stream, a);
+    if (use_bal(a.kt_split, true))
+      hipLaunchKernelGGL(gemm_bf16_nn_256_pingpong3_bal,
+                         dim3(static_cast<unsigned>(tiles256), split), dim3(kThreads2), kPP6Lds,
+                         stream, a);
+    else
+      hipLaunchKernelGGL(gemm_bf16_nn_256_pingpong3, dim3(static_cast<unsigned>(tiles256), split),
+                         dim3(kThreads2), kPP6Lds, stream, a);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     return dlbb_split_reduce_launch(ws, C, 0, M * N, split, stream);
   }
-  hipLaunchKernelGGL(gemm_bf16_nn_256_pingpong3, dim3(static_cast<unsigned>(tiles256)),
-                     dim3(kThreads2), kPP6Lds, stream, a);
+  if (use_bal(nkt, true))
+    hipLaunchKernelGGL(gemm_bf16_nn_256_pingpong3_bal, dim3(static_cast<unsigned>(tiles256)),
+                       dim3(kThreads2), kPP6Lds, stream, a);
+  else
+    hipLaunchKernelGGL(gemm_bf16_nn_256_pingpong3, dim3(static_cast<unsigned>(tiles256)),
+                       dim3(kThreads2), kPP6Lds, stream, a);
   return hipGetLastError();
 }

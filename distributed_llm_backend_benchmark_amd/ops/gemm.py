@@ -48,9 +48,17 @@ def set_stagger(mode: int) -> None:
     issued at phase 1, 3 staggered + deep restaging (one K-tile in flight), 4 = 3 as a
     persistent kernel (next tile's prologue overlaps this tile's epilogue), 6 ping-pong (the
     two waves of each SIMD alternate whole-K-tile MFMA clusters and fragment loads, 160 KiB of
-    LDS; M % 8 == 0 and N % 64 == 0, else 3 — the default). For A/B benchmarking; the library
-    default is the measured fastest (profiles/r02_gemm)."""
+    LDS; M % 8 == 0 and N % 64 == 0, else 3 — the default; balanced DMA issue per
+    :func:`set_bal`), 7 ping-pong with the balanced DMA issue forced. For A/B benchmarking; the
+    library default is the measured fastest (profiles/r02_gemm)."""
     _lib.lib().dlbb_gemm_set_stagger(int(mode))
+
+
+def set_bal(mode: int) -> None:
+    """Balanced LDS-DMA issue of the ping-pong kernels (NT forward and NN dgrad): 0 never,
+    1 always (``set_stagger(7)`` forces it for NT), 2 = always for NN and for NT when
+    K >= 2048 (default, measured: profiles/r02_gemm)."""
+    _lib.lib().dlbb_gemm_set_bal(int(mode))
 
 
 def set_wgrad_stages(nb: int) -> None:

@@ -91,21 +91,25 @@ def test_chunk_copy_and_scale():
 
 @pytest.fixture(params=[("mfma", 0, 1), ("mfma", 128, 1), ("mfma", 256, 1), ("mfma", 256, 0),
                         ("mfma", 256, 2), ("mfma", 256, 3), ("mfma", 256, 4), ("mfma", 256, 6),
-                        ("blas", 0, 1)],
+                        ("mfma", 256, 6, 0), ("mfma", 256, 7), ("blas", 0, 1)],
                 ids=["mfma_auto", "mfma_t128", "mfma_t256", "mfma_t256_lockstep",
                      "mfma_t256_early", "mfma_t256_deep", "mfma_t256_persistent",
-                     "mfma_t256_pingpong", "blas"])
+                     "mfma_t256_pingpong", "mfma_t256_pingpong_nobal", "mfma_t256_pingpong_bal",
+                     "blas"])
 def gemm_tile(request, monkeypatch):
-    from distributed_llm_backend_benchmark_amd.ops.gemm import get_stagger, set_stagger, set_tile
+    from distributed_llm_backend_benchmark_amd.ops.gemm import (get_stagger, set_bal, set_stagger,
+                                                                set_tile)
 
-    impl, tile, stagger = request.param
+    impl, tile, stagger = request.param[:3]
     monkeypatch.setenv("DLBB_GEMM", impl)
     old = get_stagger()
     set_tile(tile)
     set_stagger(stagger)
+    set_bal(request.param[3] if len(request.param) > 3 else 2)
     yield request.param
     set_tile(0)
     set_stagger(old)
+    set_bal(2)
 
 
 @pytest.mark.parametrize("M,N,K", [(256, 256, 64), (4096, 1024, 4096), (300, 200, 128),
@@ -173,16 +177,21 @@ def test_gemm_strided_A_view():
 @pytest.mark.parametrize("M,N,K", [(256, 256, 64), (16384, 768, 2304), (520, 512, 192),
                                    (8, 256, 64), (1000, 3072, 768), (2048, 768, 50304),
                                    (4096, 4096, 4096)])
-def test_dgrad_nn_matches_fp32(M, N, K):
+@pytest.mark.parametrize("bal", [0, 1])
+def test_dgrad_nn_matches_fp32(M, N, K, bal):
     """NN kernel (transposed-read W): dX = dY @ W against an fp32 reference; ragged M, one
-    K-tile, LM-head-sized reduction."""
+    K-tile, LM-head-sized reduction; plain and balanced DMA issue."""
     from distributed_llm_backend_benchmark_amd.ops import gemm
 
     dy = _randn(M, K, seed=21, scale=0.5)
     w = _randn(K, N, seed=22, scale=0.5)
     assert gemm.dgrad_supported(dy, w)
     out = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
-    gemm._dgrad_hip(dy, w, out)
+    gemm.set_bal(bal)
+    try:
+        gemm._dgrad_hip(dy, w, out)
+    finally:
+        gemm.set_bal(2)
     ref = dy.float() @ w.float()
     torch.testing.assert_close(out.float(), ref, rtol=2e-2, atol=2e-2 * (K ** 0.5))
 

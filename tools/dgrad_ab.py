@@ -50,12 +50,20 @@ def main():
         gemm._dgrad_hip(dy, w, out)
         err = float((out.float() - ref).abs().max() / ref.abs().max())
         t_ours = t_blas = 1e9
+        t_bal = {0: 1e9, 1: 1e9}
         for _ in range(args.rounds):
+            for bal in (0, 1):
+                gemm.set_bal(bal)
+                t_bal[bal] = min(t_bal[bal], timed(lambda: gemm._dgrad_hip(dy, w, out),
+                                                   args.iters))
+            gemm.set_bal(2)
             t_ours = min(t_ours, timed(lambda: gemm._dgrad_hip(dy, w, out), args.iters))
             t_blas = min(t_blas, timed(lambda: torch.matmul(dy, w, out=out), args.iters))
         fl = 2.0 * M * N * K
         print(json.dumps({"case": name, "M": M, "N": N, "K": K,
                           "nn_ms": round(t_ours * 1e3, 4), "blas_ms": round(t_blas * 1e3, 4),
+                          "nn_plain_ms": round(t_bal[0] * 1e3, 4),
+                          "nn_bal_ms": round(t_bal[1] * 1e3, 4),
                           "nn_tflops": round(fl / t_ours / 1e12, 1),
                           "hipblaslt_tflops": round(fl / t_blas / 1e12, 1),
                           "rel_err_vs_fp32": round(err, 5)}), flush=True)
