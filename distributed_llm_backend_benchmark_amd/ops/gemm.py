@@ -399,7 +399,7 @@ def _dgrad_blas(dy2, w, out, split=None, dgelu=None):
     return out
 
 
-DGRAD_CHOICES = {}    # (M, N, K, lda) -> "mfma" | "blas"
+DGRAD_CHOICES = {}    # (M, N, K, lda, fused GELU-backward act or None) -> "mfma" | "blas"
 _DGRAD_IMPLS = {"mfma": _dgrad_hip, "blas": _dgrad_blas}
 
 
