@@ -40,6 +40,8 @@ struct Args {
   int M, N, K;
   int m_per_split;
   int nsplit;          // fused db partials (BIAS) at ws + nsplit * N * K (tk == 0 blocks)
+  void* direct;        // nsplit == 1, no accumulate, no bias: store dW here (no ws, no reduce)
+  int direct_bf16;     // direct store dtype: bf16 (1) or fp32 (0)
 };
 
 // MFMA 16x16x32 operand from a [64 m][128 col] image: lane l gets column colbase + (l & 15),
@@ -179,8 +181,24 @@ __global__ void __launch_bounds__(128 * WM, WM == 2 ? 3 : 2) wgrad_kernel(Args a
     }
   }
   // D map: col = lane & 15 (output k), row = 4 (lane >> 4) + r (output n)
-  float* w = a.ws + static_cast<int64_t>(split) * a.N * a.K;
   const int fr = lane & 15, fq = lane >> 4;
+  if (!BIAS && a.direct) {    // one split: the tile is final — no fp32 partial round trip
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int64_t o = static_cast<int64_t>(n0 + wm * 64 + i * 16 + fq * 4 + r) * a.K +
+                            k0 + wn * 64 + j * 16 + fr;
+          if (a.direct_bf16)
+            static_cast<uint16_t*>(a.direct)[o] = f32_to_bf16(acc[i][j][r]);
+          else
+            static_cast<float*>(a.direct)[o] = acc[i][j][r];
+        }
+    return;
+  }
+  float* w = a.ws + static_cast<int64_t>(split) * a.N * a.K;
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -262,8 +280,11 @@ DLBB_API int dlbb_gemm_wgrad_tile(const void* A, int64_t lda, const void* B, int
   int per = (M / split + BM - 1) / BM * BM;
   if (per <= 0) per = BM;
   split = (M + per - 1) / per;
+  // one split, plain store, no bias: the kernel writes dW itself (ws may be null)
+  const bool direct = split == 1 && !accumulate && !out_bias;
+  if (!direct && !ws) return hipErrorInvalidValue;
   Args a{static_cast<const uint16_t*>(A), static_cast<const uint16_t*>(B), ws, lda, ldb, M, N, K,
-         per, split};
+         per, split, direct ? out : nullptr, dt_out == DT_BF16 ? 1 : 0};
   const dim3 grid((N / bn) * (K / BKO) * split);
   const int stages = g_wgrad_stages;
 #define WG_LAUNCH(BIASV, NBV, WMV)                                                          \
@@ -280,6 +301,7 @@ DLBB_API int dlbb_gemm_wgrad_tile(const void* A, int64_t lda, const void* B, int
   }
 #undef WG_STAGES
 #undef WG_LAUNCH
+  if (direct) return hipGetLastError();
   const int64_t n = static_cast<int64_t>(N) * K;
   const int64_t nb = out_bias ? N : 0;
   const int g = stream_grid((n + nb) / 8, 256);

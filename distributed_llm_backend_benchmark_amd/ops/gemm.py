@@ -245,10 +245,14 @@ def _wgrad_hip(dy2, x2, out, accumulate, split=None, bias_out=None, bn=128):
         # (256 x 128 tiles: at most the 512 resident slots — a 2nd partial round costs a
         # whole workgroup time)
         split = max(1, min(M // 256, (-(-768 // tiles)) if bn == 128 else 512 // tiles))
-    ws = torch.empty(split * (N * K + N), dtype=torch.float32, device=dy2.device)
+    # one split, plain store, no bias: the kernel stores dW itself (no fp32 partials, no
+    # reduce pass — the LM-head dW)
+    direct = split == 1 and not accumulate and bias_out is None
+    ws = None if direct else torch.empty(split * (N * K + N), dtype=torch.float32,
+                                         device=dy2.device)
     check(_lib.lib().dlbb_gemm_wgrad_tile(dy2.data_ptr(), dy2.stride(0), x2.data_ptr(),
                                           x2.stride(0), out.data_ptr(), _lib.dt(out),
-                                          int(accumulate), ws.data_ptr(), M, N, K, split,
+                                          int(accumulate), _lib.ptr(ws), M, N, K, split,
                                           _lib.ptr(bias_out), int(bn), _lib.stream(dy2.device)),
           "gemm_wgrad")
 
