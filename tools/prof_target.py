@@ -1,5 +1,6 @@
 """Tiny driver for PMC-counter profiling: runs ONE op a few times (no timing logic).
-usage: prof_target.py gemm256|gemm256s6|gemm128|blas|reduce8|ln|xent|xentfused|embbwd"""
+usage: prof_target.py gemm256|gemm256s6|gemm256s7|gemm128|blas|nn|nnplain|reduce8|ln|xent|xentfused|
+embbwd"""
 import os
 import sys
 
@@ -25,6 +26,15 @@ if what.startswith("gemm") or what == "blas":
 
             set_stagger(int(sched))
     fn = lambda: ops.linear(x, w)  # noqa: E731
+elif what in ("nn", "nnplain"):  # NN dgrad kernel (transposed-read W), balanced / plain DMA issue
+    from distributed_llm_backend_benchmark_amd.ops import gemm as G
+
+    M = N = K = 8192
+    dy = torch.randn(M, K, device=dev, generator=g).to(torch.bfloat16)
+    w = torch.randn(K, N, device=dev, generator=g).to(torch.bfloat16)
+    out = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    G.set_bal(0 if what == "nnplain" else 1)
+    fn = lambda: G._dgrad_hip(dy, w, out)  # noqa: E731
 elif what == "reduce8":
     srcs = [torch.randn(1 << 25, device=dev, generator=g).to(torch.bfloat16) for _ in range(8)]
     fn = lambda: ops.reduce_sum(srcs)  # noqa: E731
