@@ -127,8 +127,8 @@ def _allreduce_sweep(comm, max_mib: int):
         best = min(res, key=res.get)
         t = res[best]
         out.append({"bytes": nbytes, "impl": best, "us": round(t * 1e6, 2),
-                    "busbw_GBps": round(busbw_gbps("allreduce", nbytes, t, P), 3),
-                    "algbw_GBps": round(algbw_gbps("allreduce", nbytes, t, P), 3),
+                    "busbw_GBps": float(f"{busbw_gbps('allreduce', nbytes, t, P):.4g}"),
+                    "algbw_GBps": float(f"{algbw_gbps('allreduce', nbytes, t, P):.4g}"),
                     "us_by_impl": {k: round(v * 1e6, 2) for k, v in res.items()},
                     **({"invalid": invalid} if invalid else {})})
         del data, flat
