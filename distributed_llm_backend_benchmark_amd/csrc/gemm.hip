@@ -800,6 +800,60 @@ __device__ __forceinline__ void read_b_nn(const char* bbuf, int wc, int fr, int 
       }
 }
 
+// ---------------------------------------------------------------------------------------
+// TN operand A (weight gradient: dW[N_out, K_out] = dY[T, N_out]^T · X[T, K_out], both operands
+// row-major over the reduction T). One K-tile of A = 64 t-rows x 256 dY columns, staged as two
+// [64][128] images exactly like the NN B tile; image h holds output rows [128h, 128h + 128), so
+// the A halves of the ping-pong ("A-lo" read by wave row 0, "A-hi" by row 1) are the two images
+// and keep their 16-instruction staging (the counted waits are unchanged). Fragments come from
+// ds_read_b64_tr_b16 in PLAIN column order (the A side of the epilogue is not permuted): lane
+// (fq, fr = 4q + p) reads t-rows ks*32 + 8 fq + 4h + q, columns i*16 + 4p .. +3, with the
+// csrc/gemm_tn.hip image swizzle — 16-B chunk c of row r in slot c ^ swz_tn(r), swz_tn(r) =
+// 2 ((r & 3) | ((r >> 3) & 1) << 2), which makes every half-wave hit disjoint bank groups.
+__device__ __forceinline__ int swz_tn(int row) { return ((row & 3) | (((row >> 3) & 1) << 2)) << 1; }
+
+// image `half` of A K-tile u: 16 wave-instructions, 4 per wave of the staging wave row
+// (w4 = its wave column): instruction s = 4i + w4 loads t-rows 4s .. 4s + 3. An image wholly
+// past the last output row (rows_a <= 128) re-stages image 0 (its rows are never stored).
+__device__ __forceinline__ void stage_a_half_tn(__amdgpu_buffer_rsrc_t ra, uint32_t lda2,
+                                                int rows_a, int u, char* abuf, int half, int w4,
+                                                uint32_t aoff) {
+  const uint32_t col = rows_a > 128 * half ? static_cast<uint32_t>(half) * 256 : 0u;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int rg = i * 4 + w4;
+    bldsx4(ra, aoff, static_cast<uint32_t>(u * BK + rg * 4) * lda2 + col,
+           abuf + half * (kTile2Bytes / 2) + rg * 1024);
+  }
+}
+
+__device__ __forceinline__ void read_a_tn(const char* abuf, int wr, int fr, int fq,
+                                          bf16x8 (&af)[2][8]) {
+  // row = ks*32 + 8 fq + 4h + q has row & 3 = q and (row >> 3) & 1 = fq & 1, so swz_tn(row) is
+  // one per-lane constant S (even): chunk (2i + (p >> 1)) ^ S = (2i ^ S) + (p >> 1), and the
+  // byte offset is lane base + ((32 i) ^ 16 S) + immediate (ks, h). The 8 per-i addresses are
+  // recomputed at every call (the empty asm hides S's invariance) rather than held in VGPRs
+  // across the main loop, where the 256-register budget has no room for them.
+  const int q = fr >> 2, p = fr & 3;
+  int sx = swz_tn(q | ((fq & 1) << 3)) << 4;
+  asm volatile("" : "+v"(sx));
+  const char* lb = abuf + wr * (kTile2Bytes / 2) + (8 * fq + q) * 256 + (p >> 1) * 16 +
+                   (p & 1) * 8;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const char* ai = lb + (sx ^ (32 * i));
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const i16x4 t = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (lds_i16x4_ptr)(ai + (ks * 32 + 4 * h) * 256));
+#pragma unroll
+        for (int e = 0; e < 4; ++e) af[ks][i][4 * h + e] = t[e];
+      }
+  }
+}
+
 template <bool NN, int I0 = 0, int I1 = 8>
 __device__ __forceinline__ void stage_b_any(__amdgpu_buffer_rsrc_t rb, uint32_t ldb2, int rows_b,
                                             int u, char* bbuf, int w4, uint32_t boff) {
@@ -809,11 +863,14 @@ __device__ __forceinline__ void stage_b_any(__amdgpu_buffer_rsrc_t rb, uint32_t 
     stage_b<I0, I1>(rb, ldb2, rows_b, static_cast<uint32_t>(u) * (BK * 2), bbuf, w4, boff);
 }
 
-template <bool NN>
+template <bool NN, bool TN = false>
 __device__ __forceinline__ void read_split_any(const char* abuf, const char* bbuf, int wr, int wc,
                                                int fr, int fq, bf16x8 (&af)[2][8],
                                                bf16x8 (&bf)[2][4]) {
-  if constexpr (NN) {
+  if constexpr (TN) {
+    read_a_tn(abuf, wr, fr, fq, af);
+    read_b_nn(bbuf, wc, fr, fq, bf);
+  } else if constexpr (NN) {
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
@@ -837,9 +894,11 @@ __device__ __forceinline__ void read_split_any(const char* abuf, const char* bbu
 // B1(u+2) replaces B(u-1), last read by row 1 in interval 2u-1; row 1 retires A-lo(u+1) and
 // B1(u+1) together before the barrier ending 2u+1 (row 0 reads tile u+1 in 2u+2). B(1) stays
 // whole in row 0's prologue, so the counted waits below also hold for u = 0.
-template <bool NN, bool BAL = false>
+// TN (weight gradient, implies NN for B): A [K][lda] row-major over the reduction, staged and
+// read as transposed images (stage_a_half_tn / read_a_tn); no split-K.
+template <bool NN, bool BAL = false, bool TN = false>
 __device__ __forceinline__ void pingpong_body(GemmArgs a, char* smem) {
-  if (NN && gridDim.y > 1) {         // split-K slice blockIdx.y (wave-uniform, SGPR math)
+  if (NN && !TN && gridDim.y > 1) {         // split-K slice blockIdx.y (wave-uniform, SGPR math)
     const int s = blockIdx.y, nkt = static_cast<int>(a.K / BK);
     const int kt0 = s * a.kt_split, kt1 = kt0 + a.kt_split < nkt ? kt0 + a.kt_split : nkt;
     a.A += static_cast<int64_t>(kt0) * BK;
@@ -865,7 +924,12 @@ __device__ __forceinline__ void pingpong_body(GemmArgs a, char* smem) {
   bf16x8 af[2][8], bf[2][4];
   const int r_in = lane >> 3, chunk = (lane & 7) ^ (lane >> 3);
   const uint32_t lda2 = static_cast<uint32_t>(a.lda) * 2, ldb2 = static_cast<uint32_t>(a.ldb) * 2;
-  const uint32_t aoff = static_cast<uint32_t>(r_in) * lda2 + chunk * 16;
+  uint32_t aoff = static_cast<uint32_t>(r_in) * lda2 + chunk * 16;
+  if constexpr (TN) {   // image rows 4s + rq: swz_tn needs rq and bit 1 of the wave column
+    const int rq = lane >> 4, slot = lane & 15;
+    aoff = static_cast<uint32_t>(rq) * lda2 +
+           static_cast<uint32_t>(slot ^ (2 * (rq | (((wc >> 1) & 1) << 2)))) * 16;
+  }
   uint32_t boff;
   if constexpr (NN) {
     const int rq = lane >> 4, slot = lane & 15;
@@ -876,14 +940,21 @@ __device__ __forceinline__ void pingpong_body(GemmArgs a, char* smem) {
   }
   const int rows_a = static_cast<int>(a.M - m0), rows_b = static_cast<int>(a.N - n0);
   const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<uint16_t*>(a.A + m0 * a.lda), 0, 0x7fffffff, 0x00020000);
+      const_cast<uint16_t*>(TN ? a.A + m0 : a.A + m0 * a.lda), 0, 0x7fffffff, 0x00020000);
   const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<uint16_t*>(NN ? a.B + n0 : a.B + n0 * a.ldb), 0, 0x7fffffff, 0x00020000);
   constexpr uint32_t kStep = BK * 2;
+  // A half `half` of K-tile u into buffer `buf` (4 wave-instructions per wave either way)
+  auto stage_a = [&](int u, char* buf, int half) {
+    if constexpr (TN)
+      stage_a_half_tn(ra, lda2, rows_a, u, buf, half, wc, aoff);
+    else
+      stage_a_half(ra, lda2, rows_a, static_cast<uint32_t>(u) * kStep, buf, half, wc, aoff);
+  };
 
   if (wr == 0) {
     // prologue, row 0: A-lo(0), B(0), B(1); retire the first two
-    stage_a_half(ra, lda2, rows_a, 0, abuf0, 0, wc, aoff);
+    stage_a(0, abuf0, 0);
     stage_b_any<NN>(rb, ldb2, rows_b, 0, bbuf0, wc, boff);
     if (nk > 1) {
       stage_b_any<NN>(rb, ldb2, rows_b, 1, bbuf0 + kTile2Bytes, wc, boff);
@@ -895,11 +966,9 @@ __device__ __forceinline__ void pingpong_body(GemmArgs a, char* smem) {
     int cb = 0;                                       // B buffer of tile u
     for (int u = 0; u < nk; ++u) {
       const char* ab = abuf0 + (u & 1) * kTile2Bytes;
-      read_split_any<NN>(ab, bbuf0 + cb * kTile2Bytes, 0, wc, fr, fq, af, bf);
+      read_split_any<NN, TN>(ab, bbuf0 + cb * kTile2Bytes, 0, wc, fr, fq, af, bf);
       const bool h1 = u + 1 < nk, b2 = u + 2 < nk;
-      if (h1)
-        stage_a_half(ra, lda2, rows_a, (u + 1) * kStep, abuf0 + ((u + 1) & 1) * kTile2Bytes, 1,
-                     wc, aoff);
+      if (h1) stage_a(u + 1, abuf0 + ((u + 1) & 1) * kTile2Bytes, 1);
       if (b2) {
         const int cb2 = cb == 0 ? 2 : cb - 1;         // (u + 2) % 3
         if (BAL)
@@ -932,18 +1001,17 @@ __device__ __forceinline__ void pingpong_body(GemmArgs a, char* smem) {
     }
   } else {
     // prologue, row 1: A-hi(0), A-lo(1)
-    stage_a_half(ra, lda2, rows_a, 0, abuf0, 1, wc, aoff);
-    if (nk > 1) stage_a_half(ra, lda2, rows_a, kStep, abuf0 + kTile2Bytes, 0, wc, aoff);
+    stage_a(0, abuf0, 1);
+    if (nk > 1) stage_a(1, abuf0 + kTile2Bytes, 0);
     __builtin_amdgcn_s_barrier();                     // prologue barrier
     if (nk > 1) DLBB_WAIT_VM(4); else DLBB_WAIT_VM(0);  // A-hi(0)
     __builtin_amdgcn_s_barrier();                     // end of interval 0
     int cb = 0;
     for (int u = 0; u < nk; ++u) {
       const char* ab = abuf0 + (u & 1) * kTile2Bytes;
-      read_split_any<NN>(ab, bbuf0 + cb * kTile2Bytes, 1, wc, fr, fq, af, bf);
+      read_split_any<NN, TN>(ab, bbuf0 + cb * kTile2Bytes, 1, wc, fr, fq, af, bf);
       const bool l2 = u + 2 < nk;
-      if (l2) stage_a_half(ra, lda2, rows_a, (u + 2) * kStep, abuf0 + (u & 1) * kTile2Bytes, 0,
-                           wc, aoff);
+      if (l2) stage_a(u + 2, abuf0 + (u & 1) * kTile2Bytes, 0);
       if (BAL && l2) {
         const int cb2 = cb == 0 ? 2 : cb - 1;         // (u + 2) % 3
         stage_b_any<NN, 4, 8>(rb, ldb2, rows_b, u + 2, bbuf0 + cb2 * kTile2Bytes, wc, boff);
@@ -985,6 +1053,17 @@ __global__ void __launch_bounds__(kThreads2, 1) gemm_bf16_nn_256_pingpong3(GemmA
 __global__ void __launch_bounds__(kThreads2, 1) gemm_bf16_nn_256_pingpong3_bal(GemmArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   pingpong_body<true, true>(a, smem);
+}
+
+// weight gradient: C[M, N] = A[K, M]^T · B[K, N] (both row-major over the reduction K); host
+// contract M % 128 == 0, N % 256 == 0, K % 64 == 0.
+__global__ void __launch_bounds__(kThreads2, 1) gemm_bf16_tn_256_pingpong3(GemmArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  pingpong_body<true, false, true>(a, smem);
+}
+__global__ void __launch_bounds__(kThreads2, 1) gemm_bf16_tn_256_pingpong3_bal(GemmArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  pingpong_body<true, true, true>(a, smem);
 }
 
 }  // namespace dlbb
@@ -1129,6 +1208,37 @@ DLBB_API int dlbb_gemm_bf16_nn(const void* A, int64_t lda, const void* B, int64_
                        dim3(kThreads2), kPP6Lds, stream, a);
   else
     hipLaunchKernelGGL(gemm_bf16_nn_256_pingpong3, dim3(static_cast<unsigned>(tiles256)),
+                       dim3(kThreads2), kPP6Lds, stream, a);
+  return hipGetLastError();
+}
+
+// weight-gradient GEMM on the 256^2 ping-pong: C[M, N] = epilogue(A[K, M]^T · B[K, N]) with
+// A = dY [tokens][lda] and B = X [tokens][ldb], both read as transposed LDS images (no transpose
+// pass). epi: 0 or EPI_RESIDUAL (accumulate: residual = the bf16 output itself). One workgroup
+// per 256^2 output tile, the whole reduction in-kernel (dW stored directly, no fp32 partials).
+DLBB_API int dlbb_gemm_bf16_tn(const void* A, int64_t lda, const void* B, int64_t ldb, void* C,
+                               int64_t ldc, int64_t M, int64_t N, int64_t K, const void* residual,
+                               int64_t ldr, int epi, int out_f32, hipStream_t stream) {
+  if (M <= 0 || N <= 0) return hipSuccess;
+  if (K <= 0 || K % BK != 0 || M % 128 != 0 || N % BN2 != 0) return hipErrorInvalidValue;
+  if (lda % 8 || ldb % 8 || lda < M || ldb < N || ldc < N) return hipErrorInvalidValue;
+  if ((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(B)) & 15)
+    return hipErrorInvalidValue;
+  // 32-bit buffer offsets over all K rows of both operands
+  if (K * lda * 2 >= (1LL << 31) || K * ldb * 2 >= (1LL << 31)) return hipErrorInvalidValue;
+  if (epi != 0 && epi != EPI_RESIDUAL) return hipErrorInvalidValue;
+  if (epi == EPI_RESIDUAL && (!residual || out_f32)) return hipErrorInvalidValue;
+  auto al16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+  const int vec_ok = (ldc % 8 == 0) && al16(C) && (epi == 0 || (ldr % 8 == 0 && al16(residual)));
+  GemmArgs a{static_cast<const uint16_t*>(A), static_cast<const uint16_t*>(B), C, nullptr,
+             static_cast<const uint16_t*>(residual), nullptr, M, N, K, lda, ldb, ldc, ldr, epi,
+             out_f32, vec_ok, 0};
+  const int64_t tiles256 = ((M + BM2 - 1) / BM2) * (N / BN2);
+  if (use_bal(K / BK, true))
+    hipLaunchKernelGGL(gemm_bf16_tn_256_pingpong3_bal, dim3(static_cast<unsigned>(tiles256)),
+                       dim3(kThreads2), kPP6Lds, stream, a);
+  else
+    hipLaunchKernelGGL(gemm_bf16_tn_256_pingpong3, dim3(static_cast<unsigned>(tiles256)),
                        dim3(kThreads2), kPP6Lds, stream, a);
   return hipGetLastError();
 }

@@ -262,6 +262,30 @@ def _wgrad_hip256(dy2, x2, out, accumulate, split=None, bias_out=None):
     _wgrad_hip(dy2, x2, out, accumulate, split, bias_out, bn=256)
 
 
+def wgrad_pp_supported(dy2, x2, out, accumulate, bias_out=None) -> bool:
+    """Contract of the 256^2 ping-pong weight-gradient kernel (``dlbb_gemm_bf16_tn``): no fused
+    bias, accumulate only into bf16, output rows N % 128, columns K % 256, reduction M % 64,
+    32-bit buffer offsets over both operands."""
+    M, N = dy2.shape
+    K = x2.shape[1]
+    return (bias_out is None and (not accumulate or out.dtype == torch.bfloat16)
+            and N % 128 == 0 and K % 256 == 0 and M % 64 == 0
+            and M * dy2.stride(0) * 2 < 2 ** 31 and M * x2.stride(0) * 2 < 2 ** 31)
+
+
+def _wgrad_pp(dy2, x2, out, accumulate, split=None, bias_out=None):
+    """256 x 256 output tiles on the forward's ping-pong schedule, both operands staged as
+    transposed-read LDS images (``csrc/gemm.hip`` TN): 4x the MFMA work per staged byte of the
+    128^2 tile, whole reduction per workgroup (dW stored directly). ``split`` is ignored."""
+    M, N = dy2.shape
+    K = x2.shape[1]
+    check(_lib.lib().dlbb_gemm_bf16_tn(
+        dy2.data_ptr(), dy2.stride(0), x2.data_ptr(), x2.stride(0), out.data_ptr(), K, N, K, M,
+        out.data_ptr() if accumulate else None, K if accumulate else 0,
+        EPI_RESIDUAL if accumulate else 0, 1 if out.dtype == torch.float32 else 0,
+        _lib.stream(dy2.device)), "gemm_bf16_tn")
+
+
 def _wgrad_blas(dy2, x2, out, accumulate, split=None, bias_out=None):
     if accumulate and out.dtype == dy2.dtype:
         out.addmm_(dy2.t(), x2)             # the library GEMM accumulates (beta = 1): no add pass
@@ -279,13 +303,16 @@ def _wgrad_blas(dy2, x2, out, accumulate, split=None, bias_out=None):
             bias_out.copy_(db)
 
 
-WGRAD_CHOICES = {}    # (M, N, K, out dtype, fused bias) -> "mfma" | "mfma256" | "blas"
-_WGRAD_IMPLS = {"mfma": _wgrad_hip, "mfma256": _wgrad_hip256, "blas": _wgrad_blas}
+WGRAD_CHOICES = {}    # (M, N, K, out dtype, fused bias) -> "mfma" | "mfma256" | "pp" | "blas"
+_WGRAD_IMPLS = {"mfma": _wgrad_hip, "mfma256": _wgrad_hip256, "pp": _wgrad_pp,
+                "blas": _wgrad_blas}
 
 
 def _wgrad_choice(dy2, x2, out, bias_out=None) -> str:
     mode = os.environ.get("DLBB_GEMM", "auto").lower()
     if mode in _WGRAD_IMPLS:
+        if mode == "pp" and not wgrad_pp_supported(dy2, x2, out, False, bias_out):
+            return "mfma"
         return "mfma" if mode == "mfma256" and dy2.shape[1] % 256 else mode
     key = (dy2.shape[0], dy2.shape[1], x2.shape[1], out.dtype, bias_out is not None)
     if key in WGRAD_CHOICES:
@@ -297,6 +324,8 @@ def _wgrad_choice(dy2, x2, out, bias_out=None) -> str:
     best, best_t, times = "mfma", float("inf"), {}
     for name, fn in _WGRAD_IMPLS.items():
         if name == "mfma256" and (dy2.shape[1] % 256 or os.environ.get("DLBB_WGRAD256") == "0"):
+            continue
+        if name == "pp" and not wgrad_pp_supported(dy2, x2, out, False, bias_out):
             continue
         for _ in range(2):
             fn(dy2, x2, scratch, False, None, scratch_b)
@@ -337,6 +366,8 @@ def wgrad(dy2: torch.Tensor, x2: torch.Tensor, out: Optional[torch.Tensor] = Non
     if (use_hip(dy2, x2) and wgrad_supported(dy2, x2) and out.is_contiguous() and fused_ok
             and out.dtype in (torch.bfloat16, torch.float32)):
         choice = "mfma" if split is not None else _wgrad_choice(dy2, x2, out, bias_out)
+        if choice == "pp" and not wgrad_pp_supported(dy2, x2, out, accumulate, bias_out):
+            choice = "mfma"                 # tuned on a plain store; this call accumulates fp32
         _WGRAD_IMPLS[choice](dy2, x2, out, accumulate, split, bias_out)
         if split is None:
             k = (dy2.shape[0], dy2.shape[1], x2.shape[1], out.dtype, bias_out is not None)

@@ -196,6 +196,34 @@ def test_dgrad_nn_matches_fp32(M, N, K, bal):
     torch.testing.assert_close(out.float(), ref, rtol=2e-2, atol=2e-2 * (K ** 0.5))
 
 
+@pytest.mark.parametrize("T,N,K,bal", [(1024, 384, 768, 2), (64, 256, 256, 0), (2048, 640, 512, 1),
+                                       (16384, 896, 768, 2)])
+def test_wgrad_pingpong_tn_matches_fp32(T, N, K, bal):
+    """256^2 ping-pong weight gradient (both operands transposed-read images): dW = dY^T X
+    against an fp32 reference; output rows ragged by half a tile (N % 256 == 128: the second A
+    image re-staged, never stored), one K-tile, the GPT-2 token count; plain and balanced."""
+    from distributed_llm_backend_benchmark_amd.ops import gemm
+
+    dy = _randn(T, N, seed=41, scale=0.5)
+    x = _randn(T, K, seed=42, scale=0.5)
+    out = torch.full((N, K), float("nan"), dtype=torch.bfloat16, device=DEV)
+    assert gemm.wgrad_pp_supported(dy, x, out, False)
+    gemm.set_bal(bal)
+    try:
+        gemm._wgrad_pp(dy, x, out, False)
+    finally:
+        gemm.set_bal(2)
+    ref = dy.float().t() @ x.float()
+    torch.testing.assert_close(out.float(), ref, rtol=2e-2, atol=2e-2 * (T ** 0.5))
+    # accumulate (bf16 out, residual = out) and fp32 output
+    acc = out.clone()
+    gemm._wgrad_pp(dy, x, acc, True)
+    torch.testing.assert_close(acc.float(), 2 * ref, rtol=3e-2, atol=4e-2 * (T ** 0.5))
+    o32 = torch.empty(N, K, dtype=torch.float32, device=DEV)
+    gemm._wgrad_pp(dy, x, o32, False)
+    torch.testing.assert_close(o32, ref, rtol=1e-3, atol=1e-3 * (T ** 0.5))
+
+
 @pytest.mark.parametrize("M,N,K,split", [(2048, 768, 50304, 4), (520, 512, 64 * 7, 3),
                                          (1024, 256, 4096, 2)])
 def test_dgrad_nn_split_k(M, N, K, split):
