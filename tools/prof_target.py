@@ -1,6 +1,6 @@
 """Tiny driver for PMC-counter profiling: runs ONE op a few times (no timing logic).
-usage: prof_target.py gemm256|gemm256s6|gemm256s7|gemm128|blas|nn|nnplain|reduce8|ln|xent|xentfused|
-embbwd"""
+usage: prof_target.py gemm256|gemm256s6|gemm256s7|gemm128|blas|nn|nnplain|tn|tnplain|wgrad128|
+blastn|reduce8|ln|xent|xentfused|embbwd"""
 import os
 import sys
 
@@ -35,6 +35,18 @@ elif what in ("nn", "nnplain"):  # NN dgrad kernel (transposed-read W), balanced
     out = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
     G.set_bal(0 if what == "nnplain" else 1)
     fn = lambda: G._dgrad_hip(dy, w, out)  # noqa: E731
+elif what in ("tn", "tnplain", "wgrad128", "blastn"):  # weight gradient dW = dY^T X at 8192^3
+    from distributed_llm_backend_benchmark_amd.ops import gemm as G
+
+    T = N = K = 8192
+    dy = torch.randn(T, N, device=dev, generator=g).to(torch.bfloat16)
+    xx = torch.randn(T, K, device=dev, generator=g).to(torch.bfloat16)
+    out = torch.empty(N, K, device=dev, dtype=torch.bfloat16)
+    G.set_bal(0 if what == "tnplain" else 1)
+    fn = {"tn": lambda: G._wgrad_pp(dy, xx, out, False),
+          "tnplain": lambda: G._wgrad_pp(dy, xx, out, False),
+          "wgrad128": lambda: G._wgrad_hip(dy, xx, out, False),
+          "blastn": lambda: G._wgrad_blas(dy, xx, out, False)}[what]
 elif what == "reduce8":
     srcs = [torch.randn(1 << 25, device=dev, generator=g).to(torch.bfloat16) for _ in range(8)]
     fn = lambda: ops.reduce_sum(srcs)  # noqa: E731
