@@ -61,3 +61,22 @@ def test_mlp_train_cpu_matches_autograd():
     torch.testing.assert_close(y, ref)
     for a, b in zip(grads, ref_grads):
         torch.testing.assert_close(a, b)
+
+
+def test_wgrad_pingpong_contract():
+    """TN ping-pong weight gradient: rows N % 128, columns K % 256, tokens % 64, no fused bias,
+    accumulate only into bf16; the LM-head and 7B dW shapes qualify."""
+    bf = torch.bfloat16
+
+    def ok(T, N, K, acc=False, out_dtype=bf, bias=False):
+        dy, x = torch.empty(T, N, dtype=bf), torch.empty(T, K, dtype=bf)
+        out = torch.empty(N, K, dtype=out_dtype)
+        return gemm.wgrad_pp_supported(dy, x, out, acc, torch.empty(N, dtype=bf) if bias else None)
+
+    assert ok(16384, 50304, 768) and ok(4096, 12288, 4096) and ok(64, 128, 256)
+    assert ok(16384, 50304, 768, acc=True)
+    assert not ok(16384, 50304, 768, acc=True, out_dtype=torch.float32)
+    assert ok(16384, 50304, 768, out_dtype=torch.float32)
+    assert not ok(16384, 768, 768, bias=True)
+    assert not ok(16384, 200, 768) and not ok(16384, 768, 640) and not ok(100, 768, 768)
+    assert "pp" in gemm._WGRAD_IMPLS
