@@ -924,12 +924,11 @@ __device__ __forceinline__ void pingpong_body(GemmArgs a, char* smem) {
   bf16x8 af[2][8], bf[2][4];
   const int r_in = lane >> 3, chunk = (lane & 7) ^ (lane >> 3);
   const uint32_t lda2 = static_cast<uint32_t>(a.lda) * 2, ldb2 = static_cast<uint32_t>(a.ldb) * 2;
-  uint32_t aoff = static_cast<uint32_t>(r_in) * lda2 + chunk * 16;
-  if constexpr (TN) {   // image rows 4s + rq: swz_tn needs rq and bit 1 of the wave column
-    const int rq = lane >> 4, slot = lane & 15;
-    aoff = static_cast<uint32_t>(rq) * lda2 +
-           static_cast<uint32_t>(slot ^ (2 * (rq | (((wc >> 1) & 1) << 2)))) * 16;
-  }
+  // TN: image rows 4s + rq, so swz_tn needs rq and bit 1 of the wave column
+  const uint32_t aoff =
+      TN ? static_cast<uint32_t>(lane >> 4) * lda2 +
+               static_cast<uint32_t>((lane & 15) ^ (2 * ((lane >> 4) | (((wc >> 1) & 1) << 2)))) * 16
+         : static_cast<uint32_t>(r_in) * lda2 + chunk * 16;
   uint32_t boff;
   if constexpr (NN) {
     const int rq = lane >> 4, slot = lane & 15;
@@ -944,17 +943,17 @@ __device__ __forceinline__ void pingpong_body(GemmArgs a, char* smem) {
   const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<uint16_t*>(NN ? a.B + n0 : a.B + n0 * a.ldb), 0, 0x7fffffff, 0x00020000);
   constexpr uint32_t kStep = BK * 2;
-  // A half `half` of K-tile u into buffer `buf` (4 wave-instructions per wave either way)
-  auto stage_a = [&](int u, char* buf, int half) {
-    if constexpr (TN)
-      stage_a_half_tn(ra, lda2, rows_a, u, buf, half, wc, aoff);
-    else
-      stage_a_half(ra, lda2, rows_a, static_cast<uint32_t>(u) * kStep, buf, half, wc, aoff);
-  };
+  // TN: A half `half` of K-tile u staged as a transposed image (4 wave-instructions per wave,
+  // as stage_a_half); the NT / NN call sites below are kept verbatim (identical ISA)
+#define DLBB_STAGE_A(U, BUF, HALF, NT_CALL)                                       \
+  do {                                                                            \
+    if constexpr (TN) stage_a_half_tn(ra, lda2, rows_a, (U), (BUF), (HALF), wc, aoff); \
+    else NT_CALL;                                                                 \
+  } while (0)
 
   if (wr == 0) {
     // prologue, row 0: A-lo(0), B(0), B(1); retire the first two
-    stage_a(0, abuf0, 0);
+    DLBB_STAGE_A(0, abuf0, 0, stage_a_half(ra, lda2, rows_a, 0, abuf0, 0, wc, aoff));
     stage_b_any<NN>(rb, ldb2, rows_b, 0, bbuf0, wc, boff);
     if (nk > 1) {
       stage_b_any<NN>(rb, ldb2, rows_b, 1, bbuf0 + kTile2Bytes, wc, boff);
@@ -968,7 +967,10 @@ __device__ __forceinline__ void pingpong_body(GemmArgs a, char* smem) {
       const char* ab = abuf0 + (u & 1) * kTile2Bytes;
       read_split_any<NN, TN>(ab, bbuf0 + cb * kTile2Bytes, 0, wc, fr, fq, af, bf);
       const bool h1 = u + 1 < nk, b2 = u + 2 < nk;
-      if (h1) stage_a(u + 1, abuf0 + ((u + 1) & 1) * kTile2Bytes, 1);
+      if (h1)
+        DLBB_STAGE_A(u + 1, abuf0 + ((u + 1) & 1) * kTile2Bytes, 1,
+                     stage_a_half(ra, lda2, rows_a, (u + 1) * kStep,
+                                  abuf0 + ((u + 1) & 1) * kTile2Bytes, 1, wc, aoff));
       if (b2) {
         const int cb2 = cb == 0 ? 2 : cb - 1;         // (u + 2) % 3
         if (BAL)
@@ -1001,8 +1003,10 @@ __device__ __forceinline__ void pingpong_body(GemmArgs a, char* smem) {
     }
   } else {
     // prologue, row 1: A-hi(0), A-lo(1)
-    stage_a(0, abuf0, 1);
-    if (nk > 1) stage_a(1, abuf0 + kTile2Bytes, 0);
+    DLBB_STAGE_A(0, abuf0, 1, stage_a_half(ra, lda2, rows_a, 0, abuf0, 1, wc, aoff));
+    if (nk > 1)
+      DLBB_STAGE_A(1, abuf0 + kTile2Bytes, 0,
+                   stage_a_half(ra, lda2, rows_a, kStep, abuf0 + kTile2Bytes, 0, wc, aoff));
     __builtin_amdgcn_s_barrier();                     // prologue barrier
     if (nk > 1) DLBB_WAIT_VM(4); else DLBB_WAIT_VM(0);  // A-hi(0)
     __builtin_amdgcn_s_barrier();                     // end of interval 0
@@ -1011,7 +1015,10 @@ __device__ __forceinline__ void pingpong_body(GemmArgs a, char* smem) {
       const char* ab = abuf0 + (u & 1) * kTile2Bytes;
       read_split_any<NN, TN>(ab, bbuf0 + cb * kTile2Bytes, 1, wc, fr, fq, af, bf);
       const bool l2 = u + 2 < nk;
-      if (l2) stage_a(u + 2, abuf0 + (u & 1) * kTile2Bytes, 0);
+      if (l2)
+        DLBB_STAGE_A(u + 2, abuf0 + (u & 1) * kTile2Bytes, 0,
+                     stage_a_half(ra, lda2, rows_a, (u + 2) * kStep,
+                                  abuf0 + (u & 1) * kTile2Bytes, 0, wc, aoff));
       if (BAL && l2) {
         const int cb2 = cb == 0 ? 2 : cb - 1;         // (u + 2) % 3
         stage_b_any<NN, 4, 8>(rb, ldb2, rows_b, u + 2, bbuf0 + cb2 * kTile2Bytes, wc, boff);
@@ -1031,6 +1038,7 @@ __device__ __forceinline__ void pingpong_body(GemmArgs a, char* smem) {
     }
   }
   store_tile_256<NN>(a, acc, m0, n0, wave, lane);
+#undef DLBB_STAGE_A
 }
 
 __global__ void __launch_bounds__(kThreads2, 1) gemm_bf16_nt_256_pingpong3(GemmArgs a) {
