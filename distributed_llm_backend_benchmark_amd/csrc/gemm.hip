@@ -895,13 +895,16 @@ __device__ __forceinline__ void read_split_any(const char* abuf, const char* bbu
 // B1(u+1) together before the barrier ending 2u+1 (row 0 reads tile u+1 in 2u+2). B(1) stays
 // whole in row 0's prologue, so the counted waits below also hold for u = 0.
 // TN (weight gradient, implies NN for B): A [K][lda] row-major over the reduction, staged and
-// read as transposed images (stage_a_half_tn / read_a_tn); no split-K.
+// read as transposed images (stage_a_half_tn / read_a_tn); split-K as for NN.
 template <bool NN, bool BAL = false, bool TN = false>
 __device__ __forceinline__ void pingpong_body(GemmArgs a, char* smem) {
-  if (NN && !TN && gridDim.y > 1) {         // split-K slice blockIdx.y (wave-uniform, SGPR math)
+  if (NN && gridDim.y > 1) {         // split-K slice blockIdx.y (wave-uniform, SGPR math)
     const int s = blockIdx.y, nkt = static_cast<int>(a.K / BK);
     const int kt0 = s * a.kt_split, kt1 = kt0 + a.kt_split < nkt ? kt0 + a.kt_split : nkt;
-    a.A += static_cast<int64_t>(kt0) * BK;
+    if constexpr (TN)                  // TN: A is row-major over the reduction too
+      a.A += static_cast<int64_t>(kt0) * BK * a.lda;
+    else
+      a.A += static_cast<int64_t>(kt0) * BK;
     a.B += static_cast<int64_t>(kt0) * BK * a.ldb;
     a.K = static_cast<int64_t>(kt1 - kt0) * BK;
     a.C = static_cast<float*>(a.C) + static_cast<int64_t>(s) * a.M * a.ldc;
@@ -1224,9 +1227,12 @@ DLBB_API int dlbb_gemm_bf16_nn(const void* A, int64_t lda, const void* B, int64_
 // A = dY [tokens][lda] and B = X [tokens][ldb], both read as transposed LDS images (no transpose
 // pass). epi: 0 or EPI_RESIDUAL (accumulate: residual = the bf16 output itself). One workgroup
 // per 256^2 output tile, the whole reduction in-kernel (dW stored directly, no fp32 partials).
+// split > 1: fp32 partials [split][M][N] in ws + one reduce/cast pass (plain product, ldc == N) —
+// for grids that leave a partial last round (the LM-head dW's tail rows).
 DLBB_API int dlbb_gemm_bf16_tn(const void* A, int64_t lda, const void* B, int64_t ldb, void* C,
                                int64_t ldc, int64_t M, int64_t N, int64_t K, const void* residual,
-                               int64_t ldr, int epi, int out_f32, hipStream_t stream) {
+                               int64_t ldr, int epi, int out_f32, int split, float* ws,
+                               hipStream_t stream) {
   if (M <= 0 || N <= 0) return hipSuccess;
   if (K <= 0 || K % BK != 0 || M % 128 != 0 || N % BN2 != 0) return hipErrorInvalidValue;
   if (lda % 8 || ldb % 8 || lda < M || ldb < N || ldc < N) return hipErrorInvalidValue;
@@ -1242,7 +1248,25 @@ DLBB_API int dlbb_gemm_bf16_tn(const void* A, int64_t lda, const void* B, int64_
              static_cast<const uint16_t*>(residual), nullptr, M, N, K, lda, ldb, ldc, ldr, epi,
              out_f32, vec_ok, 0};
   const int64_t tiles256 = ((M + BM2 - 1) / BM2) * (N / BN2);
-  if (use_bal(K / BK, true))
+  const int nkt = static_cast<int>(K / BK);
+  if (split > 1) {
+    if (!ws || epi != 0 || ldc != N || split > nkt || (reinterpret_cast<uintptr_t>(ws) & 15))
+      return hipErrorInvalidValue;
+    const int dt_f32 = out_f32;
+    a.kt_split = (nkt + split - 1) / split;
+    a.C = ws;
+    a.out_f32 = 1;
+    a.vec_ok = N % 8 == 0;
+    const dim3 g(static_cast<unsigned>(tiles256), static_cast<unsigned>(split));
+    if (use_bal(a.kt_split, true))
+      hipLaunchKernelGGL(gemm_bf16_tn_256_pingpong3_bal, g, dim3(kThreads2), kPP6Lds, stream, a);
+    else
+      hipLaunchKernelGGL(gemm_bf16_tn_256_pingpong3, g, dim3(kThreads2), kPP6Lds, stream, a);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    return dlbb_split_reduce_launch(ws, C, dt_f32, M * N, split, stream);
+  }
+  if (use_bal(nkt, true))
     hipLaunchKernelGGL(gemm_bf16_tn_256_pingpong3_bal, dim3(static_cast<unsigned>(tiles256)),
                        dim3(kThreads2), kPP6Lds, stream, a);
   else

@@ -59,7 +59,7 @@ _SIGS = {
                                   c_void_p, c_int, c_int, c_int, c_void_p, c_void_p]),
     "dlbb_gemm_bf16_tn": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64,
                                   c_int64, c_int64, c_int64, c_void_p, c_int64, c_int, c_int,
-                                  c_void_p]),
+                                  c_int, c_void_p, c_void_p]),
     "dlbb_gemm_set_tile": (None, [c_int]),
     "dlbb_gemm_set_stagger": (None, [c_int]),
     "dlbb_gemm_get_stagger": (c_int, []),

@@ -273,17 +273,52 @@ def wgrad_pp_supported(dy2, x2, out, accumulate, bias_out=None) -> bool:
             and M * dy2.stride(0) * 2 < 2 ** 31 and M * x2.stride(0) * 2 < 2 ** 31)
 
 
+def _pp_launch(dy2, x2, out, accumulate, r0, r1, split):
+    """TN kernel on output rows [r0, r1) (dY columns r0..r1-1), split-K ``split``."""
+    M = dy2.shape[0]
+    K = x2.shape[1]
+    o = out[r0:r1]
+    ws = (torch.empty(split * (r1 - r0) * K, dtype=torch.float32, device=dy2.device)
+          if split > 1 else None)
+    check(_lib.lib().dlbb_gemm_bf16_tn(
+        dy2.data_ptr() + r0 * dy2.element_size(), dy2.stride(0), x2.data_ptr(), x2.stride(0),
+        o.data_ptr(), K, r1 - r0, K, M, o.data_ptr() if accumulate else None,
+        K if accumulate else 0, EPI_RESIDUAL if accumulate else 0,
+        1 if out.dtype == torch.float32 else 0, int(split), _lib.ptr(ws),
+        _lib.stream(dy2.device)), "gemm_bf16_tn")
+
+
+def pp_tail_plan(M: int, N: int, K: int, ncu: int):
+    """Row split of the TN grid: (head_rows, tail_split). A grid whose last round is at most half
+    full (the LM-head dW: 591 tiles on 256 CUs) runs its whole rounds first, then the tail rows
+    with split-K so the tail fills about one round; else (N, 1)."""
+    tiles_n = K // 256
+    m_tiles = -(-N // 256)
+    total = m_tiles * tiles_n
+    rounds, rem = divmod(total, ncu)
+    nkt = M // 64
+    if rounds < 1 or rem == 0 or 2 * rem > ncu:
+        return N, 1
+    head = (rounds * ncu // tiles_n) * 256
+    tail_tiles = -(-(N - head) // 256) * tiles_n
+    split = min(ncu // tail_tiles, nkt // 8)
+    return (head, split) if split >= 2 else (N, 1)
+
+
 def _wgrad_pp(dy2, x2, out, accumulate, split=None, bias_out=None):
     """256 x 256 output tiles on the forward's ping-pong schedule, both operands staged as
     transposed-read LDS images (``csrc/gemm.hip`` TN): 4x the MFMA work per staged byte of the
-    128^2 tile, whole reduction per workgroup (dW stored directly). ``split`` is ignored."""
+    128^2 tile, whole reduction per workgroup (dW stored directly). A partial last round is run
+    as a split-K tail (:func:`pp_tail_plan`; plain stores only). ``split`` is ignored."""
     M, N = dy2.shape
     K = x2.shape[1]
-    check(_lib.lib().dlbb_gemm_bf16_tn(
-        dy2.data_ptr(), dy2.stride(0), x2.data_ptr(), x2.stride(0), out.data_ptr(), K, N, K, M,
-        out.data_ptr() if accumulate else None, K if accumulate else 0,
-        EPI_RESIDUAL if accumulate else 0, 1 if out.dtype == torch.float32 else 0,
-        _lib.stream(dy2.device)), "gemm_bf16_tn")
+    head, tsplit = (N, 1)
+    if not accumulate and os.environ.get("DLBB_PP_TAIL", "1") != "0":
+        ncu = torch.cuda.get_device_properties(dy2.device).multi_processor_count
+        head, tsplit = pp_tail_plan(M, N, K, ncu)
+    _pp_launch(dy2, x2, out, accumulate, 0, head, 1)
+    if head < N:
+        _pp_launch(dy2, x2, out, accumulate, head, N, tsplit)
 
 
 def _wgrad_blas(dy2, x2, out, accumulate, split=None, bias_out=None):

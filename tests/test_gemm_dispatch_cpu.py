@@ -80,3 +80,12 @@ def test_wgrad_pingpong_contract():
     assert not ok(16384, 768, 768, bias=True)
     assert not ok(16384, 200, 768) and not ok(16384, 768, 640) and not ok(100, 768, 768)
     assert "pp" in gemm._WGRAD_IMPLS
+
+
+def test_wgrad_pingpong_tail_plan():
+    # LM-head dW on 256 CUs: 591 tiles -> 510 in two whole rounds, 81-tile tail split 3 ways
+    assert gemm.pp_tail_plan(16384, 50304, 768, 256) == (43520, 3)
+    # whole or mostly full last rounds: no tail
+    assert gemm.pp_tail_plan(4096, 12288, 4096, 256) == (12288, 1)
+    assert gemm.pp_tail_plan(8192, 8192, 8192, 256) == (8192, 1)
+    assert gemm.pp_tail_plan(16384, 896, 768, 256) == (896, 1)

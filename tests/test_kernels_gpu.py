@@ -224,6 +224,40 @@ def test_wgrad_pingpong_tn_matches_fp32(T, N, K, bal):
     torch.testing.assert_close(o32, ref, rtol=1e-3, atol=1e-3 * (T ** 0.5))
 
 
+@pytest.mark.parametrize("T,N,K,r0,split", [(1024, 384, 512, 0, 3), (2048, 896, 768, 256, 4),
+                                             (4096, 640, 256, 128, 2)])
+def test_wgrad_pingpong_tn_split_k(T, N, K, r0, split):
+    """TN split-K on a row range [r0, N) (the LM-head tail path): uneven K slices (16 / 3 K-tiles),
+    a row offset into dY, fp32 partials + reduce; rows outside the range untouched."""
+    from distributed_llm_backend_benchmark_amd.ops import gemm
+
+    dy = _randn(T, N, seed=43, scale=0.5)
+    x = _randn(T, K, seed=44, scale=0.5)
+    out = torch.full((N, K), 7.0, dtype=torch.bfloat16, device=DEV)
+    gemm._pp_launch(dy, x, out, False, r0, N, split)
+    ref = dy.float().t() @ x.float()
+    torch.testing.assert_close(out[r0:].float(), ref[r0:], rtol=2e-2, atol=2e-2 * (T ** 0.5))
+    assert bool((out[:r0] == 7.0).all())
+
+
+def test_wgrad_pingpong_tn_tail_plan_lmhead_scale():
+    """Whole rounds + split-K tail (grid 300 tiles on the device's CUs): matches fp32, and the
+    plan splits it."""
+    from distributed_llm_backend_benchmark_amd.ops import gemm
+
+    ncu = torch.cuda.get_device_properties(DEV).multi_processor_count
+    T, K = 1024, 256
+    N = (ncu + 44) * 256                 # one whole round + a 44-tile tail
+    head, split = gemm.pp_tail_plan(T, N, K, ncu)
+    assert head < N and split >= 2
+    dy = _randn(T, N, seed=45, scale=0.5)
+    x = _randn(T, K, seed=46, scale=0.5)
+    out = torch.empty(N, K, dtype=torch.bfloat16, device=DEV)
+    gemm._wgrad_pp(dy, x, out, False)
+    ref = dy.float().t() @ x.float()
+    torch.testing.assert_close(out.float(), ref, rtol=2e-2, atol=2e-2 * (T ** 0.5))
+
+
 @pytest.mark.parametrize("M,N,K,split", [(2048, 768, 50304, 4), (520, 512, 64 * 7, 3),
                                          (1024, 256, 4096, 2)])
 def test_dgrad_nn_split_k(M, N, K, split):

@@ -1,4 +1,5 @@
-"""A/B the 256^2 ping-pong weight-gradient kernel (TN, plain / balanced DMA issue) against the
+"""A/B the 256^2 ping-pong weight-gradient kernel (TN, plain / balanced DMA issue, with and
+without the split-K tail of a partial last round) against the
 128^2 wgrad kernel (its own split heuristic) and hipBLASLt on the GPT-2 and 7B dW shapes
 (no fused bias: the LM head; the others with a plain store as a kernel-only comparison).
 Interleaved rounds in one process, best of 5; max relative error vs an fp32 product."""
@@ -24,16 +25,18 @@ def timed(fn, iters=10):
     return s.elapsed_time(e) * 1e-3 / iters
 
 
-def pp(bal):
+def pp(bal, tail=True):
     def run(dy, x, dw):
         G.set_bal(bal)
+        os.environ["DLBB_PP_TAIL"] = "1" if tail else "0"
         G._wgrad_pp(dy, x, dw, False)
+        os.environ["DLBB_PP_TAIL"] = "1"
     return run
 
 
 def main():
     C = 768
-    impls = {"pp_plain": pp(0), "pp_bal": pp(1),
+    impls = {"pp_plain": pp(0), "pp_bal": pp(1), "pp_bal_notail": pp(1, tail=False),
              "mfma128": lambda dy, x, dw: G._wgrad_hip(dy, x, dw, False),
              "blas": lambda dy, x, dw: G._wgrad_blas(dy, x, dw, False)}
     shapes = (("gpt2_lmhead", 16384, 50304, C), ("gpt2_fc", 16384, 4 * C, C),
