@@ -31,7 +31,6 @@ import time
 # (every launcher exports it too; the driver's scaling run starts bench.py directly)
 os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
 
-HBM_PEAK_GBPS = 8000.0         # MI355X HBM3E: no all-reduce can report algBW above this
 REF_BUSBW_GBPS = 5.46          # best 3D all-reduce busBW (P=8, 64 MiB bf16)
 REF_LAT_512B_US = {2: 22.9, 8: 32.0}
 REF_BUSBW_8MIB = 7.53
@@ -117,9 +116,8 @@ def _allreduce_sweep(comm, max_mib: int):
         if not res:
             out.append({"bytes": nbytes, "impl": None, "invalid": invalid})
             continue
-        for k in [k for k, v in res.items() if algbw_gbps("allreduce", nbytes, v, P)
-                  > HBM_PEAK_GBPS]:
-            invalid.append(f"{k}:above_hbm_roofline")   # an empty call, not a measurement
+        for k in [k for k, v in res.items() if too_fast("allreduce", nbytes, v, P)]:
+            invalid.append(f"{k}:below_roofline")   # an empty call, not a measurement
             del res[k]
         if not res:
             out.append({"bytes": nbytes, "impl": None, "invalid": invalid})
@@ -133,6 +131,14 @@ def _allreduce_sweep(comm, max_mib: int):
                     **({"invalid": invalid} if invalid else {})})
         del data, flat
     return out
+
+
+def too_fast(op_name: str, nbytes: int, seconds: float, P: int):
+    """The reason a timing is physically impossible (below the traffic-based memory / xGMI
+    roofline of ``stats.bandwidth.min_seconds``: the call enqueued no work), else None."""
+    from distributed_llm_backend_benchmark_amd.stats.bandwidth import roofline_violation
+
+    return roofline_violation(op_name, nbytes, seconds, P)
 
 
 def _checked(comm, op, ref) -> bool:
@@ -216,6 +222,11 @@ def main(argv=None) -> int:
                           for nb in (128, 256)]
         if args.impl == "custom" and not cands:
             raise SystemExit("custom all-reduce unavailable (setup or self-test failed)")
+    calibration = None
+    if P > 1 and comm.is_gpu and args.impl in ("best", "custom"):
+        # the node-measured IPC-vs-RCCL crossovers the library's "auto" policy uses (rank-max,
+        # agreed on every rank; parallel/custom_allreduce.py calibrate)
+        calibration = getattr(car, "calibration", None) if car is not None else None
     trial, invalid = {}, []
     op, op_label = None, None
     ref = data.float()                  # fp32 reference sum: every candidate is checked once
@@ -260,9 +271,9 @@ def main(argv=None) -> int:
         op.ipc_kernel().raise_if_error()
     bus = busbw_gbps("allreduce", nbytes, per_step, P)
     alg = algbw_gbps("allreduce", nbytes, per_step, P)
-    if alg > HBM_PEAK_GBPS:
-        raise SystemExit(f"algBW {alg:.0f} GB/s is above the HBM roofline: {op_label} timed an "
-                         "empty call, refusing to report it")
+    why = too_fast("allreduce", nbytes, per_step, P)
+    if why:
+        raise SystemExit(f"{why}: {op_label} timed an empty call, refusing to report it")
 
     side = {}
     if not args.no_side:
@@ -365,8 +376,10 @@ def main(argv=None) -> int:
                     cop.run()
                 comm.sync()
                 t = _timed_steps(comm, cop, 10) / 10
-                res[label] = {"busbw_GBps": busbw_gbps(name, cop.message_bytes, t, P),
-                              "ms": t * 1e3}
+                why = too_fast(name, cop.message_bytes, t, P)
+                res[label] = ({"invalid": why} if why else
+                              {"busbw_GBps": busbw_gbps(name, cop.message_bytes, t, P),
+                               "ms": t * 1e3})
                 cop.close()
                 del cop
             coll[name] = res
@@ -418,6 +431,8 @@ def main(argv=None) -> int:
                       "enqueue nothing at one rank and are excluded" if P == 1 else "")),
             **side,
         }
+        if calibration:
+            rec["allreduce_calibration"] = calibration
         if coll:
             rec["collectives_same_message"] = coll
         if sweep:

@@ -94,6 +94,7 @@ def main(argv=None) -> int:
 
     t0 = time.perf_counter()
     comm = init_distributed(args.backend)
+    comm.install_tune_agreement()       # GEMM kernel choices agreed on rank-max timings
     comm.barrier()
     init_elapsed = time.perf_counter() - t0
     rank, world = comm.rank, comm.world_size
@@ -191,6 +192,7 @@ def main(argv=None) -> int:
     car = getattr(model, "ipc_allreduce", lambda: None)()
     if car is not None:                 # a timed-out IPC all-reduce must not pass silently
         car.raise_if_error()
+    calibration = car.calibration if car is not None else None
     ar_bytes = fwd_bytes
     if ev:
         metrics.metrics["forward_device_times"] = ev
@@ -213,6 +215,8 @@ def main(argv=None) -> int:
                 "distributed_llm_backend_benchmark_amd.ops.gemm", fromlist=["x"]).FALLBACKS["count"],
             "gemm_kernel_mix": __import__(
                 "distributed_llm_backend_benchmark_amd.ops.gemm", fromlist=["x"]).kernel_mix(),
+            # node-measured IPC-vs-RCCL crossovers behind allreduce=auto (None: RCCL only)
+            "allreduce_calibration": calibration,
         }
         results = {
             "experiment": config["experiment"]["name"],

@@ -133,6 +133,8 @@ def run(args, comm, overlap: bool):
         "tflops_per_gpu": model.flops_per_token(args.seq) * args.batch * args.seq
         * args.steps / dt / 1e12,
         "gemm_kernel_mix": _gemm.kernel_mix(),
+        # node-measured IPC-vs-RCCL crossovers (rank-max, agreed; None: no IPC kernel)
+        "allreduce_calibration": getattr(getattr(tr, "_car", None), "calibration", None),
     }
     if args.save_checkpoint:
         tr.save_checkpoint(args.save_checkpoint)
@@ -152,6 +154,7 @@ def main(argv=None) -> int:
     from ..utils import tracing
 
     comm = init_distributed(args.backend, timeout_s=900)
+    comm.install_tune_agreement()       # GEMM kernel choices agreed on rank-max timings
     if args.trace:
         tracing.enable()
     with tracing.torch_profile(args.torch_profile, comm.rank):

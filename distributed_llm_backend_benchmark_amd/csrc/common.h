@@ -135,6 +135,39 @@ __device__ __forceinline__ float gelu_tanh_grad(float x) {
   return 0.5f * (1.0f + t) + 0.5f * x * (1.0f - t * t) * k0 * (1.0f + 3.0f * k1 * x2);
 }
 
+// ---------------------------------------------------------------------------------------
+// Per-workgroup start / end stamps (opt-in diagnostic, dlbb_stamps_set): a stamped launch
+// writes one 32-byte record per workgroup, [t_start, t_end, HW_ID | XCC_ID << 32,
+// blockIdx.x | blockIdx.y << 32], times from s_memrealtime (100 MHz, shared by every CU).
+// Only thread 0 of a workgroup stores, once, after the workgroup's last barrier — nothing the
+// kernel computes reads a stamp. Host registry in csrc/reduce.hip; unstamped launches (the
+// default) run kernels without any stamp code.
+enum StampKind { STAMP_GEMM_NT = 1, STAMP_GEMM_NN = 2, STAMP_GEMM_TN = 3, STAMP_REDUCE = 4,
+                 STAMP_SPIN = 5 };
+// host: `nrec` records for one launch of `kind`, or nullptr (stamps off / buffer full)
+uint64_t* stamp_acquire(int kind, int64_t nrec);
+
+__device__ __forceinline__ uint64_t stamp_now() {
+  uint64_t t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) : : "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
+
+// thread 0 of the workgroup, after its final barrier
+__device__ __forceinline__ void stamp_write(uint64_t* recs, uint64_t t0) {
+  const uint64_t t1 = stamp_now();
+  const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);     // HW_REG_HW_ID
+  const uint32_t xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20);   // HW_REG_XCC_ID
+  const uint64_t wg = blockIdx.x + static_cast<uint64_t>(blockIdx.y) * gridDim.x;
+  uint64_t* r = recs + 4 * wg;
+  r[0] = t0;
+  r[1] = t1;
+  r[2] = hw | (static_cast<uint64_t>(xcc) << 32);
+  r[3] = blockIdx.x | (static_cast<uint64_t>(blockIdx.y) << 32);
+}
+
 // Grid size for memory-bound grid-stride kernels: enough blocks to fill 256 CUs several
 // times over, capped (CDNA guide, Guideline 11).
 inline int stream_grid(int64_t work_items, int block) {

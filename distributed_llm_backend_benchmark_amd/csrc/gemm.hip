@@ -896,8 +896,11 @@ __device__ __forceinline__ void read_split_any(const char* abuf, const char* bbu
 // whole in row 0's prologue, so the counted waits below also hold for u = 0.
 // TN (weight gradient, implies NN for B): A [K][lda] row-major over the reduction, staged and
 // read as transposed images (stage_a_half_tn / read_a_tn); split-K as for NN.
-template <bool NN, bool BAL = false, bool TN = false>
-__device__ __forceinline__ void pingpong_body(GemmArgs a, char* smem) {
+// STAMP (diagnostic variants only): per-workgroup start / end records into `st` (common.h).
+template <bool NN, bool BAL = false, bool TN = false, bool STAMP = false>
+__device__ __forceinline__ void pingpong_body(GemmArgs a, char* smem, uint64_t* st = nullptr) {
+  uint64_t t_start = 0;
+  if constexpr (STAMP) t_start = stamp_now();
   if (NN && gridDim.y > 1) {         // split-K slice blockIdx.y (wave-uniform, SGPR math)
     const int s = blockIdx.y, nkt = static_cast<int>(a.K / BK);
     const int kt0 = s * a.kt_split, kt1 = kt0 + a.kt_split < nkt ? kt0 + a.kt_split : nkt;
@@ -1041,6 +1044,10 @@ __device__ __forceinline__ void pingpong_body(GemmArgs a, char* smem) {
     }
   }
   store_tile_256<NN>(a, acc, m0, n0, wave, lane);
+  if constexpr (STAMP) {
+    __syncthreads();
+    if (threadIdx.x == 0) stamp_write(st, t_start);
+  }
 #undef DLBB_STAGE_A
 }
 
@@ -1077,9 +1084,35 @@ __global__ void __launch_bounds__(kThreads2, 1) gemm_bf16_tn_256_pingpong3_bal(G
   pingpong_body<true, true, true>(a, smem);
 }
 
+// Stamped diagnostic twins of the six ping-pong kernels (dlbb_stamps_set): identical schedule,
+// plus one start / end record per workgroup.
+#define DLBB_PP_STAMPED(NAME, NN_, BAL_, TN_)                                          \
+  __global__ void __launch_bounds__(kThreads2, 1) NAME##_st(GemmArgs a, uint64_t* st) { \
+    extern __shared__ __attribute__((aligned(16))) char smem[];                        \
+    pingpong_body<NN_, BAL_, TN_, true>(a, smem, st);                                  \
+  }
+DLBB_PP_STAMPED(gemm_bf16_nt_256_pingpong3, false, false, false)
+DLBB_PP_STAMPED(gemm_bf16_nt_256_pingpong3_bal, false, true, false)
+DLBB_PP_STAMPED(gemm_bf16_nn_256_pingpong3, true, false, false)
+DLBB_PP_STAMPED(gemm_bf16_nn_256_pingpong3_bal, true, true, false)
+DLBB_PP_STAMPED(gemm_bf16_tn_256_pingpong3, true, false, true)
+DLBB_PP_STAMPED(gemm_bf16_tn_256_pingpong3_bal, true, true, true)
+#undef DLBB_PP_STAMPED
+
 }  // namespace dlbb
 
 using namespace dlbb;
+
+// Launch a ping-pong kernel, or its stamped twin when stamping is on (dlbb_stamps_set).
+#define DLBB_PP_LAUNCH(KERNEL, KIND, GRID, ARGS)                                          \
+  do {                                                                                   \
+    const dim3 g_(GRID);                                                                 \
+    uint64_t* st_ = stamp_acquire(KIND, static_cast<int64_t>(g_.x) * g_.y);              \
+    if (st_)                                                                             \
+      hipLaunchKernelGGL(KERNEL##_st, g_, dim3(kThreads2), kPP6Lds, stream, ARGS, st_);  \
+    else                                                                                 \
+      hipLaunchKernelGGL(KERNEL, g_, dim3(kThreads2), kPP6Lds, stream, ARGS);            \
+  } while (0)
 
 static int dlbb_gemm_force_tile = 0;   // 0 = heuristic, 128 or 256 = force (A/B testing)
 
@@ -1146,9 +1179,9 @@ DLBB_API int dlbb_gemm_bf16_nt(const void* A, int64_t lda, const void* B, int64_
       hipLaunchKernelGGL(gemm_bf16_nt_256_persistent, dim3(static_cast<unsigned>(grid)), b,
                          2 * kBuf2Bytes, stream, a);
     } else if (mode == 7 || (mode == 6 && use_bal(K / BK, false)))
-      hipLaunchKernelGGL(gemm_bf16_nt_256_pingpong3_bal, g, b, kPP6Lds, stream, a);
+      DLBB_PP_LAUNCH(gemm_bf16_nt_256_pingpong3_bal, STAMP_GEMM_NT, g, a);
     else if (mode == 6)
-      hipLaunchKernelGGL(gemm_bf16_nt_256_pingpong3, g, b, kPP6Lds, stream, a);
+      DLBB_PP_LAUNCH(gemm_bf16_nt_256_pingpong3, STAMP_GEMM_NT, g, a);
     else if (mode == 3)
       hipLaunchKernelGGL(gemm_bf16_nt_256_kernel<3>, g, b, 2 * kBuf2Bytes, stream, a);
     else if (mode == 2)
@@ -1200,26 +1233,26 @@ DLBB_API int dlbb_gemm_bf16_nn(const void* A, int64_t lda, const void* B, int64_
     // fp32 partials [split][M][N] in ws, then one reduce + bf16 cast pass. Plain product only.
     if (!ws || epi != 0 || out_f32 || ldc != N || split > nkt) return hipErrorInvalidValue;
     a.kt_split = (nkt + split - 1) / split;
+    split = (nkt + a.kt_split - 1) / a.kt_split;   // every slice starts inside the reduction
     a.C = ws;
     a.out_f32 = 1;
     a.vec_ok = (reinterpret_cast<uintptr_t>(ws) & 15) == 0 && N % 8 == 0;
     if (use_bal(a.kt_split, true))
-      hipLaunchKernelGGL(gemm_bf16_nn_256_pingpong3_bal,
-                         dim3(static_cast<unsigned>(tiles256), split), dim3(kThreads2), kPP6Lds,
-                         stream, a);
+      DLBB_PP_LAUNCH(gemm_bf16_nn_256_pingpong3_bal, STAMP_GEMM_NN,
+                     dim3(static_cast<unsigned>(tiles256), split), a);
     else
-      hipLaunchKernelGGL(gemm_bf16_nn_256_pingpong3, dim3(static_cast<unsigned>(tiles256), split),
-                         dim3(kThreads2), kPP6Lds, stream, a);
+      DLBB_PP_LAUNCH(gemm_bf16_nn_256_pingpong3, STAMP_GEMM_NN,
+                     dim3(static_cast<unsigned>(tiles256), split), a);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     return dlbb_split_reduce_launch(ws, C, 0, M * N, split, stream);
   }
   if (use_bal(nkt, true))
-    hipLaunchKernelGGL(gemm_bf16_nn_256_pingpong3_bal, dim3(static_cast<unsigned>(tiles256)),
-                       dim3(kThreads2), kPP6Lds, stream, a);
+    DLBB_PP_LAUNCH(gemm_bf16_nn_256_pingpong3_bal, STAMP_GEMM_NN,
+                   dim3(static_cast<unsigned>(tiles256)), a);
   else
-    hipLaunchKernelGGL(gemm_bf16_nn_256_pingpong3, dim3(static_cast<unsigned>(tiles256)),
-                       dim3(kThreads2), kPP6Lds, stream, a);
+    DLBB_PP_LAUNCH(gemm_bf16_nn_256_pingpong3, STAMP_GEMM_NN,
+                   dim3(static_cast<unsigned>(tiles256)), a);
   return hipGetLastError();
 }
 
@@ -1254,23 +1287,24 @@ DLBB_API int dlbb_gemm_bf16_tn(const void* A, int64_t lda, const void* B, int64_
       return hipErrorInvalidValue;
     const int dt_f32 = out_f32;
     a.kt_split = (nkt + split - 1) / split;
+    split = (nkt + a.kt_split - 1) / a.kt_split;   // every slice starts inside the reduction
     a.C = ws;
     a.out_f32 = 1;
     a.vec_ok = N % 8 == 0;
     const dim3 g(static_cast<unsigned>(tiles256), static_cast<unsigned>(split));
     if (use_bal(a.kt_split, true))
-      hipLaunchKernelGGL(gemm_bf16_tn_256_pingpong3_bal, g, dim3(kThreads2), kPP6Lds, stream, a);
+      DLBB_PP_LAUNCH(gemm_bf16_tn_256_pingpong3_bal, STAMP_GEMM_TN, g, a);
     else
-      hipLaunchKernelGGL(gemm_bf16_tn_256_pingpong3, g, dim3(kThreads2), kPP6Lds, stream, a);
+      DLBB_PP_LAUNCH(gemm_bf16_tn_256_pingpong3, STAMP_GEMM_TN, g, a);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     return dlbb_split_reduce_launch(ws, C, dt_f32, M * N, split, stream);
   }
   if (use_bal(nkt, true))
-    hipLaunchKernelGGL(gemm_bf16_tn_256_pingpong3_bal, dim3(static_cast<unsigned>(tiles256)),
-                       dim3(kThreads2), kPP6Lds, stream, a);
+    DLBB_PP_LAUNCH(gemm_bf16_tn_256_pingpong3_bal, STAMP_GEMM_TN,
+                   dim3(static_cast<unsigned>(tiles256)), a);
   else
-    hipLaunchKernelGGL(gemm_bf16_tn_256_pingpong3, dim3(static_cast<unsigned>(tiles256)),
-                       dim3(kThreads2), kPP6Lds, stream, a);
+    DLBB_PP_LAUNCH(gemm_bf16_tn_256_pingpong3, STAMP_GEMM_TN,
+                   dim3(static_cast<unsigned>(tiles256)), a);
   return hipGetLastError();
 }

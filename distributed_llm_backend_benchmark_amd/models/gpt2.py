@@ -102,6 +102,10 @@ class GPT2(nn.Module):
         self.wpe = _param((cfg.block_size, cfg.n_embd), 0.01, device, gen)
         # gradient sinks (trainer opt-in): wpe is used once per step; wte twice (input
         # embedding + tied LM head), both uses accumulate into its .grad in-kernel
+        # both embedding tables get their gradient only from the embedding backward, the last
+        # op of the step: the DDP trainer gives them a bucket of their own (parallel/ddp.py)
+        self.wte._dlbb_late_grad = True
+        self.wpe._dlbb_late_grad = True
         self._fused_embedding = os.environ.get("DLBB_EMB", "1") != "0"   # A/B switch
         if self._fused_embedding:
             self.wpe._dlbb_single_use = True

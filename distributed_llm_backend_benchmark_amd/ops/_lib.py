@@ -35,6 +35,11 @@ _SIGS = {
                                 c_float, c_void_p]),
     "dlbb_reduce_sum_grid": (c_int, [ctypes.POINTER(c_void_p), c_int, c_void_p, c_int64, c_int,
                                      c_int, c_float, c_int, c_void_p]),
+    "dlbb_spin_ns": (c_int, [c_int64, c_int, c_void_p]),
+    "dlbb_stamps_set": (None, [c_void_p, c_int64]),
+    "dlbb_stamps_launches": (c_int64, []),
+    "dlbb_stamps_entry": (c_int, [c_int64, ctypes.POINTER(c_int), ctypes.POINTER(c_int64),
+                                  ctypes.POINTER(c_int64)]),
     "dlbb_cast": (c_int, [c_void_p, c_int, c_void_p, c_int, c_int64, c_void_p]),
     "dlbb_pack_rows": (c_int, [c_void_p, c_int, c_int64, c_void_p, c_int, c_int64, c_int64,
                                c_int64, c_void_p]),

@@ -18,6 +18,13 @@ from ._lib import check, dt, ptr, stream, use_hip
 MAX_REDUCE_SRCS = 16
 
 
+def spin_ns(ns: int, nblocks: int, device=None) -> None:
+    """Hold ``nblocks`` workgroup slots for ``ns`` nanoseconds on the current stream (the
+    link-bound duration of an emulated collective, ``csrc/reduce.hip`` spin_kernel)."""
+    dev = device or torch.device("cuda", torch.cuda.current_device())
+    check(_lib.lib().dlbb_spin_ns(int(ns), int(nblocks), stream(dev)), "spin_ns")
+
+
 def reduce_sum(srcs: Sequence[torch.Tensor], out: Optional[torch.Tensor] = None,
                out_dtype: Optional[torch.dtype] = None, scale: float = 1.0,
                nblocks: Optional[int] = None) -> torch.Tensor:

@@ -30,6 +30,32 @@ FALLBACKS = {"count": 0}
 TUNE_LOG = []         # (kind, key, {impl: median ms}, choice) per autotuned shape
 
 
+# Collective autotuning: with ranks > 1 every decision must be the same on every rank (TP ranks
+# running different kernels for one shape are rank-imbalanced, and the step waits for the
+# slowest). ``set_tune_agreement(fn)`` installs ``fn(names, times) -> times``, the element-wise
+# MAX of each candidate's time over all ranks (a host side channel,
+# ``parallel.comm.Comm.agree_max``); every rank then takes the argmin of the same numbers.
+_AGREE = None
+
+
+def set_tune_agreement(fn) -> None:
+    """Install (or with None remove) the cross-rank agreement of autotune timings."""
+    global _AGREE
+    _AGREE = fn
+
+
+def _choose(times: dict):
+    """(best candidate, the timings it was chosen on): rank-max timings when an agreement is
+    installed, first-listed candidate on ties."""
+    names = list(times)
+    vals = [float(times[n]) for n in names]
+    if _AGREE is not None:
+        vals = [float(v) for v in _AGREE(names, vals)]
+    agreed = {n: round(v, 4) for n, v in zip(names, vals)}
+    best = min(names, key=lambda n: (agreed[n], names.index(n)))
+    return best, agreed
+
+
 def _log_tune(kind, key, times, best) -> None:
     TUNE_LOG.append((kind, key, times, best))
     if os.environ.get("DLBB_TUNE_LOG") == "1":
@@ -156,7 +182,7 @@ def _autotune(key, args) -> str:
         return CHOICES[key]
     if torch.cuda.is_current_stream_capturing():
         return "mfma"
-    best, best_t, times = "mfma", float("inf"), {}
+    times = {}
     for name, fn in _IMPLS.items():
         for _ in range(2):
             fn(*args)
@@ -168,10 +194,8 @@ def _autotune(key, args) -> str:
             e.record()
             e.synchronize()
             ts.append(s.elapsed_time(e))
-        t = sorted(ts)[len(ts) // 2]
-        times[name] = round(t, 4)
-        if t < best_t:
-            best, best_t = name, t
+        times[name] = sorted(ts)[len(ts) // 2]
+    best, times = _choose(times)
     CHOICES[key] = best
     _log_tune("linear", key, times, best)
     return best
@@ -302,6 +326,9 @@ def pp_tail_plan(M: int, N: int, K: int, ncu: int):
     head = (rounds * ncu // tiles_n) * 256
     tail_tiles = -(-(N - head) // 256) * tiles_n
     split = min(ncu // tail_tiles, nkt // 8)
+    if split >= 2:                      # no empty trailing slice: as the kernel's launch clamps
+        kt = -(-nkt // split)
+        split = -(-nkt // kt)
     return (head, split) if split >= 2 else (N, 1)
 
 
@@ -356,7 +383,7 @@ def _wgrad_choice(dy2, x2, out, bias_out=None) -> str:
         return "mfma"
     scratch = torch.empty_like(out)
     scratch_b = torch.empty_like(bias_out) if bias_out is not None else None
-    best, best_t, times = "mfma", float("inf"), {}
+    times = {}
     for name, fn in _WGRAD_IMPLS.items():
         if name == "mfma256" and (dy2.shape[1] % 256 or os.environ.get("DLBB_WGRAD256") == "0"):
             continue
@@ -372,10 +399,8 @@ def _wgrad_choice(dy2, x2, out, bias_out=None) -> str:
             e0.record()
             e0.synchronize()
             ts.append(s0.elapsed_time(e0))
-        t = sorted(ts)[len(ts) // 2]
-        times[name] = round(t, 4)
-        if t < best_t:
-            best, best_t = name, t
+        times[name] = sorted(ts)[len(ts) // 2]
+    best, times = _choose(times)
     WGRAD_CHOICES[key] = best
     _log_tune("wgrad", key, times, best)
     return best
@@ -483,7 +508,7 @@ def _dgrad_choice(dy2, w, out, dgelu=None) -> str:
         return DGRAD_CHOICES[key]
     if torch.cuda.is_current_stream_capturing():
         return "mfma"
-    best, best_t, times = "mfma", float("inf"), {}
+    times = {}
     scratch = torch.empty_like(out)
     for name, fn in _DGRAD_IMPLS.items():
         for _ in range(2):
@@ -496,10 +521,8 @@ def _dgrad_choice(dy2, w, out, dgelu=None) -> str:
             e0.record()
             e0.synchronize()
             ts.append(s0.elapsed_time(e0))
-        t = sorted(ts)[len(ts) // 2]
-        times[name] = round(t, 4)
-        if t < best_t:
-            best, best_t = name, t
+        times[name] = sorted(ts)[len(ts) // 2]
+    best, times = _choose(times)
     DGRAD_CHOICES[key] = best
     _log_tune("dgrad", key, times, best)
     return best
@@ -574,5 +597,7 @@ def kernel_mix() -> dict:
     out["hand_written_time_fraction"] = round(ours / total, 4) if total else None
     out["dgrad_library_calls"] = CALLS.get(("dgrad", "library"), 0)   # not in the fraction
     out["forced"] = os.environ.get("DLBB_GEMM", "auto")
+    # True: every choice above was made on rank-max timings agreed by all ranks
+    out["agreed_across_ranks"] = _AGREE is not None
     out["contract_fallbacks"] = FALLBACKS["count"]
     return out

@@ -37,31 +37,43 @@ class FlatAdamW:
 
     @torch.no_grad()
     def step(self, grad: torch.Tensor, working_bf16: Optional[torch.Tensor] = None,
-             grad_scale: float = 1.0) -> None:
-        self.t += 1
-        b1, b2 = self.betas
+             grad_scale: float = 1.0, ranges=None, advance: bool = True) -> None:
+        """One AdamW update. ``ranges``: update only these [start, end) element ranges (one
+        kernel each; the rest of the step's ranges follow in later calls with
+        ``advance=False``, so the step count — and the bias correction — moves once)."""
         if grad.numel() != self.p.numel():
             raise ValueError("grad / master size mismatch")
-        if use_hip(self.p, grad) and self.t_dev is not None:
-            self.t_dev.add_(1)
-            check(_lib.lib().dlbb_adamw_devstep(
-                self.p.data_ptr(), self.m.data_ptr(), self.v.data_ptr(), grad.data_ptr(),
-                dt(grad), _lib.ptr(working_bf16), self.p.numel(), self.lr, b1, b2, self.eps,
-                self.wd, self.t_dev.data_ptr(), float(grad_scale), _lib.stream(self.p.device)),
-                "adamw_devstep")
-            return
-        if use_hip(self.p, grad):
-            check(_lib.lib().dlbb_adamw(
-                self.p.data_ptr(), self.m.data_ptr(), self.v.data_ptr(), grad.data_ptr(),
-                dt(grad), _lib.ptr(working_bf16), self.p.numel(), self.lr, b1, b2, self.eps,
-                self.wd, self.t, float(grad_scale), _lib.stream(self.p.device)), "adamw")
-            return
-        g = grad.float() * grad_scale
-        self.m.mul_(b1).add_(g, alpha=1 - b1)
-        self.v.mul_(b2).addcmul_(g, g, value=1 - b2)
-        bc1 = 1 - b1 ** self.t
-        bc2 = 1 - b2 ** self.t
-        denom = (self.v / bc2).sqrt_().add_(self.eps)
-        self.p.mul_(1 - self.lr * self.wd).addcdiv_(self.m, denom, value=-self.lr / bc1)
-        if working_bf16 is not None:
-            working_bf16.copy_(self.p.to(working_bf16.dtype))
+        if advance:
+            self.t += 1
+            if self.t_dev is not None and use_hip(self.p, grad):
+                self.t_dev.add_(1)
+        b1, b2 = self.betas
+        n = self.p.numel()
+        for a, e in (ranges or [(0, n)]):
+            if not 0 <= a <= e <= n:
+                raise ValueError(f"AdamW range [{a}, {e}) outside [0, {n})")
+            if e == a:
+                continue
+            p, m, v, g = self.p[a:e], self.m[a:e], self.v[a:e], grad[a:e]
+            w = working_bf16[a:e] if working_bf16 is not None else None
+            if use_hip(self.p, grad) and self.t_dev is not None:
+                check(_lib.lib().dlbb_adamw_devstep(
+                    p.data_ptr(), m.data_ptr(), v.data_ptr(), g.data_ptr(), dt(grad),
+                    _lib.ptr(w), e - a, self.lr, b1, b2, self.eps, self.wd,
+                    self.t_dev.data_ptr(), float(grad_scale), _lib.stream(self.p.device)),
+                    "adamw_devstep")
+            elif use_hip(self.p, grad):
+                check(_lib.lib().dlbb_adamw(
+                    p.data_ptr(), m.data_ptr(), v.data_ptr(), g.data_ptr(), dt(grad),
+                    _lib.ptr(w), e - a, self.lr, b1, b2, self.eps, self.wd, self.t,
+                    float(grad_scale), _lib.stream(self.p.device)), "adamw")
+            else:
+                gf = g.float() * grad_scale
+                m.mul_(b1).add_(gf, alpha=1 - b1)
+                v.mul_(b2).addcmul_(gf, gf, value=1 - b2)
+                bc1 = 1 - b1 ** self.t
+                bc2 = 1 - b2 ** self.t
+                denom = (v / bc2).sqrt_().add_(self.eps)
+                p.mul_(1 - self.lr * self.wd).addcdiv_(m, denom, value=-self.lr / bc1)
+                if w is not None:
+                    w.copy_(p.to(w.dtype))

@@ -250,8 +250,8 @@ class ReduceScatter(CollectiveOp):
         self._native = True
         self._car = None
         if self.opts.get("direct"):
-            self._car, self._rid = _direct_ipc(self.comm, self.inp,
-                                               16 // self.inp.element_size() * self.P)
+            # the kernel reduces 8-element vectors of each rank's 1/P share
+            self._car, self._rid = _direct_ipc(self.comm, self.inp, 8 * self.P)
             self._reg_owner = (self._car, self._rid)
             self.impl = "custom"
 

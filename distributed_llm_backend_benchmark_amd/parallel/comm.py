@@ -124,8 +124,51 @@ class Comm:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
+    def cpu_group(self):
+        """A gloo group over the same ranks for host-side agreement traffic that must not be
+        queued behind (or interleaved with) RCCL kernels on the device; None when the default
+        group is already gloo or there is one rank. Creating it is collective: the first call
+        must happen at the same point on every rank."""
+        if self.world_size == 1 or self.backend == "gloo":
+            return None
+        g = self._extra.get("cpu_group")
+        if g is None:
+            g = dist.new_group(backend="gloo")
+            self._extra["cpu_group"] = g
+        return g
+
+    def agree_max(self, names: Sequence[str], values: Sequence[float]) -> List[float]:
+        """Collective: the element-wise MAX of ``values`` over all ranks, through the host side
+        channel (:meth:`cpu_group`). Every rank must pass the same ``names`` in the same order
+        (checked: a mismatch raises on every rank instead of mixing candidates)."""
+        vals = [float(v) for v in values]
+        if self.world_size == 1:
+            return vals
+        out: List[Any] = [None] * self.world_size
+        dist.all_gather_object(out, (list(names), vals), group=self.cpu_group())
+        if any(o[0] != list(names) or len(o[1]) != len(vals) for o in out):
+            raise RuntimeError(f"agree_max: ranks disagree on the candidates: {[o[0] for o in out]}")
+        return [max(o[1][i] for o in out) for i in range(len(vals))]
+
+    def install_tune_agreement(self) -> None:
+        """Make the GEMM autotuner's decisions collective (ops.gemm.set_tune_agreement): every
+        rank picks the kernel with the smallest rank-max time. Collective (creates the side
+        group): call at the same point on every rank, before the first GEMM."""
+        if self.world_size == 1:
+            return
+        from ..ops import gemm
+
+        self.cpu_group()
+        gemm.set_tune_agreement(self.agree_max)
+        self._extra["tune_agreement"] = True
+
     def destroy(self) -> None:
         import sys
+
+        if self._extra.pop("tune_agreement", False):
+            from ..ops import gemm
+
+            gemm.set_tune_agreement(None)
 
         native = sys.modules.get(__package__ + ".rccl_native")
         if native is not None:          # our own RCCL communicators go first
@@ -153,14 +196,17 @@ def init_distributed(backend: str = "auto", timeout_s: float = 600.0,
         if not torch.cuda.is_available():
             raise RuntimeError("backend rccl requested but no HIP device is visible")
         ndev = torch.cuda.device_count()
-        if local_rank >= ndev:
+        local_world = int(os.environ.get("LOCAL_WORLD_SIZE", "0"))
+        if local_world > ndev:
             # RCCL refuses two ranks on one GPU only late (duplicate-device error at the first
             # collective); fail at init with the reason instead
             raise RuntimeError(
-                f"LOCAL_RANK {local_rank} but only {ndev} visible HIP device(s): RCCL needs one "
-                f"GPU per rank (launch at most {ndev} ranks per node, or use backend gloo with "
-                f"device='cuda' to share a GPU for rehearsals)")
-        dev_index = local_rank
+                f"{local_world} local ranks but only {ndev} visible HIP device(s): RCCL needs "
+                f"one GPU per rank (launch at most {ndev} ranks per node, or use backend gloo "
+                f"with device='cuda' to share a GPU for rehearsals)")
+        # launchers that set no LOCAL_RANK (mpirun / srun: LOCAL_RANK defaults to the global
+        # rank) or expose one GPU per process (ndev == 1) map by modulo
+        dev_index = local_rank % ndev
         torch.cuda.set_device(dev_index)
         dev = torch.device("cuda", dev_index)
     else:

@@ -21,6 +21,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import time
 from typing import Dict, Optional, Tuple
 
 import torch
@@ -50,6 +51,11 @@ _INSTANCES: Dict[int, "CustomAllReduce"] = {}
 #     the fastest validated one, which is what its JSON reports.
 ONESHOT_MAX_BYTES = 256 << 10
 AUTO_MAX_BYTES = 8 << 20
+# Those two constants are only the defaults: at world > 1 the instance re-derives both on the
+# node it runs on (:meth:`CustomAllReduce.calibrate`, the analogue of the reference's per-message
+# CCL_ALLREDUCE algorithm choice, collectives/3d/launch_dsccl.sh:46-47): RCCL vs one-shot /
+# two-shot / registered pull / push timed at CALIB_SIZES, rank-max, agreed by every rank.
+CALIB_SIZES = (4 << 10, 64 << 10, 512 << 10, 4 << 20, 16 << 20, 64 << 20)
 
 
 class CustomAllReduce:
@@ -96,6 +102,7 @@ class CustomAllReduce:
         self.healthy = False
         self.reg_healthy = False
         self.push_healthy = False
+        self.calibration: Optional[dict] = None
         self._regs: Dict[tuple, int] = {}
         self._reg_keep: Dict[int, torch.Tensor] = {}   # rid -> registered tensor (kept alive)
         self._reg_refs: Dict[int, int] = {}            # rid -> register() calls not released
@@ -349,6 +356,111 @@ class CustomAllReduce:
             print("[custom all-reduce] registered-buffer self-test failed (pull/push per rank): "
                   f"{flags}", flush=True)
 
+    # ------------------------------------------------------------------ calibration
+    def _time_calls(self, fn, iters: int) -> float:
+        """Seconds per call of ``iters`` back-to-back calls on this rank (barrier first, host
+        clock around a synchronize on both sides)."""
+        for _ in range(2):
+            fn()
+        torch.cuda.synchronize(self.comm.device)
+        self.comm.barrier()
+        torch.cuda.synchronize(self.comm.device)
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            fn()
+        torch.cuda.synchronize(self.comm.device)
+        return (time.perf_counter() - t0) / iters
+
+    def calibrate(self, sizes=CALIB_SIZES, iters: int = 20) -> dict:
+        """Collective: time the process group's all-reduce (RCCL) against the IPC forms —
+        staged one-shot, staged two-shot, registered in-place pull and push — at each size on
+        this node, take every candidate's RANK-MAX time (``Comm.agree_max``, a host side
+        channel), and set from it, identically on every rank:
+
+        * ``oneshot_max``: the largest size up to which one-shot is at least as fast as
+          two-shot (from the smallest size on);
+        * ``auto_max``: the largest size up to which the better staged form beats RCCL (0 when
+          RCCL wins already at the smallest size — ``auto`` then never uses the IPC kernel);
+        * ``reg_max``: the same for the registered in-place forms (long-lived buffers).
+
+        The table lands in :attr:`calibration` (result JSONs record it). Every candidate runs on
+        fresh rank-seeded data and is checked against the fp32 sum once; a candidate that fails
+        anywhere is dropped everywhere."""
+        W, dev = self.comm.world_size, self.comm.device
+        sizes = [int(n) for n in sizes if n <= self.capacity]
+        table = []
+        for n in sizes:
+            g = torch.Generator(device=dev)
+            g.manual_seed(4242 + self.comm.rank)
+            x = torch.randn(n // 2, generator=g, device=dev).to(torch.bfloat16)
+            ref = x.float()
+            dist.all_reduce(ref)
+            work = torch.empty_like(x)
+            cands = {"rccl": lambda: dist.all_reduce(work)}
+            if self.healthy and self.supports(x):
+                cands["oneshot"] = lambda: self.all_reduce(x, work, algo=ONESHOT)
+                if n % (8 * x.element_size() * W) == 0:
+                    cands["twoshot"] = lambda: self.all_reduce(x, work, algo=TWOSHOT)
+            rid = None
+            if self.reg_healthy and self.supports_registered(work):
+                rid = self.register(work)          # collective; released below
+                cands["reg_pull"] = lambda: self.all_reduce_registered(work, rid)
+                if self.push_healthy:
+                    cands["reg_push"] = lambda: self.all_reduce_registered(work, rid, push=True)
+            names = list(cands)
+            ok = []
+            for name in names:                 # correctness first, on every rank
+                try:
+                    work.copy_(x)
+                    cands[name]()
+                    torch.cuda.synchronize(dev)
+                    good = bool(torch.allclose(work.float(), ref, rtol=2e-2, atol=5e-2 * W))
+                    ok.append(1.0 if good and self.check_error() == 0 else 0.0)
+                except Exception:  # noqa: BLE001 - a failed launch fails the candidate
+                    ok.append(0.0)
+            # passed everywhere = min over ranks = -(max over ranks of -passed)
+            passed = [-v for v in self.comm.agree_max(names, [-v for v in ok])]
+            times = [self._time_calls(cands[k], iters) if good > 0 else float("inf")
+                     for k, good in zip(names, passed)]
+            agreed = self.comm.agree_max(names, times)
+            table.append({"bytes": n, "us": {k: (round(t * 1e6, 2) if t != float("inf")
+                                                 else None) for k, t in zip(names, agreed)}})
+            if rid is not None:
+                self.deregister(rid)
+        self._apply_calibration(table)
+        return self.calibration
+
+    def _apply_calibration(self, table) -> None:
+        def t(row, k):
+            v = row["us"].get(k)
+            return float("inf") if v is None else v
+
+        oneshot_max = 0
+        for row in table:
+            if t(row, "oneshot") <= t(row, "twoshot"):
+                oneshot_max = row["bytes"]
+            else:
+                break
+        auto_max = 0
+        for row in table:
+            if min(t(row, "oneshot"), t(row, "twoshot")) < t(row, "rccl"):
+                auto_max = row["bytes"]
+            else:
+                break
+        reg_max = 0
+        for row in table:
+            if min(t(row, "reg_pull"), t(row, "reg_push")) < t(row, "rccl"):
+                reg_max = row["bytes"]
+            else:
+                break
+        if table:
+            self.oneshot_max = oneshot_max
+            self.auto_max = auto_max
+        self.reg_max = reg_max
+        self.calibration = {"world": self.comm.world_size, "table": table,
+                            "oneshot_max": self.oneshot_max, "auto_max": self.auto_max,
+                            "reg_max": reg_max, "agreed": "rank-max"}
+
     def close(self) -> None:
         if getattr(self, "h", None):
             self.lib.dlbb_car_destroy(self.h)
@@ -383,6 +495,9 @@ def get_custom_allreduce(comm: Comm, self_test: bool = True) -> Optional[CustomA
             inst = CustomAllReduce(comm, capacity_bytes=cap)
             if self_test:
                 inst.self_test()
+                if (comm.world_size > 1 and inst.healthy
+                        and os.environ.get("DLBB_CUSTOM_AR_CALIBRATE", "1") != "0"):
+                    inst.calibrate()
         except RuntimeError as e:   # agreed on all ranks: fall back to RCCL everywhere
             if comm.rank == 0:
                 print(f"[custom all-reduce disabled] {e}", flush=True)

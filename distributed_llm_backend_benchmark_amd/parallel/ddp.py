@@ -38,7 +38,7 @@ import torch
 import torch.distributed as dist
 
 from ..ops import FlatAdamW
-from ..ops.elementwise import ChunkTable, ScaleTable, reduce_sum
+from ..ops.elementwise import ChunkTable, ScaleTable, reduce_sum, spin_ns
 from ..utils import tracing
 from .comm import Comm
 
@@ -59,6 +59,7 @@ class _Bucket:
         self.ready = 0
         self.launched = False
         self.work = None
+        self.done_event = None
         self.table: Optional[ChunkTable] = None
         self.table_key = None
 
@@ -68,7 +69,7 @@ class FlatParamTrainer:
                  betas=(0.9, 0.95), weight_decay: float = 0.0, bucket_mb: float = 64.0,
                  overlap: bool = True, mode: str = "view", allreduce: str = "rccl",
                  grad_dtype: torch.dtype = torch.bfloat16, comm_blocks: Optional[int] = None,
-                 emulate_comm: bool = False):
+                 emulate_comm=False, emulate_world: int = 8, split_optimizer: bool = True):
         if mode == "view" and grad_dtype != torch.bfloat16:
             raise ValueError("grad_dtype must be the parameter dtype (bf16) in mode='view': "
                              "autograd accumulates straight into the bucket views; use "
@@ -91,8 +92,18 @@ class FlatParamTrainer:
         # padded to a multiple of `bucket_align` elements (ZeRO shards need P-divisible buckets)
         cap = int(bucket_mb * (1 << 20) / torch.tensor([], dtype=grad_dtype).element_size())
         balign = max(_ALIGN, self._bucket_align())
+        # Params whose gradient completes only at the very END of backward (model opt-in
+        # ``_dlbb_late_grad``: the embedding tables — the embedding backward is the step's last
+        # op) start a bucket of their own, so the bucket all-reduced after backward holds only
+        # them, not the last blocks' gradients too (GPT-2's tail bucket was
+        # blocks 1-0 + the tied 77 MB wte, ~43 % of the gradient bytes).
         offs, spans, cur, start, total = [], [], [], 0, 0
         for i, p in enumerate(order):
+            late = getattr(p, "_dlbb_late_grad", False)
+            if late and cur and not any(getattr(q, "_dlbb_late_grad", False) for q in cur):
+                total = (total + balign - 1) // balign * balign
+                spans.append((start, total, cur))
+                cur, start = [], total
             offs.append(total)
             total += (p.numel() + _ALIGN - 1) // _ALIGN * _ALIGN
             cur.append(p)
@@ -162,13 +173,30 @@ class FlatParamTrainer:
         # stream — the local HBM traffic of one rank's all-reduce (read 2n, write n: bucket +
         # zeros -> bucket, so gradients are unchanged) — to measure what overlapped bucket
         # reductions cost the backward pass on one GPU (tools/ddp_overlap.py)
+        # emulate_comm=<GB/s> (a float) additionally makes each stand-in LINK-BOUND: after the
+        # local traffic, `comm_blocks` (default 32) workgroups hold their CU slots for the time a
+        # ring all-reduce of the bucket takes at that bus bandwidth over `emulate_world` ranks,
+        # bytes * 2(P-1)/P / busBW — so an exposed tail and long-resident comm workgroups show
+        # up on one GPU.
         self._emu_zero = None
+        self._emu_gbps = None
+        self._emu_world = int(emulate_world)
         if emulate_comm:
             if self.world != 1 or dev.type != "cuda":
                 raise ValueError("emulate_comm is a single-GPU measurement (world 1, HIP device)")
             self._comm_stream = torch.cuda.Stream(dev, priority=_COMM_PRIORITY)
             self._emu_zero = torch.zeros(max(b.end - b.start for b in self.buckets),
                                          dtype=grad_dtype, device=dev)
+            if not isinstance(emulate_comm, bool):
+                self._emu_gbps = float(emulate_comm)
+                if self._emu_gbps <= 0:
+                    raise ValueError("emulate_comm bus bandwidth must be > 0 GB/s")
+        # the optimizer runs in two ranges: everything but the last bucket as soon as those
+        # buckets are reduced, then the last bucket — whose all-reduce (it is ready only at the
+        # end of backward) overlaps the first range's AdamW instead of preceding all of it
+        self.split_optimizer = split_optimizer
+        self.timeline = False       # record comm events per bucket (comm_tail_report)
+        self._tl = None
         self.step_count = 0
 
     # ------------------------------------------------------------------ hooks for subclasses
@@ -179,8 +207,9 @@ class FlatParamTrainer:
         self.master = self.flat_param.float()
         self.opt = FlatAdamW(self.master, lr=lr, betas=betas, weight_decay=weight_decay)
 
-    def _optimizer_step(self) -> None:
-        self.opt.step(self.flat_grad, working_bf16=self.flat_param, grad_scale=1.0 / self.world)
+    def _optimizer_step(self, ranges=None, advance: bool = True) -> None:
+        self.opt.step(self.flat_grad, working_bf16=self.flat_param, grad_scale=1.0 / self.world,
+                      ranges=ranges, advance=advance)
 
     # ------------------------------------------------------------------ buckets
     def _add_bucket(self, start: int, end: int, params) -> None:
@@ -238,8 +267,16 @@ class FlatParamTrainer:
             cs = self._comm_stream
             cs.wait_stream(torch.cuda.current_stream(buf.device))
             with torch.cuda.stream(cs):
+                self._tl_mark(b, "start", cs)
                 reduce_sum([buf, self._emu_zero[:buf.numel()]], out=buf,
                            nblocks=self.comm_blocks)
+                if self._emu_gbps is not None:
+                    P = self._emu_world
+                    nbytes = buf.numel() * buf.element_size()
+                    ns = int(nbytes * 2.0 * (P - 1) / P / self._emu_gbps)   # bytes / (GB/s) = ns
+                    spin_ns(ns, self.comm_blocks or 32)
+                self._tl_mark(b, "end", cs)
+            self._mark_done(b, cs)
             b.work = "stream"
             return
         if self.world == 1:
@@ -252,8 +289,11 @@ class FlatParamTrainer:
             if ws is not None:
                 cs.wait_stream(ws)
             with torch.cuda.stream(cs):
+                self._tl_mark(b, "start", cs)
                 self._car.all_reduce_registered(buf, self._bucket_reg[b.idx],
                                                 nblocks=self.comm_blocks)
+                self._tl_mark(b, "end", cs)
+            self._mark_done(b, cs)
             b.work = "stream"
         elif self._car is not None and self._car.healthy and self._car.supports(buf):
             cs = self._comm_stream
@@ -261,7 +301,10 @@ class FlatParamTrainer:
             if ws is not None:
                 cs.wait_stream(ws)
             with torch.cuda.stream(cs):
+                self._tl_mark(b, "start", cs)
                 self._car.all_reduce_(buf, nblocks=self.comm_blocks)
+                self._tl_mark(b, "end", cs)
+            self._mark_done(b, cs)
             b.work = "stream"
         elif self._native is not None:
             # our RCCL communicator on the dedicated comm stream, ordered after the
@@ -270,7 +313,10 @@ class FlatParamTrainer:
             cs.wait_stream(torch.cuda.current_stream(buf.device))
             if ws is not None:
                 cs.wait_stream(ws)
+            self._tl_mark(b, "start", cs)
             self._native.enqueue("allreduce", buf, buf, buf.numel(), stream=cs.cuda_stream)
+            self._tl_mark(b, "end", cs)
+            self._mark_done(b, cs)
             b.work = "stream"
         elif ws is not None:
             # ProcessGroupNCCL orders its stream after the CURRENT stream: issue from the side
@@ -281,16 +327,41 @@ class FlatParamTrainer:
         else:
             b.work = dist.all_reduce(buf, async_op=True)
 
-    def finish(self) -> None:
-        """Launch what backward did not (e.g. overlap off), then wait every bucket."""
+    def _mark_done(self, b: _Bucket, cs) -> None:
+        """Per-bucket completion event on the comm stream (waited per bucket by the split
+        optimizer; a stream-wide wait would also wait for later buckets)."""
+        ev = b.done_event
+        if ev is None:
+            ev = b.done_event = torch.cuda.Event()
+        ev.record(cs)
+
+    def _tl_mark(self, b: _Bucket, what: str, stream) -> None:
+        if self._tl is None:
+            return
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record(stream)
+        self._tl["buckets"].setdefault(b.idx, {})[what] = ev
+
+    def _wait_bucket(self, b: _Bucket) -> None:
+        if b.work == "stream":
+            cur = torch.cuda.current_stream(self.flat_grad.device)
+            if b.done_event is not None:
+                cur.wait_event(b.done_event)
+            else:
+                cur.wait_stream(self._comm_stream)
+        elif b.work is not None:
+            b.work.wait()
+
+    def _launch_rest(self) -> None:
         while self._next < len(self.buckets):
             self._launch(self.buckets[self._next])
             self._next += 1
+
+    def finish(self) -> None:
+        """Launch what backward did not (e.g. overlap off), then wait every bucket."""
+        self._launch_rest()
         for b in self.buckets:
-            if b.work == "stream":
-                torch.cuda.current_stream(self.flat_grad.device).wait_stream(self._comm_stream)
-            elif b.work is not None:
-                b.work.wait()
+            self._wait_bucket(b)
         if self._wgrad_stream is not None:      # side-stream weight gradients (and copies)
             torch.cuda.current_stream(self.flat_grad.device).wait_stream(self._wgrad_stream)
 
@@ -317,16 +388,70 @@ class FlatParamTrainer:
         """One full training step: forward, backward (+ overlapped all-reduce), AdamW."""
         self.zero_grad()
         self._reset()
+        if self.timeline and not torch.cuda.is_current_stream_capturing():
+            self._tl = {"buckets": {}}
         with tracing.range("fwd"):
             loss = self.model(idx, targets)
         with tracing.range("bwd+overlapped_grad_sync"):
             loss.backward()
-        with tracing.range("grad_sync_tail"):
-            self.finish()
+        if self._tl is not None:
+            self._tl["bwd_end"] = torch.cuda.Event(enable_timing=True)
+            self._tl["bwd_end"].record(torch.cuda.current_stream(self.flat_grad.device))
         self.step_count += 1
-        with tracing.range("optimizer"):
-            self._optimizer_step()
+        if self._split_optimizer_ok():
+            with tracing.range("grad_sync_tail+optimizer"):
+                self._launch_rest()
+                head, tail = self.buckets[:-1], self.buckets[-1]
+                for b in head:
+                    self._wait_bucket(b)
+                if self._wgrad_stream is not None:
+                    torch.cuda.current_stream(self.flat_grad.device).wait_stream(
+                        self._wgrad_stream)
+                self._optimizer_step(ranges=[(0, tail.start)], advance=True)
+                self._wait_bucket(tail)
+                self._optimizer_step(ranges=[(tail.start, self.numel)], advance=False)
+        else:
+            with tracing.range("grad_sync_tail"):
+                self.finish()
+            with tracing.range("optimizer"):
+                self._optimizer_step()
+        if self._tl is not None:
+            self._tl["opt_end"] = torch.cuda.Event(enable_timing=True)
+            self._tl["opt_end"].record(torch.cuda.current_stream(self.flat_grad.device))
+            self._tl_last, self._tl = self._tl, None
         return float(loss.item()) if sync_loss else loss.detach()
+
+    def _split_optimizer_ok(self) -> bool:
+        return (self.split_optimizer and len(self.buckets) > 1 and self.mode == "view"
+                and type(self)._optimizer_step is FlatParamTrainer._optimizer_step)
+
+    def comm_tail_report(self) -> Optional[dict]:
+        """For the last step run with ``timeline = True`` (stream-issued reductions: custom,
+        native, emulated): each bucket's comm start / end relative to the end of backward, the
+        bytes whose reduction STARTED after backward ended, and the exposed comm time (last
+        reduction end minus backward end; 0 when everything finished under backward)."""
+        tl = getattr(self, "_tl_last", None)
+        if not tl or "bwd_end" not in tl:
+            return None
+        torch.cuda.synchronize(self.flat_grad.device)
+        ref = tl["bwd_end"]
+        rows, after, last_end = [], 0, float("-inf")
+        esz = self.flat_grad.element_size()
+        for b in self.buckets:
+            e = tl["buckets"].get(b.idx)
+            if not e or "start" not in e or "end" not in e:
+                continue
+            st, en = ref.elapsed_time(e["start"]), ref.elapsed_time(e["end"])
+            nbytes = (b.end - b.start) * esz
+            rows.append({"bucket": b.idx, "bytes": nbytes, "start_ms": round(st, 4),
+                         "end_ms": round(en, 4)})
+            if st >= 0:
+                after += nbytes
+            last_end = max(last_end, en)
+        return {"buckets": rows, "bytes_reduced_after_backward": after,
+                "exposed_comm_ms": round(max(0.0, last_end), 4) if rows else None,
+                "optimizer_end_ms": round(ref.elapsed_time(tl["opt_end"]), 4)
+                if "opt_end" in tl else None}
 
     # ------------------------------------------------------------------ HIP graph
     def capture_step(self, idx: torch.Tensor, targets: torch.Tensor):

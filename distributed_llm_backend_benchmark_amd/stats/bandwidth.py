@@ -79,3 +79,65 @@ def legacy_bandwidth_gbps(num_elements: int, seconds: float, num_ranks: int,
     if seconds is None or seconds <= 0:
         return None
     return (num_elements * 2 * num_ranks / seconds) / GIB
+
+
+# ------------------------------------------------------------------------------ rooflines
+# Ceilings a real measurement cannot beat (bench.py refuses a timing below them: such a call
+# enqueued no work). Generous on purpose — they catch empty calls, not slow ones.
+HBM_PEAK_GBPS = 8000.0            # MI355X HBM3E spec peak
+ONDIE_PEAK_GBPS = 17200.0         # Infinity Cache / fabric ceiling for a working set on die
+ONDIE_BYTES = 256 << 20           # Infinity Cache (MALL) capacity
+XGMI_LINK_GBPS = 153.0            # one xGMI link (7 per GPU), taken per direction: generous
+
+# minimum bytes the slowest rank's own memory reads + writes per call (message = ``nbytes`` per
+# rank, as the sweep defines it); P = 1 collectives are timed out of place (a copy)
+_LOCAL_TRAFFIC = {
+    "allreduce": lambda b, p: 2.0 * b,                 # read input, write result
+    "allgather": lambda b, p: (p + 1.0) * b,           # read own chunk, write P chunks
+    "reduce_scatter": lambda b, p: b + b / p,
+    "alltoall": lambda b, p: 2.0 * b,
+    "alltoall_moe": lambda b, p: 2.0 * b,
+    "gather": lambda b, p: (p + 1.0) * b,              # the root
+    "scatter": lambda b, p: (p + 1.0) * b,
+    "broadcast": lambda b, p: b,
+    "reduce": lambda b, p: b,
+    "sendrecv": lambda b, p: 2.0 * b,
+}
+# minimum bytes a rank must RECEIVE over its P - 1 links per call (any algorithm)
+_RECV = {
+    "allreduce": lambda b, p: b * (p - 1) / p,
+    "allgather": lambda b, p: b * (p - 1.0),
+    "reduce_scatter": lambda b, p: b * (p - 1) / p,
+    "alltoall": lambda b, p: b * (p - 1) / p,
+    "alltoall_moe": lambda b, p: b * (p - 1) / p,
+    "broadcast": lambda b, p: b,
+    "sendrecv": lambda b, p: b,
+}
+
+
+def min_seconds(op: str, nbytes: float, num_ranks: int) -> float:
+    """Lower bound on one call's time: the rank's own memory traffic at the HBM peak (the on-die
+    cache ceiling when it fits in the 256 MiB Infinity Cache) and, at P > 1, the bytes it must
+    receive spread over all P - 1 xGMI links at the link peak."""
+    p = int(num_ranks)
+    if op not in _LOCAL_TRAFFIC:
+        raise KeyError(f"unknown op {op!r}")
+    local = _LOCAL_TRAFFIC[op](float(nbytes), p)
+    peak = ONDIE_PEAK_GBPS if local <= ONDIE_BYTES else HBM_PEAK_GBPS
+    t = local / (peak * GB)
+    if p > 1 and op in _RECV:
+        t = max(t, _RECV[op](float(nbytes), p) / ((p - 1) * XGMI_LINK_GBPS * GB))
+    return t
+
+
+def roofline_violation(op: str, nbytes: float, seconds: float, num_ranks: int) -> Optional[str]:
+    """None when ``seconds`` is physically possible for ``op``; else the reason (an empty call
+    or a timing that missed the work) — never report such a number."""
+    if seconds is None or seconds <= 0:
+        return "non-positive time"
+    floor = min_seconds(op, nbytes, num_ranks)
+    if seconds < floor:
+        return (f"{op} of {int(nbytes)} B at P={num_ranks} took {seconds * 1e6:.3f} us, below "
+                f"the {floor * 1e6:.3f} us memory/link roofline")
+    return None
+

@@ -181,6 +181,39 @@ def test_custom_allreduce_registered_ranks_on_one_gpu(world):
             assert good and err == 0, (kind, nb, good, err)
 
 
+def _car_calibrate_worker(rank, world):
+    from distributed_llm_backend_benchmark_amd.parallel.comm import init_distributed
+    from distributed_llm_backend_benchmark_amd.parallel.custom_allreduce import CustomAllReduce
+
+    comm = init_distributed("gloo", device="cuda")
+    car = CustomAllReduce(comm, capacity_bytes=8 << 20)
+    car.self_test()
+    cal = car.calibrate(sizes=(4 << 10, 64 << 10, 1 << 20), iters=5)
+    live = car.reg_counts()
+    res = (cal, car.oneshot_max, car.auto_max, car.reg_max, live)
+    comm.barrier()
+    car.close()
+    comm.destroy()
+    return res
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_custom_allreduce_calibration_agreed_ranks_on_one_gpu(world):
+    """the IPC-vs-RCCL crossovers are measured on the node (rank-max,
+    agreed): every rank ends with the identical table and the identical oneshot/auto/reg
+    thresholds, every candidate passed its check, and the per-size registrations are released."""
+    res = run_multiprocess(_car_calibrate_worker, world, timeout=600)
+    cal0 = res[0][0]
+    for cal, osm, am, rm, live in res:
+        assert cal == cal0
+        assert (osm, am, rm) == (cal0["oneshot_max"], cal0["auto_max"], cal0["reg_max"])
+        assert live == (0, 0), live
+    assert [r["bytes"] for r in cal0["table"]] == [4 << 10, 64 << 10, 1 << 20]
+    for row in cal0["table"]:
+        assert set(row["us"]) == {"rccl", "oneshot", "twoshot", "reg_pull", "reg_push"}, row
+        assert all(v is not None and v > 0 for v in row["us"].values()), row
+
+
 def _car_lifecycle_worker(rank, world):
     import torch
 

@@ -406,8 +406,107 @@ def test_rccl_init_refuses_more_ranks_than_gpus(monkeypatch):
     monkeypatch.setattr(C.torch.cuda, "is_available", lambda: True)
     monkeypatch.setattr(C.torch.cuda, "device_count", lambda: 1)
     monkeypatch.setenv("LOCAL_RANK", "3")
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "4")
     monkeypatch.setenv("RANK", "3")
     monkeypatch.setenv("WORLD_SIZE", "4")
     monkeypatch.setenv("MASTER_PORT", "1")
     with pytest.raises(RuntimeError, match="one GPU per rank"):
         C.init_distributed("rccl")
+
+
+@pytest.mark.parametrize("env,ndev,expect", [
+    ({"RANK": "8", "WORLD_SIZE": "16"}, 8, 0),                 # mpirun/srun: no LOCAL_RANK
+    ({"RANK": "3", "LOCAL_RANK": "3", "WORLD_SIZE": "4"}, 1, 0),  # one GPU exposed per process
+    ({"RANK": "5", "LOCAL_RANK": "5", "LOCAL_WORLD_SIZE": "8", "WORLD_SIZE": "8"}, 8, 5),
+])
+def test_rccl_init_maps_local_rank_modulo_devices(monkeypatch, env, ndev, expect):
+    """Launchers without LOCAL_RANK (it defaults to the global rank) or with one visible GPU per
+    process map rank -> device by modulo; only more LOCAL ranks than devices is refused."""
+    from distributed_llm_backend_benchmark_amd.parallel import comm as C
+
+    picked = []
+
+    class _Stop(Exception):
+        pass
+
+    def _init_pg(**kw):
+        raise _Stop()
+
+    monkeypatch.setattr(C.torch.cuda, "is_available", lambda: True)
+    monkeypatch.setattr(C.torch.cuda, "device_count", lambda: ndev)
+    monkeypatch.setattr(C.torch.cuda, "set_device", lambda i: picked.append(i))
+    monkeypatch.setattr(C.dist, "is_initialized", lambda: False)
+    monkeypatch.setattr(C.dist, "init_process_group", _init_pg)
+    for k in ("LOCAL_RANK", "LOCAL_WORLD_SIZE"):
+        monkeypatch.delenv(k, raising=False)
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    monkeypatch.setenv("MASTER_PORT", "1")
+    with pytest.raises(_Stop):
+        C.init_distributed("rccl")
+    assert picked == [expect]
+
+
+def _agree_worker(rank, world):
+    from distributed_llm_backend_benchmark_amd.ops import gemm
+    from distributed_llm_backend_benchmark_amd.parallel.comm import init_distributed
+
+    comm = init_distributed("gloo")
+    comm.install_tune_agreement()
+    # local timings disagree: alone, rank 0 would pick mfma and rank 1 blas
+    local = [{"mfma": 1.0, "blas": 2.0}, {"mfma": 3.0, "blas": 2.5},
+             {"mfma": 0.5, "blas": 0.9}, {"mfma": 2.9, "blas": 0.1}][rank]
+    best, agreed = gemm._choose(local)
+    mismatch = None
+    try:                                   # a rank with another candidate list: refused
+        comm.agree_max(["mfma"] if rank == 0 else ["mfma", "pp"], [1.0] * (1 + (rank > 0)))
+    except RuntimeError as e:
+        mismatch = str(e)
+    comm.destroy()
+    alone, _ = (min(local, key=local.get), None)
+    return best, agreed, alone, mismatch, gemm._AGREE is None
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_gemm_autotune_choice_agreed_on_rank_max(world):
+    """autotune decisions are collective — every rank takes the argmin of
+    the rank-max timings, so ranks with opposite local preferences still run one kernel."""
+    res = run_multiprocess(_agree_worker, world)
+    bests = {r[0] for r in res}
+    assert len(bests) == 1, res
+    agreed = res[0][1]
+    assert all(r[1] == agreed for r in res)
+    assert agreed["mfma"] == max([1.0, 3.0, 0.5, 2.9][:world])
+    assert agreed["blas"] == max([2.0, 2.5, 0.9, 0.1][:world])
+    assert res[0][2] == "mfma" and res[1][2] == "blas"       # they would have disagreed
+    assert all(r[3] and "disagree" in r[3] for r in res)
+    assert all(r[4] for r in res)                            # destroy() uninstalls it
+
+
+def test_ddp_tail_bucket_holds_only_late_params_and_split_optimizer_is_exact():
+    """the embedding tables (gradient complete only at the end of backward)
+    get a bucket of their own, so nothing else waits for the embedding backward; the optimizer
+    split around that bucket (AdamW on the other buckets first) is bitwise the single update."""
+    from distributed_llm_backend_benchmark_amd.models.gpt2 import GPT2, GPT2Config
+    from distributed_llm_backend_benchmark_amd.parallel.ddp import FlatParamTrainer
+
+    cfg = GPT2Config(vocab_size=256, block_size=16, n_layer=3, n_head=2, n_embd=64)
+    g = torch.Generator().manual_seed(0)
+    idx = torch.randint(0, 256, (2, 17), generator=g)
+    finals = {}
+    for split in (True, False):
+        m = GPT2(cfg, seed=5)
+        tr = FlatParamTrainer(m, None, lr=1e-2, bucket_mb=0.05, split_optimizer=split)
+        tail = tr.buckets[-1]
+        assert {id(p) for p in tail.params} == {id(m.wte), id(m.wpe)}
+        assert all(not getattr(p, "_dlbb_late_grad", False)
+                   for b in tr.buckets[:-1] for p in b.params)
+        assert len(tr.buckets) > 2
+        assert tr._split_optimizer_ok() == split
+        for _ in range(3):
+            tr.step(idx[:, :-1], idx[:, 1:])
+        finals[split] = (tr.flat_param.clone(), tr.master.clone(), tr.opt.t)
+        tr.close()
+    assert torch.equal(finals[True][0], finals[False][0])
+    assert torch.equal(finals[True][1], finals[False][1])
+    assert finals[True][2] == finals[False][2] == 3

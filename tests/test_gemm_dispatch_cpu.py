@@ -89,3 +89,11 @@ def test_wgrad_pingpong_tail_plan():
     assert gemm.pp_tail_plan(4096, 12288, 4096, 256) == (12288, 1)
     assert gemm.pp_tail_plan(8192, 8192, 8192, 256) == (8192, 1)
     assert gemm.pp_tail_plan(16384, 896, 768, 256) == (896, 1)
+    # a large requested split leaves no empty trailing slice (advisor r02: 28 slices of
+    # ceil(256/28) = 10 K-tiles would start slices 26, 27 past the 256 K-tiles)
+    for shape in [(16384, 44288, 768, 256), (16384, 50304, 768, 256), (4096, 33024, 4096, 256)]:
+        head, split = gemm.pp_tail_plan(*shape)
+        nkt = shape[0] // 64
+        if split > 1:
+            kt = -(-nkt // split)
+            assert (split - 1) * kt < nkt, (shape, split, kt)

@@ -225,7 +225,10 @@ def test_wgrad_pingpong_tn_matches_fp32(T, N, K, bal):
 
 
 @pytest.mark.parametrize("T,N,K,r0,split", [(1024, 384, 512, 0, 3), (2048, 896, 768, 256, 4),
-                                             (4096, 640, 256, 128, 2)])
+                                             (4096, 640, 256, 128, 2),
+                                             # 10 K-tiles, split 7 -> 2 per slice: the launch
+                                             # clamps to 5 slices (7 would start 2 past K)
+                                             (640, 256, 256, 0, 7)])
 def test_wgrad_pingpong_tn_split_k(T, N, K, r0, split):
     """TN split-K on a row range [r0, N) (the LM-head tail path): uneven K slices (16 / 3 K-tiles),
     a row offset into dY, fp32 partials + reduce; rows outside the range untouched."""
@@ -259,7 +262,8 @@ def test_wgrad_pingpong_tn_tail_plan_lmhead_scale():
 
 
 @pytest.mark.parametrize("M,N,K,split", [(2048, 768, 50304, 4), (520, 512, 64 * 7, 3),
-                                         (1024, 256, 4096, 2)])
+                                         (1024, 256, 4096, 2),
+                                         (512, 256, 64 * 10, 7)])   # clamped to 5 slices
 def test_dgrad_nn_split_k(M, N, K, split):
     """Split-K NN (uneven last slice for 786 / 4 and 7 / 3 K-tiles): fp32 partials + reduce."""
     from distributed_llm_backend_benchmark_amd.ops import gemm
