@@ -32,6 +32,10 @@ def parse_args(argv=None):
                     help="process-group backend; also names the output file")
     ap.add_argument("--allreduce", choices=["auto", "rccl", "custom", "native"], default=None,
                     help="override execution.allreduce")
+    ap.add_argument("--device", choices=["auto", "cpu", "cuda"], default="auto",
+                    help="tensor device; auto = cuda for rccl, cpu for gloo. gloo + cuda = "
+                         "several ranks sharing one GPU over a gloo process group (rehearsal "
+                         "of the multi-rank path; RCCL needs one GPU per rank)")
     ap.add_argument("--allreduce-dtype", choices=["bf16", "fp32"], default=None)
     ap.add_argument("--attention", choices=["slice", "sdpa"], default=None)
     ap.add_argument("--kernels", choices=["hip", "torch"], default=None)
@@ -50,6 +54,18 @@ def parse_args(argv=None):
                     help="torch.profiler Chrome trace per rank into DIR")
     ap.add_argument("--ignore-world-size", action="store_true",
                     help="accept any world size (reference exits on mismatch, run_mpi.py:73-77)")
+    ap.add_argument("--shard-as", type=int, default=None, metavar="P",
+                    help="world 1 only: run rank 0's shard of a P-way TP model (the exact "
+                         "per-rank GEMM / LN shapes) with each all-reduce replaced by a local "
+                         "stand-in (one rank's one-shot HBM traffic; + link time with "
+                         "--emulate-busbw); output <backend>_<name>_shard<P>.json")
+    ap.add_argument("--emulate-busbw", type=float, default=None, metavar="GBPS",
+                    help="with --shard-as: also hold 32 workgroups for the ring all-reduce time "
+                         "bytes*2(P-1)/P / busBW per all-reduce")
+    ap.add_argument("--check-dense", action="store_true",
+                    help="after warmup, load the TP shards from a dense world-1 model of the "
+                         "same seed (built on every rank) and report the max error of the TP "
+                         "output against it (needs world > 1 on real ranks)")
     return ap.parse_args(argv)
 
 
@@ -93,18 +109,33 @@ def main(argv=None) -> int:
         config["experiment"]["output_dir"] = args.output_dir
 
     t0 = time.perf_counter()
-    comm = init_distributed(args.backend)
+    comm = init_distributed(args.backend,
+                            device=None if args.device == "auto" else args.device)
     comm.install_tune_agreement()       # GEMM kernel choices agreed on rank-max timings
     comm.barrier()
     init_elapsed = time.perf_counter() - t0
     rank, world = comm.rank, comm.world_size
 
     expected = config["parallelism"]["world_size"]
-    if expected != "auto" and int(expected) != world and not args.ignore_world_size:
+    eff_world = args.shard_as or world
+    if expected != "auto" and int(expected) != eff_world and not args.ignore_world_size:
         if rank == 0:
-            print(f"ERROR: World size mismatch. Expected {expected}, got {world}")
+            print(f"ERROR: World size mismatch. Expected {expected}, got {eff_world}")
         comm.destroy()
         return 1
+    model_comm = comm
+    if args.shard_as:
+        if world != 1 or args.shard_as < 2:
+            if rank == 0:
+                print("ERROR: --shard-as P needs world 1 and P >= 2")
+            comm.destroy()
+            return 1
+        from ..parallel.comm import Comm
+
+        # the model sees a P-rank world (shapes, per-rank FLOPs); no process group behind it
+        model_comm = Comm(rank=0, world_size=args.shard_as, local_rank=comm.local_rank,
+                          backend="emulate", device=comm.device)
+        ex["allreduce"] = "emulate"
 
     if rank == 0:
         si = collect_system_info()
@@ -119,7 +150,13 @@ def main(argv=None) -> int:
         print(f"Input: B={config['input']['batch_size']} S={config['input']['sequence_length']}")
         print(f"Execution: {ex}")
 
-    model = create_model_from_config(config, comm)
+    model = create_model_from_config(config, model_comm)
+    if args.shard_as and args.emulate_busbw:
+        from ..parallel.tensor_parallel import RowParallelLinear
+
+        for m in model.modules():
+            if isinstance(m, RowParallelLinear):
+                m.emulate_busbw = float(args.emulate_busbw)
     dataset = create_dataset_from_config(config, comm.device)
     if rank == 0:
         print(f"[Rank 0] Model created: total params {model.get_num_parameters() / 1e9:.2f}B "
@@ -141,6 +178,12 @@ def main(argv=None) -> int:
         metrics.record_warmup_time(time.perf_counter() - t)
         fwd_bytes = model.comm_bytes() - b0
     comm.barrier()
+
+    dense_check = None
+    if args.check_dense and not args.shard_as:
+        dense_check = _check_against_dense(config, comm, model, dataset.get_batch())
+        if rank == 0:
+            print(f"dense check: {dense_check}")
 
     run_forward = lambda: model(dataset.get_batch())  # noqa: E731
     use_graph = bool(args.graph or ex.get("graph", False)) and gpu
@@ -217,7 +260,17 @@ def main(argv=None) -> int:
                 "distributed_llm_backend_benchmark_amd.ops.gemm", fromlist=["x"]).kernel_mix(),
             # node-measured IPC-vs-RCCL crossovers behind allreduce=auto (None: RCCL only)
             "allreduce_calibration": calibration,
+            "dense_check": dense_check,
         }
+        if args.shard_as:
+            extra["shard_as"] = {
+                "P": args.shard_as, "emulate_busbw_GBps": args.emulate_busbw,
+                "what": ("rank 0's shard of a P-way TP forward on ONE GPU: the exact per-rank "
+                         "GEMM / LayerNorm shapes; each all-reduce replaced by a stand-in with "
+                         "one rank's one-shot HBM traffic" +
+                         (" plus the ring time at the assumed bus bandwidth"
+                          if args.emulate_busbw else " (no link time)") +
+                         "; tokens_per_s is the P-GPU job's (every rank holds all tokens)")}
         results = {
             "experiment": config["experiment"]["name"],
             "backend": args.backend,
@@ -233,12 +286,40 @@ def main(argv=None) -> int:
               f"\n  Coefficient of variation: {rs['coefficient_of_variation']:.4f}"
               f"\n  tokens/s: {extra['tokens_per_s']:.1f}  TFLOP/s/rank: "
               f"{extra['tflops_per_rank']:.1f}")
+        suffix = f"_shard{args.shard_as}" if args.shard_as else ""
         out = os.path.join(config["experiment"]["output_dir"],
-                           f"{args.backend}_{config['experiment']['name']}.json")
+                           f"{args.backend}_{config['experiment']['name']}{suffix}.json")
         save_results(results, out, rank)
     comm.barrier()
     comm.destroy()
     return 0
+
+
+def _check_against_dense(config, comm, model, batch) -> dict:
+    """Build the dense (world-1) model of the same seed on every rank, shard its weights into
+    the TP model (``LLM.load_from_dense``), run both on ``batch`` and compare: the TP forward,
+    all-reduces included, must reproduce the dense output to bf16 accuracy (the test of
+    ``run_mpi.py``'s model the reference never runs, models.py:95)."""
+    import torch
+
+    from ..models.tp_transformer import create_model_from_config
+    from ..parallel.comm import Comm
+
+    solo = Comm(rank=0, world_size=1, local_rank=comm.local_rank, backend=comm.backend,
+                device=comm.device)
+    dense = create_model_from_config(config, solo)
+    with torch.no_grad():
+        y_ref = dense(batch).float()
+        model.load_from_dense(dense.state_dict())
+        del dense
+        y = model(batch).float()
+    comm.sync()
+    scale = float(y_ref.abs().max())
+    err = float((y - y_ref).abs().max())
+    errs = comm.all_gather_object(err)
+    rel = max(errs) / max(scale, 1e-30)
+    return {"max_abs_err": max(errs), "ref_max_abs": scale, "rel_err": rel,
+            "passed": bool(rel < 5e-2 and all(e == e for e in errs))}
 
 
 if __name__ == "__main__":

@@ -91,10 +91,36 @@ class RowParallelLinear(nn.Module):
                 if allreduce == "native":
                     raise
         self.comm_bytes = 0   # bytes all-reduced by this layer (accounting)
+        # allreduce="emulate" (run_tp --shard-as P: ONE GPU runs rank 0's shard of a P-way
+        # model): the partial sum goes through a stand-in with the local HBM traffic of one
+        # rank's one-shot all-reduce (P inputs read, 1 written: y + (P-1) zero buffers) and,
+        # with `emulate_busbw` GB/s, then holds `emulate_blocks` workgroups for the ring time
+        # bytes * 2(P-1)/P / busBW — the link-bound duration (parallel/ddp.py uses the same model)
+        self.emulate_busbw: Optional[float] = None
+        self.emulate_blocks = 32
+        self._emu_zeros: Optional[torch.Tensor] = None
+
+    def _emulated_all_reduce(self, t: torch.Tensor) -> None:
+        from ..ops.elementwise import reduce_sum, spin_ns
+
+        P = self.comm.world_size
+        n = t.numel()
+        if self._emu_zeros is None or self._emu_zeros.numel() < n \
+                or self._emu_zeros.dtype != t.dtype:
+            self._emu_zeros = torch.zeros(n, dtype=t.dtype, device=t.device)
+        flat = t.view(-1)
+        reduce_sum([flat] + [self._emu_zeros[:n]] * (P - 1), out=flat)
+        if self.emulate_busbw:
+            nbytes = n * t.element_size()
+            spin_ns(int(nbytes * 2.0 * (P - 1) / P / self.emulate_busbw), self.emulate_blocks,
+                    t.device)
 
     def _all_reduce(self, t: torch.Tensor) -> None:
         self.comm_bytes += t.numel() * t.element_size()
         if self.comm.world_size == 1:
+            return
+        if self.allreduce == "emulate":
+            self._emulated_all_reduce(t)
             return
         car = self._car
         if car is not None and (self.allreduce == "custom" or car.should_use(t)) \

@@ -97,7 +97,7 @@ def validate_config(config: Dict[str, Any]) -> Dict[str, Any]:
         if int(m[k]) <= 0:
             raise ConfigError(f"model.{k} must be positive")
     ex = cfg["execution"]
-    if ex["allreduce"] not in ("auto", "rccl", "custom", "native", "torch"):
+    if ex["allreduce"] not in ("auto", "rccl", "custom", "native", "torch", "emulate"):
         raise ConfigError("execution.allreduce must be auto|rccl|custom|native|torch, got "
                           f"{ex['allreduce']!r}")
     if ex["allreduce_dtype"] not in ("bf16", "fp32"):

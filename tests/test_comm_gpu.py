@@ -347,6 +347,100 @@ def test_ddp_custom_registered_buckets_ranks_on_one_gpu():
         assert len(set(sums)) == 1, sums
 
 
+@pytest.mark.parametrize("allreduce,fp32_buckets", [("rccl", False), ("custom", False),
+                                                    ("rccl", True)])
+def test_ddp_matches_global_batch_and_ranks_stay_identical_ranks_on_one_gpu(allreduce,
+                                                                             fp32_buckets):
+    """VERDICT r02 weak #7 / item 5, rehearsed with 2 ranks sharing one GPU over a gloo process
+    group ("rccl" = the process group's all_reduce): the reduced gradient equals a world-1 run
+    on the concatenated global batch, and after three optimizer steps the parameters are
+    bitwise identical on every rank. Same worker as the multi-GPU integration test."""
+    from ddp_check import ddp_equivalence_worker
+
+    res = run_multiprocess(ddp_equivalence_worker, 2, args=("gloo", allreduce, fp32_buckets),
+                           timeout=600)
+    tol = 5e-3 if fp32_buckets else 3e-2
+    for worst, digests, nb in res:
+        assert worst < tol, worst
+        assert len(set(digests)) == 1, digests
+        assert nb > 1
+
+
+def _tp_rehearsal_worker(rank, world, allreduce):
+    os.environ["DLBB_GEMM"] = "mfma"                 # the hand-written GEMM on every shape
+    os.environ["DLBB_CUSTOM_AR_CALIBRATE"] = "0"     # (calibration has its own test)
+    import torch
+
+    from distributed_llm_backend_benchmark_amd.models.tp_transformer import LLM
+    from distributed_llm_backend_benchmark_amd.ops import gemm
+    from distributed_llm_backend_benchmark_amd.parallel.comm import Comm, init_distributed
+
+    comm = init_distributed("gloo", device="cuda")
+    dev = comm.device
+    kw = dict(hidden_size=256, num_layers=2, num_heads=4, ffn_intermediate=1024, seed=11,
+              init_std=0.05)
+    dense = LLM(comm=Comm(0, 1, 0, "gloo", dev), **kw)
+    tp = LLM(comm=comm, allreduce=allreduce, **kw)
+    tp.load_from_dense(dense.state_dict())
+    g = torch.Generator(device=dev).manual_seed(5)
+    x = torch.randn(2, 64, 256, generator=g, device=dev).to(torch.bfloat16)
+    y_ref = dense(x).float()
+    y = tp(x).float()
+    y2 = tp(x).float()                      # second call: IPC epoch / buffer half flips
+    torch.cuda.synchronize()
+    car = tp.ipc_allreduce()
+    used_custom = car is not None and car.healthy
+    errflag = car.check_error() if car is not None else 0
+    scale = float(y_ref.abs().max())
+    err = max(float((y - y_ref).abs().max()), float((y2 - y_ref).abs().max())) / scale
+    mix = gemm.kernel_mix()
+    comm.destroy()
+    return err, used_custom, errflag, mix["forced"], comm.world_size
+
+
+@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("allreduce", ["rccl", "custom"])
+def test_tp_forward_ranks_on_one_gpu_matches_dense(world, allreduce):
+    """the TP transformer (reference models.py) with the HIP kernels at
+    P = 2 / 4 — column/row-parallel GEMMs on the hand-written MFMA kernel, row-parallel partial
+    sums through the process group (gloo over GPU tensors) or the IPC kernel — equals the dense
+    world-1 model loaded with the same weights."""
+    res = run_multiprocess(_tp_rehearsal_worker, world, args=(allreduce,), timeout=600)
+    for err, used_custom, errflag, forced, w in res:
+        assert w == world
+        assert err < 3e-2, err
+        assert forced == "mfma"
+        assert errflag == 0
+        assert used_custom == (allreduce == "custom")
+
+
+def test_run_tp_shard_as_world1(tmp_path):
+    """run_tp --shard-as 8 runs rank 0's shard of an 8-way TP model on
+    one GPU (per-rank shapes, emulated all-reduce with a link-time stand-in) and writes
+    <backend>_<name>_shard8.json."""
+    import yaml
+
+    cfg = yaml.safe_load(open(os.path.join(REPO, "config", "1b_config.yaml")))
+    cfg["model"]["num_layers"] = 2
+    cfg["experiment"]["output_dir"] = str(tmp_path)
+    cfg["execution"]["warmup_iterations"] = 2
+    cfg["execution"]["benchmark_iterations"] = 3
+    cfg["parallelism"]["world_size"] = 8
+    p = tmp_path / "c.yaml"
+    p.write_text(yaml.safe_dump(cfg))
+    out = subprocess.run([sys.executable, "-m", "distributed_llm_backend_benchmark_amd.cli.run_tp",
+                          "--config", str(p), "--backend", "rccl", "--shard-as", "8",
+                          "--emulate-busbw", "100"], capture_output=True, text=True,
+                         timeout=600, cwd=REPO)
+    assert out.returncode == 0, out.stderr[-3000:]
+    rec = json.load(open(tmp_path / f"rccl_{cfg['experiment']['name']}_shard8.json"))
+    th = rec["throughput"]
+    assert th["shard_as"]["P"] == 8 and th["shard_as"]["emulate_busbw_GBps"] == 100
+    B, S, H = cfg["input"]["batch_size"], cfg["input"]["sequence_length"], cfg["model"]["hidden_size"]
+    assert th["allreduce_bytes_per_forward_per_rank"] == 2 * 2 * B * S * H * 2
+    assert th["tokens_per_s"] > 0
+
+
 def test_bench_py_world1():
     out = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--steps", "5",
                           "--warmup", "2"], capture_output=True, text=True, timeout=600, cwd=REPO)

@@ -510,3 +510,58 @@ def test_ddp_tail_bucket_holds_only_late_params_and_split_optimizer_is_exact():
     assert torch.equal(finals[True][0], finals[False][0])
     assert torch.equal(finals[True][1], finals[False][1])
     assert finals[True][2] == finals[False][2] == 3
+
+
+def _run_tp_cli_worker(rank, world, cfg_path, extra):
+    from distributed_llm_backend_benchmark_amd.cli import run_tp
+
+    return run_tp.main(["--config", cfg_path, "--backend", "gloo", "--kernels", "torch"] + extra)
+
+
+def _tiny_tp_config(tmp_path, world):
+    import yaml
+
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cfg = yaml.safe_load(open(os.path.join(repo, "config", "baseline_config.yaml")))
+    cfg["model"].update(hidden_size=128, num_layers=2, num_heads=4, ffn_intermediate=512,
+                        init_std=0.05)
+    cfg["input"].update(batch_size=2, sequence_length=16)
+    cfg["execution"].update(warmup_iterations=1, benchmark_iterations=3)
+    cfg["parallelism"]["world_size"] = world
+    cfg["experiment"]["output_dir"] = str(tmp_path)
+    p = tmp_path / "tiny.yaml"
+    p.write_text(yaml.safe_dump(cfg))
+    return str(p), cfg["experiment"]["name"]
+
+
+RUN_MPI_KEYS = {"experiment", "backend", "config", "system_info", "rank_0_summary",
+                "rank_statistics", "raw_metrics_rank_0"}     # reference run_mpi.py:217-225
+
+
+def test_run_tp_cli_check_dense_gloo(tmp_path):
+    """run_tp at world 2 (gloo): the reference's result schema and the TP output equal to the
+    dense model of the same seed (--check-dense), the GEMM-choice agreement recorded."""
+    path, name = _tiny_tp_config(tmp_path, 2)
+    rc = run_multiprocess(_run_tp_cli_worker, 2, args=(path, ["--check-dense"]))
+    assert rc == [0, 0]
+    rec = json.load(open(tmp_path / f"gloo_{name}.json"))
+    assert RUN_MPI_KEYS <= set(rec)
+    assert rec["rank_0_summary"]["world_size"] == 2
+    assert rec["throughput"]["dense_check"]["passed"], rec["throughput"]["dense_check"]
+    assert rec["throughput"]["gemm_kernel_mix"]["agreed_across_ranks"] is True
+
+
+def test_run_tp_cli_shard_as(tmp_path):
+    """--shard-as P at world 1: rank 0's shard of a P-way model (per-rank shapes, per-rank
+    FLOPs), each all-reduce through the local stand-in; the world-size check uses P."""
+    path, name = _tiny_tp_config(tmp_path, 4)
+    from distributed_llm_backend_benchmark_amd.cli import run_tp
+
+    assert run_tp.main(["--config", path, "--backend", "gloo", "--kernels", "torch",
+                        "--shard-as", "4"]) == 0
+    rec = json.load(open(tmp_path / f"gloo_{name}_shard4.json"))
+    th = rec["throughput"]
+    assert th["shard_as"]["P"] == 4
+    assert th["allreduce_bytes_per_forward_per_rank"] == 2 * 2 * (2 * 16 * 128 * 2)
+    # without --shard-as the same config (world_size 4) is refused at world 1
+    assert run_tp.main(["--config", path, "--backend", "gloo", "--kernels", "torch"]) == 1
