@@ -47,10 +47,21 @@ def parse_args(argv=None):
     ap.add_argument("--comm-blocks", type=int, default=None,
                     help="CU budget: workgroups per bucket-reduction launch (IPC kernel / "
                          "emulation); default = the kernel's size heuristic")
-    ap.add_argument("--emulate-comm", action="store_true",
+    ap.add_argument("--emulate-comm", nargs="?", const=True, default=False, type=float,
+                    metavar="BUSBW_GBPS",
                     help="world 1: run a bucket-sized stand-in reduction (one rank's all-reduce "
                          "HBM traffic) on the comm stream at every bucket-ready hook, to measure "
-                         "what overlapped gradient reduction costs the backward pass")
+                         "what overlapped gradient reduction costs the backward pass; with a "
+                         "value, each stand-in also lasts the ring all-reduce time at that bus "
+                         "bandwidth over --emulate-world ranks (link-bound)")
+    ap.add_argument("--emulate-world", type=int, default=8)
+    ap.add_argument("--no-late-bucket", action="store_true",
+                    help="A/B: do not give the embedding tables a bucket of their own")
+    ap.add_argument("--no-split-optimizer", action="store_true",
+                    help="A/B: one AdamW pass after every bucket is reduced")
+    ap.add_argument("--comm-timeline", action="store_true",
+                    help="after the timed steps, one more step with comm events: bytes reduced "
+                         "after backward and the exposed comm time (stream-issued reductions)")
     ap.add_argument("--zero", action="store_true",
                     help="ZeRO-2-style: reduce-scatter grads, sharded AdamW, all-gather params")
     ap.add_argument("--compare-overlap", action="store_true")
@@ -87,7 +98,9 @@ def run(args, comm, overlap: bool):
         tr = FlatParamTrainer(model, comm if comm.world_size > 1 else None, lr=args.lr,
                               bucket_mb=args.bucket_mb, overlap=overlap, mode=args.mode,
                               allreduce=args.allreduce, comm_blocks=args.comm_blocks,
-                              emulate_comm=args.emulate_comm)
+                              emulate_comm=args.emulate_comm, emulate_world=args.emulate_world,
+                              late_bucket=not args.no_late_bucket,
+                              split_optimizer=not args.no_split_optimizer)
     data = SyntheticTokenDataset(args.batch, args.seq, cfg.vocab_size, rank=comm.rank,
                                  device=comm.device)
     if args.resume_from:
@@ -136,6 +149,13 @@ def run(args, comm, overlap: bool):
         # node-measured IPC-vs-RCCL crossovers (rank-max, agreed; None: no IPC kernel)
         "allreduce_calibration": getattr(getattr(tr, "_car", None), "calibration", None),
     }
+    if args.comm_timeline and not args.zero:
+        tr.timeline = True
+        x, y = data.get_batch()
+        set_lr()
+        tr.step(x, y, sync_loss=False)
+        tr.timeline = False
+        res["comm_tail"] = tr.comm_tail_report()
     if args.save_checkpoint:
         tr.save_checkpoint(args.save_checkpoint)
         res["checkpoint"] = args.save_checkpoint
@@ -164,7 +184,9 @@ def main(argv=None) -> int:
            "config": {k: getattr(args, k) for k in ("n_layer", "n_head", "n_embd", "vocab",
                                                     "batch", "seq", "bucket_mb", "mode",
                                                     "allreduce", "zero", "comm_blocks",
-                                                    "emulate_comm")}}
+                                                    "emulate_comm", "emulate_world",
+                                                    "no_late_bucket",
+                                                    "no_split_optimizer")}}
     if args.compare_overlap:
         alt = run(args, comm, overlap=args.no_overlap)
         out["other_overlap_setting"] = alt

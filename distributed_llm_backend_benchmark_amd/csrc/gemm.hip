@@ -748,31 +748,6 @@ __device__ __forceinline__ void mfma_full(f32x4 (&acc)[8][4], const bf16x8 (&af)
                                                             0, 0);
 }
 
-// mfma_full with NP of the wave's own LDS-DMA pieces issued INSIDE its MFMA cluster (BSPLIT,
-// below): piece p after MFMA group (16 (p + 1)) / (NP + 1) - 1 of the 16 groups of 4, pinned
-// there by sched_barriers. `piece(p)` issues piece p; `on` (wave-uniform) gates the issue.
-template <int NP, typename F>
-__device__ __forceinline__ void mfma_full_dma(f32x4 (&acc)[8][4], const bf16x8 (&af)[2][8],
-                                              const bf16x8 (&bf)[2][4], bool on, F&& piece) {
-#pragma unroll
-  for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[ks][j], af[ks][i], acc[i][j], 0,
-                                                            0, 0);
-      const int g = ks * 8 + i;
-#pragma unroll
-      for (int p = 0; p < NP; ++p)
-        if (g == (16 * (p + 1)) / (NP + 1) - 1) {
-          __builtin_amdgcn_sched_barrier(0);
-          if (on) piece(p);
-          __builtin_amdgcn_sched_barrier(0);
-        }
-    }
-}
-
 // ---------------------------------------------------------------------------------------
 // NN operand B (dgrad: dX[M, N] = dY[M, K] · W[K, N], W stored [K][N] row-major — the reduction
 // runs along W's ROWS). One K-tile of B = 64 k-rows x 256 columns, staged as two [64][128]
@@ -888,17 +863,6 @@ __device__ __forceinline__ void stage_b_any(__amdgpu_buffer_rsrc_t rb, uint32_t 
     stage_b<I0, I1>(rb, ldb2, rows_b, static_cast<uint32_t>(u) * (BK * 2), bbuf, w4, boff);
 }
 
-// one B staging instruction I0 + p (p < 4, runtime-unrolled constant)
-template <bool NN, int I0>
-__device__ __forceinline__ void stage_b_piece(int p, __amdgpu_buffer_rsrc_t rb, uint32_t ldb2,
-                                              int rows_b, int u, char* bbuf, int w4,
-                                              uint32_t boff) {
-  if (p == 0) stage_b_any<NN, I0, I0 + 1>(rb, ldb2, rows_b, u, bbuf, w4, boff);
-  else if (p == 1) stage_b_any<NN, I0 + 1, I0 + 2>(rb, ldb2, rows_b, u, bbuf, w4, boff);
-  else if (p == 2) stage_b_any<NN, I0 + 2, I0 + 3>(rb, ldb2, rows_b, u, bbuf, w4, boff);
-  else stage_b_any<NN, I0 + 3, I0 + 4>(rb, ldb2, rows_b, u, bbuf, w4, boff);
-}
-
 template <bool NN, bool TN = false>
 __device__ __forceinline__ void read_split_any(const char* abuf, const char* bbuf, int wr, int wc,
                                                int fr, int fq, bf16x8 (&af)[2][8],
@@ -933,17 +897,8 @@ __device__ __forceinline__ void read_split_any(const char* abuf, const char* bbu
 // TN (weight gradient, implies NN for B): A [K][lda] row-major over the reduction, staged and
 // read as transposed images (stage_a_half_tn / read_a_tn); split-K as for NN.
 // STAMP (diagnostic variants only): per-workgroup start / end records into `st` (common.h).
-// BSPLIT (with BAL): the last BSPLIT of each wave row's 4 B pieces of tile u+2 move from its
-// memory interval into its NEXT (MFMA) interval, issued between MFMA groups. An LDS-DMA piece
-// costs ~100-185 cycles to issue in a phase that also carries ds_reads but ~60 among bare MFMAs
-// (MI355X_MICROARCH.md, constants table), and the memory interval (24 ds_read_b128 + 8 pieces)
-// is the longer of the two, so moving pieces shortens the interval pair. Issue ORDER per wave is
-// unchanged, so each counted wait drops by exactly the pieces issued after the waited-for
-// group in the same window: row 0 end-of-2u 12 -> 12 - BSPLIT, row 1 end-of-2u+1 8 -> 8 - BSPLIT;
-// the other waits keep their counts. WAR: the moved pieces land in B(u-1)'s buffer even later.
-template <bool NN, bool BAL = false, bool TN = false, bool STAMP = false, int BSPLIT = 0>
+template <bool NN, bool BAL = false, bool TN = false, bool STAMP = false>
 __device__ __forceinline__ void pingpong_body(GemmArgs a, char* smem, uint64_t* st = nullptr) {
-  static_assert(BSPLIT == 0 || (BAL && BSPLIT < 4), "BSPLIT needs the balanced issue, < 4");
   uint64_t t_start = 0;
   if constexpr (STAMP) t_start = stamp_now();
   if (NN && gridDim.y > 1) {         // split-K slice blockIdx.y (wave-uniform, SGPR math)
@@ -1022,22 +977,17 @@ __device__ __forceinline__ void pingpong_body(GemmArgs a, char* smem, uint64_t* 
         DLBB_STAGE_A(u + 1, abuf0 + ((u + 1) & 1) * kTile2Bytes, 1,
                      stage_a_half(ra, lda2, rows_a, (u + 1) * kStep,
                                   abuf0 + ((u + 1) & 1) * kTile2Bytes, 1, wc, aoff));
-      const int cb2 = cb == 0 ? 2 : cb - 1;           // (u + 2) % 3
       if (b2) {
+        const int cb2 = cb == 0 ? 2 : cb - 1;         // (u + 2) % 3
         if (BAL)
-          stage_b_any<NN, 0, 4 - BSPLIT>(rb, ldb2, rows_b, u + 2, bbuf0 + cb2 * kTile2Bytes, wc,
-                                         boff);
+          stage_b_any<NN, 0, 4>(rb, ldb2, rows_b, u + 2, bbuf0 + cb2 * kTile2Bytes, wc, boff);
         else
           stage_b_any<NN>(rb, ldb2, rows_b, u + 2, bbuf0 + cb2 * kTile2Bytes, wc, boff);
       }
       // retire A-hi(u) (issued two intervals ago; tile 0's came from row 1)
       if (BAL) {
-        if (b2) {
-          if constexpr (BSPLIT == 0) DLBB_WAIT_VM(12);
-          else if constexpr (BSPLIT == 1) DLBB_WAIT_VM(11);
-          else if constexpr (BSPLIT == 2) DLBB_WAIT_VM(10);
-          else DLBB_WAIT_VM(9);
-        } else if (h1) DLBB_WAIT_VM(8);
+        if (b2) DLBB_WAIT_VM(12);
+        else if (h1) DLBB_WAIT_VM(8);
         else DLBB_WAIT_VM(0);
       } else {
         if (b2) DLBB_WAIT_VM(20);
@@ -1048,13 +998,7 @@ __device__ __forceinline__ void pingpong_body(GemmArgs a, char* smem, uint64_t* 
       __builtin_amdgcn_sched_barrier(0);
       __builtin_amdgcn_s_barrier();                   // end of interval 2u
       __builtin_amdgcn_sched_barrier(0);
-      if constexpr (BSPLIT > 0)
-        mfma_full_dma<BSPLIT>(acc, af, bf, b2, [&](int p) {
-          stage_b_piece<NN, 4 - BSPLIT>(p, rb, ldb2, rows_b, u + 2, bbuf0 + cb2 * kTile2Bytes,
-                                        wc, boff);
-        });
-      else
-        mfma_full(acc, af, bf);
+      mfma_full(acc, af, bf);
       __builtin_amdgcn_sched_barrier(0);
       if (h1) {                                       // retire B(u+1) (BAL: its first half)
         if (b2) { if (BAL) DLBB_WAIT_VM(8); else DLBB_WAIT_VM(12); }
@@ -1081,32 +1025,19 @@ __device__ __forceinline__ void pingpong_body(GemmArgs a, char* smem, uint64_t* 
         DLBB_STAGE_A(u + 2, abuf0 + (u & 1) * kTile2Bytes, 0,
                      stage_a_half(ra, lda2, rows_a, (u + 2) * kStep,
                                   abuf0 + (u & 1) * kTile2Bytes, 0, wc, aoff));
-      const int cb2 = cb == 0 ? 2 : cb - 1;           // (u + 2) % 3
-      if (BAL && l2)
-        stage_b_any<NN, 4, 8 - BSPLIT>(rb, ldb2, rows_b, u + 2, bbuf0 + cb2 * kTile2Bytes, wc,
-                                       boff);
+      if (BAL && l2) {
+        const int cb2 = cb == 0 ? 2 : cb - 1;         // (u + 2) % 3
+        stage_b_any<NN, 4, 8>(rb, ldb2, rows_b, u + 2, bbuf0 + cb2 * kTile2Bytes, wc, boff);
+      }
       if (u + 1 < nk) {                               // retire A-lo(u+1) (BAL: and B1(u+1))
-        if (l2) {
-          if (BAL) {
-            if constexpr (BSPLIT == 0) DLBB_WAIT_VM(8);
-            else if constexpr (BSPLIT == 1) DLBB_WAIT_VM(7);
-            else if constexpr (BSPLIT == 2) DLBB_WAIT_VM(6);
-            else DLBB_WAIT_VM(5);
-          } else DLBB_WAIT_VM(4);
-        }
+        if (l2) { if (BAL) DLBB_WAIT_VM(8); else DLBB_WAIT_VM(4); }
         else DLBB_WAIT_VM(0);
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
       __builtin_amdgcn_s_barrier();                   // end of interval 2u+1
       __builtin_amdgcn_sched_barrier(0);
-      if constexpr (BSPLIT > 0)
-        mfma_full_dma<BSPLIT>(acc, af, bf, l2, [&](int p) {
-          stage_b_piece<NN, 8 - BSPLIT>(p, rb, ldb2, rows_b, u + 2, bbuf0 + cb2 * kTile2Bytes,
-                                        wc, boff);
-        });
-      else
-        mfma_full(acc, af, bf);
+      mfma_full(acc, af, bf);
       __builtin_amdgcn_sched_barrier(0);
       if (u + 1 < nk) __builtin_amdgcn_s_barrier();   // end of interval 2u+2
       cb = cb == 2 ? 0 : cb + 1;
@@ -1129,20 +1060,6 @@ __global__ void __launch_bounds__(kThreads2, 1) gemm_bf16_nt_256_pingpong3(GemmA
 __global__ void __launch_bounds__(kThreads2, 1) gemm_bf16_nt_256_pingpong3_bal(GemmArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   pingpong_body<false, true>(a, smem);
-}
-
-// A/B variants (set_stagger(8 / 9 / 10)): balanced issue + BSPLIT 1 / 2 / 3 (pingpong_body).
-__global__ void __launch_bounds__(kThreads2, 1) gemm_bf16_nt_256_pingpong3_bs1(GemmArgs a) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  pingpong_body<false, true, false, false, 1>(a, smem);
-}
-__global__ void __launch_bounds__(kThreads2, 1) gemm_bf16_nt_256_pingpong3_bs2(GemmArgs a) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  pingpong_body<false, true, false, false, 2>(a, smem);
-}
-__global__ void __launch_bounds__(kThreads2, 1) gemm_bf16_nt_256_pingpong3_bs3(GemmArgs a) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  pingpong_body<false, true, false, false, 3>(a, smem);
 }
 
 // dgrad: C[M, N] = A[M, K] · B[K, N] (B row-major over the reduction); host contract
@@ -1242,10 +1159,10 @@ DLBB_API int dlbb_gemm_bf16_nt(const void* A, int64_t lda, const void* B, int64_
     int mode = dlbb_gemm_stagger;
     // ping-pong contract: 8-row A groups and 64-row B blocks wholly in or out (uniform clamps),
     // 32-bit buffer offsets within a 256-row panel
-    if (mode >= 6 && mode <= 10 && !(M % 8 == 0 && N % 64 == 0 && M >= 8 && lda * 2 * 256 + K * 2 < (1LL << 31) &&
+    if ((mode == 6 || mode == 7) && !(M % 8 == 0 && N % 64 == 0 && M >= 8 && lda * 2 * 256 + K * 2 < (1LL << 31) &&
                        ldb * 2 * 256 + K * 2 < (1LL << 31)))
       mode = 3;
-    if (mode == 5 || mode > 10) mode = 3;
+    if (mode == 5 || mode > 7) mode = 3;
     if (mode == 4) {
       static int ncu[64] = {0};
       int dev = 0;
@@ -1261,13 +1178,7 @@ DLBB_API int dlbb_gemm_bf16_nt(const void* A, int64_t lda, const void* B, int64_
       const int64_t grid = tiles256 < ncu[dev] ? tiles256 : ncu[dev];
       hipLaunchKernelGGL(gemm_bf16_nt_256_persistent, dim3(static_cast<unsigned>(grid)), b,
                          2 * kBuf2Bytes, stream, a);
-    } else if (mode == 8)
-      hipLaunchKernelGGL(gemm_bf16_nt_256_pingpong3_bs1, g, b, kPP6Lds, stream, a);
-    else if (mode == 9)
-      hipLaunchKernelGGL(gemm_bf16_nt_256_pingpong3_bs2, g, b, kPP6Lds, stream, a);
-    else if (mode == 10)
-      hipLaunchKernelGGL(gemm_bf16_nt_256_pingpong3_bs3, g, b, kPP6Lds, stream, a);
-    else if (mode == 7 || (mode == 6 && use_bal(K / BK, false)))
+    } else if (mode == 7 || (mode == 6 && use_bal(K / BK, false)))
       DLBB_PP_LAUNCH(gemm_bf16_nt_256_pingpong3_bal, STAMP_GEMM_NT, g, a);
     else if (mode == 6)
       DLBB_PP_LAUNCH(gemm_bf16_nt_256_pingpong3, STAMP_GEMM_NT, g, a);

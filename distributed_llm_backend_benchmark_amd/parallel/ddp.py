@@ -49,6 +49,25 @@ _WGRAD_STREAM = os.environ.get("DLBB_WGRAD_STREAM", "0") == "1"
 # priority of the dedicated bucket-reduction stream: 0 = normal (default, measured), -1 = high
 # (A/B knob; see the module docstring and profiles/r02_overlap/SUMMARY.md)
 _COMM_PRIORITY = int(os.environ.get("DLBB_COMM_STREAM_PRIORITY", "0"))
+
+
+def comm_stream_priority() -> int:
+    """Priority of the bucket-reduction stream, FENCED to normal. Per-workgroup stamps of the
+    trap (profiles/r03_overlap/SUMMARY.md): with the comm stream at high priority, from the
+    first bucket reduction on every kernel launch of the step — compute and comm queue alike —
+    spreads its workgroup starts over 25-38 us instead of ~1 us (workgroup run times unchanged),
+    ~+30 us per launch, +10 ms per GPT-2 step; intermittent, absent under a profiler's kernel
+    trace. A dispatch (queue-arbitration) effect, not CU contention, so a CU mask or grid cap
+    would not fence it: high priority needs DLBB_ALLOW_HIGH_PRIO_COMM=1."""
+    p = _COMM_PRIORITY
+    if p < 0 and os.environ.get("DLBB_ALLOW_HIGH_PRIO_COMM") != "1":
+        import warnings
+
+        warnings.warn("DLBB_COMM_STREAM_PRIORITY < 0 ignored: high-priority comm streams "
+                      "stretch every kernel dispatch (profiles/r03_overlap/SUMMARY.md); set "
+                      "DLBB_ALLOW_HIGH_PRIO_COMM=1 to force it", RuntimeWarning, stacklevel=2)
+        return 0
+    return p
 _ALIGN = 64  # elements: keeps every param view 128-B aligned (16-B MFMA/glds rows)
 
 
@@ -69,7 +88,8 @@ class FlatParamTrainer:
                  betas=(0.9, 0.95), weight_decay: float = 0.0, bucket_mb: float = 64.0,
                  overlap: bool = True, mode: str = "view", allreduce: str = "rccl",
                  grad_dtype: torch.dtype = torch.bfloat16, comm_blocks: Optional[int] = None,
-                 emulate_comm=False, emulate_world: int = 8, split_optimizer: bool = True):
+                 emulate_comm=False, emulate_world: int = 8, split_optimizer: bool = True,
+                 late_bucket: bool = True):
         if mode == "view" and grad_dtype != torch.bfloat16:
             raise ValueError("grad_dtype must be the parameter dtype (bf16) in mode='view': "
                              "autograd accumulates straight into the bucket views; use "
@@ -98,9 +118,11 @@ class FlatParamTrainer:
         # them, not the last blocks' gradients too (GPT-2's tail bucket was
         # blocks 1-0 + the tied 77 MB wte, ~43 % of the gradient bytes).
         offs, spans, cur, start, total = [], [], [], 0, 0
+        def is_late(q):
+            return late_bucket and getattr(q, "_dlbb_late_grad", False)
+
         for i, p in enumerate(order):
-            late = getattr(p, "_dlbb_late_grad", False)
-            if late and cur and not any(getattr(q, "_dlbb_late_grad", False) for q in cur):
+            if is_late(p) and cur and not any(is_late(q) for q in cur):
                 total = (total + balign - 1) // balign * balign
                 spans.append((start, total, cur))
                 cur, start = [], total
@@ -153,7 +175,7 @@ class FlatParamTrainer:
             from .custom_allreduce import get_custom_allreduce
 
             self._car = get_custom_allreduce(comm)
-            self._comm_stream = torch.cuda.Stream(dev, priority=_COMM_PRIORITY)
+            self._comm_stream = torch.cuda.Stream(dev, priority=comm_stream_priority())
             # buckets are fixed slices of flat_grad: IPC-map them once, then every bucket
             # all-reduce is the in-place two-shot (no staging copy, no capacity limit)
             if self._car is not None and self._car.reg_healthy:
@@ -165,7 +187,7 @@ class FlatParamTrainer:
             from .rccl_native import get_native
 
             self._native = get_native(comm)
-            self._comm_stream = torch.cuda.Stream(dev, priority=_COMM_PRIORITY)
+            self._comm_stream = torch.cuda.Stream(dev, priority=comm_stream_priority())
         # CU budget of the bucket reductions that run beside backward: workgroups per IPC /
         # emulated reduction launch (None = the kernel's own size heuristic)
         self.comm_blocks = comm_blocks
@@ -184,7 +206,7 @@ class FlatParamTrainer:
         if emulate_comm:
             if self.world != 1 or dev.type != "cuda":
                 raise ValueError("emulate_comm is a single-GPU measurement (world 1, HIP device)")
-            self._comm_stream = torch.cuda.Stream(dev, priority=_COMM_PRIORITY)
+            self._comm_stream = torch.cuda.Stream(dev, priority=comm_stream_priority())
             self._emu_zero = torch.zeros(max(b.end - b.start for b in self.buckets),
                                          dtype=grad_dtype, device=dev)
             if not isinstance(emulate_comm, bool):

@@ -359,7 +359,7 @@ def test_ddp_matches_global_batch_and_ranks_stay_identical_ranks_on_one_gpu(allr
 
     res = run_multiprocess(ddp_equivalence_worker, 2, args=("gloo", allreduce, fp32_buckets),
                            timeout=600)
-    tol = 5e-3 if fp32_buckets else 3e-2
+    tol = 1.5e-2 if fp32_buckets else 3e-2
     for worst, digests, nb in res:
         assert worst < tol, worst
         assert len(set(digests)) == 1, digests
@@ -439,6 +439,29 @@ def test_run_tp_shard_as_world1(tmp_path):
     B, S, H = cfg["input"]["batch_size"], cfg["input"]["sequence_length"], cfg["model"]["hidden_size"]
     assert th["allreduce_bytes_per_forward_per_rank"] == 2 * 2 * B * S * H * 2
     assert th["tokens_per_s"] > 0
+
+
+def test_ddp_comm_stream_fenced_to_normal_priority(monkeypatch):
+    """The fence in action: DLBB_COMM_STREAM_PRIORITY=-1 alone yields a NORMAL-priority comm
+    stream (the high-priority dispatch trap, profiles/r03_overlap/SUMMARY.md)."""
+    import warnings
+
+    from distributed_llm_backend_benchmark_amd.models.gpt2 import GPT2, GPT2Config
+    from distributed_llm_backend_benchmark_amd.parallel import ddp
+
+    monkeypatch.setattr(ddp, "_COMM_PRIORITY", -1)
+    monkeypatch.delenv("DLBB_ALLOW_HIGH_PRIO_COMM", raising=False)
+    cfg = GPT2Config(vocab_size=256, block_size=32, n_layer=1, n_head=2, n_embd=64)
+    m = GPT2(cfg, device=torch.device("cuda"), seed=1)
+    with warnings.catch_warnings(record=True):
+        warnings.simplefilter("always")
+        tr = ddp.FlatParamTrainer(m, None, emulate_comm=True)
+    assert tr._comm_stream.priority == 0
+    tr.close()
+    monkeypatch.setenv("DLBB_ALLOW_HIGH_PRIO_COMM", "1")
+    tr = ddp.FlatParamTrainer(m, None, emulate_comm=True)
+    assert tr._comm_stream.priority < 0
+    tr.close()
 
 
 def test_bench_py_world1():
