@@ -21,6 +21,8 @@
 //     one vmcnt(0) + barrier per K-tile.
 //   * XCD-aware bijective workgroup remap (T1) + GROUP_M tile grouping for L2 reuse.
 //   * M and N may be ragged (source rows clamped, stores masked); K % 64 == 0.
+#include <utility>
+
 #include "common.h"
 
 namespace dlbb {
@@ -1099,6 +1101,245 @@ DLBB_PP_STAMPED(gemm_bf16_tn_256_pingpong3, true, false, true)
 DLBB_PP_STAMPED(gemm_bf16_tn_256_pingpong3_bal, true, true, true)
 #undef DLBB_PP_STAMPED
 
+// ---------------------------------------------------------------------------------------
+// One wave per SIMD (A/B only, set_stagger(9); profiles/r03_gemm/w4_experiment.md): 256 x 256
+// tile, 256 threads = 4 waves as 2 (M) x 2 (N), each wave 128 x 128 outputs = 64 accumulators of
+// 16x16 held in AGPRs — hipBLASLt's MT256x256x64 MI16x16 structure. The MFMAs are inline asm
+// with "+a" accumulator operands, so hipcc keeps all 256 accumulators in AGPRs across the loop
+// and never moves them through VGPRs (round 2's builtin-MFMA 4-wave build did, and spilled:
+// ~500 TF/s). Correct (bitwise equal to the ping-pong) but 1300-1340 TF/s at 8192^3 against
+// 1550 for the ping-pong and 1640-1680 for hipBLASLt: MFMA busy 64 % vs 82 / 88 %. A register-
+// staged form (buffer_load -> ds_write) measured 1300-1315 and was dropped.
+// The asm MFMAs are invisible to hipcc's hazard recognizer, so (1) every loop iteration must
+// run the SAME code — a peeled copy got its own register assignment and hipcc permuted
+// accumulators with v_accvgpr_mov right behind the MFMAs that wrote them — and (2) the
+// accumulators are read out only after s_nop padding past the last MFMA's write latency.
+constexpr int kThreadsW4 = 256;
+
+#define DLBB_FENCE() asm volatile("" ::: "memory")
+
+__device__ __forceinline__ void mfma_agpr(f32x4& acc, const bf16x8& b, const bf16x8& a) {
+  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(b), "v"(a));
+}
+
+// MFMA group g of a half: output rows i = g / 2, column blocks j = (g % 2) * 4 .. + 3
+template <int G>
+__device__ __forceinline__ void w4_mfma(f32x4 (&acc)[2][8][4], const bf16x8 (&fa)[8],
+                                        const bf16x8 (&fb)[8]) {
+  constexpr int i = G >> 1, jg = G & 1;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) mfma_agpr(acc[jg][i][j], fb[jg * 4 + j], fa[i]);
+}
+
+// ---------------------------------------------------------------------------------------
+// The one-wave-per-SIMD kernel with LDS-DMA staging in half-K-tile stages (set_stagger(9)).
+// hipBLASLt's MT256x256x64 MI16x16 kernel (disassembled from the ROCm library: 4 waves, 128
+// MFMA + 32 ds_read_b128 + 16 buffer_load...lds per K-tile, the loads spread between MFMAs,
+// vmcnt(13) kept in flight across its barriers) stages by DMA, not through registers; this is
+// that structure in HIP: staging costs no VGPRs and no ds_write, and the LDS ring is deep.
+//   * A stage is one k-step of 32: A [256 rows][64 B] + B [256][64 B] = 32 KiB; 4 stages
+//     (128 KiB) in a ring. One DMA piece = 16 rows x 64 B; 8 pieces per wave per stage (4 of A
+//     rows [64w, 64w + 64), 4 of B rows [64w, 64w + 64)).
+//   * 64-B rows: 16-B slot s of row r holds k-chunk s ^ f((r >> 2) & 3), f = {0, 3, 2, 1}:
+//     every lane group of a ds_read_b128 (groups {0-3,12-15,20-27}, {4-11,16-19,28-31}, ...)
+//     then hits 16 distinct bank quads for the MFMA fragment pattern (row = lane & 15, chunk =
+//     lane >> 4) — checked exhaustively on the host (ops/gemm.py w4_swizzle_check).
+//   * Half h (k-step h): 16 groups of 4 MFMAs on F(h); groups 0-7 also read F(h+1) (2 each),
+//     groups 8-15 issue one DMA piece each of k-step h + 4 into stage (h + 4) % 4 = h % 4.
+//     End of half: vmcnt(16) (k-step h+2 landed: only h+3, h+4's 16 pieces may stay in
+//     flight), lgkmcnt(0), barrier. One barrier per k-step.
+//   RAW: F(h+1) is read in half h; its DMA (issued in half h-3) was retired by the vmcnt of half
+//   h-1 and published by that half's barrier. WAR: k-step h+4 overwrites stage h % 4, whose
+//   fragments F(h) were read in half h-1 and retired (lgkmcnt(0)) before half h-1's barrier.
+//   Past the last k-step the DMA re-reads the last one (clamped source, dead stage) so every
+//   half runs the same code and the counted waits stay exact.
+// Host contract: M % 16 == 0, N % 64 == 0, K % 64 == 0, K >= 128, 32-bit buffer offsets.
+constexpr int kW4dStage = 2 * BM2 * 32 * 2;          // 32 KiB
+constexpr int kW4dStages = 4;
+constexpr int kW4dLds = kW4dStages * kW4dStage;      // 128 KiB
+
+__device__ __forceinline__ int w4d_f(int q) { return (4 - q) & 3; }
+
+struct W4dCtx {
+  __amdgpu_buffer_rsrc_t ra, rb;
+  uint32_t voff_a, voff_b;     // per lane: row-in-piece x ld + swizzled 16-B chunk
+  uint32_t lda2, ldb2;
+  uint32_t sa[4], sb[4];       // per piece: group row x ld (SGPR)
+  uint32_t rd_off;             // per lane: fragment row fr x 64 B + swizzled slot
+  int wr, wc;
+  char* smem;
+};
+
+template <int P>   // piece P: 0..3 A, 4..7 B
+__device__ __forceinline__ void w4d_dma(const W4dCtx& c, char* stage, int ks) {
+  const uint32_t k2 = static_cast<uint32_t>(ks) * 64;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if constexpr (P < 4)
+    bldsx4(c.ra, c.voff_a, c.sa[P] + k2, stage + (wave * 64 + P * 16) * 64);
+  else
+    bldsx4(c.rb, c.voff_b, c.sb[P - 4] + k2, stage + BM2 * 64 + (wave * 64 + (P - 4) * 16) * 64);
+}
+
+// fragment G of F(h) (order of first use: a0, b0..b7, a1..a7)
+template <int G>
+__device__ __forceinline__ void w4d_read(const W4dCtx& c, const char* stage, bf16x8 (&fa)[8],
+                                         bf16x8 (&fb)[8]) {
+  if constexpr (G == 0)
+    fa[0] = *reinterpret_cast<const bf16x8*>(stage + (c.wr * 128) * 64 + c.rd_off);
+  else if constexpr (G <= 8)
+    fb[G - 1] = *reinterpret_cast<const bf16x8*>(stage + BM2 * 64 +
+                                                 (c.wc * 128 + (G - 1) * 16) * 64 + c.rd_off);
+  else
+    fa[G - 8] = *reinterpret_cast<const bf16x8*>(stage + (c.wr * 128 + (G - 8) * 16) * 64 +
+                                                 c.rd_off);
+}
+
+// V (A/B variants, set_stagger(9 + V)): bit 0 = the 8 DMA pieces go out in groups 0-7 beside
+// the reads (else groups 8-15); bit 1 = the half's last MFMA is issued AFTER its waits, just
+// before the barrier, so the matrix pipe has work while the wave waits there.
+template <int V, int G>
+__device__ __forceinline__ void w4d_group(const W4dCtx& c, f32x4 (&acc)[2][8][4],
+                                          const bf16x8 (&ca)[8], const bf16x8 (&cb)[8],
+                                          bf16x8 (&na)[8], bf16x8 (&nb)[8], const char* rd,
+                                          char* wr_stage, int ksd) {
+  if constexpr ((V & 2) && G == 15) {
+    constexpr int i = G >> 1, jg = G & 1;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) mfma_agpr(acc[jg][i][j], cb[jg * 4 + j], ca[i]);
+  } else {
+    w4_mfma<G>(acc, ca, cb);
+  }
+  DLBB_FENCE();
+  if constexpr (G < 8) {
+    w4d_read<2 * G>(c, rd, na, nb);
+    w4d_read<2 * G + 1>(c, rd, na, nb);
+    if constexpr (V & 1) w4d_dma<G>(c, wr_stage, ksd);
+  } else {
+    if constexpr (!(V & 1)) w4d_dma<G - 8>(c, wr_stage, ksd);
+  }
+  DLBB_FENCE();
+}
+
+template <int V, int... G>
+__device__ __forceinline__ void w4d_half(const W4dCtx& c, f32x4 (&acc)[2][8][4],
+                                         const bf16x8 (&ca)[8], const bf16x8 (&cb)[8],
+                                         bf16x8 (&na)[8], bf16x8 (&nb)[8], const char* rd,
+                                         char* wr_stage, int ksd,
+                                         std::integer_sequence<int, G...>) {
+  (w4d_group<V, G>(c, acc, ca, cb, na, nb, rd, wr_stage, ksd), ...);
+  DLBB_WAIT_VM(16);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  if constexpr (V & 2) {
+    __builtin_amdgcn_sched_barrier(0);
+    mfma_agpr(acc[1][7][3], cb[7], ca[7]);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  __builtin_amdgcn_s_barrier();
+  DLBB_FENCE();
+}
+
+template <int... P>
+__device__ __forceinline__ void w4d_dma_all(const W4dCtx& c, char* stage, int ks,
+                                            std::integer_sequence<int, P...>) {
+  (w4d_dma<P>(c, stage, ks), ...);
+}
+
+template <int... G>
+__device__ __forceinline__ void w4d_read_all(const W4dCtx& c, const char* stage, bf16x8 (&fa)[8],
+                                             bf16x8 (&fb)[8], std::integer_sequence<int, G...>) {
+  (w4d_read<G>(c, stage, fa, fb), ...);
+}
+
+// epilogue quarter (column half JG, row half Q) with compile-time indices only: an array
+// indexed by a loop the unroller declines to unroll would send all 256 accumulators to scratch
+template <int JG, int Q>
+__device__ __forceinline__ void w4d_store_quarter(const GemmArgs& a, const f32x4 (&acc)[2][8][4],
+                                                  int64_t r0, int64_t c0, int lane) {
+  f32x4 part[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) part[i][j] = acc[JG][4 * Q + i][j];
+  store_tile<4>(a, part, r0 + 64 * Q, c0 + 64 * JG, lane);
+}
+
+template <int V>
+__global__ void __launch_bounds__(kThreadsW4, 1) gemm_bf16_nt_w4d(GemmArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  W4dCtx c;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  c.wr = wave >> 1;
+  c.wc = wave & 1;
+  c.smem = smem;
+  const Tile256 tl = tile_of(a, static_cast<int>(blockIdx.x));
+  const int64_t m0 = tl.m0, n0 = tl.n0;
+  const int H = static_cast<int>(a.K / 32);           // k-steps
+  c.lda2 = static_cast<uint32_t>(a.lda) * 2;
+  c.ldb2 = static_cast<uint32_t>(a.ldb) * 2;
+  const int rows_a = static_cast<int>(a.M - m0), rows_b = static_cast<int>(a.N - n0);
+  {
+    // DMA lane l -> LDS row l >> 2 of the piece, slot l & 3; it loads k-chunk slot ^ f(row)
+    const int r = lane >> 2, slot = lane & 3;
+    const int ch = slot ^ w4d_f((r >> 2) & 3);
+    c.voff_a = static_cast<uint32_t>(r) * c.lda2 + ch * 16;
+    c.voff_b = static_cast<uint32_t>(perm_brow(r)) * c.ldb2 + ch * 16;
+  }
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const int trow = wave * 64 + p * 16;
+    const int ga = trow < rows_a - 16 ? trow : rows_a - 16;
+    const int gb = (trow & ~63) < rows_b ? perm_brow(trow) : (perm_brow(trow) & 63);
+    c.sa[p] = static_cast<uint32_t>(ga) * c.lda2;
+    c.sb[p] = static_cast<uint32_t>(gb) * c.ldb2;
+  }
+  {
+    const int fr = lane & 15, fq = lane >> 4;
+    c.rd_off = static_cast<uint32_t>(fr * 64 + ((fq ^ w4d_f((fr >> 2) & 3)) << 4));
+  }
+  c.ra = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(a.A + m0 * a.lda), 0, 0x7fffffff,
+                                           0x00020000);
+  c.rb = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(a.B + n0 * a.ldb), 0, 0x7fffffff,
+                                           0x00020000);
+  f32x4 acc[2][8][4];
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[h][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 fa0[8], fb0[8], fa1[8], fb1[8];
+  constexpr auto seq8 = std::make_integer_sequence<int, 8>{};
+  constexpr auto seq16 = std::make_integer_sequence<int, 16>{};
+  // prologue: k-steps 0..3 in flight (stages 0..3), k-step 0 landed -> F(0)
+#pragma unroll
+  for (int d = 0; d < kW4dStages; ++d)
+    w4d_dma_all(c, smem + d * kW4dStage, d < H ? d : H - 1, seq8);
+  DLBB_WAIT_VM(24);
+  __builtin_amdgcn_s_barrier();
+  DLBB_FENCE();
+  w4d_read_all(c, smem, fa0, fb0, seq16);
+  for (int h = 0; h < H; h += 2) {
+    // even half: compute F(h) (fa0/fb0), read F(h+1) into fa1/fb1, DMA k-step h+4
+    w4d_half<V>(c, acc, fa0, fb0, fa1, fb1, smem + ((h + 1) & 3) * kW4dStage,
+                smem + (h & 3) * kW4dStage, h + 4 < H ? h + 4 : H - 1, seq16);
+    // odd half
+    w4d_half<V>(c, acc, fa1, fb1, fa0, fb0, smem + ((h + 2) & 3) * kW4dStage,
+                smem + ((h + 1) & 3) * kW4dStage, h + 5 < H ? h + 5 : H - 1, seq16);
+  }
+  DLBB_WAIT_VM(0);
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+  // the epilogue in 64-row quarters: fewer accumulators live in VGPRs at once (no spill)
+  w4d_store_quarter<0, 0>(a, acc, m0 + c.wr * 128, n0 + c.wc * 128, lane);
+  w4d_store_quarter<0, 1>(a, acc, m0 + c.wr * 128, n0 + c.wc * 128, lane);
+  w4d_store_quarter<1, 0>(a, acc, m0 + c.wr * 128, n0 + c.wc * 128, lane);
+  w4d_store_quarter<1, 1>(a, acc, m0 + c.wr * 128, n0 + c.wc * 128, lane);
+}
+
+static void launch_w4d(dim3 g, const GemmArgs& a, hipStream_t stream) {
+  hipLaunchKernelGGL(gemm_bf16_nt_w4d<0>, g, dim3(kThreadsW4), kW4dLds, stream, a);
+}
+
 }  // namespace dlbb
 
 using namespace dlbb;
@@ -1162,7 +1403,11 @@ DLBB_API int dlbb_gemm_bf16_nt(const void* A, int64_t lda, const void* B, int64_
     if ((mode == 6 || mode == 7) && !(M % 8 == 0 && N % 64 == 0 && M >= 8 && lda * 2 * 256 + K * 2 < (1LL << 31) &&
                        ldb * 2 * 256 + K * 2 < (1LL << 31)))
       mode = 3;
-    if (mode == 5 || mode > 7) mode = 3;
+    // one-wave-per-SIMD kernel (mode 9): M % 16, N % 64, at least two K-tiles
+    if (mode == 9 && !(M % 16 == 0 && N % 64 == 0 && K >= 2 * BK &&
+                       lda * 2 * 256 + K * 2 < (1LL << 31) && ldb * 2 * 256 + K * 2 < (1LL << 31)))
+      mode = 6;
+    if (mode == 5 || mode == 8 || mode > 9) mode = 3;
     if (mode == 4) {
       static int ncu[64] = {0};
       int dev = 0;
@@ -1178,7 +1423,9 @@ DLBB_API int dlbb_gemm_bf16_nt(const void* A, int64_t lda, const void* B, int64_
       const int64_t grid = tiles256 < ncu[dev] ? tiles256 : ncu[dev];
       hipLaunchKernelGGL(gemm_bf16_nt_256_persistent, dim3(static_cast<unsigned>(grid)), b,
                          2 * kBuf2Bytes, stream, a);
-    } else if (mode == 7 || (mode == 6 && use_bal(K / BK, false)))
+    } else if (mode == 9)
+      launch_w4d(g, a, stream);
+    else if (mode == 7 || (mode == 6 && use_bal(K / BK, false)))
       DLBB_PP_LAUNCH(gemm_bf16_nt_256_pingpong3_bal, STAMP_GEMM_NT, g, a);
     else if (mode == 6)
       DLBB_PP_LAUNCH(gemm_bf16_nt_256_pingpong3, STAMP_GEMM_NT, g, a);
