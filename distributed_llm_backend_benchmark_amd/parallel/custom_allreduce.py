@@ -106,6 +106,7 @@ class CustomAllReduce:
         self._regs: Dict[tuple, int] = {}
         self._reg_keep: Dict[int, torch.Tensor] = {}   # rid -> registered tensor (kept alive)
         self._reg_refs: Dict[int, int] = {}            # rid -> register() calls not released
+        self._owned: Dict[tuple, Tuple[torch.Tensor, int]] = {}   # (numel, dtype) -> (buf, rid)
 
     # ------------------------------------------------------------------ policy
     def supports(self, t: torch.Tensor) -> bool:
@@ -191,6 +192,19 @@ class CustomAllReduce:
         self.comm.barrier()
         if any(r != 0 for r in oks):
             raise RuntimeError(f"custom all-reduce deregistration failed (hip rc: {oks})")
+
+    def registered_buffer(self, numel: int, dtype: torch.dtype) -> Tuple[torch.Tensor, int]:
+        """Collective on first use of a (numel, dtype): a flat buffer owned by this instance,
+        IPC-registered on every rank — a producer (e.g. the row-parallel GEMM) writes straight
+        into it and :meth:`all_reduce_registered` reduces it in place. The same buffer comes
+        back on later calls (callers must consume it before the next producer writes it)."""
+        key = (int(numel), dtype)
+        ent = self._owned.get(key)
+        if ent is None:
+            buf = torch.empty(int(numel), dtype=dtype, device=self.comm.device)
+            ent = (buf, self.register(buf))
+            self._owned[key] = ent
+        return ent
 
     def reg_counts(self) -> Tuple[int, int]:
         """(live registrations, opened peer IPC mappings) of this rank."""

@@ -115,6 +115,30 @@ class RowParallelLinear(nn.Module):
             spin_ns(int(nbytes * 2.0 * (P - 1) / P / self.emulate_busbw), self.emulate_blocks,
                     t.device)
 
+    # ---- registered output buffer: the GEMM writes the partial sum straight into a buffer every
+    # rank IPC-mapped once, and the in-place registered two-shot reduces it there — no copy into
+    # the staging buffer, no capacity limit. The IPC instance owns one buffer per (shape, dtype),
+    # shared by every row-parallel layer of the model: the forward is sequential on one stream and
+    # each output is consumed (next LayerNorm) before the next row-parallel GEMM rewrites it, and
+    # the kernel's exit barrier (phase 2) guarantees no peer still reads it by then.
+    def _registered_out(self, shape, dtype) -> Optional[tuple]:
+        car = self._car
+        if car is None or not car.reg_healthy or self.allreduce not in ("custom", "auto"):
+            return None
+        numel = 1
+        for d in shape:
+            numel *= int(d)
+        esz = torch.tensor([], dtype=dtype).element_size()
+        nbytes = numel * esz
+        if nbytes <= car.oneshot_max:          # small (decode): staged one-shot is faster
+            return None
+        if nbytes % (8 * esz * self.comm.world_size):
+            return None
+        limit = getattr(car, "reg_max", None)  # calibrated: registered beats RCCL up to here
+        if self.allreduce == "auto" and nbytes > (limit if limit is not None else car.auto_max):
+            return None
+        return car.registered_buffer(numel, dtype)   # collective on first use of this shape
+
     def _all_reduce(self, t: torch.Tensor) -> None:
         self.comm_bytes += t.numel() * t.element_size()
         if self.comm.world_size == 1:
@@ -139,8 +163,18 @@ class RowParallelLinear(nn.Module):
                 y = y.float()
             self._all_reduce(y)
             return y.to(x.dtype)
-        y = ops.linear(x, self.weight, out_dtype=torch.float32 if fp32_wire else x.dtype)
-        self._all_reduce(y)
+        odt = torch.float32 if fp32_wire else x.dtype
+        reg = (self._registered_out((*x.shape[:-1], self.out_features), odt)
+               if self.comm.world_size > 1 and x.is_cuda else None)
+        if reg is not None:
+            buf, rid = reg
+            y = buf.view(*x.shape[:-1], self.out_features)
+            ops.linear(x, self.weight, out_dtype=odt, out=y)
+            self.comm_bytes += y.numel() * y.element_size()
+            self._car.all_reduce_registered(buf, rid)
+        else:
+            y = ops.linear(x, self.weight, out_dtype=odt)
+            self._all_reduce(y)
         if fp32_wire:
             return ops.cast(y, x.dtype)   # HIP cast kernel (reference models.py:98)
         return y

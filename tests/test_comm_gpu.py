@@ -380,8 +380,11 @@ def _tp_rehearsal_worker(rank, world, allreduce):
     kw = dict(hidden_size=256, num_layers=2, num_heads=4, ffn_intermediate=1024, seed=11,
               init_std=0.05)
     dense = LLM(comm=Comm(0, 1, 0, "gloo", dev), **kw)
-    tp = LLM(comm=comm, allreduce=allreduce, **kw)
+    reg = allreduce == "custom_reg"
+    tp = LLM(comm=comm, allreduce="custom" if reg else allreduce, **kw)
     tp.load_from_dense(dense.state_dict())
+    if reg:   # every message in the two-shot regime: GEMM into the registered buffer, in place
+        tp.ipc_allreduce().oneshot_max = 0
     g = torch.Generator(device=dev).manual_seed(5)
     x = torch.randn(2, 64, 256, generator=g, device=dev).to(torch.bfloat16)
     y_ref = dense(x).float()
@@ -394,24 +397,27 @@ def _tp_rehearsal_worker(rank, world, allreduce):
     scale = float(y_ref.abs().max())
     err = max(float((y - y_ref).abs().max()), float((y2 - y_ref).abs().max())) / scale
     mix = gemm.kernel_mix()
+    owned = len(car._owned) if car is not None else 0
     comm.destroy()
-    return err, used_custom, errflag, mix["forced"], comm.world_size
+    return err, used_custom, errflag, mix["forced"], comm.world_size, owned
 
 
 @pytest.mark.parametrize("world", [2, 4])
-@pytest.mark.parametrize("allreduce", ["rccl", "custom"])
+@pytest.mark.parametrize("allreduce", ["rccl", "custom", "custom_reg"])
 def test_tp_forward_ranks_on_one_gpu_matches_dense(world, allreduce):
     """the TP transformer (reference models.py) with the HIP kernels at
     P = 2 / 4 — column/row-parallel GEMMs on the hand-written MFMA kernel, row-parallel partial
     sums through the process group (gloo over GPU tensors) or the IPC kernel — equals the dense
     world-1 model loaded with the same weights."""
     res = run_multiprocess(_tp_rehearsal_worker, world, args=(allreduce,), timeout=600)
-    for err, used_custom, errflag, forced, w in res:
+    for err, used_custom, errflag, forced, w, owned in res:
         assert w == world
         assert err < 3e-2, err
         assert forced == "mfma"
         assert errflag == 0
-        assert used_custom == (allreduce == "custom")
+        assert used_custom == (allreduce != "rccl")
+        # registered in-place path: one owned buffer (shared by every row-parallel layer)
+        assert owned == (1 if allreduce == "custom_reg" else 0), owned
 
 
 def test_run_tp_shard_as_world1(tmp_path):
