@@ -136,9 +136,14 @@ def _allreduce_sweep(comm, max_mib: int):
 def too_fast(op_name: str, nbytes: int, seconds: float, P: int):
     """The reason a timing is physically impossible (below the traffic-based memory / xGMI
     roofline of ``stats.bandwidth.min_seconds``: the call enqueued no work), else None."""
+    import torch
+
     from distributed_llm_backend_benchmark_amd.stats.bandwidth import roofline_violation
 
-    return roofline_violation(op_name, nbytes, seconds, P)
+    # ranks sharing one device (a rehearsal on a one-GPU box): no xGMI link in the path
+    ndev = torch.cuda.device_count() if torch.cuda.is_available() else 0
+    colocated = P > 1 and 0 < ndev < int(os.environ.get("LOCAL_WORLD_SIZE", P))
+    return roofline_violation(op_name, nbytes, seconds, P, colocated)
 
 
 def _checked(comm, op, ref) -> bool:

@@ -1398,15 +1398,15 @@ DLBB_API int dlbb_gemm_bf16_nt(const void* A, int64_t lda, const void* B, int64_
   if (force == 256 || (force != 128 && tiles256 >= 192)) {
     const dim3 g(static_cast<unsigned>(tiles256)), b(kThreads2);
     int mode = dlbb_gemm_stagger;
+    // one-wave-per-SIMD kernel (mode 9): M % 16, N % 64, at least two K-tiles
+    if (mode == 9 && !(M % 16 == 0 && N % 64 == 0 && K >= 2 * BK &&
+                       lda * 2 * 256 + K * 2 < (1LL << 31) && ldb * 2 * 256 + K * 2 < (1LL << 31)))
+      mode = 6;                       // (then held to the ping-pong contract below)
     // ping-pong contract: 8-row A groups and 64-row B blocks wholly in or out (uniform clamps),
     // 32-bit buffer offsets within a 256-row panel
     if ((mode == 6 || mode == 7) && !(M % 8 == 0 && N % 64 == 0 && M >= 8 && lda * 2 * 256 + K * 2 < (1LL << 31) &&
                        ldb * 2 * 256 + K * 2 < (1LL << 31)))
       mode = 3;
-    // one-wave-per-SIMD kernel (mode 9): M % 16, N % 64, at least two K-tiles
-    if (mode == 9 && !(M % 16 == 0 && N % 64 == 0 && K >= 2 * BK &&
-                       lda * 2 * 256 + K * 2 < (1LL << 31) && ldb * 2 * 256 + K * 2 < (1LL << 31)))
-      mode = 6;
     if (mode == 5 || mode == 8 || mode > 9) mode = 3;
     if (mode == 4) {
       static int ncu[64] = {0};

@@ -115,14 +115,20 @@ _RECV = {
 }
 
 
-def min_seconds(op: str, nbytes: float, num_ranks: int) -> float:
+def min_seconds(op: str, nbytes: float, num_ranks: int, colocated: bool = False) -> float:
     """Lower bound on one call's time: the rank's own memory traffic at the HBM peak (the on-die
     cache ceiling when it fits in the 256 MiB Infinity Cache) and, at P > 1, the bytes it must
-    receive spread over all P - 1 xGMI links at the link peak."""
+    receive spread over all P - 1 xGMI links at the link peak. ``colocated``: all P ranks share
+    ONE device (rehearsals on a one-GPU box) — no link is crossed and the bound is the P ranks'
+    combined local traffic on that device's memory."""
     p = int(num_ranks)
     if op not in _LOCAL_TRAFFIC:
         raise KeyError(f"unknown op {op!r}")
     local = _LOCAL_TRAFFIC[op](float(nbytes), p)
+    if colocated and p > 1:
+        local *= p
+        peak = ONDIE_PEAK_GBPS if local <= ONDIE_BYTES else HBM_PEAK_GBPS
+        return local / (peak * GB)
     peak = ONDIE_PEAK_GBPS if local <= ONDIE_BYTES else HBM_PEAK_GBPS
     t = local / (peak * GB)
     if p > 1 and op in _RECV:
@@ -130,14 +136,16 @@ def min_seconds(op: str, nbytes: float, num_ranks: int) -> float:
     return t
 
 
-def roofline_violation(op: str, nbytes: float, seconds: float, num_ranks: int) -> Optional[str]:
+def roofline_violation(op: str, nbytes: float, seconds: float, num_ranks: int,
+                       colocated: bool = False) -> Optional[str]:
     """None when ``seconds`` is physically possible for ``op``; else the reason (an empty call
     or a timing that missed the work) — never report such a number."""
     if seconds is None or seconds <= 0:
         return "non-positive time"
-    floor = min_seconds(op, nbytes, num_ranks)
+    floor = min_seconds(op, nbytes, num_ranks, colocated)
     if seconds < floor:
-        return (f"{op} of {int(nbytes)} B at P={num_ranks} took {seconds * 1e6:.3f} us, below "
-                f"the {floor * 1e6:.3f} us memory/link roofline")
+        return (f"{op} of {int(nbytes)} B at P={num_ranks}"
+                f"{' (ranks on one device)' if colocated else ''} took {seconds * 1e6:.3f} us, "
+                f"below the {floor * 1e6:.3f} us memory/link roofline")
     return None
 

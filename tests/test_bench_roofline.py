@@ -53,3 +53,16 @@ def test_min_seconds_monotone_in_bytes_and_known_ops():
             assert 0 < a < b
     with pytest.raises(KeyError):
         bw.min_seconds("nonsense", MIB, 2)
+
+
+def test_colocated_ranks_bound_is_device_memory_not_links():
+    """Ranks sharing one GPU (the two-rank rehearsal on a one-GPU box) cross no xGMI link: a
+    64 MiB all-reduce at P=2 in 75 us (~4 TB/s of combined traffic) is possible there, while
+    across two GPUs it would beat the link peak."""
+    nbytes = 64 * MIB
+    assert bw.roofline_violation("allreduce", nbytes, 75e-6, 2) is not None
+    assert bw.roofline_violation("allreduce", nbytes, 75e-6, 2, colocated=True) is None
+    # an empty call is still caught
+    assert bw.roofline_violation("allreduce", nbytes, 2e-6, 2, colocated=True) is not None
+    assert bw.min_seconds("allreduce", nbytes, 2, colocated=True) > bw.min_seconds(
+        "allreduce", nbytes, 1)
