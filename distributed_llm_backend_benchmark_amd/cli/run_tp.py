@@ -62,6 +62,11 @@ def parse_args(argv=None):
     ap.add_argument("--emulate-busbw", type=float, default=None, metavar="GBPS",
                     help="with --shard-as: also hold 32 workgroups for the ring all-reduce time "
                          "bytes*2(P-1)/P / busBW per all-reduce")
+    ap.add_argument("--overlap-chunks", type=int, default=None, metavar="N",
+                    help="split the batch into N micro-batches and interleave them so each "
+                         "row-parallel all-reduce (side comm stream) runs under the next "
+                         "micro-batch's GEMMs (execution.overlap_chunks; 1 = blocking, as the "
+                         "reference)")
     ap.add_argument("--check-dense", action="store_true",
                     help="after warmup, load the TP shards from a dense world-1 model of the "
                          "same seed (built on every rank) and report the max error of the TP "
@@ -96,6 +101,8 @@ def main(argv=None) -> int:
         ex["attention"] = args.attention
     if args.kernels:
         ex["kernels"] = args.kernels
+    if args.overlap_chunks:
+        ex["overlap_chunks"] = args.overlap_chunks
     if args.model_size:
         config["model"].update(MODEL_CONFIGS[args.model_size])
         config["model"]["size"] = args.model_size
@@ -261,6 +268,9 @@ def main(argv=None) -> int:
             # node-measured IPC-vs-RCCL crossovers behind allreduce=auto (None: RCCL only)
             "allreduce_calibration": calibration,
             "dense_check": dense_check,
+            # micro-batches interleaved so all-reduces run under GEMMs (1 = blocking)
+            "overlap_chunks": model.overlap_split(
+                torch.empty(B, 1, device="meta")),
         }
         if args.shard_as:
             extra["shard_as"] = {
@@ -287,6 +297,8 @@ def main(argv=None) -> int:
               f"\n  tokens/s: {extra['tokens_per_s']:.1f}  TFLOP/s/rank: "
               f"{extra['tflops_per_rank']:.1f}")
         suffix = f"_shard{args.shard_as}" if args.shard_as else ""
+        if extra["overlap_chunks"] > 1:
+            suffix += f"_ov{extra['overlap_chunks']}"
         out = os.path.join(config["experiment"]["output_dir"],
                            f"{args.backend}_{config['experiment']['name']}{suffix}.json")
         save_results(results, out, rank)

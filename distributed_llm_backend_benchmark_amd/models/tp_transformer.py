@@ -13,6 +13,7 @@ MI355X-specific: all compute on-device in bf16 through the gfx950 kernels (MFMA 
 GELU, fused residual+LayerNorm); the residual add of each sublayer is fused into the NEXT
 LayerNorm, so the block is ``LN1 → QKV → out-proj → AR → (add+LN2) → up+GELU → down → AR →
 (add+LN1 of the next block)``. ``attention="sdpa"`` swaps the stub for real causal attention.
+``overlap_chunks`` > 1 interleaves micro-batches so the all-reduces run under GEMMs (forward()).
 """
 
 from __future__ import annotations
@@ -89,20 +90,39 @@ class TransformerBlock(nn.Module):
     def forward(self, y1: torch.Tensor, h: torch.Tensor):
         """``y1`` = LN1(h) (computed by the caller's fused add+LN); returns (d, h) where the
         block output is ``h + d`` (added inside the next fused LayerNorm)."""
+        gen = self.steps(y1, h)
+        try:
+            while True:
+                next(gen)
+        except StopIteration as e:
+            return e.value
+
+    def steps(self, y1: torch.Tensor, h: torch.Tensor, slot: int = 0, stream=None):
+        """The block as a generator that yields after launching each of its two all-reduces
+        (the event to wait on before the all-reduced tensor is read; None when inline) —
+        :meth:`LLM.forward` interleaves micro-batches on it. Returns ``(d, h)``."""
         qkv = self.qkv_proj(y1)
-        a = self.out_proj(self._attn(qkv))
+        a, ev = self.out_proj.launch(self._attn(qkv), slot, stream)
+        yield ev
         y2, h = self.ln2(a, residual=h, kernels=self.kernels)          # h = h + attn_out
         u = self.ffn_up(y2, act="gelu")                                 # GELU fused (erf)
-        d = self.ffn_down(u)
+        d, ev = self.ffn_down.launch(u, slot, stream)
+        yield ev
         return d, h
 
 
 class LLM(nn.Module):
     def __init__(self, hidden_size: int, num_layers: int, num_heads: int, ffn_intermediate: int,
                  comm: Comm, seed: int = 0, init_std: float = 1.0, allreduce: str = "rccl",
-                 allreduce_dtype: str = "bf16", attention: str = "slice", kernels: str = "hip"):
+                 allreduce_dtype: str = "bf16", attention: str = "slice", kernels: str = "hip",
+                 overlap_chunks: int = 1):
         super().__init__()
         self.hidden_size, self.num_layers = hidden_size, num_layers
+        # > 1: split the batch into this many micro-batches and interleave them so every
+        # row-parallel all-reduce (on a side comm stream) runs under the next micro-batch's
+        # GEMMs — see forward()
+        self.overlap_chunks = max(1, int(overlap_chunks))
+        self._comm_stream = None
         self.num_heads, self.ffn_intermediate = num_heads, ffn_intermediate
         self.comm = comm
         self.world_size = comm.world_size
@@ -124,15 +144,65 @@ class LLM(nn.Module):
                 return car
         return None
 
-    def forward(self, x: torch.Tensor) -> torch.Tensor:
-        y, h = self.layers[0].ln1(x, kernels=self.kernels) if self.layers else (x, x)
-        for i, layer in enumerate(self.layers):
-            d, h = layer(y, h)
-            nxt = self.layers[i + 1].ln1 if i + 1 < len(self.layers) else self.ln_final
-            y, h = nxt(d, residual=h, kernels=self.kernels)
+    def _micro_batch(self, x: torch.Tensor, slot: int = 0, stream=None):
+        """One micro-batch's forward as a generator over its all-reduces (see
+        :meth:`TransformerBlock.steps`); returns the final LayerNorm output."""
         if not self.layers:
             y, _ = self.ln_final(x, kernels=self.kernels)
+            return y
+        y, h = self.layers[0].ln1(x, kernels=self.kernels)
+        for i, layer in enumerate(self.layers):
+            d, h = yield from layer.steps(y, h, slot, stream)
+            nxt = self.layers[i + 1].ln1 if i + 1 < len(self.layers) else self.ln_final
+            y, h = nxt(d, residual=h, kernels=self.kernels)
         return y
+
+    def overlap_split(self, x: torch.Tensor) -> int:
+        """Micro-batches the forward of ``x`` runs as: ``overlap_chunks`` when the batch splits
+        evenly (and the model is TP over more than one rank), else 1."""
+        n = self.overlap_chunks
+        if n <= 1 or self.world_size <= 1 or x.shape[0] % n:
+            return 1
+        return n
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        """Plain: one pass, each all-reduce inline. Overlapped (``overlap_chunks`` = n > 1): the
+        batch is split into n micro-batches run round-robin, each advancing to its next
+        all-reduce; the all-reduce goes to a side comm stream (normal priority — see
+        parallel/ddp.comm_stream_priority) and the micro-batch resumes only after its compute
+        stream waited for it. So all-reduce k of micro-batch A runs under the GEMMs of
+        micro-batch B, and every rank issues its collectives in the same order on one comm
+        stream. The reference blocks on each all-reduce (models.py:95)."""
+        n = self.overlap_split(x)
+        if n == 1:
+            gen = self._micro_batch(x)
+            try:
+                while True:
+                    next(gen)
+            except StopIteration as e:
+                return e.value
+        stream = None
+        if x.is_cuda:
+            if self._comm_stream is None:
+                self._comm_stream = torch.cuda.Stream(device=x.device, priority=0)
+            stream = self._comm_stream
+        cur = torch.cuda.current_stream(x.device) if x.is_cuda else None
+        gens = [self._micro_batch(xc, slot, stream) for slot, xc in enumerate(x.chunk(n, 0))]
+        pending = [None] * n
+        outs = [None] * n
+        live = n
+        while live:
+            for c in range(n):
+                if gens[c] is None:
+                    continue
+                if pending[c] is not None:
+                    cur.wait_event(pending[c])
+                try:
+                    pending[c] = next(gens[c])
+                except StopIteration as e:
+                    outs[c], gens[c], pending[c] = e.value, None, None
+                    live -= 1
+        return torch.cat(outs, 0)
 
     @torch.no_grad()
     def load_from_dense(self, dense_state: Dict[str, torch.Tensor]) -> None:
@@ -199,4 +269,5 @@ def create_model_from_config(config: Dict, comm: Comm) -> LLM:
                init_std=float(m.get("init_std", 1.0)),
                allreduce="rccl" if allreduce in ("torch",) else allreduce,
                allreduce_dtype=ex.get("allreduce_dtype", "bf16"),
-               attention=ex.get("attention", "slice"), kernels=ex.get("kernels", "hip"))
+               attention=ex.get("attention", "slice"), kernels=ex.get("kernels", "hip"),
+               overlap_chunks=int(ex.get("overlap_chunks", 1)))

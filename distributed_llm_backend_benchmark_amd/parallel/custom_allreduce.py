@@ -106,7 +106,7 @@ class CustomAllReduce:
         self._regs: Dict[tuple, int] = {}
         self._reg_keep: Dict[int, torch.Tensor] = {}   # rid -> registered tensor (kept alive)
         self._reg_refs: Dict[int, int] = {}            # rid -> register() calls not released
-        self._owned: Dict[tuple, Tuple[torch.Tensor, int]] = {}   # (numel, dtype) -> (buf, rid)
+        self._owned: Dict[tuple, Tuple[torch.Tensor, int]] = {}   # (numel, dtype, slot) -> ...
 
     # ------------------------------------------------------------------ policy
     def supports(self, t: torch.Tensor) -> bool:
@@ -193,12 +193,14 @@ class CustomAllReduce:
         if any(r != 0 for r in oks):
             raise RuntimeError(f"custom all-reduce deregistration failed (hip rc: {oks})")
 
-    def registered_buffer(self, numel: int, dtype: torch.dtype) -> Tuple[torch.Tensor, int]:
+    def registered_buffer(self, numel: int, dtype: torch.dtype,
+                          slot: int = 0) -> Tuple[torch.Tensor, int]:
         """Collective on first use of a (numel, dtype): a flat buffer owned by this instance,
         IPC-registered on every rank — a producer (e.g. the row-parallel GEMM) writes straight
         into it and :meth:`all_reduce_registered` reduces it in place. The same buffer comes
-        back on later calls (callers must consume it before the next producer writes it)."""
-        key = (int(numel), dtype)
+        back on later calls (callers must consume it before the next producer writes it);
+        ``slot`` keeps separate buffers for producers in flight at once (micro-batches)."""
+        key = (int(numel), dtype, int(slot))
         ent = self._owned.get(key)
         if ent is None:
             buf = torch.empty(int(numel), dtype=dtype, device=self.comm.device)

@@ -121,7 +121,7 @@ class RowParallelLinear(nn.Module):
     # shared by every row-parallel layer of the model: the forward is sequential on one stream and
     # each output is consumed (next LayerNorm) before the next row-parallel GEMM rewrites it, and
     # the kernel's exit barrier (phase 2) guarantees no peer still reads it by then.
-    def _registered_out(self, shape, dtype) -> Optional[tuple]:
+    def _registered_out(self, shape, dtype, slot: int = 0) -> Optional[tuple]:
         car = self._car
         if car is None or not car.reg_healthy or self.allreduce not in ("custom", "auto"):
             return None
@@ -137,7 +137,7 @@ class RowParallelLinear(nn.Module):
         limit = getattr(car, "reg_max", None)  # calibrated: registered beats RCCL up to here
         if self.allreduce == "auto" and nbytes > (limit if limit is not None else car.auto_max):
             return None
-        return car.registered_buffer(numel, dtype)   # collective on first use of this shape
+        return car.registered_buffer(numel, dtype, slot)   # collective on first use
 
     def _all_reduce(self, t: torch.Tensor) -> None:
         self.comm_bytes += t.numel() * t.element_size()
@@ -156,25 +156,51 @@ class RowParallelLinear(nn.Module):
             dist.all_reduce(t)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
+        y, _ = self.launch(x)
+        return y
+
+    def launch(self, x: torch.Tensor, slot: int = 0, stream=None):
+        """GEMM on the current stream, then the all-reduce — on ``stream`` when given (a
+        side comm stream: returns ``(y, event)``, and the caller makes its stream wait on the
+        event before reading ``y``; the overlapped TP forward runs another micro-batch's GEMMs
+        meanwhile), else inline (``event`` None). ``slot``: which registered output buffer (one
+        per micro-batch in flight)."""
         fp32_wire = self.allreduce_dtype == "fp32"
         if self.kernels == "torch":
             y = x @ self.weight.t()
             if fp32_wire:
                 y = y.float()
-            self._all_reduce(y)
-            return y.to(x.dtype)
+            return self._reduce_then(y, x.dtype, None, stream)
         odt = torch.float32 if fp32_wire else x.dtype
-        reg = (self._registered_out((*x.shape[:-1], self.out_features), odt)
+        reg = (self._registered_out((*x.shape[:-1], self.out_features), odt, slot)
                if self.comm.world_size > 1 and x.is_cuda else None)
         if reg is not None:
             buf, rid = reg
             y = buf.view(*x.shape[:-1], self.out_features)
             ops.linear(x, self.weight, out_dtype=odt, out=y)
-            self.comm_bytes += y.numel() * y.element_size()
-            self._car.all_reduce_registered(buf, rid)
         else:
             y = ops.linear(x, self.weight, out_dtype=odt)
-            self._all_reduce(y)
-        if fp32_wire:
-            return ops.cast(y, x.dtype)   # HIP cast kernel (reference models.py:98)
-        return y
+        return self._reduce_then(y, x.dtype, reg, stream)
+
+    def _reduce_then(self, y, out_dtype, reg, stream):
+        def reduce_and_cast():
+            if reg is not None:
+                self.comm_bytes += y.numel() * y.element_size()
+                self._car.all_reduce_registered(reg[0], reg[1])
+            else:
+                self._all_reduce(y)
+            if y.dtype == out_dtype:
+                return y
+            if self.kernels == "torch":
+                return y.to(out_dtype)
+            return ops.cast(y, out_dtype)   # HIP cast kernel (reference models.py:98)
+
+        if stream is None or not y.is_cuda:
+            return reduce_and_cast(), None
+        cur = torch.cuda.current_stream(y.device)
+        stream.wait_stream(cur)                 # the partial sum is complete
+        with torch.cuda.stream(stream):
+            out = reduce_and_cast()
+            ev = torch.cuda.Event()
+            ev.record(stream)
+        return out, ev

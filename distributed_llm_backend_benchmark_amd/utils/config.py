@@ -17,6 +17,8 @@ Additions (all optional, defaults keep reference behaviour):
   ``models.py:84``).
 * ``execution.attention``: ``slice`` (reference stub ``models.py:162-167``) | ``sdpa``.
 * ``execution.kernels``: ``hip`` (hand-written gfx950 kernels) | ``torch``.
+* ``execution.overlap_chunks``: micro-batches the TP forward interleaves so each row-parallel
+  all-reduce runs under another micro-batch's GEMMs (1 = the reference's blocking order).
 """
 
 from __future__ import annotations
@@ -45,6 +47,7 @@ DEFAULT_CONFIG: Dict[str, Any] = {
         "allreduce_dtype": "bf16",
         "attention": "slice",
         "kernels": "hip",
+        "overlap_chunks": 1,
     },
     "system": {"omp_num_threads": 14, "mkl_num_threads": 14},
 }
@@ -106,6 +109,8 @@ def validate_config(config: Dict[str, Any]) -> Dict[str, Any]:
         raise ConfigError("execution.attention must be slice|sdpa")
     if ex["kernels"] not in ("hip", "torch"):
         raise ConfigError("execution.kernels must be hip|torch")
+    if not isinstance(ex["overlap_chunks"], int) or ex["overlap_chunks"] < 1:
+        raise ConfigError("execution.overlap_chunks must be a positive int")
     return cfg
 
 

@@ -366,7 +366,7 @@ def test_ddp_matches_global_batch_and_ranks_stay_identical_ranks_on_one_gpu(allr
         assert nb > 1
 
 
-def _tp_rehearsal_worker(rank, world, allreduce):
+def _tp_rehearsal_worker(rank, world, allreduce, overlap=1):
     os.environ["DLBB_GEMM"] = "mfma"                 # the hand-written GEMM on every shape
     os.environ["DLBB_CUSTOM_AR_CALIBRATE"] = "0"     # (calibration has its own test)
     import torch
@@ -381,7 +381,7 @@ def _tp_rehearsal_worker(rank, world, allreduce):
               init_std=0.05)
     dense = LLM(comm=Comm(0, 1, 0, "gloo", dev), **kw)
     reg = allreduce == "custom_reg"
-    tp = LLM(comm=comm, allreduce="custom" if reg else allreduce, **kw)
+    tp = LLM(comm=comm, allreduce="custom" if reg else allreduce, overlap_chunks=overlap, **kw)
     tp.load_from_dense(dense.state_dict())
     if reg:   # every message in the two-shot regime: GEMM into the registered buffer, in place
         tp.ipc_allreduce().oneshot_max = 0
@@ -418,6 +418,19 @@ def test_tp_forward_ranks_on_one_gpu_matches_dense(world, allreduce):
         assert used_custom == (allreduce != "rccl")
         # registered in-place path: one owned buffer (shared by every row-parallel layer)
         assert owned == (1 if allreduce == "custom_reg" else 0), owned
+
+
+@pytest.mark.parametrize("allreduce", ["rccl", "custom", "custom_reg"])
+def test_tp_overlapped_forward_ranks_on_one_gpu_matches_dense(allreduce):
+    """The micro-batch interleaved TP forward (overlap_chunks=2: each all-reduce on a side comm
+    stream under the other micro-batch's GEMMs) at P = 2 equals the dense model; the registered
+    path keeps one IPC buffer per micro-batch in flight."""
+    res = run_multiprocess(_tp_rehearsal_worker, 2, args=(allreduce, 2), timeout=600)
+    for err, used_custom, errflag, forced, w, owned in res:
+        assert err < 3e-2, err
+        assert errflag == 0
+        assert used_custom == (allreduce != "rccl")
+        assert owned == (2 if allreduce == "custom_reg" else 0), owned
 
 
 def test_run_tp_shard_as_world1(tmp_path):

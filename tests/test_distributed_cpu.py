@@ -86,16 +86,27 @@ def _tp_worker(rank, world, attention):
     tp32.load_from_dense(dense.state_dict())
     err32 = float((tp32(x).float() - y_ref).abs().max())
     nbytes = tp.comm_bytes()
+    # micro-batch interleaved forward: same weights, same result (per-token math is unchanged;
+    # the all-reduces just run in a different order)
+    tpo = LLM(comm=comm, overlap_chunks=2, **kw)
+    tpo.load_from_dense(dense.state_dict())
+    y_ov = tpo(x).float()
+    ov_diff = float((y_ov - y_tp).abs().max())
+    ov_split = tpo.overlap_split(x)
+    odd = tpo.overlap_split(x[:1])              # batch 1 does not split: plain forward
     comm.destroy()
-    return err, err32, nbytes
+    return err, err32, nbytes, ov_diff, ov_split, odd, tpo.comm_bytes()
 
 
 @pytest.mark.parametrize("attention", ["slice", "sdpa"])
 def test_tensor_parallel_matches_dense(attention):
     res = run_multiprocess(_tp_worker, 2, args=(attention,), timeout=300)
-    for err, err32, nbytes in res:
+    for err, err32, nbytes, ov_diff, ov_split, odd, ov_bytes in res:
         assert err < 0.1 and err32 < 0.1, (err, err32)
         assert nbytes == 2 * 2 * (2 * 16 * 128 * 2)   # 2 layers x 2 AR x [B,S,H] bf16
+        assert ov_split == 2 and odd == 1
+        assert ov_diff == 0.0, ov_diff
+        assert ov_bytes == nbytes
 
 
 def _ddp_worker(rank, world, bucket_mb, overlap, mode):
