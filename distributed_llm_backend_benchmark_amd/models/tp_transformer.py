@@ -25,6 +25,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .. import ops
+from ..ops import gemm as gemm_ops
 from ..parallel.comm import Comm
 from ..parallel.tensor_parallel import ColumnParallelLinear, RowParallelLinear
 
@@ -33,6 +34,14 @@ MODEL_CONFIGS: Dict[str, Dict[str, int]] = {
     "7B": {"hidden_size": 4096, "num_layers": 32, "num_heads": 32, "ffn_intermediate": 16384},
     "13B": {"hidden_size": 5120, "num_layers": 40, "num_heads": 40, "ffn_intermediate": 20480},
 }
+
+
+class _NullCtx:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        return False
 
 
 class LayerNormParams(nn.Module):
@@ -122,7 +131,14 @@ class LLM(nn.Module):
         # row-parallel all-reduce (on a side comm stream) runs under the next micro-batch's
         # GEMMs — see forward()
         self.overlap_chunks = max(1, int(overlap_chunks))
+        # overlapped forward, A/B knob: each micro-batch on a compute stream of its own (so two
+        # micro-batches' small per-rank GEMMs could share the chip) instead of one compute
+        # stream. Measured worse (tools/diag/tp_overlap_probe.py, profiles/r03_tp): with three
+        # busy streams the all-reduces stop overlapping at all (7B shard-8 at 300 GB/s: 25.0 vs
+        # 18.0 ms), so the default is one compute stream + the comm stream.
+        self.chunk_streams = False
         self._comm_stream = None
+        self._chunk_streams = []
         self.num_heads, self.ffn_intermediate = num_heads, ffn_intermediate
         self.comm = comm
         self.world_size = comm.world_size
@@ -182,26 +198,40 @@ class LLM(nn.Module):
             except StopIteration as e:
                 return e.value
         stream = None
+        cur = torch.cuda.current_stream(x.device) if x.is_cuda else None
+        work = [cur] * n                        # the stream each micro-batch computes on
         if x.is_cuda:
             if self._comm_stream is None:
                 self._comm_stream = torch.cuda.Stream(device=x.device, priority=0)
             stream = self._comm_stream
-        cur = torch.cuda.current_stream(x.device) if x.is_cuda else None
+            if self.chunk_streams:
+                while len(self._chunk_streams) < n:
+                    self._chunk_streams.append(torch.cuda.Stream(device=x.device, priority=0))
+                work = self._chunk_streams[:n]
+                for s in work:                  # fork: x (and last call's frees) are ready
+                    s.wait_stream(cur)
         gens = [self._micro_batch(xc, slot, stream) for slot, xc in enumerate(x.chunk(n, 0))]
         pending = [None] * n
         outs = [None] * n
         live = n
-        while live:
-            for c in range(n):
-                if gens[c] is None:
-                    continue
-                if pending[c] is not None:
-                    cur.wait_event(pending[c])
-                try:
-                    pending[c] = next(gens[c])
-                except StopIteration as e:
-                    outs[c], gens[c], pending[c] = e.value, None, None
-                    live -= 1
+        with gemm_ops.concurrent_comm():       # no persistent library GEMM beside comm kernels
+            while live:
+                for c in range(n):
+                    if gens[c] is None:
+                        continue
+                    ctx = torch.cuda.stream(work[c]) if x.is_cuda else _NullCtx()
+                    with ctx:
+                        if pending[c] is not None:
+                            work[c].wait_event(pending[c])
+                        try:
+                            pending[c] = next(gens[c])
+                        except StopIteration as e:
+                            outs[c], gens[c], pending[c] = e.value, None, None
+                            live -= 1
+        if x.is_cuda:
+            for s in work:                      # join
+                if s is not cur:
+                    cur.wait_stream(s)
         return torch.cat(outs, 0)
 
     @torch.no_grad()

@@ -174,6 +174,27 @@ CALLS = {}            # ("linear" | "wgrad", key) -> calls since import (kernel-
 _IMPLS = {"mfma": _mfma_linear, "blas": _blas_linear}
 
 
+# > 0 while GEMMs share the chip with communication kernels on another stream (the overlapped
+# TP forward). hipBLASLt's bf16 kernels here are persistent Stream-K grids (one workgroup per CU,
+# all assumed co-resident): with comm workgroups holding CUs, part of the grid waits for a
+# second round and the GEMM takes up to twice as long — measured: 7B shard-8 overlapped forward
+# 27.8 ms with one such GEMM vs 17.4 ms on our (non-persistent) grids. Shapes tuned in this state
+# get their own keys (suffix "concurrent") and only the hand-written candidates.
+_CONCURRENT = [0]
+
+
+class concurrent_comm:
+    """Context: GEMMs issued inside run beside comm kernels (see ``_CONCURRENT``)."""
+
+    def __enter__(self):
+        _CONCURRENT[0] += 1
+        return self
+
+    def __exit__(self, *exc):
+        _CONCURRENT[0] -= 1
+        return False
+
+
 def _autotune(key, args) -> str:
     mode = os.environ.get("DLBB_GEMM", "auto").lower()
     if mode in _IMPLS:
@@ -183,7 +204,8 @@ def _autotune(key, args) -> str:
     if torch.cuda.is_current_stream_capturing():
         return "mfma"
     times = {}
-    for name, fn in _IMPLS.items():
+    impls = {"mfma": _IMPLS["mfma"]} if key[-1] == "concurrent" else _IMPLS
+    for name, fn in impls.items():
         for _ in range(2):
             fn(*args)
         ts = []
@@ -241,6 +263,8 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
             return out
         key = (M, N, K, x2.stride(0), act, bias is not None, r2 is not None, out.dtype,
                preact is not None)
+        if _CONCURRENT[0]:
+            key = key + ("concurrent",)
         args = (x2, w, bias, act, r2, o2, preact)
         _IMPLS[_autotune(key, args)](*args)
         CALLS[("linear", key)] = CALLS.get(("linear", key), 0) + 1

@@ -701,3 +701,21 @@ def test_embedding_backward_into_sinks_deterministic():
     torch.testing.assert_close(grads[0][0].float(), ref_e, rtol=1e-2, atol=3e-2)
     torch.testing.assert_close(grads[0][1].float(), ref_p, rtol=1e-2, atol=3e-2)
     assert torch.equal(grads[0][0], grads[1][0]) and torch.equal(grads[0][1], grads[1][1])
+
+
+def test_gemm_autotune_beside_comm_keeps_to_hand_written_kernels(monkeypatch):
+    """Inside ``gemm.concurrent_comm()`` (the overlapped TP forward) a shape is tuned under its
+    own key and only among the non-persistent hand-written kernels: hipBLASLt's persistent
+    Stream-K grids stall when comm workgroups hold CUs."""
+    from distributed_llm_backend_benchmark_amd.ops import gemm, linear
+
+    monkeypatch.setenv("DLBB_GEMM", "auto")
+    x = _randn(1024, 512, seed=3, scale=0.5)
+    w = _randn(768, 512, seed=4, scale=0.5)
+    with gemm.concurrent_comm():
+        y = linear(x, w, out_dtype=torch.float32)
+    keys = [k for k in gemm.CHOICES if k[:3] == (1024, 768, 512) and k[-1] == "concurrent"]
+    assert keys and all(gemm.CHOICES[k] == "mfma" for k in keys), gemm.CHOICES
+    ref = x.float() @ w.float().t()
+    torch.testing.assert_close(y, ref, rtol=2e-3, atol=2e-3 * 512 ** 0.5)
+    assert gemm._CONCURRENT[0] == 0

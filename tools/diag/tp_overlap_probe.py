@@ -55,6 +55,7 @@ def main():
     ap.add_argument("--busbw", type=float, default=300.0)
     ap.add_argument("--layers", type=int, default=32)
     ap.add_argument("--iters", type=int, default=5)
+    ap.add_argument("--streams", default="1", help="chunk_streams settings to run (0,1)")
     args = ap.parse_args()
 
     import torch
@@ -69,10 +70,15 @@ def main():
     torch.cuda.set_device(dev)
     comm = Comm(rank=0, world_size=args.P, local_rank=0, backend="emulate", device=dev)
     x = torch.randn(8, 512, 4096, device=dev).to(torch.bfloat16)
+    cfgs = []
     for n in [int(c) for c in args.chunks.split(",")]:
+        for cs in ([1] if n == 1 else [int(v) for v in args.streams.split(",")]):
+            cfgs.append((n, cs))
+    for n, cs in cfgs:
         model = LLM(hidden_size=4096, num_layers=args.layers, num_heads=32,
                     ffn_intermediate=16384, comm=comm, seed=42, allreduce="emulate",
                     overlap_chunks=n)
+        model.chunk_streams = bool(cs)
         rows = [m for m in model.modules() if isinstance(m, RowParallelLinear)]
         for variant in args.variants.split(","):
             for m in rows:
@@ -113,7 +119,8 @@ def main():
             span = (max(b for _, b in comm_iv + gemm_iv) - min(a for a, _ in comm_iv + gemm_iv)
                     if comm_iv or gemm_iv else 0.0)
             print(json.dumps({
-                "P": args.P, "chunks": n, "variant": variant, "busbw": args.busbw,
+                "P": args.P, "chunks": n, "chunk_streams": bool(cs), "variant": variant,
+                "busbw": args.busbw,
                 "forward_ms": round(ms, 3), "stamped_launches": len(launches),
                 "stamped_span_ms": round(span / 1e6, 3),
                 "comm_busy_ms": round(busy_c / 1e6, 3), "gemm_busy_ms": round(busy_g / 1e6, 3),
