@@ -226,10 +226,21 @@ def init_distributed(backend: str = "auto", timeout_s: float = 600.0,
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
             if "MASTER_PORT" not in os.environ:
                 raise RuntimeError("MASTER_PORT must be set when WORLD_SIZE is set")
-        if be == "nccl":
+        eager = be == "nccl" and os.environ.get("DLBB_RCCL_EAGER_INIT", "0") == "1"
+        if eager:
             kwargs["device_id"] = dev  # eager RCCL communicator init, fixed device binding
         dist.init_process_group(**kwargs)
         owns = True
+        if be == "nccl" and not eager:
+            # Lazy communicator creation, forced now by one tiny all-reduce on the bound device.
+            # The eager path (init_process_group(device_id=...)) leaves this process in a state
+            # where kernels on two streams stop running concurrently: the overlapped TP forward
+            # (one compute + one comm stream) measured 28.6 ms after an eager world-1 init vs
+            # 17.6 ms after a lazy one, same code (tools/diag/tp_overlap_probe.py --pg-eager,
+            # profiles/r03_tp/overlap_probe); DLBB_RCCL_EAGER_INIT=1 restores it for A/B.
+            t = torch.zeros(1, device=dev)
+            dist.all_reduce(t)
+            torch.cuda.synchronize(dev)
     else:
         rank, world = dist.get_rank(), dist.get_world_size()
     return Comm(rank=rank, world_size=world, local_rank=local_rank, backend=be,

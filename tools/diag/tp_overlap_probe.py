@@ -56,9 +56,28 @@ def main():
     ap.add_argument("--layers", type=int, default=32)
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--streams", default="1", help="chunk_streams settings to run (0,1)")
+    ap.add_argument("--pg-eager", action="store_true",
+                    help="with --init-pg: eager communicator init (device_id=, as "
+                         "parallel.comm.init_distributed does)")
+    ap.add_argument("--init-pg", action="store_true",
+                    help="first bring up a world-1 RCCL process group and run one all-reduce "
+                         "(as run_tp does), to see what its streams do to the overlap")
     args = ap.parse_args()
 
     import torch
+
+    if args.init_pg:
+        import torch.distributed as dist
+
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29533")
+        torch.cuda.set_device(0)
+        kw = {"device_id": torch.device("cuda", 0)} if args.pg_eager else {}
+        dist.init_process_group("nccl", rank=0, world_size=1, **kw)
+        if not args.pg_eager:
+            t = torch.ones(1024, device="cuda")
+            dist.all_reduce(t)
+        torch.cuda.synchronize()
 
     from distributed_llm_backend_benchmark_amd.models.tp_transformer import LLM
     from distributed_llm_backend_benchmark_amd.ops.elementwise import spin_ns
@@ -100,9 +119,14 @@ def main():
                     model(x)
                 torch.cuda.synchronize()
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                import time as _time
+
+                issue = []
                 e0.record()
                 for _ in range(args.iters):
+                    t0 = _time.perf_counter()
                     model(x)
+                    issue.append(_time.perf_counter() - t0)
                 e1.record()
                 torch.cuda.synchronize()
                 ms = e0.elapsed_time(e1) / args.iters
@@ -120,8 +144,11 @@ def main():
                     if comm_iv or gemm_iv else 0.0)
             print(json.dumps({
                 "P": args.P, "chunks": n, "chunk_streams": bool(cs), "variant": variant,
-                "busbw": args.busbw,
+                "busbw": args.busbw, "init_pg": args.init_pg, "pg_eager": args.pg_eager,
+                "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"),
                 "forward_ms": round(ms, 3), "stamped_launches": len(launches),
+                "host_issue_ms": round(1e3 * sorted(issue)[len(issue) // 2], 3),
+                "cpu_affinity": len(os.sched_getaffinity(0)),
                 "stamped_span_ms": round(span / 1e6, 3),
                 "comm_busy_ms": round(busy_c / 1e6, 3), "gemm_busy_ms": round(busy_g / 1e6, 3),
                 "comm_under_gemm_ms": round(_overlap(uc, ug) / 1e6, 3),
