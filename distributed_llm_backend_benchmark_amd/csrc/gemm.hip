@@ -21,6 +21,7 @@
 //     one vmcnt(0) + barrier per K-tile.
 //   * XCD-aware bijective workgroup remap (T1) + GROUP_M tile grouping for L2 reuse.
 //   * M and N may be ragged (source rows clamped, stores masked); K % 64 == 0.
+#include <cstdlib>
 #include <utility>
 
 #include "common.h"
@@ -1102,6 +1103,187 @@ DLBB_PP_STAMPED(gemm_bf16_tn_256_pingpong3_bal, true, true, true)
 #undef DLBB_PP_STAMPED
 
 // ---------------------------------------------------------------------------------------
+// Persistent ping-pong (set_stagger(10), NT): one workgroup per CU walks the output tiles
+// blockIdx.x, blockIdx.x + gridDim.x, ... as ONE continuous stream of K-tiles g = 0 .. G-1
+// (tile i = g / nk, K-tile g % nk). The non-persistent kernel pays a fixed cost per tile —
+// prologue DMA latency, the pipeline fill (row 1 idle in interval 0) and drain (row 0 idle in
+// the last interval), the epilogue with the matrix pipe idle, workgroup launch: ~6.5 us per
+// 256² tile in multi-round grids, ~7 % at K = 4096 and far more at short K
+// (tools/diag/pp_tile_overhead.py: median workgroup time = 10.6 us + 1.37 us per K-tile in one
+// round). Here the schedule of pingpong_body<false, BAL> simply continues across tiles: the DMA
+// of g + 1 / g + 2 already targets the next tile while the current one finishes, and each wave
+// row stores its finished accumulators at the START of its first memory interval of the next
+// tile (before that interval's ds_reads, so the epilogue's temporaries never coexist with the
+// fragments), then zeroes them.
+// Counted waits with stores in flight: every count below is the number of LOADS (DMA) issued
+// after the one being retired. Loads return in order; a store may complete earlier or later
+// than a load, but it only ever ADDS to the outstanding count — so vmcnt <= (younger loads)
+// still implies the target load is done (stores can only make a wait longer, never unsafe).
+// Host contract as the ping-pong (M % 8, N % 64, 32-bit panel offsets) plus nk >= 2.
+template <bool BAL>
+__device__ __forceinline__ void pp_persist_body(GemmArgs a, char* smem) {
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = wave >> 2, wc = wave & 3;
+  const int fr = lane & 15, fq = lane >> 4;
+  const int nk = static_cast<int>(a.K / BK);
+  const int tiles = static_cast<int>(((a.M + BM2 - 1) / BM2) * ((a.N + BN2 - 1) / BN2));
+  const int nwg = static_cast<int>(gridDim.x), wg = static_cast<int>(blockIdx.x);
+  const int mine = wg < tiles ? (tiles - wg + nwg - 1) / nwg : 0;
+  if (mine == 0) return;
+  const int G = mine * nk;                      // this workgroup's virtual K-tiles
+  char* const abuf0 = smem;
+  char* const bbuf0 = smem + 2 * kTile2Bytes;
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 af[2][8], bf[2][4];
+  const int r_in = lane >> 3, chunk = (lane & 7) ^ (lane >> 3);
+  const uint32_t lda2 = static_cast<uint32_t>(a.lda) * 2, ldb2 = static_cast<uint32_t>(a.ldb) * 2;
+  const uint32_t aoff = static_cast<uint32_t>(r_in) * lda2 + chunk * 16;
+  const uint32_t boff = static_cast<uint32_t>(perm_brow(r_in)) * ldb2 + chunk * 16;
+  constexpr uint32_t kStep = BK * 2;
+#define DLBB_RSRC(P) \
+  __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(P), 0, 0x7fffffff, 0x00020000)
+
+  Tile256 tc = tile_of(a, wg);                  // the tile being multiplied
+  {
+    const __amdgpu_buffer_rsrc_t ra = DLBB_RSRC(a.A + tc.m0 * a.lda);
+    const __amdgpu_buffer_rsrc_t rb = DLBB_RSRC(a.B + tc.n0 * a.ldb);
+    const int rows_a = static_cast<int>(a.M - tc.m0), rows_b = static_cast<int>(a.N - tc.n0);
+    if (wr == 0) {                              // prologue (nk >= 2): A-lo(0), B(0), B(1)
+      stage_a_half(ra, lda2, rows_a, 0, abuf0, 0, wc, aoff);
+      stage_b(rb, ldb2, rows_b, 0, bbuf0, wc, boff);
+      stage_b(rb, ldb2, rows_b, kStep, bbuf0 + kTile2Bytes, wc, boff);
+      DLBB_WAIT_VM(8);
+      __builtin_amdgcn_s_barrier();
+    } else {                                    // A-hi(0), A-lo(1)
+      stage_a_half(ra, lda2, rows_a, 0, abuf0, 1, wc, aoff);
+      stage_a_half(ra, lda2, rows_a, kStep, abuf0 + kTile2Bytes, 0, wc, aoff);
+      __builtin_amdgcn_s_barrier();
+      DLBB_WAIT_VM(4);
+      __builtin_amdgcn_s_barrier();             // end of interval 0
+    }
+  }
+  // A wave row stores its part of finished tile T at the start of its FIRST memory interval of
+  // tile T + 1 (before the ds_reads: the fragments are dead there, so the epilogue fits beside
+  // the accumulators). It first retires its own outstanding DMA (vmcnt(0)) — the loads that
+  // interval's and the next interval's counted waits would otherwise retire with the stores
+  // queued behind them — and those two waits are skipped at the boundary. The lane-dependent
+  // epilogue addresses are recomputed here (the empty asm), not hoisted into the K loop.
+#define DLBB_PP_FLUSH(T)                                                           \
+  do {                                                                             \
+    __builtin_amdgcn_sched_barrier(0);                                             \
+    int ln_ = lane;                                                                \
+    asm volatile("" : "+v"(ln_));                                                  \
+    store_tile_256<false>(a, acc, (T).m0, (T).n0, wave, ln_);                      \
+    _Pragma("unroll") for (int x_ = 0; x_ < 8; ++x_)                                \
+      _Pragma("unroll") for (int y_ = 0; y_ < 4; ++y_)                              \
+        acc[x_][y_] = f32x4{0.f, 0.f, 0.f, 0.f};                                    \
+    __builtin_amdgcn_sched_barrier(0);                                             \
+  } while (0)
+  int cb = 0;                                   // B buffer of virtual K-tile g (g % 3)
+  for (int i = 0; i < mine; ++i) {
+    const Tile256 tn = i + 1 < mine ? tile_of(a, wg + (i + 1) * nwg) : tc;   // next tile
+    const __amdgpu_buffer_rsrc_t ra = DLBB_RSRC(a.A + tc.m0 * a.lda);
+    const __amdgpu_buffer_rsrc_t rb = DLBB_RSRC(a.B + tc.n0 * a.ldb);
+    const __amdgpu_buffer_rsrc_t ran = DLBB_RSRC(a.A + tn.m0 * a.lda);
+    const __amdgpu_buffer_rsrc_t rbn = DLBB_RSRC(a.B + tn.n0 * a.ldb);
+    const int rows_a = static_cast<int>(a.M - tc.m0), rows_b = static_cast<int>(a.N - tc.n0);
+    const int rows_an = static_cast<int>(a.M - tn.m0), rows_bn = static_cast<int>(a.N - tn.n0);
+    if (wr == 0) {
+      for (int k = 0; k < nk; ++k) {
+        const int g = i * nk + k;
+        const bool bnd = k == 0 && i > 0;       // first K-tile of a new output tile
+        read_split(abuf0 + (g & 1) * kTile2Bytes, bbuf0 + cb * kTile2Bytes, 0, wc, fr, fq, af, bf);
+        const bool h1 = g + 1 < G, b2 = g + 2 < G;
+        char* const an = abuf0 + ((g + 1) & 1) * kTile2Bytes;
+        if (h1) {                               // A-hi(g+1): this tile's K-tile or the next's 0
+          if (k + 1 < nk) stage_a_half(ra, lda2, rows_a, (k + 1) * kStep, an, 1, wc, aoff);
+          else stage_a_half(ran, lda2, rows_an, 0, an, 1, wc, aoff);
+        }
+        if (b2) {                               // B(g+2) (BAL: its first half)
+          char* const bn = bbuf0 + (cb == 0 ? 2 : cb - 1) * kTile2Bytes;
+          const bool here = k + 2 < nk;
+          const uint32_t k2 = static_cast<uint32_t>(here ? k + 2 : k + 2 - nk) * kStep;
+          if (BAL) stage_b<0, 4>(here ? rb : rbn, ldb2, here ? rows_b : rows_bn, k2, bn, wc, boff);
+          else stage_b<0, 8>(here ? rb : rbn, ldb2, here ? rows_b : rows_bn, k2, bn, wc, boff);
+        }
+        if (bnd) {
+          // A-hi(g) retired at the top: no wait, so the stores are never drained here
+        } else if (BAL) {
+          if (b2) DLBB_WAIT_VM(12);
+          else if (h1) DLBB_WAIT_VM(8);
+          else DLBB_WAIT_VM(0);
+        } else {
+          if (b2) DLBB_WAIT_VM(20);
+          else if (h1) DLBB_WAIT_VM(12);
+          else DLBB_WAIT_VM(0);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_barrier();           // end of interval 2g
+        __builtin_amdgcn_sched_barrier(0);
+        mfma_full(acc, af, bf);
+        __builtin_amdgcn_sched_barrier(0);
+        if (h1 && !bnd) {                       // (boundary: B(g+1) retired at the top)
+          if (b2) { if (BAL) DLBB_WAIT_VM(8); else DLBB_WAIT_VM(12); }
+          else DLBB_WAIT_VM(4);
+        }
+        __builtin_amdgcn_s_barrier();           // end of interval 2g+1
+        cb = cb == 2 ? 0 : cb + 1;
+      }
+    } else {
+      for (int k = 0; k < nk; ++k) {
+        const int g = i * nk + k;
+        const bool bnd = k == 0 && i > 0;
+        read_split(abuf0 + (g & 1) * kTile2Bytes, bbuf0 + cb * kTile2Bytes, 1, wc, fr, fq, af, bf);
+        const bool l2 = g + 2 < G;
+        if (l2) {                               // A-lo(g+2) (BAL: and B1(g+2))
+          const bool here = k + 2 < nk;
+          const uint32_t k2 = static_cast<uint32_t>(here ? k + 2 : k + 2 - nk) * kStep;
+          stage_a_half(here ? ra : ran, lda2, here ? rows_a : rows_an, k2,
+                       abuf0 + (g & 1) * kTile2Bytes, 0, wc, aoff);
+          if (BAL)
+            stage_b<4, 8>(here ? rb : rbn, ldb2, here ? rows_b : rows_bn, k2,
+                          bbuf0 + (cb == 0 ? 2 : cb - 1) * kTile2Bytes, wc, boff);
+        }
+        if (g + 1 < G && !bnd) {               // (boundary: A-lo(g+1) retired at the top)
+          if (l2) { if (BAL) DLBB_WAIT_VM(8); else DLBB_WAIT_VM(4); }
+          else DLBB_WAIT_VM(0);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_barrier();           // end of interval 2g+1
+        __builtin_amdgcn_sched_barrier(0);
+        mfma_full(acc, af, bf);
+        __builtin_amdgcn_sched_barrier(0);
+        if (g + 1 < G) __builtin_amdgcn_s_barrier();   // end of interval 2g+2
+        cb = cb == 2 ? 0 : cb + 1;
+      }
+    }
+    // this row's part of tile i, at the start of its first memory interval of tile i + 1
+    DLBB_WAIT_VM(0);
+    DLBB_PP_FLUSH(tc);
+    tc = tn;
+  }
+#undef DLBB_PP_FLUSH
+#undef DLBB_RSRC
+}
+
+__global__ void __launch_bounds__(kThreads2, 1) gemm_bf16_nt_256_pp_persist(GemmArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  pp_persist_body<false>(a, smem);
+}
+__global__ void __launch_bounds__(kThreads2, 1) gemm_bf16_nt_256_pp_persist_bal(GemmArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  pp_persist_body<true>(a, smem);
+}
+
+// ---------------------------------------------------------------------------------------
 // One wave per SIMD (A/B only, set_stagger(9); profiles/r03_gemm/w4_experiment.md): 256 x 256
 // tile, 256 threads = 4 waves as 2 (M) x 2 (N), each wave 128 x 128 outputs = 64 accumulators of
 // 16x16 held in AGPRs — hipBLASLt's MT256x256x64 MI16x16 structure. The MFMAs are inline asm
@@ -1357,6 +1539,22 @@ using namespace dlbb;
 
 static int dlbb_gemm_force_tile = 0;   // 0 = heuristic, 128 or 256 = force (A/B testing)
 
+// compute units of the current device (cached per device): persistent grids
+static int num_cus() {
+  static int ncu[64] = {0};
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  if (dev < 0 || dev >= 64) dev = 0;
+  if (ncu[dev] == 0) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        n <= 0)
+      n = 256;
+    ncu[dev] = n;
+  }
+  return ncu[dev];
+}
+
 static int dlbb_gemm_stagger = 6;      // 256^2 schedule (set_stagger): 6 = ping-pong, 160 KiB LDS, measured fastest
 // Balanced DMA issue (BAL) for the ping-pong kernels: 0 never, 1 always, 2 (default) = always
 // for NN (dgrad: +1-5 % on every measured shape, K 768 .. 50304) and for NT when the reduction
@@ -1364,6 +1562,15 @@ static int dlbb_gemm_stagger = 6;      // 256^2 schedule (set_stagger): 6 = ping
 // (profiles/r02_gemm/gemm_ab_pingpong_bal.jsonl, dgrad_ab_nn_bal.jsonl)
 static int dlbb_gemm_bal = 2;
 constexpr int64_t kBalMinKTiles = 32;
+constexpr int64_t kPersistMaxKTiles = 48;
+// DLBB_GEMM_PERSIST=0: never upgrade the default ping-pong to the persistent form (A/B)
+static bool persist_enabled() {
+  static const int on = [] {
+    const char* e = getenv("DLBB_GEMM_PERSIST");
+    return (e && e[0] == '0') ? 0 : 1;
+  }();
+  return on != 0;
+}
 static bool use_bal(int64_t k_tiles, bool nn) {
   return dlbb_gemm_bal == 1 || (dlbb_gemm_bal == 2 && (nn || k_tiles >= kBalMinKTiles));
 }
@@ -1402,12 +1609,29 @@ DLBB_API int dlbb_gemm_bf16_nt(const void* A, int64_t lda, const void* B, int64_
     if (mode == 9 && !(M % 16 == 0 && N % 64 == 0 && K >= 2 * BK &&
                        lda * 2 * 256 + K * 2 < (1LL << 31) && ldb * 2 * 256 + K * 2 < (1LL << 31)))
       mode = 6;                       // (then held to the ping-pong contract below)
+    // default ping-pong on a multi-round grid with a short reduction: the persistent form
+    // (tools/gemm_ab.py, profiles/r03_gemm/persistent_ab.jsonl: +6.6 % GPT-2 fc, +10.6 % LM head
+    // at K = 768; neutral at K = 4096 over 3 rounds; -2 % on one-round grids)
+    if (mode == 6 && persist_enabled() && tiles256 > num_cus() && K / BK <= kPersistMaxKTiles)
+      mode = 10;
+    // persistent ping-pong (mode 10): the ping-pong contract plus at least two K-tiles
+    if (mode == 10 && K < 2 * BK) mode = 6;
     // ping-pong contract: 8-row A groups and 64-row B blocks wholly in or out (uniform clamps),
     // 32-bit buffer offsets within a 256-row panel
-    if ((mode == 6 || mode == 7) && !(M % 8 == 0 && N % 64 == 0 && M >= 8 && lda * 2 * 256 + K * 2 < (1LL << 31) &&
+    if ((mode == 6 || mode == 7 || mode == 10) && !(M % 8 == 0 && N % 64 == 0 && M >= 8 && lda * 2 * 256 + K * 2 < (1LL << 31) &&
                        ldb * 2 * 256 + K * 2 < (1LL << 31)))
       mode = 3;
-    if (mode == 5 || mode == 8 || mode > 9) mode = 3;
+    if (mode == 5 || mode == 8 || mode > 10) mode = 3;
+    if (mode == 10) {
+      const int64_t grid = tiles256 < num_cus() ? tiles256 : num_cus();
+      if (use_bal(K / BK, false))
+        hipLaunchKernelGGL(gemm_bf16_nt_256_pp_persist_bal, dim3(static_cast<unsigned>(grid)),
+                           dim3(kThreads2), kPP6Lds, stream, a);
+      else
+        hipLaunchKernelGGL(gemm_bf16_nt_256_pp_persist, dim3(static_cast<unsigned>(grid)),
+                           dim3(kThreads2), kPP6Lds, stream, a);
+      return hipGetLastError();
+    }
     if (mode == 4) {
       static int ncu[64] = {0};
       int dev = 0;

@@ -219,7 +219,8 @@ class LLM(nn.Module):
                 for c in range(n):
                     if gens[c] is None:
                         continue
-                    ctx = torch.cuda.stream(work[c]) if x.is_cuda else _NullCtx()
+                    ctx = (torch.cuda.stream(work[c]) if x.is_cuda and work[c] is not cur
+                           else _NullCtx())
                     with ctx:
                         if pending[c] is not None:
                             work[c].wait_event(pending[c])

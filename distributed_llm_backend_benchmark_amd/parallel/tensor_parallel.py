@@ -99,6 +99,7 @@ class RowParallelLinear(nn.Module):
         self.emulate_busbw: Optional[float] = None
         self.emulate_blocks = 32
         self._emu_zeros: Optional[torch.Tensor] = None
+        self._events = {}     # micro-batch slot -> (ready, done) events (overlapped forward)
 
     def _emulated_all_reduce(self, t: torch.Tensor) -> None:
         from ..ops.elementwise import reduce_sum, spin_ns
@@ -170,7 +171,7 @@ class RowParallelLinear(nn.Module):
             y = x @ self.weight.t()
             if fp32_wire:
                 y = y.float()
-            return self._reduce_then(y, x.dtype, None, stream)
+            return self._reduce_then(y, x.dtype, None, stream, slot)
         odt = torch.float32 if fp32_wire else x.dtype
         reg = (self._registered_out((*x.shape[:-1], self.out_features), odt, slot)
                if self.comm.world_size > 1 and x.is_cuda else None)
@@ -180,9 +181,9 @@ class RowParallelLinear(nn.Module):
             ops.linear(x, self.weight, out_dtype=odt, out=y)
         else:
             y = ops.linear(x, self.weight, out_dtype=odt)
-        return self._reduce_then(y, x.dtype, reg, stream)
+        return self._reduce_then(y, x.dtype, reg, stream, slot)
 
-    def _reduce_then(self, y, out_dtype, reg, stream):
+    def _reduce_then(self, y, out_dtype, reg, stream, slot=0):
         def reduce_and_cast():
             if reg is not None:
                 self.comm_bytes += y.numel() * y.element_size()
@@ -197,10 +198,17 @@ class RowParallelLinear(nn.Module):
 
         if stream is None or not y.is_cuda:
             return reduce_and_cast(), None
-        cur = torch.cuda.current_stream(y.device)
-        stream.wait_stream(cur)                 # the partial sum is complete
+        # two events per micro-batch slot, reused every call (host cost: the overlapped forward
+        # issues 2 x layers x micro-batches of these): each is waited on before it is recorded
+        # again — `ready` by the comm stream right below, `done` by the caller before it
+        # resumes this micro-batch
+        evs = self._events.get(slot)
+        if evs is None:
+            evs = self._events[slot] = (torch.cuda.Event(), torch.cuda.Event())
+        ready, done = evs
+        ready.record(torch.cuda.current_stream(y.device))
+        stream.wait_event(ready)                # the partial sum is complete
         with torch.cuda.stream(stream):
             out = reduce_and_cast()
-            ev = torch.cuda.Event()
-            ev.record(stream)
-        return out, ev
+            done.record(stream)
+        return out, done
