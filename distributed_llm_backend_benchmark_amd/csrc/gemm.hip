@@ -1120,6 +1120,35 @@ DLBB_PP_STAMPED(gemm_bf16_tn_256_pingpong3_bal, true, true, true)
 // than a load, but it only ever ADDS to the outstanding count — so vmcnt <= (younger loads)
 // still implies the target load is done (stores can only make a wait longer, never unsafe).
 // Host contract as the ping-pong (M % 8, N % 64, 32-bit panel offsets) plus nk >= 2.
+// Lean epilogue of one wave's 128 x 64 block for the persistent kernel: plain bf16 output, vector
+// stores only (host contract: no bias / activation / residual / pre-activation, bf16 C, vec_ok;
+// N % 64 == 0 makes every 16-column lane group whole). The general epilogue (store_tile) inside
+// the tile loop measured 7-15 % slower on the same shapes (persistent_ab_general_epilogue.jsonl).
+__device__ __forceinline__ void store_plain_bf16(const GemmArgs& a, const f32x4 (&acc)[8][4],
+                                                 int64_t row0, int64_t col0, int lane) {
+  const int fr = lane & 15, fq = lane >> 4;
+  const int64_t cbase = col0 + fq * 16;
+  if (cbase >= a.N) return;
+  const int64_t rbase = row0 + fr;
+  const int rows_left = static_cast<int>(a.M - rbase);
+  uint16_t* cb = static_cast<uint16_t*>(a.C) + rbase * a.ldc + cbase;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    if (i * 16 >= rows_left) break;
+    u16x8 o0, o1;
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        o0[j * 4 + r] = f32_to_bf16(acc[i][j][r]);
+        o1[j * 4 + r] = f32_to_bf16(acc[i][j + 2][r]);
+      }
+    u16x8* o = reinterpret_cast<u16x8*>(cb + static_cast<int64_t>(i) * 16 * a.ldc);
+    o[0] = o0;
+    o[1] = o1;
+  }
+}
+
 template <bool BAL>
 __device__ __forceinline__ void pp_persist_body(GemmArgs a, char* smem) {
   const int lane = threadIdx.x & 63;
@@ -1179,7 +1208,7 @@ __device__ __forceinline__ void pp_persist_body(GemmArgs a, char* smem) {
     __builtin_amdgcn_sched_barrier(0);                                             \
     int ln_ = lane;                                                                \
     asm volatile("" : "+v"(ln_));                                                  \
-    store_tile_256<false>(a, acc, (T).m0, (T).n0, wave, ln_);                      \
+    store_plain_bf16(a, acc, (T).m0 + (wave >> 2) * 128, (T).n0 + (wave & 3) * 64, ln_); \
     _Pragma("unroll") for (int x_ = 0; x_ < 8; ++x_)                                \
       _Pragma("unroll") for (int y_ = 0; y_ < 4; ++y_)                              \
         acc[x_][y_] = f32x4{0.f, 0.f, 0.f, 0.f};                                    \
@@ -1610,12 +1639,16 @@ DLBB_API int dlbb_gemm_bf16_nt(const void* A, int64_t lda, const void* B, int64_
                        lda * 2 * 256 + K * 2 < (1LL << 31) && ldb * 2 * 256 + K * 2 < (1LL << 31)))
       mode = 6;                       // (then held to the ping-pong contract below)
     // default ping-pong on a multi-round grid with a short reduction: the persistent form
-    // (tools/gemm_ab.py, profiles/r03_gemm/persistent_ab.jsonl: +6.6 % GPT-2 fc, +10.6 % LM head
-    // at K = 768; neutral at K = 4096 over 3 rounds; -2 % on one-round grids)
-    if (mode == 6 && persist_enabled() && tiles256 > num_cus() && K / BK <= kPersistMaxKTiles)
+    // (tools/gemm_ab.py, profiles/r03_gemm/persistent_ab.jsonl, plain bf16: +6.6 % at
+    // 16384 x 3072 x 768, +10.6 % GPT-2 LM head; neutral at K = 4096 over 3 rounds; -2 % on
+    // one-round grids)
+    const bool plain = epi == 0 && !out_f32 && !preact && vec_ok;
+    if (mode == 6 && plain && persist_enabled() && tiles256 > num_cus() &&
+        K / BK <= kPersistMaxKTiles)
       mode = 10;
-    // persistent ping-pong (mode 10): the ping-pong contract plus at least two K-tiles
-    if (mode == 10 && K < 2 * BK) mode = 6;
+    // persistent ping-pong (mode 10): the ping-pong contract, at least two K-tiles and the lean
+    // epilogue's (plain bf16 output, vector stores)
+    if (mode == 10 && (K < 2 * BK || !plain)) mode = 6;
     // ping-pong contract: 8-row A groups and 64-row B blocks wholly in or out (uniform clamps),
     // 32-bit buffer offsets within a 256-row panel
     if ((mode == 6 || mode == 7 || mode == 10) && !(M % 8 == 0 && N % 64 == 0 && M >= 8 && lda * 2 * 256 + K * 2 < (1LL << 31) &&
