@@ -460,6 +460,37 @@ def test_run_tp_shard_as_world1(tmp_path):
     assert th["tokens_per_s"] > 0
 
 
+@pytest.mark.parametrize("graph", [False, True])
+def test_run_tp_shard_as_overlapped(tmp_path, graph):
+    """run_tp --shard-as 4 --overlap-chunks 2 (micro-batch interleaved forward: all-reduce
+    stand-ins on a side comm stream), eagerly and captured in a HIP graph (fork / join of the
+    comm stream inside the capture); the output file carries the _ov2 suffix and the setting."""
+    import yaml
+
+    cfg = yaml.safe_load(open(os.path.join(REPO, "config", "1b_config.yaml")))
+    cfg["model"]["num_layers"] = 2
+    cfg["experiment"]["output_dir"] = str(tmp_path)
+    cfg["execution"]["warmup_iterations"] = 2
+    cfg["execution"]["benchmark_iterations"] = 3
+    cfg["parallelism"]["world_size"] = 4
+    p = tmp_path / "c.yaml"
+    p.write_text(yaml.safe_dump(cfg))
+    cmd = [sys.executable, "-m", "distributed_llm_backend_benchmark_amd.cli.run_tp",
+           "--config", str(p), "--backend", "rccl", "--shard-as", "4", "--overlap-chunks", "2",
+           "--emulate-busbw", "100"] + (["--graph"] if graph else [])
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=REPO)
+    assert out.returncode == 0, out.stderr[-3000:]
+    rec = json.load(open(tmp_path / f"rccl_{cfg['experiment']['name']}_shard4_ov2.json"))
+    th = rec["throughput"]
+    assert th["overlap_chunks"] == 2 and th["hip_graph"] == graph
+    B, S, H = cfg["input"]["batch_size"], cfg["input"]["sequence_length"], cfg["model"]["hidden_size"]
+    assert th["allreduce_bytes_per_forward_per_rank"] == 2 * 2 * B * S * H * 2
+    # the overlapped GEMMs were tuned beside comm: hand-written kernels only
+    keys = [t["key"] for t in th["gemm_kernel_mix"]["linear"]["tuned"]]
+    assert keys and all(k[-1] == "concurrent" for k in keys), keys
+    assert th["gemm_kernel_mix"]["hand_written_time_fraction"] == 1.0
+
+
 def test_ddp_comm_stream_fenced_to_normal_priority(monkeypatch):
     """The fence in action: DLBB_COMM_STREAM_PRIORITY=-1 alone yields a NORMAL-priority comm
     stream (the high-priority dispatch trap, profiles/r03_overlap/SUMMARY.md)."""
