@@ -27,6 +27,7 @@ import torch.nn.functional as F
 from .. import ops
 from ..ops import gemm as gemm_ops
 from ..parallel.comm import Comm
+from ..parallel.streams import concurrent_stream
 from ..parallel.tensor_parallel import ColumnParallelLinear, RowParallelLinear
 
 MODEL_CONFIGS: Dict[str, Dict[str, int]] = {
@@ -202,11 +203,12 @@ class LLM(nn.Module):
         work = [cur] * n                        # the stream each micro-batch computes on
         if x.is_cuda:
             if self._comm_stream is None:
-                self._comm_stream = torch.cuda.Stream(device=x.device, priority=0)
+                self._comm_stream = concurrent_stream(x.device, "tp_comm")
             stream = self._comm_stream
             if self.chunk_streams:
                 while len(self._chunk_streams) < n:
-                    self._chunk_streams.append(torch.cuda.Stream(device=x.device, priority=0))
+                    self._chunk_streams.append(
+                        concurrent_stream(x.device, f"tp_chunk{len(self._chunk_streams)}"))
                 work = self._chunk_streams[:n]
                 for s in work:                  # fork: x (and last call's frees) are ready
                     s.wait_stream(cur)

@@ -41,6 +41,7 @@ from ..ops import FlatAdamW
 from ..ops.elementwise import ChunkTable, ScaleTable, reduce_sum, spin_ns
 from ..utils import tracing
 from .comm import Comm
+from .streams import concurrent_stream
 
 _GRAD_SINKS = os.environ.get("DLBB_GRAD_SINKS", "1") != "0"   # A/B switch for the sinks
 # opt-in: sink dW GEMMs on a side stream. Measured +4 % step time on GPT-2 (the concurrent
@@ -150,8 +151,9 @@ class FlatParamTrainer:
         self._params = order
         # weight-gradient GEMMs of sink params run on this side stream (off the backward's
         # critical path); bucket reductions and the optimizer are ordered after it
-        self._wgrad_stream = (torch.cuda.Stream(dev) if mode == "view" and dev.type == "cuda"
-                              and _GRAD_SINKS and _WGRAD_STREAM else None)
+        self._wgrad_stream = (concurrent_stream(dev, "ddp_wgrad")
+                              if mode == "view" and dev.type == "cuda" and _GRAD_SINKS
+                              and _WGRAD_STREAM else None)
         if mode == "view":
             for p, o in zip(order, offs):
                 p.grad = self.flat_grad[o:o + p.numel()].view_as(p)
@@ -175,7 +177,7 @@ class FlatParamTrainer:
             from .custom_allreduce import get_custom_allreduce
 
             self._car = get_custom_allreduce(comm)
-            self._comm_stream = torch.cuda.Stream(dev, priority=comm_stream_priority())
+            self._comm_stream = concurrent_stream(dev, "ddp_comm", comm_stream_priority())
             # buckets are fixed slices of flat_grad: IPC-map them once, then every bucket
             # all-reduce is the in-place two-shot (no staging copy, no capacity limit)
             if self._car is not None and self._car.reg_healthy:
@@ -187,7 +189,7 @@ class FlatParamTrainer:
             from .rccl_native import get_native
 
             self._native = get_native(comm)
-            self._comm_stream = torch.cuda.Stream(dev, priority=comm_stream_priority())
+            self._comm_stream = concurrent_stream(dev, "ddp_comm", comm_stream_priority())
         # CU budget of the bucket reductions that run beside backward: workgroups per IPC /
         # emulated reduction launch (None = the kernel's own size heuristic)
         self.comm_blocks = comm_blocks
@@ -206,7 +208,7 @@ class FlatParamTrainer:
         if emulate_comm:
             if self.world != 1 or dev.type != "cuda":
                 raise ValueError("emulate_comm is a single-GPU measurement (world 1, HIP device)")
-            self._comm_stream = torch.cuda.Stream(dev, priority=comm_stream_priority())
+            self._comm_stream = concurrent_stream(dev, "ddp_comm", comm_stream_priority())
             self._emu_zero = torch.zeros(max(b.end - b.start for b in self.buckets),
                                          dtype=grad_dtype, device=dev)
             if not isinstance(emulate_comm, bool):

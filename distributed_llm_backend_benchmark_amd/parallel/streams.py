@@ -1,0 +1,89 @@
+"""Side streams that really run beside the compute stream.
+
+A HIP stream is served by one of the process's hardware queues (``GPU_MAX_HW_QUEUES``, 4 on
+this pool). More streams than queues share them, and two streams on ONE hardware queue execute
+in order: a "side" stream that landed on the compute stream's queue silently serialises
+everything it was meant to overlap. ``torch.cuda.Stream()`` hands out pool streams round-robin,
+so whether a new side stream collides depends on how many streams the process (RCCL included)
+created before — measured on MI355X (``profiles/r03_tp/overlap_probe``, ``profiles/r03_overlap``):
+
+* the overlapped TP forward: 17.6 ms vs 28.6 ms depending only on how the RCCL communicator was
+  initialised before the comm stream was created (no overlap at all in the second case);
+* the DDP tail runs: one trainer in four stalled its backward behind the comm stream (+2.1 ms at
+  100 GB/s), a different one after changing the communicator init — the stall moved with the
+  stream order, not with the configuration.
+
+:func:`concurrent_stream` therefore PROBES candidates: a 1-workgroup spin kernel (~100 us) on
+the reference (compute) stream and one on the candidate, started together; if the pair takes
+about one spin, the candidate runs concurrently. It also has to run beside every side stream
+handed out before on that device (DDP's weight-gradient and comm streams must not share a queue
+either). The verified stream is cached per (device, role, priority).
+"""
+
+from __future__ import annotations
+
+import warnings
+from typing import Dict, Optional, Tuple
+
+import torch
+
+_CACHE: Dict[Tuple[int, str, int], "torch.cuda.Stream"] = {}
+_PROBE_NS = 100_000
+_TRIES = 12
+
+
+def _pair_ms(a, b, ns: int, device) -> float:
+    from ..ops.elementwise import spin_ns
+
+    e0 = torch.cuda.Event(enable_timing=True)
+    e1 = torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize(device)
+    e0.record(a)
+    b.wait_event(e0)
+    with torch.cuda.stream(a):
+        spin_ns(ns, 1, device)
+    with torch.cuda.stream(b):
+        spin_ns(ns, 1, device)
+    a.wait_stream(b)
+    e1.record(a)
+    e1.synchronize()
+    return e0.elapsed_time(e1)
+
+
+def runs_concurrently(a, b, device=None, ns: int = _PROBE_NS) -> bool:
+    """True if kernels on streams ``a`` and ``b`` overlap in time (best of two probes: a pair of
+    ``ns`` spins finishing in well under two spins)."""
+    dev = device or torch.device("cuda", torch.cuda.current_device())
+    t = min(_pair_ms(a, b, ns, dev) for _ in range(2))
+    return t < 1.5 * ns * 1e-6
+
+
+def concurrent_stream(device, role: str, priority: int = 0,
+                      ref: Optional["torch.cuda.Stream"] = None) -> "torch.cuda.Stream":
+    """A stream for ``role`` on ``device`` verified to run beside ``ref`` (default: the current
+    stream) and beside every side stream already handed out on that device. Falls back, with a
+    warning, to the last candidate if none of ``_TRIES`` pool streams qualifies."""
+    dev = torch.device(device)
+    key = (dev.index if dev.index is not None else torch.cuda.current_device(), role, int(priority))
+    if key in _CACHE:
+        return _CACHE[key]
+    ref = ref or torch.cuda.current_stream(dev)
+    others = [s for k, s in _CACHE.items() if k[0] == key[0]]
+    cand = None
+    for _ in range(_TRIES):
+        cand = torch.cuda.Stream(dev, priority=priority)
+        if cand == ref or any(cand == o for o in others):
+            continue
+        if runs_concurrently(ref, cand, dev) and all(runs_concurrently(o, cand, dev)
+                                                     for o in others):
+            break
+    else:
+        warnings.warn(f"no pool stream ran concurrently with the compute stream for {role!r}; "
+                      "overlap on this device will serialise", RuntimeWarning, stacklevel=2)
+    _CACHE[key] = cand
+    return cand
+
+
+def reset() -> None:
+    """Forget the handed-out streams (tests)."""
+    _CACHE.clear()
