@@ -67,6 +67,9 @@ def parse_args(argv=None):
                          "row-parallel all-reduce (side comm stream) runs under the next "
                          "micro-batch's GEMMs (execution.overlap_chunks; 1 = blocking, as the "
                          "reference)")
+    ap.add_argument("--chunk-streams", action="store_true",
+                    help="with --overlap-chunks: each micro-batch on a compute stream of its own "
+                         "(verified concurrent, parallel/streams.py)")
     ap.add_argument("--check-dense", action="store_true",
                     help="after warmup, load the TP shards from a dense world-1 model of the "
                          "same seed (built on every rank) and report the max error of the TP "
@@ -158,6 +161,7 @@ def main(argv=None) -> int:
         print(f"Execution: {ex}")
 
     model = create_model_from_config(config, model_comm)
+    model.chunk_streams = bool(args.chunk_streams)
     if args.shard_as and args.emulate_busbw:
         from ..parallel.tensor_parallel import RowParallelLinear
 
@@ -271,6 +275,7 @@ def main(argv=None) -> int:
             # micro-batches interleaved so all-reduces run under GEMMs (1 = blocking)
             "overlap_chunks": model.overlap_split(
                 torch.empty(B, 1, device="meta")),
+            "chunk_streams": bool(args.chunk_streams),
         }
         if args.shard_as:
             extra["shard_as"] = {
@@ -298,7 +303,7 @@ def main(argv=None) -> int:
               f"{extra['tflops_per_rank']:.1f}")
         suffix = f"_shard{args.shard_as}" if args.shard_as else ""
         if extra["overlap_chunks"] > 1:
-            suffix += f"_ov{extra['overlap_chunks']}"
+            suffix += f"_ov{extra['overlap_chunks']}" + ("cs" if args.chunk_streams else "")
         out = os.path.join(config["experiment"]["output_dir"],
                            f"{args.backend}_{config['experiment']['name']}{suffix}.json")
         save_results(results, out, rank)

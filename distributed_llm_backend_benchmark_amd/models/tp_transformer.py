@@ -205,7 +205,9 @@ class LLM(nn.Module):
             if self._comm_stream is None:
                 self._comm_stream = concurrent_stream(x.device, "tp_comm")
             stream = self._comm_stream
-            if self.chunk_streams:
+            # (not under HIP-graph capture: a capture forking the per-micro-batch streams crashed
+            # the process on MI355X; the capture keeps one compute stream + the comm stream)
+            if self.chunk_streams and not torch.cuda.is_current_stream_capturing():
                 while len(self._chunk_streams) < n:
                     self._chunk_streams.append(
                         concurrent_stream(x.device, f"tp_chunk{len(self._chunk_streams)}"))
