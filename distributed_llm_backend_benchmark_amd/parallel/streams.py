@@ -84,6 +84,38 @@ def concurrent_stream(device, role: str, priority: int = 0,
     return cand
 
 
+_GROUPS: Dict[Tuple[int, str, int], list] = {}
+
+
+def concurrent_group(device, n: int, role: str) -> list:
+    """``n`` streams that all run concurrently with each other (not necessarily with the
+    current stream): e.g. the W per-rank launches of the virtual-rank harness, whose spinning
+    kernels wait for each other — two of them on one hardware queue would serialise until the
+    kernels' wall-clock bound. Cached per (device, role, n); with fewer than ``n`` distinct
+    queues reachable it returns the best effort (warning)."""
+    dev = torch.device(device)
+    key = (dev.index if dev.index is not None else torch.cuda.current_device(), role, int(n))
+    if key in _GROUPS:
+        return _GROUPS[key]
+    picked: list = []
+    for _ in range(_TRIES + 4 * n):
+        if len(picked) == n:
+            break
+        cand = torch.cuda.Stream(dev)
+        if any(cand == p for p in picked):
+            continue
+        if all(runs_concurrently(p, cand, dev) for p in picked):
+            picked.append(cand)
+    if len(picked) < n:
+        warnings.warn(f"only {len(picked)} of {n} mutually concurrent streams found for "
+                      f"{role!r}", RuntimeWarning, stacklevel=2)
+        while len(picked) < n:
+            picked.append(torch.cuda.Stream(dev))
+    _GROUPS[key] = picked
+    return picked
+
+
 def reset() -> None:
     """Forget the handed-out streams (tests)."""
     _CACHE.clear()
+    _GROUPS.clear()

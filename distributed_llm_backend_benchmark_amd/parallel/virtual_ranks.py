@@ -13,7 +13,8 @@ Two launch forms, both executing the production device code:
   launcher refuses grids larger than the device's resident capacity for that kernel.
 * ``streams``: the per-rank production launch (``dlbb_car_allreduce`` etc.) of every rank on its
   own HIP stream, i.e. W concurrent kernels exactly as W processes would enqueue them. Needs
-  ``W <= GPU_MAX_HW_QUEUES`` (4 here) distinct hardware queues: two ranks on one queue serialize,
+  ``W <= GPU_MAX_HW_QUEUES`` (4 here) distinct hardware queues, so the W streams are picked by
+  a concurrency probe (``parallel.streams.concurrent_group``): two ranks on one queue serialize,
   the first waits out its wall-clock bound (``custom_allreduce.set_timeout_ms``) and flags the
   timeout, which :meth:`errors` reports — never a hang.
 
@@ -31,6 +32,7 @@ from typing import List, Optional, Sequence
 import torch
 
 from ..ops import _lib
+from .streams import concurrent_group
 
 K_ONESHOT, K_TWOSHOT, K_REG, K_PUSH, K_AG, K_A2A, K_RS = 1, 2, 3, 4, 5, 6, 7
 KIND_NAMES = {K_ONESHOT: "oneshot", K_TWOSHOT: "twoshot", K_REG: "reg_pull", K_PUSH: "reg_push",
@@ -258,7 +260,10 @@ def emulation_summary(worlds=(2, 4, 8), small_bytes: int = 512,
                     us = time_calls(lambda: V.all_reduce(xs, got, algo=kind, nblocks=nb), iters)
                 rec[key] = {"valid": not any(V.errors()), "us": round(us, 2), "nblocks": nb}
                 if kind == K_ONESHOT and W <= 4:
-                    sts = [torch.cuda.Stream() for _ in range(W)]
+                    # W streams on W distinct hardware queues (parallel/streams.py): two
+                    # ranks on one queue would serialise behind each other's spin-waits
+                    sts = concurrent_group(torch.device("cuda", torch.cuda.current_device()),
+                                           W, "virtual_ranks")
                     for g_ in got:
                         g_.zero_()
                     V.all_reduce_streams(xs, got, sts, algo=kind, nblocks=nb)
