@@ -1124,32 +1124,120 @@ DLBB_PP_STAMPED(gemm_bf16_tn_256_pingpong3_bal, true, true, true)
 // stores only (host contract: no bias / activation / residual / pre-activation, bf16 C, vec_ok;
 // N % 64 == 0 makes every 16-column lane group whole). The general epilogue (store_tile) inside
 // the tile loop measured 7-15 % slower on the same shapes (persistent_ab_general_epilogue.jsonl).
-__device__ __forceinline__ void store_plain_bf16(const GemmArgs& a, const f32x4 (&acc)[8][4],
-                                                 int64_t row0, int64_t col0, int lane) {
+// LEAN epilogue kinds of the persistent kernel, bf16 output with vector stores: NT plain, + bias,
+// + bias -> GELU (tanh / erf) with an optional bf16 pre-activation store (the GPT-2 QKV / FC
+// forwards on multi-round grids of 12 K-tiles); NN plain and the GELU backward C = (A·B)·gelu'(u)
+// (the GPT-2 MLP-proj dgrad). Each kind is its own instantiation, so the tile loop carries only
+// the code its shape needs (the general store_tile in the loop measured 7-15 % slower).
+enum PpLean : int {
+  PP_PLAIN = 0, PP_BIAS = 1, PP_BIAS_GELU_TANH = 2, PP_BIAS_GELU_ERF = 3,
+  PP_DGELU_TANH = 4, PP_DGELU_ERF = 5,
+};
+
+// What the epilogue reads (the bias of the lane's 16 columns, or its 8 x 16 values of u) is loaded
+// by the caller BEFORE the wave drains its DMA with vmcnt(0), so the load latency hides in that
+// drain instead of stalling the flush. The fragments are dead there, so u's 64 VGPRs fit.
+#ifndef DLBB_UPRE
+#define DLBB_UPRE 1
+#endif
+struct LeanPre { u16x8 v[8]; };   // bias: v[0..1]; GELU backward: u of row blocks 0..3
+
+template <int LEAN>
+__device__ __forceinline__ void lean_pre(const GemmArgs& a, LeanPre& p, int64_t row0,
+                                         int64_t col0, int lane) {
+  const int64_t cbase = col0 + (lane >> 4) * 16;
+  if (cbase >= a.N) return;
+  if constexpr (LEAN == PP_BIAS || LEAN == PP_BIAS_GELU_TANH || LEAN == PP_BIAS_GELU_ERF) {
+    const u16x8* bp = reinterpret_cast<const u16x8*>(a.bias + cbase);
+    p.v[0] = bp[0];
+    p.v[1] = bp[1];
+  } else if constexpr (LEAN == PP_DGELU_TANH || LEAN == PP_DGELU_ERF) {
+    const int64_t rbase = row0 + (lane & 15);
+    const int rows_left = static_cast<int>(a.M - rbase);
+    const uint16_t* up = a.residual + rbase * a.ldr + cbase;
+#pragma unroll
+    for (int i = 0; i < DLBB_UPRE; ++i) {    // (all eight blocks' 64 VGPRs beside the accumulators spill)
+      if (i * 16 >= rows_left) break;
+      const u16x8* q = reinterpret_cast<const u16x8*>(up + static_cast<int64_t>(i) * 16 * a.ldr);
+      p.v[2 * i] = q[0];
+      p.v[2 * i + 1] = q[1];
+    }
+  }
+}
+
+template <bool NN, int LEAN>
+__device__ __forceinline__ void store_lean_bf16(const GemmArgs& a, const f32x4 (&acc)[8][4],
+                                                int64_t row0, int64_t col0, int lane,
+                                                const LeanPre& p) {
+  constexpr bool kBias = LEAN == PP_BIAS || LEAN == PP_BIAS_GELU_TANH || LEAN == PP_BIAS_GELU_ERF;
+  constexpr bool kDgelu = LEAN == PP_DGELU_TANH || LEAN == PP_DGELU_ERF;
   const int fr = lane & 15, fq = lane >> 4;
+  const bool odd = NN && (fq & 1);      // NN fragments: 4-column groups swapped (read_b_nn)
   const int64_t cbase = col0 + fq * 16;
   if (cbase >= a.N) return;
   const int64_t rbase = row0 + fr;
   const int rows_left = static_cast<int>(a.M - rbase);
   uint16_t* cb = static_cast<uint16_t*>(a.C) + rbase * a.ldc + cbase;
+  float bias[16];
+  if constexpr (kBias) {
+#pragma unroll
+    for (int c = 0; c < 8; ++c) { bias[c] = bf16_to_f32(p.v[0][c]); bias[8 + c] = bf16_to_f32(p.v[1][c]); }
+  }
+  uint16_t* pb = ((LEAN == PP_BIAS_GELU_TANH || LEAN == PP_BIAS_GELU_ERF) && a.preact)
+                     ? a.preact + rbase * a.ldc + cbase : nullptr;
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     if (i * 16 >= rows_left) break;
-    u16x8 o0, o1;
+    float v[16];
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < 4; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        o0[j * 4 + r] = f32_to_bf16(acc[i][j][r]);
-        o1[j * 4 + r] = f32_to_bf16(acc[i][j + 2][r]);
+        const float x = odd ? acc[i][j ^ 1][r] : acc[i][j][r];
+        v[j * 4 + r] = kBias ? x + bias[j * 4 + r] : x;
       }
-    u16x8* o = reinterpret_cast<u16x8*>(cb + static_cast<int64_t>(i) * 16 * a.ldc);
+    const int64_t oc = static_cast<int64_t>(i) * 16 * a.ldc;
+    if (pb) {
+      u16x8 p0, p1;
+#pragma unroll
+      for (int c = 0; c < 8; ++c) { p0[c] = f32_to_bf16(v[c]); p1[c] = f32_to_bf16(v[8 + c]); }
+      reinterpret_cast<u16x8*>(pb + oc)[0] = p0;
+      reinterpret_cast<u16x8*>(pb + oc)[1] = p1;
+    }
+    if constexpr (LEAN == PP_BIAS_GELU_TANH) {
+#pragma unroll
+      for (int c = 0; c < 16; ++c) v[c] = gelu_tanh(v[c]);
+    } else if constexpr (LEAN == PP_BIAS_GELU_ERF) {
+#pragma unroll
+      for (int c = 0; c < 16; ++c) v[c] = gelu_erf(v[c]);
+    } else if constexpr (kDgelu) {
+      u16x8 ua, ub;
+      if (i < DLBB_UPRE) {
+        ua = p.v[2 * i];
+        ub = p.v[2 * i + 1];
+      } else {                          // blocks 4..7: loaded here (latency exposed)
+        const u16x8* q = reinterpret_cast<const u16x8*>(a.residual + (rbase + i * 16) * a.ldr +
+                                                        cbase);
+        ua = q[0];
+        ub = q[1];
+      }
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        const float u0 = bf16_to_f32(ua[c]), u1 = bf16_to_f32(ub[c]);
+        v[c] *= LEAN == PP_DGELU_TANH ? gelu_tanh_grad(u0) : gelu_erf_grad(u0);
+        v[8 + c] *= LEAN == PP_DGELU_TANH ? gelu_tanh_grad(u1) : gelu_erf_grad(u1);
+      }
+    }
+    u16x8 o0, o1;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) { o0[c] = f32_to_bf16(v[c]); o1[c] = f32_to_bf16(v[8 + c]); }
+    u16x8* o = reinterpret_cast<u16x8*>(cb + oc);
     o[0] = o0;
     o[1] = o1;
   }
 }
 
-template <bool BAL>
+template <bool NN, bool BAL, int LEAN = PP_PLAIN>
 __device__ __forceinline__ void pp_persist_body(GemmArgs a, char* smem) {
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1173,20 +1261,35 @@ __device__ __forceinline__ void pp_persist_body(GemmArgs a, char* smem) {
   const int r_in = lane >> 3, chunk = (lane & 7) ^ (lane >> 3);
   const uint32_t lda2 = static_cast<uint32_t>(a.lda) * 2, ldb2 = static_cast<uint32_t>(a.ldb) * 2;
   const uint32_t aoff = static_cast<uint32_t>(r_in) * lda2 + chunk * 16;
-  const uint32_t boff = static_cast<uint32_t>(perm_brow(r_in)) * ldb2 + chunk * 16;
+  uint32_t boff;
+  if constexpr (NN) {                           // as pingpong_body: transposed-read B images
+    const int rq = lane >> 4, slot = lane & 15;
+    boff = static_cast<uint32_t>(rq) * ldb2 +
+           static_cast<uint32_t>(slot ^ rq ^ (((wc >> 1) & 1) << 3)) * 16;
+  } else {
+    boff = static_cast<uint32_t>(perm_brow(r_in)) * ldb2 + chunk * 16;
+  }
   constexpr uint32_t kStep = BK * 2;
 #define DLBB_RSRC(P) \
   __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(P), 0, 0x7fffffff, 0x00020000)
 
   Tile256 tc = tile_of(a, wg);                  // the tile being multiplied
+  // bias kinds: the bias of the tile being multiplied is loaded one tile ahead (8 VGPRs held
+  // across the K loop) — loaded at the flush it stalled every tile boundary (+6 us on the GPT-2
+  // QKV forward); the GELU backward's u is too large to hold and is loaded at the boundary
+  constexpr bool kBiasAhead =
+      LEAN == PP_BIAS || LEAN == PP_BIAS_GELU_TANH || LEAN == PP_BIAS_GELU_ERF;
+  LeanPre bias_ahead;
+  if constexpr (kBiasAhead)
+    lean_pre<LEAN>(a, bias_ahead, tc.m0 + (wave >> 2) * 128, tc.n0 + (wave & 3) * 64, lane);
   {
     const __amdgpu_buffer_rsrc_t ra = DLBB_RSRC(a.A + tc.m0 * a.lda);
-    const __amdgpu_buffer_rsrc_t rb = DLBB_RSRC(a.B + tc.n0 * a.ldb);
+    const __amdgpu_buffer_rsrc_t rb = DLBB_RSRC(NN ? a.B + tc.n0 : a.B + tc.n0 * a.ldb);
     const int rows_a = static_cast<int>(a.M - tc.m0), rows_b = static_cast<int>(a.N - tc.n0);
     if (wr == 0) {                              // prologue (nk >= 2): A-lo(0), B(0), B(1)
       stage_a_half(ra, lda2, rows_a, 0, abuf0, 0, wc, aoff);
-      stage_b(rb, ldb2, rows_b, 0, bbuf0, wc, boff);
-      stage_b(rb, ldb2, rows_b, kStep, bbuf0 + kTile2Bytes, wc, boff);
+      stage_b_any<NN>(rb, ldb2, rows_b, 0, bbuf0, wc, boff);
+      stage_b_any<NN>(rb, ldb2, rows_b, 1, bbuf0 + kTile2Bytes, wc, boff);
       DLBB_WAIT_VM(8);
       __builtin_amdgcn_s_barrier();
     } else {                                    // A-hi(0), A-lo(1)
@@ -1208,7 +1311,8 @@ __device__ __forceinline__ void pp_persist_body(GemmArgs a, char* smem) {
     __builtin_amdgcn_sched_barrier(0);                                             \
     int ln_ = lane;                                                                \
     asm volatile("" : "+v"(ln_));                                                  \
-    store_plain_bf16(a, acc, (T).m0 + (wave >> 2) * 128, (T).n0 + (wave & 3) * 64, ln_); \
+    store_lean_bf16<NN, LEAN>(a, acc, (T).m0 + (wave >> 2) * 128, (T).n0 + (wave & 3) * 64,  \
+                              ln_, pre_);                                          \
     _Pragma("unroll") for (int x_ = 0; x_ < 8; ++x_)                                \
       _Pragma("unroll") for (int y_ = 0; y_ < 4; ++y_)                              \
         acc[x_][y_] = f32x4{0.f, 0.f, 0.f, 0.f};                                    \
@@ -1218,16 +1322,17 @@ __device__ __forceinline__ void pp_persist_body(GemmArgs a, char* smem) {
   for (int i = 0; i < mine; ++i) {
     const Tile256 tn = i + 1 < mine ? tile_of(a, wg + (i + 1) * nwg) : tc;   // next tile
     const __amdgpu_buffer_rsrc_t ra = DLBB_RSRC(a.A + tc.m0 * a.lda);
-    const __amdgpu_buffer_rsrc_t rb = DLBB_RSRC(a.B + tc.n0 * a.ldb);
+    const __amdgpu_buffer_rsrc_t rb = DLBB_RSRC(NN ? a.B + tc.n0 : a.B + tc.n0 * a.ldb);
     const __amdgpu_buffer_rsrc_t ran = DLBB_RSRC(a.A + tn.m0 * a.lda);
-    const __amdgpu_buffer_rsrc_t rbn = DLBB_RSRC(a.B + tn.n0 * a.ldb);
+    const __amdgpu_buffer_rsrc_t rbn = DLBB_RSRC(NN ? a.B + tn.n0 : a.B + tn.n0 * a.ldb);
     const int rows_a = static_cast<int>(a.M - tc.m0), rows_b = static_cast<int>(a.N - tc.n0);
     const int rows_an = static_cast<int>(a.M - tn.m0), rows_bn = static_cast<int>(a.N - tn.n0);
     if (wr == 0) {
       for (int k = 0; k < nk; ++k) {
         const int g = i * nk + k;
         const bool bnd = k == 0 && i > 0;       // first K-tile of a new output tile
-        read_split(abuf0 + (g & 1) * kTile2Bytes, bbuf0 + cb * kTile2Bytes, 0, wc, fr, fq, af, bf);
+        read_split_any<NN>(abuf0 + (g & 1) * kTile2Bytes, bbuf0 + cb * kTile2Bytes, 0, wc, fr, fq, af,
+                           bf);
         const bool h1 = g + 1 < G, b2 = g + 2 < G;
         char* const an = abuf0 + ((g + 1) & 1) * kTile2Bytes;
         if (h1) {                               // A-hi(g+1): this tile's K-tile or the next's 0
@@ -1237,9 +1342,11 @@ __device__ __forceinline__ void pp_persist_body(GemmArgs a, char* smem) {
         if (b2) {                               // B(g+2) (BAL: its first half)
           char* const bn = bbuf0 + (cb == 0 ? 2 : cb - 1) * kTile2Bytes;
           const bool here = k + 2 < nk;
-          const uint32_t k2 = static_cast<uint32_t>(here ? k + 2 : k + 2 - nk) * kStep;
-          if (BAL) stage_b<0, 4>(here ? rb : rbn, ldb2, here ? rows_b : rows_bn, k2, bn, wc, boff);
-          else stage_b<0, 8>(here ? rb : rbn, ldb2, here ? rows_b : rows_bn, k2, bn, wc, boff);
+          const int ub = here ? k + 2 : k + 2 - nk;       // K-tile index within its tile
+          if (BAL)
+            stage_b_any<NN, 0, 4>(here ? rb : rbn, ldb2, here ? rows_b : rows_bn, ub, bn, wc, boff);
+          else
+            stage_b_any<NN, 0, 8>(here ? rb : rbn, ldb2, here ? rows_b : rows_bn, ub, bn, wc, boff);
         }
         if (bnd) {
           // A-hi(g) retired at the top: no wait, so the stores are never drained here
@@ -1269,16 +1376,18 @@ __device__ __forceinline__ void pp_persist_body(GemmArgs a, char* smem) {
       for (int k = 0; k < nk; ++k) {
         const int g = i * nk + k;
         const bool bnd = k == 0 && i > 0;
-        read_split(abuf0 + (g & 1) * kTile2Bytes, bbuf0 + cb * kTile2Bytes, 1, wc, fr, fq, af, bf);
+        read_split_any<NN>(abuf0 + (g & 1) * kTile2Bytes, bbuf0 + cb * kTile2Bytes, 1, wc, fr, fq, af,
+                           bf);
         const bool l2 = g + 2 < G;
         if (l2) {                               // A-lo(g+2) (BAL: and B1(g+2))
           const bool here = k + 2 < nk;
-          const uint32_t k2 = static_cast<uint32_t>(here ? k + 2 : k + 2 - nk) * kStep;
-          stage_a_half(here ? ra : ran, lda2, here ? rows_a : rows_an, k2,
-                       abuf0 + (g & 1) * kTile2Bytes, 0, wc, aoff);
+          const int ub = here ? k + 2 : k + 2 - nk;
+          stage_a_half(here ? ra : ran, lda2, here ? rows_a : rows_an,
+                       static_cast<uint32_t>(ub) * kStep, abuf0 + (g & 1) * kTile2Bytes, 0, wc,
+                       aoff);
           if (BAL)
-            stage_b<4, 8>(here ? rb : rbn, ldb2, here ? rows_b : rows_bn, k2,
-                          bbuf0 + (cb == 0 ? 2 : cb - 1) * kTile2Bytes, wc, boff);
+            stage_b_any<NN, 4, 8>(here ? rb : rbn, ldb2, here ? rows_b : rows_bn, ub,
+                                  bbuf0 + (cb == 0 ? 2 : cb - 1) * kTile2Bytes, wc, boff);
         }
         if (g + 1 < G && !bnd) {               // (boundary: A-lo(g+1) retired at the top)
           if (l2) { if (BAL) DLBB_WAIT_VM(8); else DLBB_WAIT_VM(4); }
@@ -1295,21 +1404,35 @@ __device__ __forceinline__ void pp_persist_body(GemmArgs a, char* smem) {
       }
     }
     // this row's part of tile i, at the start of its first memory interval of tile i + 1
+    LeanPre pre_;
+    if constexpr (kBiasAhead) pre_ = bias_ahead;
+    else lean_pre<LEAN>(a, pre_, tc.m0 + (wave >> 2) * 128, tc.n0 + (wave & 3) * 64, lane);
     DLBB_WAIT_VM(0);
     DLBB_PP_FLUSH(tc);
+    if constexpr (kBiasAhead)   // issued after the stores: older than every later counted load
+      if (i + 1 < mine)
+        lean_pre<LEAN>(a, bias_ahead, tn.m0 + (wave >> 2) * 128, tn.n0 + (wave & 3) * 64, lane);
     tc = tn;
   }
 #undef DLBB_PP_FLUSH
 #undef DLBB_RSRC
 }
 
+template <int LEAN>
 __global__ void __launch_bounds__(kThreads2, 1) gemm_bf16_nt_256_pp_persist(GemmArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  pp_persist_body<false>(a, smem);
+  pp_persist_body<false, false, LEAN>(a, smem);
 }
+template <int LEAN>
 __global__ void __launch_bounds__(kThreads2, 1) gemm_bf16_nt_256_pp_persist_bal(GemmArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  pp_persist_body<true>(a, smem);
+  pp_persist_body<false, true, LEAN>(a, smem);
+}
+// NN (dgrad) persistent form: balanced DMA issue (NN's measured default at every K)
+template <int LEAN>
+__global__ void __launch_bounds__(kThreads2, 1) gemm_bf16_nn_256_pp_persist_bal(GemmArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  pp_persist_body<true, true, LEAN>(a, smem);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1600,6 +1723,16 @@ static bool persist_enabled() {
   }();
   return on != 0;
 }
+// DLBB_GEMM_PERSIST_EPI=0 (or dlbb_gemm_set_persist_epi(0)): keep bias / bias-GELU epilogues on
+// the non-persistent ping-pong (A/B)
+static int dlbb_persist_epi = -1;
+static bool persist_epi_enabled() {
+  if (dlbb_persist_epi < 0) {
+    const char* e = getenv("DLBB_GEMM_PERSIST_EPI");
+    dlbb_persist_epi = (e && e[0] == '0') ? 0 : 1;
+  }
+  return dlbb_persist_epi != 0;
+}
 static bool use_bal(int64_t k_tiles, bool nn) {
   return dlbb_gemm_bal == 1 || (dlbb_gemm_bal == 2 && (nn || k_tiles >= kBalMinKTiles));
 }
@@ -1607,6 +1740,7 @@ static bool use_bal(int64_t k_tiles, bool nn) {
 DLBB_API void dlbb_gemm_set_tile(int tile) { dlbb_gemm_force_tile = tile; }
 DLBB_API void dlbb_gemm_set_stagger(int on) { dlbb_gemm_stagger = on; }
 DLBB_API int dlbb_gemm_get_stagger() { return dlbb_gemm_stagger; }
+DLBB_API void dlbb_gemm_set_persist_epi(int on) { dlbb_persist_epi = on ? 1 : 0; }
 DLBB_API void dlbb_gemm_set_bal(int mode) { dlbb_gemm_bal = mode >= 0 && mode <= 2 ? mode : 2; }
 
 DLBB_API int dlbb_gemm_bf16_nt(const void* A, int64_t lda, const void* B, int64_t ldb, void* C,
@@ -1642,13 +1776,22 @@ DLBB_API int dlbb_gemm_bf16_nt(const void* A, int64_t lda, const void* B, int64_
     // (tools/gemm_ab.py, profiles/r03_gemm/persistent_ab.jsonl, plain bf16: +6.6 % at
     // 16384 x 3072 x 768, +10.6 % GPT-2 LM head; neutral at K = 4096 over 3 rounds; -2 % on
     // one-round grids)
-    const bool plain = epi == 0 && !out_f32 && !preact && vec_ok;
-    if (mode == 6 && plain && persist_enabled() && tiles256 > num_cus() &&
+    // lean epilogue kinds (bf16 output, vector stores, nothing read but the bias): plain, bias,
+    // bias -> GELU with an optional pre-activation store; -1 = the general epilogue only
+    int lean = -1;
+    if (!out_f32 && vec_ok) {
+      if (epi == 0 && !preact) lean = PP_PLAIN;
+      else if (epi == EPI_BIAS && !preact) lean = PP_BIAS;
+      else if (epi == (EPI_BIAS | EPI_GELU_TANH)) lean = PP_BIAS_GELU_TANH;
+      else if (epi == (EPI_BIAS | EPI_GELU_ERF)) lean = PP_BIAS_GELU_ERF;
+    }
+    if (lean > PP_PLAIN && !persist_epi_enabled()) lean = -1;
+    if (mode == 6 && lean >= 0 && persist_enabled() && tiles256 > num_cus() &&
         K / BK <= kPersistMaxKTiles)
       mode = 10;
-    // persistent ping-pong (mode 10): the ping-pong contract, at least two K-tiles and the lean
-    // epilogue's (plain bf16 output, vector stores)
-    if (mode == 10 && (K < 2 * BK || !plain)) mode = 6;
+    // persistent ping-pong (mode 10): the ping-pong contract, at least two K-tiles and a lean
+    // epilogue
+    if (mode == 10 && (K < 2 * BK || lean < 0)) mode = 6;
     // ping-pong contract: 8-row A groups and 64-row B blocks wholly in or out (uniform clamps),
     // 32-bit buffer offsets within a 256-row panel
     if ((mode == 6 || mode == 7 || mode == 10) && !(M % 8 == 0 && N % 64 == 0 && M >= 8 && lda * 2 * 256 + K * 2 < (1LL << 31) &&
@@ -1657,12 +1800,20 @@ DLBB_API int dlbb_gemm_bf16_nt(const void* A, int64_t lda, const void* B, int64_
     if (mode == 5 || mode == 8 || mode > 10) mode = 3;
     if (mode == 10) {
       const int64_t grid = tiles256 < num_cus() ? tiles256 : num_cus();
-      if (use_bal(K / BK, false))
-        hipLaunchKernelGGL(gemm_bf16_nt_256_pp_persist_bal, dim3(static_cast<unsigned>(grid)),
-                           dim3(kThreads2), kPP6Lds, stream, a);
-      else
-        hipLaunchKernelGGL(gemm_bf16_nt_256_pp_persist, dim3(static_cast<unsigned>(grid)),
-                           dim3(kThreads2), kPP6Lds, stream, a);
+      const dim3 gp(static_cast<unsigned>(grid)), bp(kThreads2);
+      const bool bal = use_bal(K / BK, false);
+#define DLBB_PP_PERSIST_LAUNCH(L)                                                          \
+  do {                                                                                     \
+    if (bal) hipLaunchKernelGGL(gemm_bf16_nt_256_pp_persist_bal<L>, gp, bp, kPP6Lds, stream, a); \
+    else hipLaunchKernelGGL(gemm_bf16_nt_256_pp_persist<L>, gp, bp, kPP6Lds, stream, a);   \
+  } while (0)
+      switch (lean) {
+        case PP_BIAS: DLBB_PP_PERSIST_LAUNCH(PP_BIAS); break;
+        case PP_BIAS_GELU_TANH: DLBB_PP_PERSIST_LAUNCH(PP_BIAS_GELU_TANH); break;
+        case PP_BIAS_GELU_ERF: DLBB_PP_PERSIST_LAUNCH(PP_BIAS_GELU_ERF); break;
+        default: DLBB_PP_PERSIST_LAUNCH(PP_PLAIN); break;
+      }
+#undef DLBB_PP_PERSIST_LAUNCH
       return hipGetLastError();
     }
     if (mode == 4) {
@@ -1750,6 +1901,31 @@ DLBB_API int dlbb_gemm_bf16_nn(const void* A, int64_t lda, const void* B, int64_
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     return dlbb_split_reduce_launch(ws, C, 0, M * N, split, stream);
+  }
+  // multi-round grid with a short reduction: the persistent form (plain bf16 or the GELU
+  // backward, operands of the epilogue prefetched before the DMA drain; the GPT-2 MLP-proj dX,
+  // 768 tiles x 12 K-tiles)
+  if (persist_enabled() && persist_epi_enabled() && tiles256 > num_cus() && nkt >= 2 &&
+      nkt <= kPersistMaxKTiles && use_bal(nkt, true) && !out_f32 && vec_ok && !preact) {
+    const int lean = epi == 0 ? PP_PLAIN
+                     : epi == EPI_DGELU_TANH ? PP_DGELU_TANH
+                     : epi == EPI_DGELU_ERF ? PP_DGELU_ERF : -1;
+    const dim3 gp(static_cast<unsigned>(num_cus())), bp(kThreads2);
+    switch (lean) {
+      case PP_PLAIN:
+        hipLaunchKernelGGL(gemm_bf16_nn_256_pp_persist_bal<PP_PLAIN>, gp, bp, kPP6Lds, stream, a);
+        return hipGetLastError();
+      case PP_DGELU_TANH:
+        hipLaunchKernelGGL(gemm_bf16_nn_256_pp_persist_bal<PP_DGELU_TANH>, gp, bp, kPP6Lds,
+                           stream, a);
+        return hipGetLastError();
+      case PP_DGELU_ERF:
+        hipLaunchKernelGGL(gemm_bf16_nn_256_pp_persist_bal<PP_DGELU_ERF>, gp, bp, kPP6Lds,
+                           stream, a);
+        return hipGetLastError();
+      default:
+        break;
+    }
   }
   if (use_bal(nkt, true))
     DLBB_PP_LAUNCH(gemm_bf16_nn_256_pingpong3_bal, STAMP_GEMM_NN,

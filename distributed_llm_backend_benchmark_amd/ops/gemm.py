@@ -87,6 +87,12 @@ def set_bal(mode: int) -> None:
     _lib.lib().dlbb_gemm_set_bal(int(mode))
 
 
+def set_persist_epi(on: bool) -> None:
+    """Persistent NT kernel for bias / bias-GELU epilogues on multi-round short-K grids (default
+    on; ``DLBB_GEMM_PERSIST_EPI=0`` or ``set_persist_epi(False)`` keeps them on the ping-pong)."""
+    _lib.lib().dlbb_gemm_set_persist_epi(int(bool(on)))
+
+
 def set_wgrad_stages(nb: int) -> None:
     """LDS ring depth of the weight-gradient kernel (2, 3 or 4 stages); for A/B benchmarking."""
     _lib.lib().dlbb_gemm_wgrad_set_stages(int(nb))

@@ -164,6 +164,37 @@ def test_gemm_epilogues(act, gemm_tile):
     torch.testing.assert_close(pre.float(), u, rtol=1e-2, atol=3e-2)
 
 
+@pytest.mark.parametrize("M,N,K,act,with_pre", [
+    (16384, 2304, 768, None, False),          # GPT-2 QKV: bias, 576 tiles on 256 CUs
+    (8192 + 40, 3072, 768, "gelu_tanh", True),  # GPT-2 FC (ragged last row block), preact
+    (8192, 3072, 256, "gelu", True),            # erf GELU, 4 K-tiles
+    (8192, 2048 + 64, 2560, "gelu_tanh", False),  # 40 K-tiles (balanced DMA), N % 256 == 64
+])
+@pytest.mark.parametrize("persist_epi", [True, False])
+def test_gemm_persistent_lean_epilogues(M, N, K, act, with_pre, persist_epi, monkeypatch):
+    """Persistent NT kernel with the bias / bias-GELU (+ pre-activation) epilogue stored at the next
+    tile's first memory interval, against fp32; the non-persistent ping-pong (persist_epi off) is
+    held to the same reference."""
+    from distributed_llm_backend_benchmark_amd.ops import gemm, linear
+
+    x = _randn(M, K, seed=31, scale=0.3)
+    w = _randn(N, K, seed=32, scale=0.3)
+    b = _randn(N, seed=33)
+    pre = torch.empty(M, N, dtype=torch.bfloat16, device=DEV) if with_pre else None
+    u = x.float() @ w.float().t() + b.float()
+    ref = u if act is None else F.gelu(u, approximate="tanh" if act == "gelu_tanh" else "none")
+    monkeypatch.setenv("DLBB_GEMM", "mfma")
+    gemm.set_persist_epi(persist_epi)
+    try:
+        y = linear(x, w, bias=b, act=act, preact=pre)
+    finally:
+        gemm.set_persist_epi(True)
+    torch.cuda.synchronize()
+    torch.testing.assert_close(y.float(), ref, rtol=2e-2, atol=2e-2)
+    if with_pre:
+        torch.testing.assert_close(pre.float(), u, rtol=2e-2, atol=2e-2)
+
+
 def test_gemm_strided_A_view():
     """The TP attention stub passes qkv[..., :H/P] (lda = 3H/P) straight into the GEMM."""
     from distributed_llm_backend_benchmark_amd.ops import linear
@@ -417,6 +448,32 @@ def test_dgrad_fused_gelu_backward(act, impl, monkeypatch):
     g = F.gelu(uf, approximate="tanh" if act == "gelu_tanh" else "none")
     g.backward(dy.float() @ w.float())
     torch.testing.assert_close(out.float(), uf.grad, rtol=2e-2, atol=3e-2)
+
+
+@pytest.mark.parametrize("M,N,K,act", [(16384, 3072, 768, "gelu_tanh"), (8192 + 40, 2048, 512, "gelu"),
+                                       (16384, 3072, 768, None), (4096 + 8, 4096, 2048, None)])
+@pytest.mark.parametrize("persist", [True, False])
+def test_dgrad_persistent_matches_fp32(M, N, K, act, persist):
+    """NN dgrad on multi-round short-K grids: the persistent form (plain / GELU backward with the
+    epilogue's u read at the tile boundary; ragged last row block) and the non-persistent ping-pong
+    against fp32."""
+    from distributed_llm_backend_benchmark_amd.ops import gemm
+
+    dy = _randn(M, K, seed=41, scale=0.5)
+    w = _randn(K, N, seed=42, scale=0.05)
+    u = _randn(M, N, seed=43, scale=2.0) if act else None
+    out = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+    gemm.set_persist_epi(persist)
+    try:
+        gemm._dgrad_hip(dy, w, out, None, (u, act) if act else None)
+    finally:
+        gemm.set_persist_epi(True)
+    g = dy.float() @ w.float()
+    if act:
+        uf = u.float().requires_grad_(True)
+        F.gelu(uf, approximate="tanh" if act == "gelu_tanh" else "none").backward(g)
+        g = uf.grad
+    torch.testing.assert_close(out.float(), g, rtol=2e-2, atol=3e-2)
 
 
 @pytest.mark.parametrize("sinks", [False, True])

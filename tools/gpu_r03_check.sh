@@ -1,0 +1,12 @@
+#!/bin/bash
+# Re-entry check of the restored tree: GPU test suite, smoke, 1-GPU bench.
+set -u -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+O=gpurun_out/r03_reentry; mkdir -p $O
+export HSA_ENABLE_IPC_MODE_LEGACY=0
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 200 --timeout-method thread --deselect tests/test_native_host_asan.py::test_host_asan_with_device > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 1; }
+tail -2 $O/pytest.log
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { tail -30 $O/smoke.log; exit 1; }
+tail -1 $O/smoke.log
+timeout -k 10 600 python bench.py > $O/bench.log 2>&1 || { tail -30 $O/bench.log; exit 1; }
+tail -1 $O/bench.log | cut -c1-400
