@@ -71,6 +71,10 @@ def main():
         rec["fwd_epi_nopersist_us"] = t_best(lambda: G._mfma_linear(xf, w, b, act, None, y,
                                                                     pre if act else None))
         G.set_persist_epi(True)
+        G.set_tile(128)
+        rec["fwd_epi_t128_us"] = t_best(lambda: G._mfma_linear(xf, w, b, act, None, y,
+                                                               pre if act else None))
+        G.set_tile(0)
         rec["fwd_plain_us"] = t_best(lambda: G._mfma_linear(xf, w, None, None, None, y, None))
         rec["fwd_blas_epi_us"] = t_best(lambda: G._blas_linear(xf, w, b, act, None, y,
                                                                pre if act else None))
