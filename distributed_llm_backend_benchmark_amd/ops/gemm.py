@@ -88,8 +88,10 @@ def set_bal(mode: int) -> None:
 
 
 def set_persist_epi(on: bool) -> None:
-    """Persistent NT kernel for bias / bias-GELU epilogues on multi-round short-K grids (default
-    on; ``DLBB_GEMM_PERSIST_EPI=0`` or ``set_persist_epi(False)`` keeps them on the ping-pong)."""
+    """Persistent forms with lean epilogues on multi-round short-K grids: NT bias / bias-GELU
+    (+ pre-activation) and NN plain / GELU backward (default on; ``DLBB_GEMM_PERSIST_EPI=0`` or
+    ``set_persist_epi(False)`` keeps them on the non-persistent ping-pong; the NT plain form
+    follows ``DLBB_GEMM_PERSIST``)."""
     _lib.lib().dlbb_gemm_set_persist_epi(int(bool(on)))
 
 
