@@ -65,10 +65,10 @@ __device__ __forceinline__ bf16x8 frag(const char* img, int kbase, int colbase, 
 // One stage = BM rows of m of the NA = WM / 2 A sub-images ([BM][128 cols of dY] each) and the B
 // image ([BM][128 cols of X]); every 4-row x 256-B wave-instruction of the stage is one slot
 // j = wave * per + q of NIMG * BM / 4, spread evenly over the workgroup's waves.
-template <int WM>
+template <int WM, int WJ = 4>
 __device__ __forceinline__ void stage_all(const Args& a, int m0, int n0, int k0, char* buf,
                                           int wave, int lane) {
-  constexpr int NA = WM / 2, NIMG = NA + 1, RG = BM / 4, NW = 2 * WM;
+  constexpr int NA = WM / 2, NIMG = NA + WJ / 4, RG = BM / 4, NW = 2 * WM;
   constexpr int PER = NIMG * RG / NW;
   static_assert(NIMG * RG % NW == 0, "stage slots must divide evenly over the waves");
   const int rq = lane >> 4, slot = lane & 15;
@@ -81,7 +81,7 @@ __device__ __forceinline__ void stage_all(const Args& a, int m0, int n0, int k0,
     const bool is_a = img < NA;
     const uint16_t* X = is_a ? a.A : a.B;
     const int64_t ld = is_a ? a.lda : a.ldb;
-    const int c0 = is_a ? n0 + img * 128 : k0;
+    const int c0 = is_a ? n0 + img * 128 : k0 + (img - NA) * 128;
     const uint16_t* src = X + static_cast<int64_t>(m0 + row) * ld + c0 + chunk * 8;
     __builtin_amdgcn_global_load_lds(src, (lds_vptr_t)(buf + img * kTile + rg * 4 * 256), 16, 0,
                                      0);
@@ -93,10 +93,15 @@ __device__ __forceinline__ void stage_all(const Args& a, int m0, int n0, int k0,
 // workgroup in 64-row wave blocks — 2: 128 x 128 tile, 4 waves, three workgroups per CU;
 // 4: 256 x 128 tile, 8 waves, two per CU: 1.33x the MFMA work per byte staged through L2 (the
 // 128 x 128 tile needs ~64 FLOP per L2 byte, more than the L2 delivers at the MFMA rate).
-template <bool BIAS, int NB, int WM>
-__global__ void __launch_bounds__(128 * WM, WM == 2 ? 3 : 2) wgrad_kernel(Args a) {
+// WJ: 16-column B fragments per wave — 4: 64 x 64 per wave (128 output columns per tile), 8:
+// 64 x 128 per wave (256 columns per tile): 25 % fewer LDS fragment bytes per MFMA and 2/3 of the
+// DMA per output of the 128 x 128 tile; the 128-column kernels are LDS-bound (GPT-2 dW shapes).
+template <bool BIAS, int NB, int WM, int WJ = 4>
+__global__ void __launch_bounds__(128 * WM, WJ == 8 ? 2 : (WM == 2 ? 3 : 2))
+    wgrad_kernel(Args a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  constexpr int NIMG = WM / 2 + 1;
+  constexpr int NIMG = WM / 2 + WJ / 4;
+  constexpr int TBK = 32 * WJ;                    // output columns (K) per tile
   constexpr int kStage = NIMG * kTile;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -107,22 +112,22 @@ __global__ void __launch_bounds__(128 * WM, WM == 2 ? 3 : 2) wgrad_kernel(Args a
   // re-read by the tiles_k workgroups of a row and its X blocks by every row — from that L2
   // instead of from the Infinity Cache / HBM (the default round-robin puts neighbours on
   // different XCDs, so every workgroup fetched its panels from beyond L2).
-  const int tiles_k = a.K / BKO;
+  const int tiles_k = a.K / TBK;
   const int tiles = (a.N / (64 * WM)) * tiles_k;
   const int nwg = gridDim.x, xcd = blockIdx.x % 8, q = nwg / 8, r = nwg % 8;
   const int wid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + blockIdx.x / 8;
   const int split = wid / tiles, t = wid % tiles;
   const int tn = t / tiles_k, tk = t % tiles_k;
-  const int n0 = tn * 64 * WM, k0 = tk * BKO;
+  const int n0 = tn * 64 * WM, k0 = tk * TBK;
   const int mb = split * a.m_per_split;
   const int me = mb + a.m_per_split < a.M ? mb + a.m_per_split : a.M;
   const int nsteps = (me - mb) / BM;
 
-  f32x4 acc[4][4];
+  f32x4 acc[4][WJ];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < WJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   // bias: wave (wm, wn) of a column-block-0 workgroup sums fragments i = 2 wn, 2 wn + 1
   const bool do_bias = BIAS && tk == 0;
   f32x4 bacc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
@@ -133,10 +138,12 @@ __global__ void __launch_bounds__(128 * WM, WM == 2 ? 3 : 2) wgrad_kernel(Args a
   auto stg = [&](int c) { return smem + c * kStage; };
   // this wave's A sub-image (128 dY columns) and the row offset of its 64 inside it
   const int asub = (wm * 64) / 128, acol = (wm * 64) % 128;
+  // and its B image / column offset (WJ = 8: one whole 128-column image per wave)
+  const int bsub = WM / 2 + (wn * 16 * WJ) / 128, bcol = (wn * 16 * WJ) % 128;
   constexpr int kLoadsPerStage = NIMG * (BM / 4) / (2 * WM);   // global_load_lds per wave
 #pragma unroll
   for (int p = 0; p < NB - 1; ++p)
-    if (p < nsteps) stage_all<WM>(a, mb + p * BM, n0, k0, stg(p), wave, lane);
+    if (p < nsteps) stage_all<WM, WJ>(a, mb + p * BM, n0, k0, stg(p), wave, lane);
   for (int s = 0; s < nsteps; ++s) {
     const int cur = s % NB;
     // stage s landed: later stages (up to NB - 2 of them) may still be in flight
@@ -151,21 +158,21 @@ __global__ void __launch_bounds__(128 * WM, WM == 2 ? 3 : 2) wgrad_kernel(Args a
     // the buffer of stage s - 1 (every wave finished it), which stage s + NB - 1 now refills
     __builtin_amdgcn_s_barrier();
     if (s + NB - 1 < nsteps)
-      stage_all<WM>(a, mb + (s + NB - 1) * BM, n0, k0, stg((s + NB - 1) % NB), wave, lane);
+      stage_all<WM, WJ>(a, mb + (s + NB - 1) * BM, n0, k0, stg((s + NB - 1) % NB), wave, lane);
     const char* ia = stg(cur) + asub * kTile;
-    const char* ib = stg(cur) + (NIMG - 1) * kTile;
+    const char* ib = stg(cur) + bsub * kTile;
 #pragma unroll
     for (int ks = 0; ks < BM / 32; ++ks) {
-      bf16x8 af[4], bfr[4];
+      bf16x8 af[4], bfr[WJ];
 #pragma unroll
       for (int i = 0; i < 4; ++i) af[i] = frag(ia, 32 * ks, acol + i * 16, lane);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) bfr[j] = frag(ib, 32 * ks, wn * 64 + j * 16, lane);
+      for (int j = 0; j < WJ; ++j) bfr[j] = frag(ib, 32 * ks, bcol + j * 16, lane);
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
+        for (int j = 0; j < WJ; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
       if (do_bias) {   // wave-uniform branches on wn (a runtime index into af[] would
                        // become v_cndmask chains over every fragment register)
@@ -186,11 +193,11 @@ __global__ void __launch_bounds__(128 * WM, WM == 2 ? 3 : 2) wgrad_kernel(Args a
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
+      for (int j = 0; j < WJ; ++j)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int64_t o = static_cast<int64_t>(n0 + wm * 64 + i * 16 + fq * 4 + r) * a.K +
-                            k0 + wn * 64 + j * 16 + fr;
+                            k0 + wn * 16 * WJ + j * 16 + fr;
           if (a.direct_bf16)
             static_cast<uint16_t*>(a.direct)[o] = f32_to_bf16(acc[i][j][r]);
           else
@@ -202,11 +209,11 @@ __global__ void __launch_bounds__(128 * WM, WM == 2 ? 3 : 2) wgrad_kernel(Args a
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
+    for (int j = 0; j < WJ; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int n = n0 + wm * 64 + i * 16 + fq * 4 + r;
-        const int k = k0 + wn * 64 + j * 16 + fr;
+        const int k = k0 + wn * 16 * WJ + j * 16 + fr;
         w[static_cast<int64_t>(n) * a.K + k] = acc[i][j][r];
       }
   if (do_bias && fr == 0) {   // every D column holds the same sum; lanes 0/16/32/48 write
@@ -267,13 +274,16 @@ DLBB_API void dlbb_gemm_wgrad_set_stages(int nb) { g_wgrad_stages = nb >= 2 && n
 // bn = 128 (128 x 128 tiles) or 256 (256 x 128 tiles). ws: fp32 workspace of
 // split * (N * K + N) floats. out: bf16 (dt_out 1) or fp32 (0), dense [N][K]. out_bias
 // (optional, same dtype as out, N elements): fused db = column sums of A.
-DLBB_API int dlbb_gemm_wgrad_tile(const void* A, int64_t lda, const void* B, int64_t ldb,
-                                  void* out, int dt_out, int accumulate, float* ws, int M, int N,
-                                  int K, int split, void* out_bias, int bn, hipStream_t stream) {
+// bk: output columns (K) per tile, 128 or 256 (the latter with bn = 128 only: 64 x 128 per wave).
+DLBB_API int dlbb_gemm_wgrad_tile2(const void* A, int64_t lda, const void* B, int64_t ldb,
+                                   void* out, int dt_out, int accumulate, float* ws, int M, int N,
+                                   int K, int split, void* out_bias, int bn, int bk,
+                                   hipStream_t stream) {
   using namespace dlbb::tn;
   if (M <= 0 || N <= 0 || K <= 0) return hipSuccess;
   if (bn != 128 && bn != 256) return hipErrorInvalidValue;
-  if (M % BM || N % bn || K % BKO || lda % 8 || ldb % 8 || split < 1) return hipErrorInvalidValue;
+  if (bk != 128 && !(bk == 256 && bn == 128)) return hipErrorInvalidValue;
+  if (M % BM || N % bn || K % bk || lda % 8 || ldb % 8 || split < 1) return hipErrorInvalidValue;
   if ((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(B) |
        reinterpret_cast<uintptr_t>(ws)) & 15)
     return hipErrorInvalidValue;
@@ -285,19 +295,21 @@ DLBB_API int dlbb_gemm_wgrad_tile(const void* A, int64_t lda, const void* B, int
   if (!direct && !ws) return hipErrorInvalidValue;
   Args a{static_cast<const uint16_t*>(A), static_cast<const uint16_t*>(B), ws, lda, ldb, M, N, K,
          per, split, direct ? out : nullptr, dt_out == DT_BF16 ? 1 : 0};
-  const dim3 grid((N / bn) * (K / BKO) * split);
+  const dim3 grid((N / bn) * (K / bk) * split);
   const int stages = g_wgrad_stages;
-#define WG_LAUNCH(BIASV, NBV, WMV)                                                          \
-  hipLaunchKernelGGL((wgrad_kernel<BIASV, NBV, WMV>), grid, dim3(128 * (WMV)),             \
-                     NBV * ((WMV) / 2 + 1) * kTile, stream, a)
-#define WG_STAGES(BIASV, WMV)                \
-  if (stages == 4) WG_LAUNCH(BIASV, 4, WMV); \
-  else if (stages == 3) WG_LAUNCH(BIASV, 3, WMV); \
-  else WG_LAUNCH(BIASV, 2, WMV)
-  if (bn == 256) {
-    if (out_bias) { WG_STAGES(true, 4); } else { WG_STAGES(false, 4); }
+#define WG_LAUNCH(BIASV, NBV, WMV, WJV)                                                     \
+  hipLaunchKernelGGL((wgrad_kernel<BIASV, NBV, WMV, WJV>), grid, dim3(128 * (WMV)),        \
+                     NBV * ((WMV) / 2 + (WJV) / 4) * kTile, stream, a)
+#define WG_STAGES(BIASV, WMV, WJV)                \
+  if (stages == 4) WG_LAUNCH(BIASV, 4, WMV, WJV); \
+  else if (stages == 3) WG_LAUNCH(BIASV, 3, WMV, WJV); \
+  else WG_LAUNCH(BIASV, 2, WMV, WJV)
+  if (bk == 256) {
+    if (out_bias) { WG_STAGES(true, 2, 8); } else { WG_STAGES(false, 2, 8); }
+  } else if (bn == 256) {
+    if (out_bias) { WG_STAGES(true, 4, 4); } else { WG_STAGES(false, 4, 4); }
   } else {
-    if (out_bias) { WG_STAGES(true, 2); } else { WG_STAGES(false, 2); }
+    if (out_bias) { WG_STAGES(true, 2, 4); } else { WG_STAGES(false, 2, 4); }
   }
 #undef WG_STAGES
 #undef WG_LAUNCH
@@ -312,6 +324,13 @@ DLBB_API int dlbb_gemm_wgrad_tile(const void* A, int64_t lda, const void* B, int
     hipLaunchKernelGGL(split_reduce_kernel<DT_F32>, dim3(g), dim3(256), 0, stream, ws, out, n,
                        out_bias, nb, split, accumulate);
   return hipGetLastError();
+}
+
+DLBB_API int dlbb_gemm_wgrad_tile(const void* A, int64_t lda, const void* B, int64_t ldb,
+                                  void* out, int dt_out, int accumulate, float* ws, int M, int N,
+                                  int K, int split, void* out_bias, int bn, hipStream_t stream) {
+  return dlbb_gemm_wgrad_tile2(A, lda, B, ldb, out, dt_out, accumulate, ws, M, N, K, split,
+                               out_bias, bn, 128, stream);
 }
 
 // out (bf16, or fp32 when dt_f32) = sum over `split` fp32 slices of n elements (n % 8 == 0);

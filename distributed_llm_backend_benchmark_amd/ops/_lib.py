@@ -91,6 +91,9 @@ _SIGS = {
     "dlbb_gemm_wgrad_tile": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int,
                                      c_int, c_void_p, c_int, c_int, c_int, c_int, c_void_p,
                                      c_int, c_void_p]),
+    "dlbb_gemm_wgrad_tile2": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int,
+                                     c_int, c_void_p, c_int, c_int, c_int, c_int, c_void_p,
+                                     c_int, c_int, c_void_p]),
     "dlbb_embedding_fwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int, c_int,
                                    c_int64, c_void_p]),
     "dlbb_embedding_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int,

@@ -64,6 +64,26 @@ def _log_tune(kind, key, times, best) -> None:
         print(f"[tune] {kind} {key} {times} -> {best}", file=sys.stderr, flush=True)
 
 
+def _time_interleaved(cands: dict, rounds: int = 4, reps: int = 3) -> dict:
+    """Per candidate ``name -> fn()``: ms per call, the best of ``rounds`` interleaved rounds of
+    ``reps`` back-to-back calls (one warm-up call before each). Candidates alternate within every
+    round, so clock / thermal drift during the tuning hits them alike; a single-call median per
+    candidate in sequence flipped near-ties between boxes (TP 7B shard-2 FFN-up: 0.208 vs 0.218
+    ms on one box, 0.222 vs 0.222 on the next)."""
+    best = {n: float("inf") for n in cands}
+    for _ in range(rounds):
+        for name, fn in cands.items():
+            fn()
+            s0, e0 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s0.record()
+            for _ in range(reps):
+                fn()
+            e0.record()
+            e0.synchronize()
+            best[name] = min(best[name], s0.elapsed_time(e0) / reps)
+    return best
+
+
 def set_tile(tile: int) -> None:
     """Force the 128^2 or 256^2 MFMA kernel (0 = size heuristic); for A/B benchmarking."""
     _lib.lib().dlbb_gemm_set_tile(int(tile))
@@ -211,20 +231,8 @@ def _autotune(key, args) -> str:
         return CHOICES[key]
     if torch.cuda.is_current_stream_capturing():
         return "mfma"
-    times = {}
     impls = {"mfma": _IMPLS["mfma"]} if key[-1] == "concurrent" else _IMPLS
-    for name, fn in impls.items():
-        for _ in range(2):
-            fn(*args)
-        ts = []
-        for _ in range(5):
-            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            s.record()
-            fn(*args)
-            e.record()
-            e.synchronize()
-            ts.append(s.elapsed_time(e))
-        times[name] = sorted(ts)[len(ts) // 2]
+    times = _time_interleaved({n: (lambda f=f: f(*args)) for n, f in impls.items()})
     best, times = _choose(times)
     CHOICES[key] = best
     _log_tune("linear", key, times, best)
@@ -290,32 +298,40 @@ def wgrad_supported(dy2: torch.Tensor, x2: torch.Tensor) -> bool:
             and dy2.data_ptr() % 16 == 0 and x2.data_ptr() % 16 == 0)
 
 
-def _wgrad_hip(dy2, x2, out, accumulate, split=None, bias_out=None, bn=128):
+def _wgrad_hip(dy2, x2, out, accumulate, split=None, bias_out=None, bn=128, bk=128):
     M, N = dy2.shape
     K = x2.shape[1]
-    tiles = (N // bn) * (K // 128)
+    tiles = (N // bn) * (K // bk)
     if split is None:
         # about one resident wave of workgroups (3 per CU x 256 CUs for 128 x 128 tiles, 2 per
-        # CU for 256 x 128): measured best with the XCD-aware tile order
+        # CU for 256 x 128 and 128 x 256): measured best with the XCD-aware tile order
         # (profiles/r01_gpt2/wgrad_split_xcd.jsonl)
-        # (256 x 128 tiles: at most the 512 resident slots — a 2nd partial round costs a
+        # (two-per-CU tiles: at most the 512 resident slots — a 2nd partial round costs a
         # whole workgroup time)
-        split = max(1, min(M // 256, (-(-768 // tiles)) if bn == 128 else 512 // tiles))
+        split = max(1, min(M // 256, (-(-768 // tiles)) if bn == bk == 128
+                           else max(1, 512 // tiles)))
     # one split, plain store, no bias: the kernel stores dW itself (no fp32 partials, no
     # reduce pass — the LM-head dW)
     direct = split == 1 and not accumulate and bias_out is None
     ws = None if direct else torch.empty(split * (N * K + N), dtype=torch.float32,
                                          device=dy2.device)
-    check(_lib.lib().dlbb_gemm_wgrad_tile(dy2.data_ptr(), dy2.stride(0), x2.data_ptr(),
-                                          x2.stride(0), out.data_ptr(), _lib.dt(out),
-                                          int(accumulate), _lib.ptr(ws), M, N, K, split,
-                                          _lib.ptr(bias_out), int(bn), _lib.stream(dy2.device)),
+    check(_lib.lib().dlbb_gemm_wgrad_tile2(dy2.data_ptr(), dy2.stride(0), x2.data_ptr(),
+                                           x2.stride(0), out.data_ptr(), _lib.dt(out),
+                                           int(accumulate), _lib.ptr(ws), M, N, K, split,
+                                           _lib.ptr(bias_out), int(bn), int(bk),
+                                           _lib.stream(dy2.device)),
           "gemm_wgrad")
 
 
 def _wgrad_hip256(dy2, x2, out, accumulate, split=None, bias_out=None):
     """256 x 128 output tiles (8 waves): 1.33x the MFMA work per L2 byte of the 128^2 tile."""
     _wgrad_hip(dy2, x2, out, accumulate, split, bias_out, bn=256)
+
+
+def _wgrad_hip_wide(dy2, x2, out, accumulate, split=None, bias_out=None):
+    """128 x 256 output tiles, 4 waves of 64 x 128: 25 % fewer LDS fragment bytes per MFMA than
+    the 64 x 64-per-wave tiles (the GPT-2 dW shapes are LDS-bound there); needs K % 256."""
+    _wgrad_hip(dy2, x2, out, accumulate, split, bias_out, bn=128, bk=256)
 
 
 def wgrad_pp_supported(dy2, x2, out, accumulate, bias_out=None) -> bool:
@@ -398,8 +414,8 @@ def _wgrad_blas(dy2, x2, out, accumulate, split=None, bias_out=None):
 
 
 WGRAD_CHOICES = {}    # (M, N, K, out dtype, fused bias) -> "mfma" | "mfma256" | "pp" | "blas"
-_WGRAD_IMPLS = {"mfma": _wgrad_hip, "mfma256": _wgrad_hip256, "pp": _wgrad_pp,
-                "blas": _wgrad_blas}
+_WGRAD_IMPLS = {"mfma": _wgrad_hip, "mfma256": _wgrad_hip256, "mfma_wide": _wgrad_hip_wide,
+                "pp": _wgrad_pp, "blas": _wgrad_blas}
 
 
 def _wgrad_choice(dy2, x2, out, bias_out=None) -> str:
@@ -407,7 +423,10 @@ def _wgrad_choice(dy2, x2, out, bias_out=None) -> str:
     if mode in _WGRAD_IMPLS:
         if mode == "pp" and not wgrad_pp_supported(dy2, x2, out, False, bias_out):
             return "mfma"
-        return "mfma" if mode == "mfma256" and dy2.shape[1] % 256 else mode
+        if (mode == "mfma256" and dy2.shape[1] % 256) or (mode == "mfma_wide" and
+                                                           x2.shape[1] % 256):
+            return "mfma"
+        return mode
     key = (dy2.shape[0], dy2.shape[1], x2.shape[1], out.dtype, bias_out is not None)
     if key in WGRAD_CHOICES:
         return WGRAD_CHOICES[key]
@@ -415,23 +434,16 @@ def _wgrad_choice(dy2, x2, out, bias_out=None) -> str:
         return "mfma"
     scratch = torch.empty_like(out)
     scratch_b = torch.empty_like(bias_out) if bias_out is not None else None
-    times = {}
+    cands = {}
     for name, fn in _WGRAD_IMPLS.items():
         if name == "mfma256" and (dy2.shape[1] % 256 or os.environ.get("DLBB_WGRAD256") == "0"):
             continue
+        if name == "mfma_wide" and x2.shape[1] % 256:
+            continue
         if name == "pp" and not wgrad_pp_supported(dy2, x2, out, False, bias_out):
             continue
-        for _ in range(2):
-            fn(dy2, x2, scratch, False, None, scratch_b)
-        ts = []
-        for _ in range(5):
-            s0, e0 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            s0.record()
-            fn(dy2, x2, scratch, False, None, scratch_b)
-            e0.record()
-            e0.synchronize()
-            ts.append(s0.elapsed_time(e0))
-        times[name] = sorted(ts)[len(ts) // 2]
+        cands[name] = lambda f=fn: f(dy2, x2, scratch, False, None, scratch_b)
+    times = _time_interleaved(cands)
     best, times = _choose(times)
     WGRAD_CHOICES[key] = best
     _log_tune("wgrad", key, times, best)
@@ -540,20 +552,9 @@ def _dgrad_choice(dy2, w, out, dgelu=None) -> str:
         return DGRAD_CHOICES[key]
     if torch.cuda.is_current_stream_capturing():
         return "mfma"
-    times = {}
     scratch = torch.empty_like(out)
-    for name, fn in _DGRAD_IMPLS.items():
-        for _ in range(2):
-            fn(dy2, w, scratch, dgelu=dgelu)
-        ts = []
-        for _ in range(5):
-            s0, e0 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            s0.record()
-            fn(dy2, w, scratch, dgelu=dgelu)
-            e0.record()
-            e0.synchronize()
-            ts.append(s0.elapsed_time(e0))
-        times[name] = sorted(ts)[len(ts) // 2]
+    times = _time_interleaved({n: (lambda f=f: f(dy2, w, scratch, dgelu=dgelu))
+                               for n, f in _DGRAD_IMPLS.items()})
     best, times = _choose(times)
     DGRAD_CHOICES[key] = best
     _log_tune("dgrad", key, times, best)
@@ -608,7 +609,7 @@ def dgrad(dy2: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None
 def kernel_mix() -> dict:
     """Which implementation each autotuned GEMM shape runs, for result JSONs (the
     kernel choice must be visible next to the throughput it produced). Per kind: shape count by
-    choice plus every shape's measured median ms per candidate."""
+    choice plus every shape's measured ms per candidate (best of interleaved rounds)."""
     out = {}
     ours = total = 0.0
     for kind, table in (("linear", CHOICES), ("wgrad", WGRAD_CHOICES), ("dgrad", DGRAD_CHOICES)):

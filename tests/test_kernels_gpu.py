@@ -275,6 +275,32 @@ def test_wgrad_pingpong_tn_split_k(T, N, K, r0, split):
     assert bool((out[:r0] == 7.0).all())
 
 
+@pytest.mark.parametrize("T,N,K,split", [(16384, 3072, 768, None), (16384, 768, 3072, None),
+                                         (16384, 768, 768, None), (2048, 256, 512, 3),
+                                         (1024, 128, 256, 1)])
+def test_wgrad_wide_matches_fp32(T, N, K, split):
+    """128 x 256 weight-gradient tiles (4 waves of 64 x 128): dW and the fused bias gradient
+    against fp32; split-K reduce, one split with a direct store, accumulate into bf16 and fp32."""
+    from distributed_llm_backend_benchmark_amd.ops import gemm
+
+    dy = _randn(T, N, seed=51, scale=0.5)
+    x = _randn(T, K, seed=52, scale=0.5)
+    ref = dy.float().t() @ x.float()
+    rb = dy.float().sum(0)
+    out = torch.full((N, K), float("nan"), dtype=torch.bfloat16, device=DEV)
+    db = torch.full((N,), float("nan"), dtype=torch.bfloat16, device=DEV)
+    gemm._wgrad_hip_wide(dy, x, out, False, split, db)
+    tol = 2e-2 * (T ** 0.5)
+    torch.testing.assert_close(out.float(), ref, rtol=2e-2, atol=tol)
+    torch.testing.assert_close(db.float(), rb, rtol=2e-2, atol=tol)
+    plain = torch.full((N, K), float("nan"), dtype=torch.bfloat16, device=DEV)
+    gemm._wgrad_hip_wide(dy, x, plain, False, split)          # no bias (direct store at split 1)
+    torch.testing.assert_close(plain.float(), ref, rtol=2e-2, atol=tol)
+    o32 = torch.ones(N, K, dtype=torch.float32, device=DEV)
+    gemm._wgrad_hip_wide(dy, x, o32, True, split)
+    torch.testing.assert_close(o32, ref + 1, rtol=1e-2, atol=1e-2 * (T ** 0.5))
+
+
 def test_wgrad_pingpong_tn_tail_plan_lmhead_scale():
     """Whole rounds + split-K tail (grid 300 tiles on the device's CUs): matches fp32, and the
     plan splits it."""

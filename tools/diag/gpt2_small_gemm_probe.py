@@ -49,6 +49,11 @@ def main():
         if N % 256 == 0:
             rec["wgrad256x128_bias_us"] = t_best(lambda: G._wgrad_hip256(dy, x, out, False, None,
                                                                          db))
+        rec["wgrad_wide_bias_us"] = t_best(lambda: G._wgrad_hip_wide(dy, x, out, False, None,
+                                                                     db))
+        for sw in (1, 2, 4, 8):
+            rec[f"wgrad_wide_bias_s{sw}_us"] = t_best(
+                lambda: G._wgrad_hip_wide(dy, x, out, False, sw, db))
         ref = (dy.float().t() @ x.float())
         pp = {}
         for s in (2, 3, 4, 6, 7, 8, 9, 12, 16, 28):
