@@ -70,6 +70,21 @@ def _time_interleaved(cands: dict, rounds: int = 4, reps: int = 3) -> dict:
     round, so clock / thermal drift during the tuning hits them alike; a single-call median per
     candidate in sequence flipped near-ties between boxes (TP 7B shard-2 FFN-up: 0.208 vs 0.218
     ms on one box, 0.222 vs 0.222 on the next)."""
+    if os.environ.get("DLBB_TUNE_TIMING") == "single":   # A/B: the round-1..3 method
+        out = {}
+        for name, fn in cands.items():
+            for _ in range(2):
+                fn()
+            ts = []
+            for _ in range(5):
+                s0, e0 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                s0.record()
+                fn()
+                e0.record()
+                e0.synchronize()
+                ts.append(s0.elapsed_time(e0))
+            out[name] = sorted(ts)[len(ts) // 2]
+        return out
     best = {n: float("inf") for n in cands}
     for _ in range(rounds):
         for name, fn in cands.items():

@@ -44,9 +44,13 @@ from .comm import Comm
 from .streams import concurrent_stream
 
 _GRAD_SINKS = os.environ.get("DLBB_GRAD_SINKS", "1") != "0"   # A/B switch for the sinks
-# opt-in: sink dW GEMMs on a side stream. Measured +4 % step time on GPT-2 (the concurrent
-# GEMMs take CUs from the critical-path dgrad chain), so off by default
-_WGRAD_STREAM = os.environ.get("DLBB_WGRAD_STREAM", "0") == "1"
+# sink dW GEMMs on a side stream (default on; DLBB_WGRAD_STREAM=0 for the A/B). Rounds 1-2
+# measured +4 % step time on GPT-2 with a pool stream; since the side streams are chosen by the
+# concurrency probe (parallel/streams.py: a pool stream could share the compute stream's
+# hardware queue) the weight gradients fill the CUs the 192-tile dgrad grids leave idle: 19.30 ->
+# 18.90 ms, and 19.17 -> 18.58 ms with the interleaved autotune timing
+# (profiles/r03_lean/tune_ab)
+_WGRAD_STREAM = os.environ.get("DLBB_WGRAD_STREAM", "1") == "1"
 # priority of the dedicated bucket-reduction stream: 0 = normal (default, measured), -1 = high
 # (A/B knob; see the module docstring and profiles/r02_overlap/SUMMARY.md)
 _COMM_PRIORITY = int(os.environ.get("DLBB_COMM_STREAM_PRIORITY", "0"))
