@@ -61,25 +61,36 @@ def runs_concurrently(a, b, device=None, ns: int = _PROBE_NS) -> bool:
 def concurrent_stream(device, role: str, priority: int = 0,
                       ref: Optional["torch.cuda.Stream"] = None) -> "torch.cuda.Stream":
     """A stream for ``role`` on ``device`` verified to run beside ``ref`` (default: the current
-    stream) and beside every side stream already handed out on that device. Falls back, with a
-    warning, to the last candidate if none of ``_TRIES`` pool streams qualifies."""
+    stream) and beside every side stream already handed out on that device. With more side
+    roles than free hardware queues no candidate can satisfy both; it then settles for a stream
+    that still runs beside ``ref`` (sharing a queue with another side role: those two roles
+    serialise with each other, never with the compute stream), with a warning; only if none of
+    ``_TRIES`` pool streams runs beside ``ref`` does it return a serialising one."""
     dev = torch.device(device)
     key = (dev.index if dev.index is not None else torch.cuda.current_device(), role, int(priority))
     if key in _CACHE:
         return _CACHE[key]
     ref = ref or torch.cuda.current_stream(dev)
     others = [s for k, s in _CACHE.items() if k[0] == key[0]]
-    cand = None
+    cand, beside_ref = None, None
     for _ in range(_TRIES):
         cand = torch.cuda.Stream(dev, priority=priority)
         if cand == ref or any(cand == o for o in others):
             continue
-        if runs_concurrently(ref, cand, dev) and all(runs_concurrently(o, cand, dev)
-                                                     for o in others):
-            break
+        if runs_concurrently(ref, cand, dev):
+            if all(runs_concurrently(o, cand, dev) for o in others):
+                break
+            beside_ref = beside_ref or cand
     else:
-        warnings.warn(f"no pool stream ran concurrently with the compute stream for {role!r}; "
-                      "overlap on this device will serialise", RuntimeWarning, stacklevel=2)
+        if beside_ref is not None:
+            warnings.warn(f"side stream for {role!r} shares a hardware queue with another side "
+                          "role (more side roles than free queues); it still overlaps the "
+                          "compute stream", RuntimeWarning, stacklevel=2)
+            cand = beside_ref
+        else:
+            warnings.warn(f"no pool stream ran concurrently with the compute stream for "
+                          f"{role!r}; overlap on this device will serialise", RuntimeWarning,
+                          stacklevel=2)
     _CACHE[key] = cand
     return cand
 

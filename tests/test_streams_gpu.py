@@ -11,6 +11,9 @@ def test_concurrent_stream_overlaps_compute_and_is_cached():
 
     dev = torch.device("cuda", 0)
     cur = torch.cuda.current_stream(dev)
+    # side streams handed out by earlier tests in this process (DDP weight-gradient / comm,
+    # TP comm, ...) may hold every free hardware queue: start from a clean table
+    streams.reset()
     a = streams.concurrent_stream(dev, "test_a")
     b = streams.concurrent_stream(dev, "test_b")
     assert a != cur and b != cur and a != b
@@ -27,3 +30,21 @@ def test_same_stream_is_not_concurrent():
 
     cur = torch.cuda.current_stream()
     assert not streams.runs_concurrently(cur, cur)
+
+
+def test_crowded_device_falls_back_beside_the_compute_stream():
+    """More side roles than free hardware queues: later roles share a queue with another side
+    role but still overlap the compute stream (never the serialising fallback)."""
+    import warnings
+
+    from distributed_llm_backend_benchmark_amd.parallel import streams
+
+    dev = torch.device("cuda", 0)
+    cur = torch.cuda.current_stream(dev)
+    streams.reset()
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore", RuntimeWarning)
+        side = [streams.concurrent_stream(dev, f"crowd_{i}") for i in range(6)]
+    for s in side:
+        assert streams.runs_concurrently(cur, s, dev)
+    streams.reset()

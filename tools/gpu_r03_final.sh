@@ -28,5 +28,5 @@ step gpt2 600 python -m distributed_llm_backend_benchmark_amd.cli.train_ddp --st
 cd /tmp && export TMPDIR=/tmp PYTHONPATH=$R
 step prof_tp7b 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/final/prof_tp7b" -o tp7b -- python3 -m distributed_llm_backend_benchmark_amd.cli.run_tp --config "$R/config/7b_config.yaml" --backend rccl --output-dir "$R/gpurun_out/final/tp_prof"
 step prof_gpt2 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/final/prof_gpt2" -o gpt2 -- python3 -m distributed_llm_backend_benchmark_amd.cli.train_ddp --steps 5 --warmup 2
-step asan_probe 200 bash -c "cd $R && ASAN_OPTIONS=detect_leaks=1:verify_asan_link_order=0 LSAN_OPTIONS=suppressions=$R/tests/native/lsan.supp timeout -k 5 150 build/asan/host_checks"
+[ -x build/asan/host_checks ] && step asan_probe 200 bash -c "cd $R && ASAN_OPTIONS=detect_leaks=1:verify_asan_link_order=0 LSAN_OPTIONS=suppressions=$R/tests/native/lsan.supp timeout -k 5 150 build/asan/host_checks" || echo "asan probe skipped (build/asan is gpurun-ignored; run tools/build_host_asan.py and un-ignore to include it)"
 echo done
