@@ -89,6 +89,11 @@ def run(args, comm, overlap: bool):
 
     cfg = GPT2Config(vocab_size=args.vocab, block_size=args.seq, n_layer=args.n_layer,
                      n_head=args.n_head, n_embd=args.n_embd)
+    if comm.device.type == "cuda" and not os.environ.get("DLBB_TUNE_TIMING"):
+        # a GPU-bound training step: autotune on back-to-back timings (ops.gemm.set_tune_timing)
+        from ..ops import gemm as _g
+
+        _g.set_tune_timing("interleaved")
     model = GPT2(cfg, device=comm.device)
     if args.zero:
         from ..parallel.zero import ShardedTrainer

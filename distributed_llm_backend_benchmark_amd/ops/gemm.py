@@ -64,13 +64,29 @@ def _log_tune(kind, key, times, best) -> None:
         print(f"[tune] {kind} {key} {times} -> {best}", file=sys.stderr, flush=True)
 
 
+_TUNE_TIMING = [None]    # None: DLBB_TUNE_TIMING or "single"; set_tune_timing overrides
+
+
+def set_tune_timing(mode: str) -> None:
+    """How the autotuners time candidates. ``"single"`` (default): median of single calls, each
+    bracketed by events — the implementation's host issue cost is inside the span, which is what
+    an eager, partly host-bound forward pays (TP 7B shard-4 forward: 12.7-13.1 ms with these
+    choices vs 14.7 ms with the interleaved ones, which picked hipBLASLt everywhere).
+    ``"interleaved"``: best of interleaved rounds of 3 back-to-back calls — host issue hidden
+    behind the previous call, as in a GPU-bound training step (GPT-2 step 18.96 / 18.84 ->
+    18.52 / 18.64 ms; ``cli.train_ddp`` selects it). ``profiles/r03_lean/tune_ab``."""
+    if mode not in ("single", "interleaved"):
+        raise ValueError(mode)
+    _TUNE_TIMING[0] = mode
+
+
 def _time_interleaved(cands: dict, rounds: int = 4, reps: int = 3) -> dict:
-    """Per candidate ``name -> fn()``: ms per call, the best of ``rounds`` interleaved rounds of
-    ``reps`` back-to-back calls (one warm-up call before each). Candidates alternate within every
-    round, so clock / thermal drift during the tuning hits them alike; a single-call median per
-    candidate in sequence flipped near-ties between boxes (TP 7B shard-2 FFN-up: 0.208 vs 0.218
-    ms on one box, 0.222 vs 0.222 on the next)."""
-    if os.environ.get("DLBB_TUNE_TIMING") == "single":   # A/B: the round-1..3 method
+    """Per candidate ``name -> fn()``: ms per call under the selected timing (set_tune_timing).
+    Interleaved: the best of ``rounds`` rounds of ``reps`` back-to-back calls (one warm-up call
+    before each), candidates alternating within every round so clock / thermal drift hits them
+    alike. Single: 2 warm-up calls, then the median of 5 event-bracketed single calls."""
+    mode = _TUNE_TIMING[0] or os.environ.get("DLBB_TUNE_TIMING", "single")
+    if mode == "single":
         out = {}
         for name, fn in cands.items():
             for _ in range(2):
