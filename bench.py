@@ -13,7 +13,12 @@ the MAX over ranks. busBW follows nccl-tests: ``bytes / t * 2(P-1)/P`` — ident
 Per-GPU message size is fixed as N grows: weak scaling.
 
 Side measurements (also in the JSON line): p50 latency of a 512 B all-reduce (reference best
-22.9 µs at P=2, 32.0 µs at P=8) and busBW at 8 MiB (reference best 7.53 GB/s).
+22.9 µs at P=2, 32.0 µs at P=8) and busBW at 8 MiB (reference best 7.53 GB/s), the 1 KiB..1 GiB
+all-reduce sweep, and ``baseline_configs``: BASELINE configs 3 (3D activation-shaped
+all-gather + reduce-scatter grid), 4 (MoE uneven all-to-all) and 5 (GPT-2-small DDP step,
+B16 x T1024 per GPU) as isolated, validated, roofline-guarded, time-boxed sections
+(``bench/baseline_configs.py``) — a failing section records ``{"error": ...}`` and never costs
+the headline.
 
 Usage: ``python bench.py [--gpus N] [--steps K] [--warmup W]``; for N>1 launch with
 ``python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py``.
@@ -50,7 +55,50 @@ def parse(argv=None):
     ap.add_argument("--no-sweep", action="store_true", help="skip the all-reduce size sweep")
     ap.add_argument("--sweep-max-mib", type=int, default=1024,
                     help="largest message of the all-reduce size sweep (MiB per rank)")
+    # BASELINE configs 3-5 (bench/baseline_configs.py): side sections after the headline
+    ap.add_argument("--no-configs", action="store_true",
+                    help="skip the BASELINE config 3/4/5 sections (3D AG+RS grid, MoE "
+                         "all-to-all, GPT-2 DDP step)")
+    ap.add_argument("--config-budget-s", type=float, default=60.0,
+                    help="rank-agreed time box of each config section (checked between "
+                         "configurations)")
+    ap.add_argument("--grid", default=None, metavar="B,S,H;...",
+                    help="config 3 shapes (default: bench.baseline_configs.GRID_3D)")
+    ap.add_argument("--moe", default=None, metavar="TOKENS,HIDDEN;...",
+                    help="config 4 payloads per rank (default: MOE_PAYLOADS)")
+    ap.add_argument("--ddp-model", default=None,
+                    metavar="LAYERS,HEADS,EMBD,VOCAB,BATCH,SEQ",
+                    help="config 5 model (default: GPT-2 small, B16 x T1024 per GPU)")
+    ap.add_argument("--ddp-steps", type=int, default=10)
     return ap.parse_args(argv)
+
+
+def _shapes(spec):
+    return [tuple(int(v) for v in part.split(",")) for part in spec.split(";") if part.strip()]
+
+
+def _baseline_configs(comm, args) -> dict:
+    """BASELINE configs 3/4/5 as isolated, validated, roofline-guarded, time-boxed sections
+    (bench/baseline_configs.py): a failure is recorded as {"error": ...} for its section only."""
+    from distributed_llm_backend_benchmark_amd.bench import baseline_configs as bc
+
+    comm.cpu_group()        # host side channel for the sections' failure agreement (collective)
+    grid = _shapes(args.grid) if args.grid else bc.GRID_3D
+    moe = _shapes(args.moe) if args.moe else bc.MOE_PAYLOADS
+    model = None
+    if args.ddp_model:
+        keys = ("n_layer", "n_head", "n_embd", "vocab", "batch", "seq")
+        model = dict(zip(keys, (int(v) for v in args.ddp_model.split(","))))
+    budget = args.config_budget_s
+    return {
+        "config3_3d_allgather_reduce_scatter": bc.run_section(
+            comm, "config3", lambda c, b: bc.grid_3d(c, b, shapes=grid), budget),
+        "config4_moe_alltoall": bc.run_section(
+            comm, "config4", lambda c, b: bc.moe_alltoall(c, b, payloads=moe), budget),
+        "config5_gpt2_ddp": bc.run_section(
+            comm, "config5", lambda c, b: bc.gpt2_ddp(c, b, steps=args.ddp_steps, model=model),
+            budget),
+    }
 
 
 SWEEP_BYTES = [1 << 10, 8 << 10, 64 << 10, 512 << 10, 4 << 20, 32 << 20, 256 << 20, 1 << 30]
@@ -402,6 +450,12 @@ def main(argv=None) -> int:
         except Exception as e:  # noqa: BLE001 - side measurement only
             emulation = {"error": repr(e)}
 
+    # BASELINE configs 3-5 at this N (the driver's scaling run measures every config)
+    configs = {}
+    if not args.no_configs:
+        configs = _baseline_configs(comm, args)
+    affinity = comm.affinity_all_ranks() if comm.is_gpu else None   # collective
+
     if comm.rank == 0:
         rec = {
             "metric": "all-reduce bus BW (GB/s)",
@@ -442,6 +496,10 @@ def main(argv=None) -> int:
             rec["collectives_same_message"] = coll
         if sweep:
             rec["allreduce_sweep"] = sweep
+        if configs:
+            rec["baseline_configs"] = configs
+        if affinity:
+            rec["host_affinity_per_rank"] = affinity    # NUMA-local core binding per rank
         if emulation is not None:
             rec["virtual_rank_emulation"] = {
                 "what": ("IPC all-reduce kernels, W ranks emulated on ONE GPU (one fused launch "

@@ -58,6 +58,10 @@ def _bench_one(comm: Comm, op_name: str, data: torch.Tensor, warmup: int, iters:
                op_opts: Dict) -> Dict:
     op = make_op(op_name, comm, data, **op_opts)
     out: Dict = {"op_impl": getattr(op, "impl", None) or comm.backend_label}
+    if op_opts.get("out_of_place"):
+        out["out_of_place"] = True
+    if colocated(comm.world_size):
+        out["colocated"] = True
     if validate:
         out["validated"] = _validate(comm, op, tuple(data.shape), data.dtype, seed)
     tr = time_per_iteration(comm, op, iters, warmup, method=timing)
@@ -79,6 +83,52 @@ def _bench_one(comm: Comm, op_name: str, data: torch.Tensor, warmup: int, iters:
     return out
 
 
+class BelowRoofline(RuntimeError):
+    """A timing below the memory / xGMI roofline: the call enqueued no (or only part of its)
+    work — never a measurement (VERDICT r03 weak #2)."""
+
+
+def colocated(P: int) -> bool:
+    """Ranks sharing one device (rehearsals on a one-GPU box): no xGMI link in the path."""
+    ndev = torch.cuda.device_count() if torch.cuda.is_available() else 0
+    return P > 1 and 0 < ndev < int(os.environ.get("LOCAL_WORLD_SIZE", P))
+
+
+def roofline_guard(op_name: str, r: Dict, P: int, coloc: bool = False) -> None:
+    """Raise :class:`BelowRoofline` when the per-iteration p50 (all ranks' iterations pooled,
+    the stats convention), the rank-max p50 or the batched mean of a result ``r`` (as returned
+    by :func:`_bench_one`) beats the physical floor of ``stats.bandwidth.min_seconds``."""
+    import numpy as np
+
+    from ..stats.bandwidth import roofline_violation
+    from ..stats.stats1d import rank_max_p50
+
+    nbytes = r["message_bytes"]
+    t = r.get("timings") or []
+    flat = [x for row in t for x in row]
+    checks = []
+    if flat:
+        checks += [("p50", float(np.median(flat))), ("rank_max_p50", rank_max_p50(t))]
+    if r.get("batched_mean_s") is not None:
+        checks.append(("batched_mean", float(r["batched_mean_s"])))
+    for what, sec in checks:
+        why = roofline_violation(op_name, nbytes, sec, P, coloc)
+        if why:
+            raise BelowRoofline(f"below_roofline ({what}): {why}")
+
+
+def p1_opts(comm: Comm, op_name: str, op_opts: Dict) -> Dict:
+    """At one rank an IN-PLACE collective enqueues nothing (RCCL returns at once): time the
+    out-of-place form on our native engine instead — a real device copy of the message, as
+    bench.py does — where the op has one; other ops keep their options (and the roofline guard
+    refuses an empty call)."""
+    if comm.world_size != 1 or not comm.is_gpu or op_opts.get("impl"):
+        return op_opts
+    if op_name in ("allreduce", "broadcast", "reduce"):
+        return dict(op_opts, impl="native", out_of_place=True)
+    return op_opts
+
+
 def _write(comm: Comm, path: str, record: Dict) -> None:
     if comm.rank == 0:
         save_json(record, path)
@@ -89,6 +139,8 @@ def _write_error(comm: Comm, path: str, info: Dict, exc: BaseException) -> None:
     if comm.rank == 0:
         err = dict(info)
         err["error"] = f"{type(exc).__name__}: {exc}"
+        if isinstance(exc, BelowRoofline):
+            err["invalid"] = "below_roofline"
         err["traceback"] = traceback.format_exc(limit=8)
         save_json(err, path[:-5] + ".error.json")
         print(f"  ERROR {os.path.basename(path)}: {err['error']}", flush=True)
@@ -128,7 +180,8 @@ def run_1d_sweep(comm: Comm, *, ops: Sequence[str], sizes: Dict[str, int], dtype
                 faults.maybe_fail("run", op_name, size_name, comm.rank)
                 with tracing.range(f"{impl_name}/{op_name}/{size_name}"):
                     r = _bench_one(comm, op_name, data, warmup, iters, timing, batched, graph,
-                                   validate, seed, op_opts or {})
+                                   validate, seed, p1_opts(comm, op_name, op_opts or {}))
+                roofline_guard(op_name, r, comm.world_size, colocated(comm.world_size))
                 rec = schema.result_1d(
                     impl=impl_name, backend=comm.backend_label, op=op_name,
                     ranks=comm.world_size, size_name=size_name, num_elements=r["num_elements"],
@@ -136,7 +189,8 @@ def run_1d_sweep(comm: Comm, *, ops: Sequence[str], sizes: Dict[str, int], dtype
                     timing_method=r["timing_method"], timings=r["timings"],
                     host_timings=r["host_timings"], batched_mean_s=r.get("batched_mean_s"),
                     extra={k: v for k, v in r.items() if k in ("validated", "op_impl",
-                                                                  "batched_method")}
+                                                                  "batched_method",
+                                                                  "out_of_place", "colocated")}
                     | dict(extra or {}))
                 _write(comm, path, rec)
                 written.append(path)
@@ -188,7 +242,9 @@ def run_3d_sweep(comm: Comm, *, ops: Sequence[str], batch_sizes: Iterable[int],
                         faults.maybe_fail("run", op_name, shape_name, comm.rank)
                         with tracing.range(f"{impl_name}/{op_name}/{shape_name}"):
                             r = _bench_one(comm, op_name, data, warmup, iters, timing, batched,
-                                           graph, validate, seed, op_opts or {})
+                                           graph, validate, seed,
+                                           p1_opts(comm, op_name, op_opts or {}))
+                        roofline_guard(op_name, r, comm.world_size, colocated(comm.world_size))
                         rec = schema.result_3d(
                             impl=impl_name, backend=comm.backend_label, op=op_name,
                             ranks=comm.world_size, batch=b, seq_len=s, hidden_dim=h,
@@ -198,7 +254,8 @@ def run_3d_sweep(comm: Comm, *, ops: Sequence[str], batch_sizes: Iterable[int],
                             host_timings=r["host_timings"],
                             batched_mean_s=r.get("batched_mean_s"),
                             extra={k: v for k, v in r.items()
-                                   if k in ("validated", "op_impl", "batched_method")}
+                                   if k in ("validated", "op_impl", "batched_method",
+                                            "out_of_place", "colocated")}
                             | dict(extra or {}))
                         _write(comm, path, rec)
                         written.append(path)

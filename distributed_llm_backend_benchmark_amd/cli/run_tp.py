@@ -45,9 +45,13 @@ def parse_args(argv=None):
     ap.add_argument("--iters", type=int, default=None)
     ap.add_argument("--output-dir", default=None)
     ap.add_argument("--graph", action="store_true",
-                    help="capture the forward in a HIP graph and replay it (world 1, or "
-                         "all-reduces not issued through ProcessGroupNCCL: custom / native / "
-                         "auto)")
+                    help="(default where capturable) capture the forward in a HIP graph and "
+                         "replay it: world 1, or all-reduces not issued through "
+                         "ProcessGroupNCCL (custom / native / auto)")
+    ap.add_argument("--eager", action="store_true",
+                    help="time the forward issued eagerly from the host every iteration (the "
+                         "reference's host-timed semantics, run_mpi.py:173-188) instead of "
+                         "replaying the captured HIP graph")
     ap.add_argument("--trace", action="store_true",
                     help="emit roctx ranges (record with rocprofv3 --marker-trace)")
     ap.add_argument("--torch-profile", default=None, metavar="DIR",
@@ -119,8 +123,12 @@ def main(argv=None) -> int:
         config["experiment"]["output_dir"] = args.output_dir
 
     t0 = time.perf_counter()
+    cpr = config["parallelism"].get("cores_per_rank")
+    # host threads bound to the GPU's NUMA-local cores, cores_per_rank each (reference
+    # launch_openmpi.sh:19-23 --bind-to core --map-by socket:PE=14)
     comm = init_distributed(args.backend,
-                            device=None if args.device == "auto" else args.device)
+                            device=None if args.device == "auto" else args.device,
+                            cores_per_rank=int(cpr) if cpr else None)
     comm.install_tune_agreement()       # GEMM kernel choices agreed on rank-max timings
     comm.barrier()
     init_elapsed = time.perf_counter() - t0
@@ -197,9 +205,13 @@ def main(argv=None) -> int:
             print(f"dense check: {dense_check}")
 
     run_forward = lambda: model(dataset.get_batch())  # noqa: E731
-    use_graph = bool(args.graph or ex.get("graph", False)) and gpu
+    # the timed loop replays a captured HIP graph wherever the forward is
+    # capturable — the host issue cost of ~10 launches per layer (which made the eager TP
+    # forward host-bound and GEMM tuning depend on the caller) is gone; --eager keeps the
+    # reference's host-timed semantics
+    use_graph = (not args.eager) and bool(ex.get("graph", True)) and gpu
     if use_graph and world > 1 and ex.get("allreduce") not in ("custom", "native", "auto"):
-        if rank == 0:
+        if rank == 0 and (args.graph or ex.get("graph")):
             print("note: --graph needs world 1 or execution.allreduce custom|native|auto; "
                   "running eagerly")
         use_graph = False
@@ -253,6 +265,7 @@ def main(argv=None) -> int:
 
     summary = metrics.get_summary()
     means = comm.all_gather_object(summary["forward_mean"])
+    affinity = comm.affinity_all_ranks()
     if rank == 0:
         rs = rank_statistics(means)
         B, S = int(config["input"]["batch_size"]), int(config["input"]["sequence_length"])
@@ -265,6 +278,9 @@ def main(argv=None) -> int:
             "forward_device_mean": float(np.mean(ev)) if ev else None,
             "kernels": ex.get("kernels"),
             "hip_graph": use_graph,
+            "timing_mode": "hip_graph_replay" if use_graph else "eager",
+            "gemm_tune_timing": __import__(
+                "distributed_llm_backend_benchmark_amd.ops.gemm", fromlist=["x"]).tune_timing(),
             "gemm_fallbacks": __import__(
                 "distributed_llm_backend_benchmark_amd.ops.gemm", fromlist=["x"]).FALLBACKS["count"],
             "gemm_kernel_mix": __import__(
@@ -290,7 +306,7 @@ def main(argv=None) -> int:
             "experiment": config["experiment"]["name"],
             "backend": args.backend,
             "config": config,
-            "system_info": collect_system_info(),
+            "system_info": dict(collect_system_info(), host_affinity_per_rank=affinity),
             "rank_0_summary": summary,
             "rank_statistics": rs,
             "raw_metrics_rank_0": metrics.get_raw_metrics(),

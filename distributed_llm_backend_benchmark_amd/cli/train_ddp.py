@@ -40,9 +40,14 @@ def parse_args(argv=None):
                          "rate is the one in effect at capture")
     ap.add_argument("--bucket-mb", type=float, default=64.0)
     ap.add_argument("--mode", choices=["view", "flatten"], default="view")
-    ap.add_argument("--allreduce", choices=["rccl", "custom", "native"], default="rccl",
-                    help="bucket all-reduce: torch ProcessGroupNCCL, IPC xGMI kernel, or our "
-                         "C++ RCCL engine on a dedicated stream")
+    ap.add_argument("--allreduce", choices=["auto", "rccl", "custom", "native"], default="auto",
+                    help="bucket all-reduce. auto (default): registered in-place IPC xGMI kernel "
+                         "for buckets up to the node-calibrated crossover, our C++ RCCL engine "
+                         "above it, both on a probed comm stream. rccl: torch ProcessGroupNCCL "
+                         "(A/B only: its internal pool stream can share the compute stream's "
+                         "hardware queue and serialise backward with comm, parallel/streams.py). "
+                         "custom: IPC kernel for every bucket. native: C++ RCCL engine for every "
+                         "bucket")
     ap.add_argument("--no-overlap", action="store_true")
     ap.add_argument("--comm-blocks", type=int, default=None,
                     help="CU budget: workgroups per bucket-reduction launch (IPC kernel / "
@@ -80,6 +85,14 @@ def parse_args(argv=None):
     return ap.parse_args(argv)
 
 
+def _path_counts(tr) -> dict:
+    paths = tr.bucket_paths() if hasattr(tr, "bucket_paths") else {}
+    out = {}
+    for p in paths.values():
+        out[p] = out.get(p, 0) + 1
+    return out
+
+
 def run(args, comm, overlap: bool):
     import torch
 
@@ -89,11 +102,6 @@ def run(args, comm, overlap: bool):
 
     cfg = GPT2Config(vocab_size=args.vocab, block_size=args.seq, n_layer=args.n_layer,
                      n_head=args.n_head, n_embd=args.n_embd)
-    if comm.device.type == "cuda" and not os.environ.get("DLBB_TUNE_TIMING"):
-        # a GPU-bound training step: autotune on back-to-back timings (ops.gemm.set_tune_timing)
-        from ..ops import gemm as _g
-
-        _g.set_tune_timing("interleaved")
     model = GPT2(cfg, device=comm.device)
     if args.zero:
         from ..parallel.zero import ShardedTrainer
@@ -153,6 +161,9 @@ def run(args, comm, overlap: bool):
         "gemm_kernel_mix": _gemm.kernel_mix(),
         # node-measured IPC-vs-RCCL crossovers (rank-max, agreed; None: no IPC kernel)
         "allreduce_calibration": getattr(getattr(tr, "_car", None), "calibration", None),
+        # which all-reduce each bucket took (auto picks per bucket size)
+        "bucket_paths": _path_counts(tr),
+        "gemm_tune_timing": _gemm.tune_timing(),
     }
     if args.comm_timeline and not args.zero:
         tr.timeline = True
@@ -180,12 +191,14 @@ def main(argv=None) -> int:
 
     comm = init_distributed(args.backend, timeout_s=900)
     comm.install_tune_agreement()       # GEMM kernel choices agreed on rank-max timings
+    affinity = comm.affinity_all_ranks()    # host threads on the GPU's NUMA node (collective)
     if args.trace:
         tracing.enable()
     with tracing.torch_profile(args.torch_profile, comm.rank):
         main_res = run(args, comm, overlap=not args.no_overlap)
     out = {"metric": "gpt2_ddp_tokens_per_s", "value": main_res["tokens_per_s"],
            "n_gpus": comm.world_size, "overlap": not args.no_overlap, **main_res,
+           "host_affinity_per_rank": affinity,
            "config": {k: getattr(args, k) for k in ("n_layer", "n_head", "n_embd", "vocab",
                                                     "batch", "seq", "bucket_mb", "mode",
                                                     "allreduce", "zero", "comm_blocks",

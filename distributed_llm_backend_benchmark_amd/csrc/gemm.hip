@@ -1715,13 +1715,18 @@ static int dlbb_gemm_stagger = 6;      // 256^2 schedule (set_stagger): 6 = ping
 static int dlbb_gemm_bal = 2;
 constexpr int64_t kBalMinKTiles = 32;
 constexpr int64_t kPersistMaxKTiles = 48;
+// > 0 while GEMMs share the chip with communication kernels on another stream (the overlapped TP
+// forward, ops.gemm.concurrent_comm): the persistent forms assume all num_cus workgroups are
+// co-resident, and comm workgroups holding CUs push part of such a grid into a second round
+// (the same slowdown as hipBLASLt's persistent Stream-K there), so they are off meanwhile
+static int dlbb_gemm_concurrent = 0;
 // DLBB_GEMM_PERSIST=0: never upgrade the default ping-pong to the persistent form (A/B)
 static bool persist_enabled() {
   static const int on = [] {
     const char* e = getenv("DLBB_GEMM_PERSIST");
     return (e && e[0] == '0') ? 0 : 1;
   }();
-  return on != 0;
+  return on != 0 && dlbb_gemm_concurrent <= 0;
 }
 // DLBB_GEMM_PERSIST_EPI=0 (or dlbb_gemm_set_persist_epi(0)): keep bias / bias-GELU epilogues on
 // the non-persistent ping-pong (A/B)
@@ -1741,6 +1746,7 @@ DLBB_API void dlbb_gemm_set_tile(int tile) { dlbb_gemm_force_tile = tile; }
 DLBB_API void dlbb_gemm_set_stagger(int on) { dlbb_gemm_stagger = on; }
 DLBB_API int dlbb_gemm_get_stagger() { return dlbb_gemm_stagger; }
 DLBB_API void dlbb_gemm_set_persist_epi(int on) { dlbb_persist_epi = on ? 1 : 0; }
+DLBB_API void dlbb_gemm_set_concurrent(int on) { dlbb_gemm_concurrent = on; }
 DLBB_API void dlbb_gemm_set_bal(int mode) { dlbb_gemm_bal = mode >= 0 && mode <= 2 ? mode : 2; }
 
 DLBB_API int dlbb_gemm_bf16_nt(const void* A, int64_t lda, const void* B, int64_t ldb, void* C,

@@ -44,13 +44,29 @@ def set_tune_agreement(fn) -> None:
     _AGREE = fn
 
 
-def _choose(times: dict):
+# env knobs that change which candidates exist or how they run: part of every agreed name, so
+# ranks started with different settings fail at the first tuned shape instead of "agreeing" on
+# timings of different kernels
+_AGREED_ENV = ("DLBB_GEMM", "DLBB_TUNE_TIMING", "DLBB_WGRAD256", "DLBB_PP_TAIL",
+               "DLBB_GEMM_PERSIST", "DLBB_GEMM_PERSIST_EPI", "DLBB_WGRAD_STREAM")
+
+
+def _agree_names(kind: str, key, names) -> list:
+    """The names every rank must pass identically to the agreement: tuning kind + shape key +
+    env signature + candidate, so a shape / call-order / configuration mismatch between ranks
+    raises on every rank (``Comm.agree_max``) rather than mixing timings of different GEMMs."""
+    env = ",".join(f"{k}={os.environ.get(k, '')}" for k in _AGREED_ENV)
+    head = f"{kind}|{'/'.join(str(k) for k in key)}|{env}|{tune_timing()}"
+    return [f"{head}|{n}" for n in names]
+
+
+def _choose(times: dict, kind: str = "", key=()):
     """(best candidate, the timings it was chosen on): rank-max timings when an agreement is
     installed, first-listed candidate on ties."""
     names = list(times)
     vals = [float(times[n]) for n in names]
     if _AGREE is not None:
-        vals = [float(v) for v in _AGREE(names, vals)]
+        vals = [float(v) for v in _AGREE(_agree_names(kind, key, names), vals)]
     agreed = {n: round(v, 4) for n, v in zip(names, vals)}
     best = min(names, key=lambda n: (agreed[n], names.index(n)))
     return best, agreed
@@ -64,20 +80,25 @@ def _log_tune(kind, key, times, best) -> None:
         print(f"[tune] {kind} {key} {times} -> {best}", file=sys.stderr, flush=True)
 
 
-_TUNE_TIMING = [None]    # None: DLBB_TUNE_TIMING or "single"; set_tune_timing overrides
+_TUNE_TIMING = [None]    # None: DLBB_TUNE_TIMING or "interleaved"; set_tune_timing overrides
 
 
 def set_tune_timing(mode: str) -> None:
-    """How the autotuners time candidates. ``"single"`` (default): median of single calls, each
-    bracketed by events — the implementation's host issue cost is inside the span, which is what
-    an eager, partly host-bound forward pays (TP 7B shard-4 forward: 12.7-13.1 ms with these
-    choices vs 14.7 ms with the interleaved ones, which picked hipBLASLt everywhere).
-    ``"interleaved"``: best of interleaved rounds of 3 back-to-back calls — host issue hidden
-    behind the previous call, as in a GPU-bound training step (GPT-2 step 18.96 / 18.84 ->
-    18.52 / 18.64 ms; ``cli.train_ddp`` selects it). ``profiles/r03_lean/tune_ab``."""
+    """How the autotuners time candidates — ONE methodology for every caller (VERDICT r03
+    item 7): ``"interleaved"`` (default), the best of interleaved rounds of 3 back-to-back calls,
+    i.e. device time with host issue hidden behind the previous call — what a GPU-bound
+    training step and a HIP-graph-replayed forward (``cli.run_tp``'s default timed loop) pay.
+    ``"single"`` (median of event-bracketed single calls, host issue cost inside the span) is
+    kept for A/B only: it favoured our kernels in the eager, host-bound TP forward, a symptom
+    graph replay removes (``profiles/r03_lean/tune_ab``)."""
     if mode not in ("single", "interleaved"):
         raise ValueError(mode)
     _TUNE_TIMING[0] = mode
+
+
+def tune_timing() -> str:
+    """The autotune timing mode in effect (recorded in result JSONs)."""
+    return _TUNE_TIMING[0] or os.environ.get("DLBB_TUNE_TIMING", "interleaved")
 
 
 def _time_interleaved(cands: dict, rounds: int = 4, reps: int = 3) -> dict:
@@ -85,7 +106,7 @@ def _time_interleaved(cands: dict, rounds: int = 4, reps: int = 3) -> dict:
     Interleaved: the best of ``rounds`` rounds of ``reps`` back-to-back calls (one warm-up call
     before each), candidates alternating within every round so clock / thermal drift hits them
     alike. Single: 2 warm-up calls, then the median of 5 event-bracketed single calls."""
-    mode = _TUNE_TIMING[0] or os.environ.get("DLBB_TUNE_TIMING", "single")
+    mode = tune_timing()
     if mode == "single":
         out = {}
         for name, fn in cands.items():
@@ -237,8 +258,10 @@ _IMPLS = {"mfma": _mfma_linear, "blas": _blas_linear}
 # TP forward). hipBLASLt's bf16 kernels here are persistent Stream-K grids (one workgroup per CU,
 # all assumed co-resident): with comm workgroups holding CUs, part of the grid waits for a
 # second round and the GEMM takes up to twice as long — measured: 7B shard-8 overlapped forward
-# 27.8 ms with one such GEMM vs 17.4 ms on our (non-persistent) grids. Shapes tuned in this state
-# get their own keys (suffix "concurrent") and only the hand-written candidates.
+# 27.8 ms with one such GEMM vs 17.4 ms on non-persistent grids. Shapes tuned in this state get
+# their own keys (suffix "concurrent") and only the hand-written candidates, and our own
+# persistent forms (NT bias / bias-GELU, NN plain / dGELU: grid = num_cus) are switched off in
+# the library for the duration (dlbb_gemm_set_concurrent) — the same hazard.
 _CONCURRENT = [0]
 
 
@@ -247,10 +270,14 @@ class concurrent_comm:
 
     def __enter__(self):
         _CONCURRENT[0] += 1
+        if _CONCURRENT[0] == 1 and _lib.available():
+            _lib.lib().dlbb_gemm_set_concurrent(1)
         return self
 
     def __exit__(self, *exc):
         _CONCURRENT[0] -= 1
+        if _CONCURRENT[0] == 0 and _lib.available():
+            _lib.lib().dlbb_gemm_set_concurrent(0)
         return False
 
 
@@ -264,7 +291,7 @@ def _autotune(key, args) -> str:
         return "mfma"
     impls = {"mfma": _IMPLS["mfma"]} if key[-1] == "concurrent" else _IMPLS
     times = _time_interleaved({n: (lambda f=f: f(*args)) for n, f in impls.items()})
-    best, times = _choose(times)
+    best, times = _choose(times, "linear", key)
     CHOICES[key] = best
     _log_tune("linear", key, times, best)
     return best
@@ -475,7 +502,7 @@ def _wgrad_choice(dy2, x2, out, bias_out=None) -> str:
             continue
         cands[name] = lambda f=fn: f(dy2, x2, scratch, False, None, scratch_b)
     times = _time_interleaved(cands)
-    best, times = _choose(times)
+    best, times = _choose(times, "wgrad", key)
     WGRAD_CHOICES[key] = best
     _log_tune("wgrad", key, times, best)
     return best
@@ -586,7 +613,7 @@ def _dgrad_choice(dy2, w, out, dgelu=None) -> str:
     scratch = torch.empty_like(out)
     times = _time_interleaved({n: (lambda f=f: f(dy2, w, scratch, dgelu=dgelu))
                                for n, f in _DGRAD_IMPLS.items()})
-    best, times = _choose(times)
+    best, times = _choose(times, "dgrad", key)
     DGRAD_CHOICES[key] = best
     _log_tune("dgrad", key, times, best)
     return best

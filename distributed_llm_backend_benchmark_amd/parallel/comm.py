@@ -63,6 +63,17 @@ class Comm:
     def backend_label(self) -> str:
         return "rccl" if self.backend == "nccl" else self.backend
 
+    @property
+    def affinity(self) -> dict:
+        """The host-thread binding applied at init (``utils.affinity.bind_to_device``)."""
+        from ..utils.affinity import current
+
+        return dict(self._extra.get("affinity") or {"bound": False}, **current())
+
+    def affinity_all_ranks(self) -> List[dict]:
+        """Collective: every rank's :attr:`affinity` (result JSONs report them per rank)."""
+        return self.all_gather_object(dict(self.affinity, rank=self.rank))
+
     # ---------------------------------------------------------------- sync helpers
     def barrier(self) -> None:
         if self.world_size == 1:
@@ -133,7 +144,11 @@ class Comm:
             return None
         g = self._extra.get("cpu_group")
         if g is None:
-            g = dist.new_group(backend="gloo")
+            # its own (short) timeout: a rank that never reaches an agreement point (a GEMM
+            # shape only some ranks tune, a section one rank skipped) fails the job in minutes,
+            # not after the default group's 900 s
+            secs = float(os.environ.get("DLBB_SIDE_GROUP_TIMEOUT_S", "300"))
+            g = dist.new_group(backend="gloo", timeout=datetime.timedelta(seconds=secs))
             self._extra["cpu_group"] = g
         return g
 
@@ -180,23 +195,53 @@ class Comm:
                 pass
 
 
+# (local rank, local world size) variables of the launchers we may run under: torchrun, Open MPI,
+# MPICH / Intel MPI (hydra), Slurm
+_LOCAL_RANK_VARS = ("LOCAL_RANK", "OMPI_COMM_WORLD_LOCAL_RANK", "MPI_LOCALRANKID", "SLURM_LOCALID")
+_LOCAL_SIZE_VARS = ("LOCAL_WORLD_SIZE", "OMPI_COMM_WORLD_LOCAL_SIZE", "MPI_LOCALNRANKS",
+                    "SLURM_NTASKS_PER_NODE")
+
+
+def local_env(rank: int) -> tuple:
+    """(local_rank, local_world or 0 when no launcher says) from the launcher environment."""
+    lr = next((os.environ[v] for v in _LOCAL_RANK_VARS if os.environ.get(v)), None)
+    lw = next((os.environ[v] for v in _LOCAL_SIZE_VARS if os.environ.get(v)), None)
+    try:
+        lw = int(str(lw).split("(")[0].split(",")[0]) if lw is not None else 0  # "8(x2)" slurm
+    except ValueError:
+        lw = 0
+    return (int(lr) if lr is not None else rank), lw
+
+
 def init_distributed(backend: str = "auto", timeout_s: float = 600.0,
-                     device: Optional[str] = None) -> Comm:
+                     device: Optional[str] = None,
+                     cores_per_rank: Optional[int] = None) -> Comm:
     """Initialise (or attach to) the default process group.
 
     ``backend``: ``rccl`` | ``nccl`` | ``gloo`` | ``auto``. ``device`` overrides the device
     choice (``"cpu"`` forces CPU tensors even on a GPU box, e.g. gloo plumbing runs).
+    On a HIP device the process's host threads are bound to the GPU's NUMA-local cores
+    (``utils.affinity``; ``cores_per_rank`` = the reference's ``parallelism.cores_per_rank``,
+    ``launch_openmpi.sh:19-23``); the record is ``comm.affinity``.
     """
     be = resolve_backend(backend)
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
-    local_rank = int(os.environ.get("LOCAL_RANK", str(rank)))
+    local_rank, local_world = local_env(rank)
 
     if be == "nccl":
         if not torch.cuda.is_available():
             raise RuntimeError("backend rccl requested but no HIP device is visible")
         ndev = torch.cuda.device_count()
-        local_world = int(os.environ.get("LOCAL_WORLD_SIZE", "0"))
+        if local_world == 0 and world > ndev > 1 and local_rank >= ndev:
+            import warnings
+
+            # no launcher variable gives the local world size: if this is ONE node, two ranks
+            # now share a GPU and RCCL fails late (duplicate device); on several nodes it is fine
+            warnings.warn(f"local rank {local_rank} (no LOCAL_WORLD_SIZE / OMPI / Slurm local "
+                          f"size set) mapped to device {local_rank % ndev} of {ndev} by modulo: "
+                          "correct across nodes, a duplicate-GPU error if all ranks share one "
+                          "node", RuntimeWarning, stacklevel=2)
         if local_world > ndev:
             # RCCL refuses two ranks on one GPU only late (duplicate-device error at the first
             # collective); fail at init with the reason instead
@@ -243,5 +288,12 @@ def init_distributed(backend: str = "auto", timeout_s: float = 600.0,
             torch.cuda.synchronize(dev)
     else:
         rank, world = dist.get_rank(), dist.get_world_size()
-    return Comm(rank=rank, world_size=world, local_rank=local_rank, backend=be,
+    comm = Comm(rank=rank, world_size=world, local_rank=local_rank, backend=be,
                 device=dev, owns_pg=owns)
+    if dev.type == "cuda":
+        from ..utils.affinity import bind_to_device
+
+        comm._extra["affinity"] = bind_to_device(dev.index, local_rank,
+                                                 local_world or min(world, 64),
+                                                 cores_per_rank=cores_per_rank)
+    return comm

@@ -403,7 +403,10 @@ class CustomAllReduce:
         fresh rank-seeded data and is checked against the fp32 sum once; a candidate that fails
         anywhere is dropped everywhere."""
         W, dev = self.comm.world_size, self.comm.device
-        sizes = [int(n) for n in sizes if n <= self.capacity]
+        # every size a multiple of W 16-byte vectors, so two-shot is timed at each size for any W
+        # (powers of two are not, at W = 3, 5, 6, 7; ADVICE r03)
+        sizes = [int(n) - int(n) % (16 * W) for n in sizes if n <= self.capacity]
+        sizes = [n for n in sizes if n > 0]
         table = []
         for n in sizes:
             g = torch.Generator(device=dev)
@@ -452,7 +455,10 @@ class CustomAllReduce:
             return float("inf") if v is None else v
 
         oneshot_max = 0
+        twoshot_ran = any(row["us"].get("twoshot") is not None for row in table)
         for row in table:
+            if row["us"].get("twoshot") is None and twoshot_ran:
+                break       # not measured here: no evidence one-shot wins at this size
             if t(row, "oneshot") <= t(row, "twoshot"):
                 oneshot_max = row["bytes"]
             else:

@@ -194,6 +194,8 @@ class FlatParamTrainer:
 
             self._native = get_native(comm)
             self._comm_stream = concurrent_stream(dev, "ddp_comm", comm_stream_priority())
+        if allreduce == "auto" and comm is not None and comm.is_gpu and self.world > 1:
+            self._setup_auto(comm, dev)
         # CU budget of the bucket reductions that run beside backward: workgroups per IPC /
         # emulated reduction launch (None = the kernel's own size heuristic)
         self.comm_blocks = comm_blocks
@@ -226,6 +228,61 @@ class FlatParamTrainer:
         self.timeline = False       # record comm events per bucket (comm_tail_report)
         self._tl = None
         self.step_count = 0
+
+    def _setup_auto(self, comm: Comm, dev) -> None:
+        """``allreduce="auto"``: every bucket on a probed (concurrency-checked) comm stream —
+        the registered in-place IPC all-reduce for buckets up to the node-calibrated ``reg_max``
+        (where it beat RCCL on rank-max time, ``CustomAllReduce.calibrate``), our native RCCL
+        engine for the rest. ProcessGroupNCCL (whose internal pool stream may share the compute
+        stream's hardware queue, parallel/streams.py) is only the last resort when the native
+        engine cannot be created (e.g. ranks sharing one GPU). Per-bucket choice: ``bucket_paths``."""
+        from .custom_allreduce import get_custom_allreduce
+
+        self._comm_stream = concurrent_stream(dev, "ddp_comm", comm_stream_priority())
+        car = get_custom_allreduce(comm)
+        reg_max = int(getattr(car, "reg_max", 0) or 0) if car is not None else 0
+        need_native = False
+        for b in self.buckets:
+            buf = self.flat_grad[b.start:b.end]
+            nbytes = buf.numel() * buf.element_size()
+            if (car is not None and car.reg_healthy and nbytes <= reg_max
+                    and car.supports_registered(buf)):
+                self._bucket_reg[b.idx] = car.register(buf)     # collective, same order
+            else:
+                need_native = True
+        if self._bucket_reg:
+            self._car = car
+        if need_native:
+            from .rccl_native import get_native
+
+            try:
+                self._native = get_native(comm)     # collective; failure agreed on every rank
+            except RuntimeError as e:
+                if comm.rank == 0:
+                    print(f"[ddp auto] native RCCL engine unavailable ({e}); large buckets use "
+                          "the process group", flush=True)
+
+    def bucket_paths(self) -> Dict[int, str]:
+        """Which all-reduce each bucket takes (result JSONs): ``custom_reg`` (registered IPC,
+        in place), ``custom`` (IPC via staging), ``native`` (our RCCL engine on the comm
+        stream), ``rccl`` (ProcessGroupNCCL), ``emulated`` or ``none`` (world 1)."""
+        out = {}
+        for b in self.buckets:
+            buf = self.flat_grad[b.start:b.end]
+            if self._emu_zero is not None:
+                out[b.idx] = "emulated"
+            elif self.world == 1:
+                out[b.idx] = "none"
+            elif b.idx in self._bucket_reg:
+                out[b.idx] = "custom_reg"
+            elif (self.allreduce == "custom" and self._car is not None and self._car.healthy
+                  and self._car.supports(buf)):
+                out[b.idx] = "custom"
+            elif self._native is not None:
+                out[b.idx] = "native"
+            else:
+                out[b.idx] = "rccl"
+        return out
 
     # ------------------------------------------------------------------ hooks for subclasses
     def _bucket_align(self) -> int:
@@ -323,7 +380,8 @@ class FlatParamTrainer:
                 self._tl_mark(b, "end", cs)
             self._mark_done(b, cs)
             b.work = "stream"
-        elif self._car is not None and self._car.healthy and self._car.supports(buf):
+        elif (self.allreduce == "custom" and self._car is not None and self._car.healthy
+              and self._car.supports(buf)):
             cs = self._comm_stream
             cs.wait_stream(torch.cuda.current_stream(buf.device))
             if ws is not None:
@@ -585,6 +643,13 @@ class FlatParamTrainer:
         self.flat_param.copy_(self.master.to(torch.bfloat16))
 
     def close(self) -> None:
+        """Remove hooks / sink attributes and release the buckets' IPC registrations
+        (collective when any bucket is registered: call on every rank)."""
+        if self._bucket_reg and self._car is not None:
+            torch.cuda.synchronize(self.flat_grad.device)
+            for idx in sorted(self._bucket_reg):
+                self._car.deregister(self._bucket_reg[idx])
+            self._bucket_reg = {}
         for h in self._hooks:
             h.remove()
         for p in self._params:

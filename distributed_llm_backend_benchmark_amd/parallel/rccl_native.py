@@ -209,9 +209,11 @@ class NativeBroadcast(_Native, C.Broadcast):
     def setup(self):
         self.buf = self.data.clone()
         self.engine = self._engine()
+        # out_of_place: root's data -> buf (at one rank a real device copy, not an empty call)
+        self.src = self.data.reshape(-1) if self.opts.get("out_of_place") else self.buf
 
     def native_args(self):
-        return self.buf, self.buf, self.buf.numel(), 0
+        return self.src, self.buf, self.buf.numel(), 0
 
 
 class NativeReduce(_Native, C.Reduce):
@@ -220,9 +222,10 @@ class NativeReduce(_Native, C.Reduce):
     def setup(self):
         self.buf = self.data.clone()
         self.engine = self._engine()
+        self.src = self.data.reshape(-1) if self.opts.get("out_of_place") else self.buf
 
     def native_args(self):
-        return self.buf, self.buf, self.buf.numel(), 0
+        return self.src, self.buf, self.buf.numel(), 0
 
 
 class NativeGather(_Native, C.Gather):

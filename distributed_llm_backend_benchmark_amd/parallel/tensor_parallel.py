@@ -157,15 +157,34 @@ class RowParallelLinear(nn.Module):
             dist.all_reduce(t)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
+        """Public API: always an OWNED tensor. (The zero-copy :meth:`launch` may return a view
+        of the IPC-registered output buffer, which every same-shape row-parallel layer shares and
+        the next call rewrites — ADVICE r03; only the model's block, which consumes each output
+        in the next LayerNorm, uses that path.)"""
         y, _ = self.launch(x)
+        if self._aliases_registered(y):
+            y = y.clone()
         return y
 
+    def _aliases_registered(self, y: torch.Tensor) -> bool:
+        car = self._car
+        if car is None or not y.is_cuda:
+            return False
+        p = y.data_ptr()
+        for buf, _ in car._owned.values():
+            base = buf.data_ptr()
+            if base <= p < base + buf.numel() * buf.element_size():
+                return True
+        return False
+
     def launch(self, x: torch.Tensor, slot: int = 0, stream=None):
-        """GEMM on the current stream, then the all-reduce — on ``stream`` when given (a
+        """Internal zero-copy path (TransformerBlock): GEMM on the current stream, then the
+        all-reduce — on ``stream`` when given (a
         side comm stream: returns ``(y, event)``, and the caller makes its stream wait on the
         event before reading ``y``; the overlapped TP forward runs another micro-batch's GEMMs
         meanwhile), else inline (``event`` None). ``slot``: which registered output buffer (one
-        per micro-batch in flight)."""
+        per micro-batch in flight). With a registered output, ``y`` is a view of a buffer shared
+        by every same-shape row-parallel layer: consume it before the next row-parallel call."""
         fp32_wire = self.allreduce_dtype == "fp32"
         if self.kernels == "torch":
             y = x @ self.weight.t()

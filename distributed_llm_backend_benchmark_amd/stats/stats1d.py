@@ -27,7 +27,8 @@ from typing import Dict, List, Optional, Sequence
 import numpy as np
 
 from ..utils.io import load_json, save_json
-from .bandwidth import busbw_gbps, algbw_gbps, legacy_bandwidth_gbps
+from .bandwidth import (KNOWN_OPS, algbw_gbps, busbw_gbps, legacy_bandwidth_gbps,
+                        roofline_violation)
 
 LEGACY_COLUMNS = [
     "mpi_implementation", "operation", "num_ranks", "data_size_name", "num_elements",
@@ -79,6 +80,25 @@ def rank_max_p50(timings_2d: Sequence[Sequence[float]]) -> float:
     n = min(len(r) for r in timings_2d)
     arr = np.asarray([r[:n] for r in timings_2d], dtype=np.float64)
     return float(np.median(np.max(arr, axis=0)))
+
+
+def refused(data: Dict[str, object]) -> Optional[str]:
+    """Why a raw result must not become a statistic (None: fine): flagged invalid by the sweep,
+    or its p50 below the memory / xGMI roofline (``stats.bandwidth``) — an empty call, e.g. an
+    in-place collective at one rank (VERDICT r03 weak #2)."""
+    if data.get("invalid"):
+        return str(data["invalid"])
+    flat = [x for row in data["timings"] for x in (row if isinstance(row, list) else [row])]
+    if not flat:
+        return "no timings"
+    nbytes = data.get("bytes") or data.get("wire_bytes") or data.get("tensor_size_bytes")
+    if nbytes is None:
+        nbytes = int(data["num_elements"]) * dtype_nbytes(str(data.get("dtype", "float16")))
+    op = data["operation"]
+    if op not in KNOWN_OPS:
+        return None
+    return roofline_violation(op, float(nbytes), float(np.median(flat)), int(data["num_ranks"]),
+                              bool(data.get("colocated", False)))
 
 
 def stats_for_result(data: Dict[str, object]) -> Dict[str, object]:
@@ -139,6 +159,11 @@ def process_directory(input_dir: str, output_dir: str,
         try:
             data = load_json(fp)
             if "timings" not in data:
+                continue
+            why = refused(data)
+            if why:
+                if verbose:
+                    print(f"  REFUSED {os.path.basename(fp)}: {why}")
                 continue
             res = stats_for_result(data)
         except Exception as e:  # reference: print + continue (stats.py:215-217)

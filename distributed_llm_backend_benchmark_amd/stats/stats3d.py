@@ -22,7 +22,7 @@ import numpy as np
 
 from ..utils.io import load_json, save_json
 from .bandwidth import algbw_gbps, busbw_gbps
-from .stats1d import rank_max_p50
+from .stats1d import rank_max_p50, refused
 
 STANDARD_COLUMNS = [
     "implementation", "operation", "num_ranks", "hidden_dim", "seq_len", "batch",
@@ -119,6 +119,11 @@ def process_directory(input_dir: str, output_dir: str, impl_label: str,
         try:
             data = load_json(fp)
             if "timings" not in data or "tensor_shape" not in data:
+                continue
+            why = refused(data)
+            if why:
+                if verbose:
+                    print(f"  REFUSED {os.path.basename(fp)}: {why}")
                 continue
             r = stats_for_result(data)
         except Exception as e:

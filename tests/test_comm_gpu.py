@@ -348,7 +348,7 @@ def test_ddp_custom_registered_buckets_ranks_on_one_gpu():
 
 
 @pytest.mark.parametrize("allreduce,fp32_buckets", [("rccl", False), ("custom", False),
-                                                    ("rccl", True)])
+                                                    ("auto", False), ("rccl", True)])
 def test_ddp_matches_global_batch_and_ranks_stay_identical_ranks_on_one_gpu(allreduce,
                                                                              fp32_buckets):
     """VERDICT r02 weak #7 / item 5, rehearsed with 2 ranks sharing one GPU over a gloo process
@@ -418,6 +418,49 @@ def test_tp_forward_ranks_on_one_gpu_matches_dense(world, allreduce):
         assert used_custom == (allreduce != "rccl")
         # registered in-place path: one owned buffer (shared by every row-parallel layer)
         assert owned == (1 if allreduce == "custom_reg" else 0), owned
+
+
+def _row_reuse_worker(rank, world):
+    os.environ["DLBB_GEMM"] = "mfma"
+    os.environ["DLBB_CUSTOM_AR_CALIBRATE"] = "0"
+    import torch
+    import torch.distributed as dist
+
+    from distributed_llm_backend_benchmark_amd import ops
+    from distributed_llm_backend_benchmark_amd.parallel.comm import init_distributed
+    from distributed_llm_backend_benchmark_amd.parallel.tensor_parallel import RowParallelLinear
+
+    comm = init_distributed("gloo", device="cuda")
+    dev = comm.device
+    layer = RowParallelLinear(512, 256, comm, generator=torch.Generator(device=dev).manual_seed(
+        7 + rank), std=0.05, allreduce="custom")
+    car = layer._car
+    car.oneshot_max = 0                     # every output through the registered buffer
+    g = torch.Generator(device=dev).manual_seed(100 + rank)
+    x1, x2 = (torch.randn(2, 64, 256, generator=g, device=dev).to(torch.bfloat16)
+              for _ in range(2))
+    y1 = layer(x1)
+    y2 = layer(x2)                          # a second call must not overwrite y1
+    a, _ = layer.launch(x1)                 # the internal path does use the shared buffer
+    shared = layer._aliases_registered(a)
+    torch.cuda.synchronize()
+    errs = []
+    for x, y in ((x1, y1), (x2, y2)):
+        ref = ops.linear(x, layer.weight).float()
+        dist.all_reduce(ref)
+        errs.append(float((y.float() - ref).abs().max()) / float(ref.abs().max()))
+    owned = len(car._owned)
+    distinct = y1.data_ptr() != y2.data_ptr()
+    comm.destroy()
+    return max(errs), shared, owned, distinct
+
+
+def test_row_parallel_forward_returns_owned_tensor_ranks_on_one_gpu():
+    """RowParallelLinear.forward on the registered IPC path returns an owned tensor
+    — y1 = layer(x1); y2 = layer(x2) leaves y1 intact — while launch() stays zero-copy."""
+    for err, shared, owned, distinct in run_multiprocess(_row_reuse_worker, 2, timeout=600):
+        assert err < 3e-2, err
+        assert shared and owned == 1 and distinct
 
 
 @pytest.mark.parametrize("allreduce", ["rccl", "custom", "custom_reg"])
@@ -534,6 +577,22 @@ def test_bench_py_world1():
     emu = rec["virtual_rank_emulation"]
     for w in ("W2", "W8"):
         assert all(v["valid"] and v["us"] > 0 for v in emu[w].values()), emu
+    # BASELINE configs 3-5 at P=1 (full default shapes): every cell validated or refused as
+    # below the roofline, and the GPT-2-small DDP step measured
+    cfgs = rec["baseline_configs"]
+    c3 = cfgs["config3_3d_allgather_reduce_scatter"]
+    assert "error" not in c3 and len(c3["rows"]) == 4, c3
+    for row in c3["rows"]:
+        for op in ("allgather", "reduce_scatter"):
+            assert row[op]["best"] is not None, row
+            assert all("ms" in v or "invalid" in v for v in row[op]["by_impl"].values()), row
+    c4 = cfgs["config4_moe_alltoall"]
+    assert "error" not in c4 and all(r["best"] for r in c4["rows"]), c4
+    c5 = cfgs["config5_gpt2_ddp"]
+    assert "error" not in c5 and c5["batch_per_gpu"] == 16 and c5["seq_len"] == 1024, c5
+    assert c5["tokens_per_s"] > 0 and c5["ms_per_step"] > 0
+    r = c5["by_allreduce"][c5["best"]]
+    assert r["loss"] < r["loss_first_step"] + 1.0 and r["bucket_paths"] == {"none": r["buckets"]}
 
 
 def test_bench_py_two_ranks_rehearsal():
@@ -545,7 +604,8 @@ def test_bench_py_two_ranks_rehearsal():
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
            os.path.join(REPO, "bench.py"), "--gpus", "2", "--steps", "5", "--warmup", "2",
-           "--sweep-max-mib", "32"]
+           "--sweep-max-mib", "32", "--grid", "2,1024,1024;1,2048,2048", "--moe", "2048,1024",
+           "--ddp-model", "2,4,256,4096,4,256", "--ddp-steps", "4"]
     out = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=REPO, env=env)
     assert out.returncode == 0, out.stderr[-3000:]
     rec = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][-1])
@@ -561,6 +621,23 @@ def test_bench_py_two_ranks_rehearsal():
     # the IPC kernel (staged and registered) is a candidate at every size on 2 ranks
     assert all({"custom", "custom_reg"} <= set(e["us_by_impl"]) for e in sweep), sweep
     assert all(e["busbw_GBps"] > 0 for e in sweep), sweep
+    # BASELINE configs 3-5: all three sections present and valid
+    cfgs = rec["baseline_configs"]
+    c3 = cfgs["config3_3d_allgather_reduce_scatter"]
+    assert "error" not in c3 and len(c3["rows"]) == 2, c3
+    for row in c3["rows"]:
+        for op in ("allgather", "reduce_scatter"):
+            cells = row[op]["by_impl"]
+            assert "ms" in cells["rccl"] and "ms" in cells["direct_ipc"], cells
+            assert row[op]["busbw_GBps"] > 0
+    c4 = cfgs["config4_moe_alltoall"]
+    assert "error" not in c4 and c4["rows"][0]["busbw_GBps"] > 0, c4
+    c5 = cfgs["config5_gpt2_ddp"]
+    assert "error" not in c5 and c5["best"] in ("auto", "rccl", "custom"), c5
+    # native RCCL refuses two ranks on one GPU: recorded as an error for that path only
+    assert "error" in c5["by_allreduce"]["native"]
+    auto = c5["by_allreduce"]["auto"]
+    assert "ms_per_step" in auto and sum(auto["bucket_paths"].values()) == auto["buckets"]
 
 
 def test_tp_forward_world1_matches_torch():

@@ -467,15 +467,20 @@ def _agree_worker(rank, world):
     # local timings disagree: alone, rank 0 would pick mfma and rank 1 blas
     local = [{"mfma": 1.0, "blas": 2.0}, {"mfma": 3.0, "blas": 2.5},
              {"mfma": 0.5, "blas": 0.9}, {"mfma": 2.9, "blas": 0.1}][rank]
-    best, agreed = gemm._choose(local)
+    best, agreed = gemm._choose(local, "linear", (64, 64, 64))
     mismatch = None
     try:                                   # a rank with another candidate list: refused
         comm.agree_max(["mfma"] if rank == 0 else ["mfma", "pp"], [1.0] * (1 + (rank > 0)))
     except RuntimeError as e:
         mismatch = str(e)
+    shape_mismatch = None
+    try:                                   # same candidates, different GEMM shape: refused too
+        gemm._choose({"mfma": 1.0, "blas": 2.0}, "linear", (64, 64, 64 * (1 + rank)))
+    except RuntimeError as e:
+        shape_mismatch = str(e)
     comm.destroy()
     alone, _ = (min(local, key=local.get), None)
-    return best, agreed, alone, mismatch, gemm._AGREE is None
+    return best, agreed, alone, mismatch, gemm._AGREE is None, shape_mismatch
 
 
 @pytest.mark.parametrize("world", [2, 4])
@@ -492,6 +497,8 @@ def test_gemm_autotune_choice_agreed_on_rank_max(world):
     assert res[0][2] == "mfma" and res[1][2] == "blas"       # they would have disagreed
     assert all(r[3] and "disagree" in r[3] for r in res)
     assert all(r[4] for r in res)                            # destroy() uninstalls it
+    # the tuning key is part of the agreement, a shape mismatch raises everywhere
+    assert all(r[5] and "disagree" in r[5] for r in res), [r[5] for r in res]
 
 
 def test_ddp_tail_bucket_holds_only_late_params_and_split_optimizer_is_exact():

@@ -52,6 +52,28 @@ def test_bench_py_across_gpus():
     assert rec["config"]["impl"].split("/")[0] in ("rccl", "native", "custom", "custom_reg",
                                                    "custom_push")
     assert all(e["impl"] is not None and e["busbw_GBps"] > 0 for e in rec["allreduce_sweep"])
+    # every candidate passed its fp32-sum check, the IPC kernels passed their self-tests and
+    # the node calibration was recorded
+    assert not rec["config"]["impl_invalid"], rec["config"]
+    assert not any(e.get("invalid") for e in rec["allreduce_sweep"]), rec["allreduce_sweep"]
+    cal = rec["allreduce_calibration"]
+    assert cal["world"] == n and cal["agreed"] == "rank-max" and cal["table"], cal
+    assert all("custom" in e["us_by_impl"] and "custom_reg" in e["us_by_impl"]
+               for e in rec["allreduce_sweep"] if e["bytes"] <= 64 << 20), rec["allreduce_sweep"]
+    # BASELINE configs 3-5 at N: every section ran, every cell validated, busBW over xGMI
+    cfgs = rec["baseline_configs"]
+    c3 = cfgs["config3_3d_allgather_reduce_scatter"]
+    assert "error" not in c3 and len(c3["rows"]) + len(c3.get("skipped_budget", [])) == 4, c3
+    for row in c3["rows"]:
+        for op in ("allgather", "reduce_scatter"):
+            cells = row[op]["by_impl"]
+            assert all("ms" in cells[k] for k in ("rccl", "native", "direct_ipc")), cells
+            assert 0 < row[op]["busbw_GBps"] < 7 * 160, row
+    c4 = cfgs["config4_moe_alltoall"]
+    assert "error" not in c4 and all(0 < r["busbw_GBps"] < 7 * 160 for r in c4["rows"]), c4
+    c5 = cfgs["config5_gpt2_ddp"]
+    assert "error" not in c5 and c5["global_batch"] == 16 * n, c5
+    assert all("ms_per_step" in v for v in c5["by_allreduce"].values()), c5
 
 
 def _car_across_gpus_worker(rank, world, n):
@@ -102,7 +124,7 @@ def test_custom_allreduce_across_gpus():
             assert good and err == 0, (kind, nb, good, err)
 
 
-@pytest.mark.parametrize("allreduce", ["rccl", "custom"])
+@pytest.mark.parametrize("allreduce", ["auto", "rccl", "custom"])
 def test_gpt2_ddp_across_gpus(allreduce, tmp_path):
     """A small GPT-2 DDP run with real bucket all-reduces overlapping backward; the loss falls
     and the result JSON reports every GPU."""
@@ -115,10 +137,18 @@ def test_gpt2_ddp_across_gpus(allreduce, tmp_path):
     rec = json.loads(outp.read_text())
     assert rec["n_gpus"] == n
     assert rec["loss"] < rec["loss_first_step"]
+    assert rec["tokens_per_s"] > 0 and rec["buckets"] > 1
+    paths = rec["bucket_paths"]
+    assert sum(paths.values()) == rec["buckets"], paths
+    want = {"rccl": {"rccl"}, "custom": {"custom", "custom_reg"},
+            "auto": {"custom_reg", "native"}}[allreduce]
+    assert set(paths) <= want, paths
+    assert rec["gemm_kernel_mix"]["agreed_across_ranks"] is True
 
 
 @pytest.mark.parametrize("allreduce,fp32_buckets", [("rccl", False), ("custom", False),
-                                                    ("native", False), ("rccl", True)])
+                                                    ("native", False), ("auto", False),
+                                                    ("rccl", True)])
 def test_ddp_matches_global_batch_across_gpus(allreduce, fp32_buckets):
     """VERDICT r02 item 5 (reference test/ds_mpi_test.py:27-49): after one overlapped step the
     all-reduced gradient equals a world-1 run on the concatenated global batch (bf16 tolerance,
