@@ -122,7 +122,7 @@ def p1_opts(comm: Comm, op_name: str, op_opts: Dict) -> Dict:
     out-of-place form on our native engine instead — a real device copy of the message, as
     bench.py does — where the op has one; other ops keep their options (and the roofline guard
     refuses an empty call)."""
-    if comm.world_size != 1 or not comm.is_gpu or op_opts.get("impl"):
+    if comm.world_size != 1 or not comm.is_gpu or op_opts.get("impl") == "custom":
         return op_opts
     if op_name in ("allreduce", "broadcast", "reduce"):
         return dict(op_opts, impl="native", out_of_place=True)

@@ -74,6 +74,10 @@ def parse_args(argv=None):
                     help="torch.profiler Chrome trace per rank into DIR")
     ap.add_argument("--seed", type=int, default=42)
     ap.add_argument("--timeout", type=float, default=900.0, help="process-group timeout (s)")
+    ap.add_argument("--device", choices=["auto", "cpu", "cuda"], default="auto",
+                    help="tensor device; auto = cuda for rccl, cpu for gloo. gloo + cuda = ranks "
+                         "sharing one GPU over a gloo process group (rehearsal of the multi-rank "
+                         "sweep; RCCL needs one GPU per rank)")
     return ap.parse_args(argv)
 
 
@@ -90,7 +94,8 @@ def main(argv=None) -> int:
     from ..parallel.collectives import REFERENCE_1D_OPS, REFERENCE_3D_OPS
     from ..parallel.comm import init_distributed
 
-    comm = init_distributed(args.backend, timeout_s=args.timeout)
+    comm = init_distributed(args.backend, timeout_s=args.timeout,
+                            device=None if args.device == "auto" else args.device)
     impl = args.impl_name or comm.backend_label
     if args.ops:
         ops = [o.strip() for o in args.ops.split(",") if o.strip()]

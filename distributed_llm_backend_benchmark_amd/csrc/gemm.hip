@@ -211,10 +211,12 @@ struct Tile256 {
 };
 
 // virtual workgroup id -> output tile: XCD-aware bijective remap (T1), then GROUP_M ordering
+// (BNT: tile width, 256 or 192)
+template <int BNT = BN2>
 __device__ __forceinline__ Tile256 tile_of(const GemmArgs& a, int vb) {
   // 32-bit index math (tile counts < 2^31): 64-bit divisions cost SGPRs and SALU time
   const int tiles_m = static_cast<int>((a.M + BM2 - 1) / BM2);
-  const int tiles_n = static_cast<int>((a.N + BN2 - 1) / BN2);
+  const int tiles_n = static_cast<int>((a.N + BNT - 1) / BNT);
   const int nwg = tiles_m * tiles_n;
   const int q = nwg >> 3, r = nwg & 7, x = vb & 7;
   const int wid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (vb >> 3);
@@ -224,7 +226,7 @@ __device__ __forceinline__ Tile256 tile_of(const GemmArgs& a, int vb) {
   const int gm = (tiles_m - first_m) < kGroupM ? (tiles_m - first_m) : kGroupM;
   const int in_group = wid - group * group_size;
   return Tile256{static_cast<int64_t>(first_m + in_group % gm) * BM2,
-                 static_cast<int64_t>(in_group / gm) * BN2};
+                 static_cast<int64_t>(in_group / gm) * BNT};
 }
 
 // Deep-pipeline prologue: all four sections of K-tile 0 and S0, S1 of K-tile 1 (6 sections).
@@ -885,6 +887,133 @@ __device__ __forceinline__ void read_split_any(const char* abuf, const char* bbu
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// 256 x 192 output tiles (NJ = 3 MFMA column fragments per wave instead of 4: each of the 4 wave
+// columns owns 48 output columns). For grids whose 256² form ends in a partial round of the
+// 256 CUs — the GPT-2 projections N = 768 (192 tiles of 256², 0.75 round -> 256 tiles, one full
+// round), QKV N = 2304 (576 tiles, 2.25 rounds -> 768, 3 full rounds) — the same work fills every
+// CU. Host contract: N % 192 == 0 (every 48-row B block wholly in bounds).
+// B row order inside a wave column's 48-row block (the perm_brow analogue): LDS image row
+// L = 16 j + 4 fq + r (fragment j, lane quad fq, accumulator r) holds B row 12 fq + 4 j + r, so
+// lane (fr, fq) ends with 12 consecutive output columns, acc[i][j][r] = column 4 j + r. In the
+// 8-row DMA groups L = 8 g + r_in this is separable: row = g48_base(g) + g48_lane(r_in).
+__device__ __forceinline__ int g48_base(int g) { return 24 * (g & 1) + 4 * (g >> 1); }
+__device__ __forceinline__ int g48_lane(int r_in) { return 12 * (r_in >> 2) + (r_in & 3); }
+
+// B tile of 192 rows = 24 groups of 8: instruction s = 4 i + w4 stages group s (wave column
+// block s / 6, group g = s % 6) — 6 per wave of the staging row. [I0, I1) slices as stage_b.
+template <int I0 = 0, int I1 = 6>
+__device__ __forceinline__ void stage_b192(__amdgpu_buffer_rsrc_t rb, uint32_t ldb2, uint32_t k2,
+                                           char* bbuf, int w4, uint32_t boff) {
+#pragma unroll
+  for (int i = I0; i < I1; ++i) {
+    const int s = i * 4 + w4;
+    const int blk = s / 6, g = s - blk * 6;
+    bldsx4(rb, boff, static_cast<uint32_t>(blk * 48 + g48_base(g)) * ldb2 + k2,
+           bbuf + s * 8 * (BK * 2));
+  }
+}
+
+// Epilogue of one wave's 128 x 48 block: lane (fr, fq) holds rows row0 + 16 i + fr, columns
+// col0 + 12 fq + 4 j + r. The 12 columns are 24 B of bf16 (8-B aligned): three 8-B stores per
+// row; fp32 output three 16-B stores. Host contract N % 192 == 0: every column group is whole.
+template <int MI>
+__device__ __forceinline__ void store_tile12(const GemmArgs& a, const f32x4 (&acc)[MI][3],
+                                             int64_t row0, int64_t col0, int lane) {
+  const int fr = lane & 15, fq = lane >> 4;
+  const int epi = a.epi;
+  const int64_t cbase = col0 + fq * 12;
+  const int64_t rbase = row0 + fr;
+  const int rows_left = static_cast<int>(a.M - rbase);
+  const bool vec = a.vec_ok != 0;
+  float bias[12];
+#pragma unroll
+  for (int c = 0; c < 12; ++c) bias[c] = 0.f;
+  if (epi & EPI_BIAS) {
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      const u16x4 bv = vec ? reinterpret_cast<const u16x4*>(a.bias + cbase)[q]
+                           : u16x4{a.bias[cbase + 4 * q], a.bias[cbase + 4 * q + 1],
+                                   a.bias[cbase + 4 * q + 2], a.bias[cbase + 4 * q + 3]};
+#pragma unroll
+      for (int c = 0; c < 4; ++c) bias[4 * q + c] = bf16_to_f32(bv[c]);
+    }
+  }
+  float* cf = static_cast<float*>(a.C) + rbase * a.ldc + cbase;
+  uint16_t* cb = static_cast<uint16_t*>(a.C) + rbase * a.ldc + cbase;
+  uint16_t* pb = a.preact ? a.preact + rbase * a.ldc + cbase : nullptr;
+  const uint16_t* rb = (epi & EPI_READS_R) ? a.residual + rbase * a.ldr + cbase : nullptr;
+#pragma unroll
+  for (int i = 0; i < MI; ++i) {
+    if (i * 16 >= rows_left) break;
+    float v[12];
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[j * 4 + r] = acc[i][j][r] + bias[j * 4 + r];
+    const int64_t oc = static_cast<int64_t>(i) * 16 * a.ldc, orr = static_cast<int64_t>(i) * 16 * a.ldr;
+    if (vec) {
+      if (pb) {
+#pragma unroll
+        for (int q = 0; q < 3; ++q)
+          reinterpret_cast<u16x4*>(pb + oc)[q] =
+              u16x4{f32_to_bf16(v[4 * q]), f32_to_bf16(v[4 * q + 1]), f32_to_bf16(v[4 * q + 2]),
+                    f32_to_bf16(v[4 * q + 3])};
+      }
+      if (epi & (EPI_GELU_ERF | EPI_GELU_TANH)) {
+#pragma unroll
+        for (int c = 0; c < 12; ++c) v[c] = apply_act(v[c], epi);
+      }
+      if (rb) {
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+          const u16x4 rv = reinterpret_cast<const u16x4*>(rb + orr)[q];
+#pragma unroll
+          for (int c = 0; c < 4; ++c) v[4 * q + c] = apply_r(v[4 * q + c], bf16_to_f32(rv[c]), epi);
+        }
+      }
+      if (a.out_f32) {
+        float4* o = reinterpret_cast<float4*>(cf + oc);
+#pragma unroll
+        for (int q = 0; q < 3; ++q)
+          o[q] = make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+      } else {
+#pragma unroll
+        for (int q = 0; q < 3; ++q)
+          reinterpret_cast<u16x4*>(cb + oc)[q] =
+              u16x4{f32_to_bf16(v[4 * q]), f32_to_bf16(v[4 * q + 1]), f32_to_bf16(v[4 * q + 2]),
+                    f32_to_bf16(v[4 * q + 3])};
+      }
+    } else {
+#pragma unroll
+      for (int c = 0; c < 12; ++c) {
+        float x = v[c];
+        if (pb) pb[oc + c] = f32_to_bf16(x);
+        x = apply_act(x, epi);
+        if (rb) x = apply_r(x, bf16_to_f32(rb[orr + c]), epi);
+        if (a.out_f32) cf[oc + c] = x; else cb[oc + c] = f32_to_bf16(x);
+      }
+    }
+  }
+}
+
+// counted LDS-DMA wait with a compile-time count (the 192-wide tile changes every count)
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  static_assert(N >= 0 && N <= 24, "vmcnt range");
+  if constexpr (N == 0) DLBB_WAIT_VM(0);
+  else if constexpr (N == 3) DLBB_WAIT_VM(3);
+  else if constexpr (N == 4) DLBB_WAIT_VM(4);
+  else if constexpr (N == 6) DLBB_WAIT_VM(6);
+  else if constexpr (N == 7) DLBB_WAIT_VM(7);
+  else if constexpr (N == 8) DLBB_WAIT_VM(8);
+  else if constexpr (N == 10) DLBB_WAIT_VM(10);
+  else if constexpr (N == 12) DLBB_WAIT_VM(12);
+  else if constexpr (N == 16) DLBB_WAIT_VM(16);
+  else if constexpr (N == 20) DLBB_WAIT_VM(20);
+  else static_assert(N < 0, "add this count to wait_vm");
+}
+
 // The ping-pong schedule, for B stored [N][K] (NT: forward, C = A · B^T) or [K][N] (NN: dgrad).
 // Both B layouts stage 32 wave-instructions per K-tile from wave row 0, so the counted waits
 // are identical.
@@ -900,8 +1029,14 @@ __device__ __forceinline__ void read_split_any(const char* abuf, const char* bbu
 // TN (weight gradient, implies NN for B): A [K][lda] row-major over the reduction, staged and
 // read as transposed images (stage_a_half_tn / read_a_tn); split-K as for NN.
 // STAMP (diagnostic variants only): per-workgroup start / end records into `st` (common.h).
-template <bool NN, bool BAL = false, bool TN = false, bool STAMP = false>
+// NJ: MFMA column fragments per wave — 4 (256-wide tile) or 3 (256 x 192, NT only; see
+// stage_b192). NBI = B DMA instructions per staging wave per K-tile (2 NJ): every counted wait
+// below is written in it (NJ = 4 gives the original literals).
+template <bool NN, bool BAL = false, bool TN = false, bool STAMP = false, int NJ = 4>
 __device__ __forceinline__ void pingpong_body(GemmArgs a, char* smem, uint64_t* st = nullptr) {
+  static_assert(NJ == 4 || (NJ == 3 && !NN && !TN), "192-wide tiles: NT only");
+  constexpr int NBI = 2 * NJ;                 // B DMA instructions per staging wave per K-tile
+  constexpr int kTileB = NJ * 64 * BK * 2;    // bytes of one B tile buffer
   uint64_t t_start = 0;
   if constexpr (STAMP) t_start = stamp_now();
   if (NN && gridDim.y > 1) {         // split-K slice blockIdx.y (wave-uniform, SGPR math)
@@ -919,18 +1054,18 @@ __device__ __forceinline__ void pingpong_body(GemmArgs a, char* smem, uint64_t* 
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wr = wave >> 2, wc = wave & 3;
   const int fr = lane & 15, fq = lane >> 4;
-  const Tile256 tl = tile_of(a, static_cast<int>(blockIdx.x));
+  const Tile256 tl = tile_of<NJ * 64>(a, static_cast<int>(blockIdx.x));
   const int64_t m0 = tl.m0, n0 = tl.n0;
   const int nk = static_cast<int>(a.K / BK);
   char* const abuf0 = smem;
   char* const bbuf0 = smem + 2 * kTile2Bytes;
 
-  f32x4 acc[8][4];
+  f32x4 acc[8][NJ];
 #pragma unroll
   for (int i = 0; i < 8; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  bf16x8 af[2][8], bf[2][4];
+    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 af[2][8], bf[2][NJ];
   const int r_in = lane >> 3, chunk = (lane & 7) ^ (lane >> 3);
   const uint32_t lda2 = static_cast<uint32_t>(a.lda) * 2, ldb2 = static_cast<uint32_t>(a.ldb) * 2;
   // TN: image rows 4s + rq, so swz_tn needs rq and bit 1 of the wave column
@@ -943,6 +1078,8 @@ __device__ __forceinline__ void pingpong_body(GemmArgs a, char* smem, uint64_t* 
     const int rq = lane >> 4, slot = lane & 15;
     boff = static_cast<uint32_t>(rq) * ldb2 +
            static_cast<uint32_t>(slot ^ rq ^ (((wc >> 1) & 1) << 3)) * 16;
+  } else if constexpr (NJ == 3) {
+    boff = static_cast<uint32_t>(g48_lane(r_in)) * ldb2 + chunk * 16;
   } else {
     boff = static_cast<uint32_t>(perm_brow(r_in)) * ldb2 + chunk * 16;
   }
@@ -952,6 +1089,44 @@ __device__ __forceinline__ void pingpong_body(GemmArgs a, char* smem, uint64_t* 
   const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<uint16_t*>(NN ? a.B + n0 : a.B + n0 * a.ldb), 0, 0x7fffffff, 0x00020000);
   constexpr uint32_t kStep = BK * 2;
+  // B tile u into buffer `bb`, instruction slice [I0, I1) of the staging wave
+  auto stage_bt = [&](auto i0, auto i1, int u, char* bb) {
+    constexpr int I0 = decltype(i0)::value, I1 = decltype(i1)::value;
+    if constexpr (NJ == 3)
+      stage_b192<I0, I1>(rb, ldb2, static_cast<uint32_t>(u) * kStep, bb, wc, boff);
+    else
+      stage_b_any<NN, I0, I1>(rb, ldb2, rows_b, u, bb, wc, boff);
+  };
+  using Z = std::integral_constant<int, 0>;
+  using H = std::integral_constant<int, NBI / 2>;
+  using F = std::integral_constant<int, NBI>;
+  auto read_frags = [&](const char* ab, const char* bb, int row) {
+    if constexpr (NJ == 3) {
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) af[ks][i] = read_frag(ab, row * 128 + i * 16 + fr, ks * 4 + fq);
+#pragma unroll
+        for (int j = 0; j < 3; ++j) bf[ks][j] = read_frag(bb, wc * 48 + j * 16 + fr, ks * 4 + fq);
+      }
+    } else {
+      read_split_any<NN, TN>(ab, bb, row, wc, fr, fq, af, bf);
+    }
+  };
+  auto mfma_all = [&]() {
+    if constexpr (NJ == 3) {
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+          for (int j = 0; j < 3; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[ks][j], af[ks][i], acc[i][j],
+                                                                0, 0, 0);
+    } else {
+      mfma_full(acc, af, bf);
+    }
+  };
   // TN: A half `half` of K-tile u staged as a transposed image (4 wave-instructions per wave,
   // as stage_a_half); the NT / NN call sites below are kept verbatim (identical ISA)
 #define DLBB_STAGE_A(U, BUF, HALF, NT_CALL)                                       \
@@ -963,10 +1138,10 @@ __device__ __forceinline__ void pingpong_body(GemmArgs a, char* smem, uint64_t* 
   if (wr == 0) {
     // prologue, row 0: A-lo(0), B(0), B(1); retire the first two
     DLBB_STAGE_A(0, abuf0, 0, stage_a_half(ra, lda2, rows_a, 0, abuf0, 0, wc, aoff));
-    stage_b_any<NN>(rb, ldb2, rows_b, 0, bbuf0, wc, boff);
+    stage_bt(Z{}, F{}, 0, bbuf0);
     if (nk > 1) {
-      stage_b_any<NN>(rb, ldb2, rows_b, 1, bbuf0 + kTile2Bytes, wc, boff);
-      DLBB_WAIT_VM(8);
+      stage_bt(Z{}, F{}, 1, bbuf0 + kTileB);
+      wait_vm<NBI>();
     } else {
       DLBB_WAIT_VM(0);
     }
@@ -974,7 +1149,7 @@ __device__ __forceinline__ void pingpong_body(GemmArgs a, char* smem, uint64_t* 
     int cb = 0;                                       // B buffer of tile u
     for (int u = 0; u < nk; ++u) {
       const char* ab = abuf0 + (u & 1) * kTile2Bytes;
-      read_split_any<NN, TN>(ab, bbuf0 + cb * kTile2Bytes, 0, wc, fr, fq, af, bf);
+      read_frags(ab, bbuf0 + cb * kTileB, 0);
       const bool h1 = u + 1 < nk, b2 = u + 2 < nk;
       if (h1)
         DLBB_STAGE_A(u + 1, abuf0 + ((u + 1) & 1) * kTile2Bytes, 1,
@@ -983,29 +1158,29 @@ __device__ __forceinline__ void pingpong_body(GemmArgs a, char* smem, uint64_t* 
       if (b2) {
         const int cb2 = cb == 0 ? 2 : cb - 1;         // (u + 2) % 3
         if (BAL)
-          stage_b_any<NN, 0, 4>(rb, ldb2, rows_b, u + 2, bbuf0 + cb2 * kTile2Bytes, wc, boff);
+          stage_bt(Z{}, H{}, u + 2, bbuf0 + cb2 * kTileB);
         else
-          stage_b_any<NN>(rb, ldb2, rows_b, u + 2, bbuf0 + cb2 * kTile2Bytes, wc, boff);
+          stage_bt(Z{}, F{}, u + 2, bbuf0 + cb2 * kTileB);
       }
       // retire A-hi(u) (issued two intervals ago; tile 0's came from row 1)
       if (BAL) {
-        if (b2) DLBB_WAIT_VM(12);
-        else if (h1) DLBB_WAIT_VM(8);
-        else DLBB_WAIT_VM(0);
+        if (b2) wait_vm<NBI + 4>();
+        else if (h1) wait_vm<NBI / 2 + 4>();
+        else wait_vm<0>();
       } else {
-        if (b2) DLBB_WAIT_VM(20);
-        else if (h1) DLBB_WAIT_VM(12);
-        else DLBB_WAIT_VM(0);
+        if (b2) wait_vm<2 * NBI + 4>();
+        else if (h1) wait_vm<NBI + 4>();
+        else wait_vm<0>();
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
       __builtin_amdgcn_s_barrier();                   // end of interval 2u
       __builtin_amdgcn_sched_barrier(0);
-      mfma_full(acc, af, bf);
+      mfma_all();
       __builtin_amdgcn_sched_barrier(0);
       if (h1) {                                       // retire B(u+1) (BAL: its first half)
-        if (b2) { if (BAL) DLBB_WAIT_VM(8); else DLBB_WAIT_VM(12); }
-        else DLBB_WAIT_VM(4);
+        if (b2) { if (BAL) wait_vm<4 + NBI / 2>(); else wait_vm<4 + NBI>(); }
+        else wait_vm<4>();
       }
       __builtin_amdgcn_s_barrier();                   // end of interval 2u+1
       cb = cb == 2 ? 0 : cb + 1;
@@ -1022,7 +1197,7 @@ __device__ __forceinline__ void pingpong_body(GemmArgs a, char* smem, uint64_t* 
     int cb = 0;
     for (int u = 0; u < nk; ++u) {
       const char* ab = abuf0 + (u & 1) * kTile2Bytes;
-      read_split_any<NN, TN>(ab, bbuf0 + cb * kTile2Bytes, 1, wc, fr, fq, af, bf);
+      read_frags(ab, bbuf0 + cb * kTileB, 1);
       const bool l2 = u + 2 < nk;
       if (l2)
         DLBB_STAGE_A(u + 2, abuf0 + (u & 1) * kTile2Bytes, 0,
@@ -1030,23 +1205,26 @@ __device__ __forceinline__ void pingpong_body(GemmArgs a, char* smem, uint64_t* 
                                   abuf0 + (u & 1) * kTile2Bytes, 0, wc, aoff));
       if (BAL && l2) {
         const int cb2 = cb == 0 ? 2 : cb - 1;         // (u + 2) % 3
-        stage_b_any<NN, 4, 8>(rb, ldb2, rows_b, u + 2, bbuf0 + cb2 * kTile2Bytes, wc, boff);
+        stage_bt(H{}, F{}, u + 2, bbuf0 + cb2 * kTileB);
       }
       if (u + 1 < nk) {                               // retire A-lo(u+1) (BAL: and B1(u+1))
-        if (l2) { if (BAL) DLBB_WAIT_VM(8); else DLBB_WAIT_VM(4); }
-        else DLBB_WAIT_VM(0);
+        if (l2) { if (BAL) wait_vm<4 + NBI / 2>(); else wait_vm<4>(); }
+        else wait_vm<0>();
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
       __builtin_amdgcn_s_barrier();                   // end of interval 2u+1
       __builtin_amdgcn_sched_barrier(0);
-      mfma_full(acc, af, bf);
+      mfma_all();
       __builtin_amdgcn_sched_barrier(0);
       if (u + 1 < nk) __builtin_amdgcn_s_barrier();   // end of interval 2u+2
       cb = cb == 2 ? 0 : cb + 1;
     }
   }
-  store_tile_256<NN>(a, acc, m0, n0, wave, lane);
+  if constexpr (NJ == 3)
+    store_tile12<8>(a, acc, m0 + (wave >> 2) * 128, n0 + (wave & 3) * 48, lane);
+  else
+    store_tile_256<NN>(a, acc, m0, n0, wave, lane);
   if constexpr (STAMP) {
     __syncthreads();
     if (threadIdx.x == 0) stamp_write(st, t_start);
@@ -1063,6 +1241,17 @@ __global__ void __launch_bounds__(kThreads2, 1) gemm_bf16_nt_256_pingpong3(GemmA
 __global__ void __launch_bounds__(kThreads2, 1) gemm_bf16_nt_256_pingpong3_bal(GemmArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   pingpong_body<false, true>(a, smem);
+}
+
+// 256 x 192 tiles (N % 192 == 0): grids that end in a partial round of 256² tiles
+constexpr int kPP192Lds = 2 * kTile2Bytes + 3 * (3 * 64 * BK * 2);   // 136 KiB
+__global__ void __launch_bounds__(kThreads2, 1) gemm_bf16_nt_192_pingpong3(GemmArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  pingpong_body<false, false, false, false, 3>(a, smem);
+}
+__global__ void __launch_bounds__(kThreads2, 1) gemm_bf16_nt_192_pingpong3_bal(GemmArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  pingpong_body<false, true, false, false, 3>(a, smem);
 }
 
 // dgrad: C[M, N] = A[M, K] · B[K, N] (B row-major over the reduction); host contract
@@ -1749,10 +1938,26 @@ DLBB_API void dlbb_gemm_set_persist_epi(int on) { dlbb_persist_epi = on ? 1 : 0;
 DLBB_API void dlbb_gemm_set_concurrent(int on) { dlbb_gemm_concurrent = on; }
 DLBB_API void dlbb_gemm_set_bal(int mode) { dlbb_gemm_bal = mode >= 0 && mode <= 2 ? mode : 2; }
 
+// NT GEMM with an explicit kernel variant (the autotuner's candidates, ops/gemm.py):
+//   0 = the size heuristic below (256² ping-pong / persistent / 128² small grids)
+//   1 = 256 x 192 ping-pong tiles (N % 192 == 0, M % 8 == 0; otherwise variant 0)
+DLBB_API int dlbb_gemm_bf16_nt_v(const void* A, int64_t lda, const void* B, int64_t ldb, void* C,
+                                 int64_t ldc, int64_t M, int64_t N, int64_t K, const void* bias,
+                                 const void* residual, int64_t ldr, void* preact, int epi,
+                                 int out_f32, int variant, hipStream_t stream);
+
 DLBB_API int dlbb_gemm_bf16_nt(const void* A, int64_t lda, const void* B, int64_t ldb, void* C,
                                int64_t ldc, int64_t M, int64_t N, int64_t K, const void* bias,
                                const void* residual, int64_t ldr, void* preact, int epi,
                                int out_f32, hipStream_t stream) {
+  return dlbb_gemm_bf16_nt_v(A, lda, B, ldb, C, ldc, M, N, K, bias, residual, ldr, preact, epi,
+                             out_f32, 0, stream);
+}
+
+DLBB_API int dlbb_gemm_bf16_nt_v(const void* A, int64_t lda, const void* B, int64_t ldb, void* C,
+                                 int64_t ldc, int64_t M, int64_t N, int64_t K, const void* bias,
+                                 const void* residual, int64_t ldr, void* preact, int epi,
+                                 int out_f32, int variant, hipStream_t stream) {
   if (M <= 0 || N <= 0) return hipSuccess;
   if (K <= 0 || K % BK != 0) return hipErrorInvalidValue;
   if (lda % 8 || ldb % 8) return hipErrorInvalidValue;          // 16-byte rows for glds
@@ -1769,6 +1974,15 @@ DLBB_API int dlbb_gemm_bf16_nt(const void* A, int64_t lda, const void* B, int64_
              static_cast<uint16_t*>(preact), M, N, K, lda, ldb, ldc, ldr, epi, out_f32,
              vec_ok, 0};
   const int64_t tiles256 = ((M + BM2 - 1) / BM2) * ((N + BN2 - 1) / BN2);
+  if (variant == 1 && N % 192 == 0 && M % 8 == 0 && M >= 8 &&
+      lda * 2 * 256 + K * 2 < (1LL << 31) && ldb * 2 * 192 + K * 2 < (1LL << 31)) {
+    const dim3 g(static_cast<unsigned>(((M + BM2 - 1) / BM2) * (N / 192))), b(kThreads2);
+    if (use_bal(K / BK, false))
+      hipLaunchKernelGGL(gemm_bf16_nt_192_pingpong3_bal, g, b, kPP192Lds, stream, a);
+    else
+      hipLaunchKernelGGL(gemm_bf16_nt_192_pingpong3, g, b, kPP192Lds, stream, a);
+    return hipGetLastError();
+  }
   // the 256^2 schedule needs >= ~1 workgroup per CU to fill the chip; otherwise 128^2 tiles
   const int force = dlbb_gemm_force_tile;
   if (force == 256 || (force != 128 && tiles256 >= 192)) {

@@ -59,6 +59,9 @@ _SIGS = {
     "dlbb_gemm_bf16_nt": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64,
                                   c_int64, c_int64, c_int64, c_void_p, c_void_p, c_int64,
                                   c_void_p, c_int, c_int, c_void_p]),
+    "dlbb_gemm_bf16_nt_v": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64,
+                                    c_int64, c_int64, c_int64, c_void_p, c_void_p, c_int64,
+                                    c_void_p, c_int, c_int, c_int, c_void_p]),
     "dlbb_gemm_bf16_nn": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64,
                                   c_int64, c_int64, c_int64, c_void_p, c_void_p, c_int64,
                                   c_void_p, c_int, c_int, c_int, c_void_p, c_void_p]),

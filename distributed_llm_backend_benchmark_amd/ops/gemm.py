@@ -199,7 +199,7 @@ def _torch_linear(x2, w, bias, act, residual, out_dtype, preact):
     return y.to(out_dtype)
 
 
-def _mfma_linear(x2, w, bias, act, r2, out, preact):
+def _mfma_linear(x2, w, bias, act, r2, out, preact, variant: int = 0):
     M, K = x2.shape
     N = w.shape[0]
     epi = ACTS[act]
@@ -207,12 +207,23 @@ def _mfma_linear(x2, w, bias, act, r2, out, preact):
         epi |= EPI_BIAS
     if r2 is not None:
         epi |= EPI_RESIDUAL
-    check(_lib.lib().dlbb_gemm_bf16_nt(
+    check(_lib.lib().dlbb_gemm_bf16_nt_v(
         x2.data_ptr(), x2.stride(0), w.data_ptr(), w.stride(0), out.data_ptr(), N, M, N, K,
         _lib.ptr(bias), _lib.ptr(r2), r2.stride(0) if r2 is not None else 0,
-        _lib.ptr(preact), epi, 1 if out.dtype == torch.float32 else 0,
+        _lib.ptr(preact), epi, 1 if out.dtype == torch.float32 else 0, int(variant),
         _lib.stream(x2.device)), "gemm_bf16_nt")
     return out
+
+
+def _mfma192_linear(x2, w, bias, act, r2, out, preact):
+    """256 x 192 output tiles (``csrc/gemm.hip`` ``gemm_bf16_nt_192_pingpong3``): for N % 192 ==
+    0 grids whose 256² form ends in a partial round of the CUs (GPT-2 projections N = 768:
+    0.75 round -> one full round)."""
+    return _mfma_linear(x2, w, bias, act, r2, out, preact, variant=1)
+
+
+def mfma192_ok(M: int, N: int) -> bool:
+    return N % 192 == 0 and M % 8 == 0 and M >= 8
 
 
 _APPROX = {"gelu": 0, "gelu_erf": 0, "gelu_tanh": 1}
@@ -249,9 +260,9 @@ def _blas_linear(x2, w, bias, act, r2, out, preact):
     return out
 
 
-CHOICES = {}          # (M, N, K, epi-signature) -> "mfma" | "blas"
+CHOICES = {}          # (M, N, K, epi-signature) -> "mfma" | "mfma192" | "blas"
 CALLS = {}            # ("linear" | "wgrad", key) -> calls since import (kernel-mix accounting)
-_IMPLS = {"mfma": _mfma_linear, "blas": _blas_linear}
+_IMPLS = {"mfma": _mfma_linear, "mfma192": _mfma192_linear, "blas": _blas_linear}
 
 
 # > 0 while GEMMs share the chip with communication kernels on another stream (the overlapped
@@ -289,7 +300,11 @@ def _autotune(key, args) -> str:
         return CHOICES[key]
     if torch.cuda.is_current_stream_capturing():
         return "mfma"
-    impls = {"mfma": _IMPLS["mfma"]} if key[-1] == "concurrent" else _IMPLS
+    impls = dict(_IMPLS)
+    if key[-1] == "concurrent":
+        del impls["blas"]
+    if not mfma192_ok(key[0], key[1]):
+        del impls["mfma192"]
     times = _time_interleaved({n: (lambda f=f: f(*args)) for n, f in impls.items()})
     best, times = _choose(times, "linear", key)
     CHOICES[key] = best

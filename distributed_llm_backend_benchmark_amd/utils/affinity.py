@@ -16,7 +16,8 @@ Done in-process at ``init_distributed`` — no ``numactl`` relaunch and no exec 
 3. the local ranks whose GPUs share that CPU list split it into disjoint slices
    (``cores_per_rank`` each when given, else an even share), intersected with the CPUs this
    process may use (cgroup / launcher mask), then ``os.sched_setaffinity``;
-4. ``torch.set_num_threads`` / ``OMP_NUM_THREADS`` / ``MKL_NUM_THREADS`` follow the slice.
+4. with an explicit ``cores_per_rank``, ``torch.set_num_threads`` / ``OMP_NUM_THREADS`` /
+   ``MKL_NUM_THREADS`` follow the slice (otherwise the launcher's thread settings stand).
 
 ``DLBB_BIND=0`` disables it. The applied binding is recorded in result JSONs.
 """
@@ -172,11 +173,15 @@ def bind_to_device(device_index: int, local_rank: int, local_world: int,
         rec["reason"] = f"sched_setaffinity: {e}"
         return rec
     n = len(cpus)
-    os.environ["OMP_NUM_THREADS"] = os.environ["MKL_NUM_THREADS"] = str(n)
-    try:
-        torch.set_num_threads(n)
-    except RuntimeError:
-        pass
+    if cores_per_rank:
+        # an explicit per-rank core budget (reference: OMP/MKL threads = cores per rank,
+        # config/baseline_config.yaml system section): intra-op threads follow it; without one
+        # the launcher's thread settings are left alone
+        os.environ["OMP_NUM_THREADS"] = os.environ["MKL_NUM_THREADS"] = str(n)
+        try:
+            torch.set_num_threads(n)
+        except RuntimeError:
+            pass
     rec.update(bound=True, cpus=format_cpulist(cpus), ncpus=n,
                cores_per_rank=cores_per_rank)
     return rec

@@ -195,6 +195,49 @@ def test_gemm_persistent_lean_epilogues(M, N, K, act, with_pre, persist_epi, mon
         torch.testing.assert_close(pre.float(), u, rtol=2e-2, atol=2e-2)
 
 
+@pytest.mark.parametrize("M,N,K", [(16384, 768, 768), (16384, 768, 3072), (520, 192, 128),
+                                   (4096, 2304, 64), (8, 384, 192), (1024 + 8, 1536, 4096)])
+@pytest.mark.parametrize("epi", ["plain_f32", "bias_res", "bias_gelu_pre", "plain_bf16"])
+@pytest.mark.parametrize("bal", [0, 1])
+def test_gemm_nt_192_tiles_match_fp32(M, N, K, epi, bal, monkeypatch):
+    """256 x 192 ping-pong tiles (variant 1, the partial-round fix for N % 192 == 0) against an
+    fp32 reference: ragged M, 1 .. 64 K-tiles, every epilogue (bias, residual, GELU with the
+    pre-activation store, fp32 / bf16 output), plain and balanced DMA issue."""
+    from distributed_llm_backend_benchmark_amd.ops import gemm
+
+    x = _randn(M, K, seed=41, scale=0.3)
+    w = _randn(N, K, seed=42, scale=0.3)
+    b = _randn(N, seed=43)
+    r = _randn(M, N, seed=44)
+    u = x.float() @ w.float().t()
+    gemm.set_bal(bal)
+    try:
+        if epi == "plain_f32":
+            y = torch.empty(M, N, dtype=torch.float32, device=DEV)
+            gemm._mfma192_linear(x, w, None, None, None, y, None)
+            torch.testing.assert_close(y, u, rtol=2e-3, atol=2e-3 * K ** 0.5)
+        elif epi == "plain_bf16":
+            y = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+            gemm._mfma192_linear(x, w, None, None, None, y, None)
+            torch.testing.assert_close(y.float(), u, rtol=2e-2, atol=2e-2 * K ** 0.5)
+        elif epi == "bias_res":
+            y = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+            gemm._mfma192_linear(x, w, b, None, r, y, None)
+            torch.testing.assert_close(y.float(), u + b.float() + r.float(), rtol=2e-2,
+                                       atol=2e-2 * K ** 0.5)
+        else:
+            y = torch.empty(M, N, dtype=torch.float32, device=DEV)
+            pre = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+            gemm._mfma192_linear(x, w, b, "gelu_tanh", None, y, pre)
+            ub = u + b.float()
+            torch.testing.assert_close(y, F.gelu(ub, approximate="tanh"), rtol=2e-3,
+                                       atol=2e-3 * K ** 0.5)
+            torch.testing.assert_close(pre.float(), ub, rtol=2e-2, atol=2e-2 * K ** 0.5)
+    finally:
+        gemm.set_bal(2)
+    torch.cuda.synchronize()
+
+
 def test_gemm_strided_A_view():
     """The TP attention stub passes qkv[..., :H/P] (lda = 3H/P) straight into the GEMM."""
     from distributed_llm_backend_benchmark_amd.ops import linear

@@ -198,3 +198,14 @@ def test_run_tp_across_gpus(allreduce, tmp_path):
     assert th["dense_check"]["passed"], th["dense_check"]
     assert th["gemm_kernel_mix"]["agreed_across_ranks"] is True
 
+
+
+def test_collectives_sweep_across_gpus(tmp_path):
+    """the sweep engine itself across GPUs — cli.collectives 1D (9 ops,
+    2 reference sizes, --validate) and 3D (RCCL and --direct-ipc), cli.stats, cli.compare against
+    the reference CSVs; every record validated, busBW > 0, none refused by the roofline guard."""
+    from sweep_pipeline import check_pipeline, run_pipeline
+
+    n = _ngpus()
+    res = run_pipeline(tmp_path, n, backend="rccl", direct_ipc=True, timeout=900)
+    check_pipeline(res, n)

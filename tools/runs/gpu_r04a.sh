@@ -5,5 +5,5 @@ export TMPDIR=/tmp
 O=gpurun_out/r04a
 mkdir -p $O
 T="python -u -m pytest -x -v --timeout 600 --timeout-method thread"
-/usr/bin/time -v timeout -k 10 400 python bench.py > $O/bench_w1.json 2> $O/bench_w1.err || exit $?
+S=$(date +%s); timeout -k 10 400 python bench.py > $O/bench_w1.json 2> $O/bench_w1.err || exit $?; echo "bench wall $(( $(date +%s) - S )) s" > $O/bench_wall.txt
 timeout -k 10 900 $T tests/test_comm_gpu.py -k "bench_py or ddp_matches_global" > $O/tests.log 2>&1 || exit $?

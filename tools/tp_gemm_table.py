@@ -5,7 +5,8 @@ interleaved rounds, uniform random operands (CDNA guide §5.4 rules 24/25). One 
     python tools/tp_gemm_table.py [--model 7B] [--ps 1,2,4,8] [--rounds 5] [--modes auto]
 
 ``--modes``: comma list of our-kernel variants to time: ``auto`` = the library dispatch
-(``DLBB_GEMM=mfma``), ``t128`` / ``t256`` force the tile, ``s<N>`` = set_stagger(N).
+(``DLBB_GEMM=mfma``), ``t128`` / ``t256`` force the tile, ``s<N>`` = set_stagger(N), ``v192`` =
+the 256 x 192 tile variant (N % 192 == 0 shapes only). ``--gpt2`` adds the GPT-2 forward GEMMs.
 """
 import argparse
 import json
@@ -61,6 +62,8 @@ def main():
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--modes", default="auto")
     ap.add_argument("--lmhead", action="store_true", help="also the GPT-2 LM head forward")
+    ap.add_argument("--gpt2", action="store_true",
+                    help="also every GPT-2-small forward GEMM (B16 x T1024 = 16384 tokens)")
     ap.add_argument("--shapes", default=None, help="comma list of case names to keep")
     args = ap.parse_args()
     os.environ["DLBB_GEMM"] = "mfma"
@@ -68,8 +71,11 @@ def main():
     shapes = []
     for P in [int(p) for p in args.ps.split(",")]:
         shapes += tp_shapes(args.model, P, args.tokens)
-    if args.lmhead:
+    if args.lmhead or args.gpt2:
         shapes.append(("gpt2_lmhead", 16384, 50304, 768))
+    if args.gpt2:
+        shapes += [("gpt2_qkv", 16384, 2304, 768), ("gpt2_proj", 16384, 768, 768),
+                   ("gpt2_fc", 16384, 3072, 768), ("gpt2_mproj", 16384, 768, 3072)]
     if args.shapes:
         keep = set(args.shapes.split(","))
         shapes = [s for s in shapes if s[0] in keep]
@@ -79,22 +85,29 @@ def main():
         w = (torch.rand(N, K, device="cuda", generator=g) * 2 - 1).to(torch.bfloat16)
         ref = (x.float() @ w.float().t())
         errs = {}
-        for m in modes:
+        ms = [m for m in modes if m != "v192" or gemm.mfma192_ok(M, N)]
+        out = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+
+        def run(m):
+            if m == "v192":      # 256 x 192 tiles (variant 1)
+                return gemm._mfma192_linear(x, w, None, None, None, out, None)
+            return ops.linear(x, w)
+        for m in ms:
             set_mode(m)
-            y = ops.linear(x, w)
+            y = run(m)
             errs[m] = float((y.float() - ref).abs().max() / ref.abs().max())
-        best = {m: 1e9 for m in modes}
+        best = {m: 1e9 for m in ms}
         best_blas = 1e9
         for _ in range(args.rounds):
-            for m in modes:
+            for m in ms:
                 set_mode(m)
-                best[m] = min(best[m], timed(lambda: ops.linear(x, w), args.iters))
+                best[m] = min(best[m], timed(lambda: run(m), args.iters))
             best_blas = min(best_blas, timed(lambda: torch.matmul(x, w.t()), args.iters))
         set_mode("auto")
         fl = 2.0 * M * N * K
         print(json.dumps({"case": name, "M": M, "N": N, "K": K,
-                          **{f"{m}_ms": round(best[m] * 1e3, 4) for m in modes},
-                          **{f"{m}_tflops": round(fl / best[m] / 1e12, 1) for m in modes},
+                          **{f"{m}_ms": round(best[m] * 1e3, 4) for m in ms},
+                          **{f"{m}_tflops": round(fl / best[m] / 1e12, 1) for m in ms},
                           "blas_ms": round(best_blas * 1e3, 4),
                           "blas_tflops": round(fl / best_blas / 1e12, 1),
                           "ours_vs_blas": round(best_blas / min(best.values()), 3),
