@@ -83,9 +83,13 @@ def _baseline_configs(comm, args) -> dict:
     from distributed_llm_backend_benchmark_amd.bench import baseline_configs as bc
 
     comm.cpu_group()        # host side channel for the sections' failure agreement (collective)
-    grid = _shapes(args.grid) if args.grid else bc.GRID_3D
-    moe = _shapes(args.moe) if args.moe else bc.MOE_PAYLOADS
+    gpu = comm.is_gpu
+    # CPU (gloo plumbing) runs default to reduced shapes — the BASELINE shapes are GPU sizes
+    grid = _shapes(args.grid) if args.grid else (bc.GRID_3D if gpu else [(1, 512, 1024)])
+    moe = _shapes(args.moe) if args.moe else (bc.MOE_PAYLOADS if gpu else [(512, 1024)])
     model = None
+    if not gpu and not args.ddp_model:
+        model = dict(n_layer=2, n_head=2, n_embd=64, vocab=256, batch=2, seq=32)
     if args.ddp_model:
         keys = ("n_layer", "n_head", "n_embd", "vocab", "batch", "seq")
         model = dict(zip(keys, (int(v) for v in args.ddp_model.split(","))))

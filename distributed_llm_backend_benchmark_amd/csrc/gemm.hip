@@ -1032,21 +1032,28 @@ __device__ __forceinline__ void wait_vm() {
 // NJ: MFMA column fragments per wave — 4 (256-wide tile) or 3 (256 x 192, NT only; see
 // stage_b192). NBI = B DMA instructions per staging wave per K-tile (2 NJ): every counted wait
 // below is written in it (NJ = 4 gives the original literals).
-template <bool NN, bool BAL = false, bool TN = false, bool STAMP = false, int NJ = 4>
+// PHASES (diagnostic only, dlbb_gemm_nt_phase_probe): thread 0 stamps start / first MFMA (after
+// the prologue waits) / end of the K-loop / end of the stores: 4 u64 per workgroup into `st`.
+template <bool NN, bool BAL = false, bool TN = false, bool STAMP = false, int NJ = 4,
+          bool PHASES = false>
 __device__ __forceinline__ void pingpong_body(GemmArgs a, char* smem, uint64_t* st = nullptr) {
   static_assert(NJ == 4 || (NJ == 3 && !NN && !TN), "192-wide tiles: NT only");
   constexpr int NBI = 2 * NJ;                 // B DMA instructions per staging wave per K-tile
   constexpr int kTileB = NJ * 64 * BK * 2;    // bytes of one B tile buffer
   uint64_t t_start = 0;
-  if constexpr (STAMP) t_start = stamp_now();
-  if (NN && gridDim.y > 1) {         // split-K slice blockIdx.y (wave-uniform, SGPR math)
+  if constexpr (STAMP || PHASES) t_start = stamp_now();
+  uint64_t t_first = 0, t_loop = 0;
+  if (gridDim.y > 1) {               // split-K slice blockIdx.y (wave-uniform, SGPR math)
     const int s = blockIdx.y, nkt = static_cast<int>(a.K / BK);
     const int kt0 = s * a.kt_split, kt1 = kt0 + a.kt_split < nkt ? kt0 + a.kt_split : nkt;
     if constexpr (TN)                  // TN: A is row-major over the reduction too
       a.A += static_cast<int64_t>(kt0) * BK * a.lda;
     else
       a.A += static_cast<int64_t>(kt0) * BK;
-    a.B += static_cast<int64_t>(kt0) * BK * a.ldb;
+    if constexpr (NN)                  // NN / TN: B row-major over the reduction
+      a.B += static_cast<int64_t>(kt0) * BK * a.ldb;
+    else                               // NT: B [N][K], the slice is a column offset
+      a.B += static_cast<int64_t>(kt0) * BK;
     a.K = static_cast<int64_t>(kt1 - kt0) * BK;
     a.C = static_cast<float*>(a.C) + static_cast<int64_t>(s) * a.M * a.ldc;
   }
@@ -1146,6 +1153,7 @@ __device__ __forceinline__ void pingpong_body(GemmArgs a, char* smem, uint64_t* 
       DLBB_WAIT_VM(0);
     }
     __builtin_amdgcn_s_barrier();
+    if constexpr (PHASES) t_first = stamp_now();
     int cb = 0;                                       // B buffer of tile u
     for (int u = 0; u < nk; ++u) {
       const char* ab = abuf0 + (u & 1) * kTile2Bytes;
@@ -1185,6 +1193,7 @@ __device__ __forceinline__ void pingpong_body(GemmArgs a, char* smem, uint64_t* 
       __builtin_amdgcn_s_barrier();                   // end of interval 2u+1
       cb = cb == 2 ? 0 : cb + 1;
     }
+    if constexpr (PHASES) t_loop = stamp_now();
   } else {
     // prologue, row 1: A-hi(0), A-lo(1)
     DLBB_STAGE_A(0, abuf0, 1, stage_a_half(ra, lda2, rows_a, 0, abuf0, 1, wc, aoff));
@@ -1229,6 +1238,16 @@ __device__ __forceinline__ void pingpong_body(GemmArgs a, char* smem, uint64_t* 
     __syncthreads();
     if (threadIdx.x == 0) stamp_write(st, t_start);
   }
+  if constexpr (PHASES) {
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      uint64_t* r = st + 4 * (blockIdx.x + static_cast<uint64_t>(blockIdx.y) * gridDim.x);
+      r[0] = t_start;
+      r[1] = t_first;
+      r[2] = t_loop;
+      r[3] = stamp_now();
+    }
+  }
 #undef DLBB_STAGE_A
 }
 
@@ -1252,6 +1271,16 @@ __global__ void __launch_bounds__(kThreads2, 1) gemm_bf16_nt_192_pingpong3(GemmA
 __global__ void __launch_bounds__(kThreads2, 1) gemm_bf16_nt_192_pingpong3_bal(GemmArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   pingpong_body<false, true, false, false, 3>(a, smem);
+}
+
+// phase-stamped twins (diagnostic): tools/diag/pp_phases.py
+__global__ void __launch_bounds__(kThreads2, 1) gemm_nt_pp_phases(GemmArgs a, uint64_t* st) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  pingpong_body<false, true, false, false, 4, true>(a, smem, st);
+}
+__global__ void __launch_bounds__(kThreads2, 1) gemm_nt_pp192_phases(GemmArgs a, uint64_t* st) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  pingpong_body<false, true, false, false, 3, true>(a, smem, st);
 }
 
 // dgrad: C[M, N] = A[M, K] · B[K, N] (B row-major over the reduction); host contract
@@ -1937,6 +1966,121 @@ DLBB_API int dlbb_gemm_get_stagger() { return dlbb_gemm_stagger; }
 DLBB_API void dlbb_gemm_set_persist_epi(int on) { dlbb_persist_epi = on ? 1 : 0; }
 DLBB_API void dlbb_gemm_set_concurrent(int on) { dlbb_gemm_concurrent = on; }
 DLBB_API void dlbb_gemm_set_bal(int mode) { dlbb_gemm_bal = mode >= 0 && mode <= 2 ? mode : 2; }
+
+// ---------------------------------------------------------------------------------------
+// NT split-K (grids well below one round of the CUs — the 7B TP projections at P = 8: 96-128
+// tiles on 256 CUs — VERDICT r03 item 2): slice s of the reduction writes fp32 partials
+// [M][N] into ws + s M N (ping-pong body, plain fp32 epilogue), then ONE pass sums the slices
+// and applies the whole epilogue: + bias -> pre-activation store -> GELU -> + residual ->
+// bf16 | fp32 store. 4 consecutive columns per thread (N % 4 == 0, 8-B aligned rows).
+__global__ void __launch_bounds__(256) nt_split_epilogue_kernel(
+    const float* __restrict__ ws, int split, int64_t M, int64_t N, const uint16_t* bias,
+    const uint16_t* residual, int64_t ldr, uint16_t* preact, void* C, int64_t ldc, int out_f32,
+    int epi) {
+  const int64_t nq = N >> 2, total = M * nq, slab = M * N;
+  for (int64_t q = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; q < total;
+       q += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    const int64_t m = q / nq, n = (q - m * nq) << 2;
+    const float* p = ws + m * N + n;
+    float4 v = *reinterpret_cast<const float4*>(p);
+    for (int s = 1; s < split; ++s) {
+      const float4 w = *reinterpret_cast<const float4*>(p + s * slab);
+      v.x += w.x; v.y += w.y; v.z += w.z; v.w += w.w;
+    }
+    float x[4] = {v.x, v.y, v.z, v.w};
+    if (epi & EPI_BIAS) {
+      const u16x4 b = *reinterpret_cast<const u16x4*>(bias + n);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) x[c] += bf16_to_f32(b[c]);
+    }
+    if (preact)
+      *reinterpret_cast<u16x4*>(preact + m * ldc + n) =
+          u16x4{f32_to_bf16(x[0]), f32_to_bf16(x[1]), f32_to_bf16(x[2]), f32_to_bf16(x[3])};
+#pragma unroll
+    for (int c = 0; c < 4; ++c) x[c] = apply_act(x[c], epi);
+    if (epi & EPI_RESIDUAL) {
+      const u16x4 r = *reinterpret_cast<const u16x4*>(residual + m * ldr + n);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) x[c] += bf16_to_f32(r[c]);
+    }
+    if (out_f32)
+      *reinterpret_cast<float4*>(static_cast<float*>(C) + m * ldc + n) =
+          make_float4(x[0], x[1], x[2], x[3]);
+    else
+      *reinterpret_cast<u16x4*>(static_cast<uint16_t*>(C) + m * ldc + n) =
+          u16x4{f32_to_bf16(x[0]), f32_to_bf16(x[1]), f32_to_bf16(x[2]), f32_to_bf16(x[3])};
+  }
+}
+
+// Split-K NT GEMM: nj = 4 (256² tiles, N % 64 == 0) or 3 (256 x 192, N % 192 == 0); ws holds
+// split x M x N floats (16-B aligned). Same result contract as dlbb_gemm_bf16_nt except the
+// dGELU epilogues (forward only).
+DLBB_API int dlbb_gemm_bf16_nt_sk(const void* A, int64_t lda, const void* B, int64_t ldb, void* C,
+                                  int64_t ldc, int64_t M, int64_t N, int64_t K, const void* bias,
+                                  const void* residual, int64_t ldr, void* preact, int epi,
+                                  int out_f32, int nj, int split, float* ws,
+                                  hipStream_t stream) {
+  if (M <= 0 || N <= 0) return hipSuccess;
+  const int64_t nkt = K / BK;
+  if (K <= 0 || K % BK != 0 || split < 2 || split > nkt || !ws) return hipErrorInvalidValue;
+  if (lda % 8 || ldb % 8 || ldc % 4 || M % 8 || M < 8) return hipErrorInvalidValue;
+  if ((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(B) |
+       reinterpret_cast<uintptr_t>(ws)) & 15)
+    return hipErrorInvalidValue;
+  if (nj == 3 ? N % 192 != 0 : (nj != 4 || N % 64 != 0)) return hipErrorInvalidValue;
+  if (lda * 2 * 256 + K * 2 >= (1LL << 31) || ldb * 2 * 256 + K * 2 >= (1LL << 31))
+    return hipErrorInvalidValue;
+  if (epi & ~(EPI_BIAS | EPI_GELU_ERF | EPI_GELU_TANH | EPI_RESIDUAL)) return hipErrorInvalidValue;
+  if ((epi & EPI_BIAS) && (!bias || (reinterpret_cast<uintptr_t>(bias) & 7)))
+    return hipErrorInvalidValue;
+  if ((epi & EPI_RESIDUAL) && (!residual || ldr % 4 || (reinterpret_cast<uintptr_t>(residual) & 7)))
+    return hipErrorInvalidValue;
+  if ((reinterpret_cast<uintptr_t>(C) & 15) || (preact && (reinterpret_cast<uintptr_t>(preact) & 7)))
+    return hipErrorInvalidValue;
+  GemmArgs a{static_cast<const uint16_t*>(A), static_cast<const uint16_t*>(B), ws, nullptr,
+             nullptr, nullptr, M, N, K, lda, ldb, N, 0, 0, 1, 1, 0};
+  a.kt_split = static_cast<int>((nkt + split - 1) / split);
+  split = static_cast<int>((nkt + a.kt_split - 1) / a.kt_split);   // no empty trailing slice
+  const int64_t tiles = ((M + BM2 - 1) / BM2) * ((N + 64 * nj - 1) / (64 * nj));
+  const dim3 g(static_cast<unsigned>(tiles), static_cast<unsigned>(split)), b(kThreads2);
+  const bool bal = use_bal(a.kt_split, false);
+  if (nj == 3) {
+    if (bal) hipLaunchKernelGGL(gemm_bf16_nt_192_pingpong3_bal, g, b, kPP192Lds, stream, a);
+    else hipLaunchKernelGGL(gemm_bf16_nt_192_pingpong3, g, b, kPP192Lds, stream, a);
+  } else {
+    if (bal) hipLaunchKernelGGL(gemm_bf16_nt_256_pingpong3_bal, g, b, kPP6Lds, stream, a);
+    else hipLaunchKernelGGL(gemm_bf16_nt_256_pingpong3, g, b, kPP6Lds, stream, a);
+  }
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  const int64_t work = M * (N / 4);
+  const int64_t blocks = (work + 255) / 256 < 4096 ? (work + 255) / 256 : 4096;
+  hipLaunchKernelGGL(nt_split_epilogue_kernel, dim3(static_cast<unsigned>(blocks)), dim3(256), 0,
+                     stream, ws, split, M, N, static_cast<const uint16_t*>(bias),
+                     static_cast<const uint16_t*>(residual), ldr, static_cast<uint16_t*>(preact),
+                     C, ldc, out_f32, epi);
+  return hipGetLastError();
+}
+
+// Diagnostic: one plain bf16 NT GEMM on the balanced ping-pong (nj = 4: 256², 3: 256 x 192) with
+// per-workgroup phase stamps (4 u64 each: start, first MFMA, K-loop end, stores end) into recs
+// (gridDim.x records). Contract as the ping-pong; no autotuning, no epilogue.
+DLBB_API int dlbb_gemm_nt_phase_probe(const void* A, int64_t lda, const void* B, int64_t ldb,
+                                      void* C, int64_t M, int64_t N, int64_t K, int nj,
+                                      uint64_t* recs, hipStream_t stream) {
+  if (M % 8 || (nj == 3 ? N % 192 : N % 64) || K % BK || K < 2 * BK || !recs)
+    return hipErrorInvalidValue;
+  GemmArgs a{static_cast<const uint16_t*>(A), static_cast<const uint16_t*>(B), C, nullptr,
+             nullptr, nullptr, M, N, K, lda, ldb, N, 0, 0, 0, 1, 0};
+  const int64_t tiles = ((M + BM2 - 1) / BM2) * ((N + 64 * nj - 1) / (64 * nj));
+  if (nj == 3)
+    hipLaunchKernelGGL(gemm_nt_pp192_phases, dim3(static_cast<unsigned>(tiles)), dim3(kThreads2),
+                       kPP192Lds, stream, a, recs);
+  else
+    hipLaunchKernelGGL(gemm_nt_pp_phases, dim3(static_cast<unsigned>(tiles)), dim3(kThreads2),
+                       kPP6Lds, stream, a, recs);
+  return hipGetLastError();
+}
 
 // NT GEMM with an explicit kernel variant (the autotuner's candidates, ops/gemm.py):
 //   0 = the size heuristic below (256² ping-pong / persistent / 128² small grids)

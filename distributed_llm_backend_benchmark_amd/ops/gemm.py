@@ -226,6 +226,81 @@ def mfma192_ok(M: int, N: int) -> bool:
     return N % 192 == 0 and M % 8 == 0 and M >= 8
 
 
+_NCU = {}
+
+
+def _num_cus(device) -> int:
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    if idx not in _NCU:
+        _NCU[idx] = torch.cuda.get_device_properties(idx).multi_processor_count
+    return _NCU[idx]
+
+
+def nt_split_plan(M: int, N: int, K: int, nj: int, ncu: int) -> int:
+    """Split-K factor for the NT ping-pong on a grid well below one round of the CUs (1 = no
+    split): the smallest split whose grid fills >= 90 % of its last round (else the best fill),
+    keeping >= 8 K-tiles per slice. 7B TP at P = 8, 4096 x 1536 x 4096 on 256² tiles: 96 tiles
+    -> split 5 (480 of 512 slots); on 256 x 192 tiles 128 -> split 2 (one full round)."""
+    tiles = -(-M // 256) * -(-N // (64 * nj))
+    nkt = K // 64
+    if tiles <= 0 or tiles >= 0.75 * ncu:
+        return 1
+    best, best_fill = 1, tiles / (-(-tiles // ncu) * ncu)
+    for sp in range(2, 9):
+        if nkt // sp < 8:
+            break
+        n = tiles * sp
+        fill = n / (-(-n // ncu) * ncu)
+        if fill >= 0.9:
+            return sp
+        if fill > best_fill + 1e-9:
+            best, best_fill = sp, fill
+    return best
+
+
+def _mfma_sk_linear(x2, w, bias, act, r2, out, preact, nj: int = 4):
+    """Split-K NT ping-pong (fp32 partials, one fused reduce + epilogue pass): grids well below
+    one round of the CUs (``csrc/gemm.hip`` ``dlbb_gemm_bf16_nt_sk``)."""
+    M, K = x2.shape
+    N = w.shape[0]
+    split = nt_split_plan(M, N, K, nj, _num_cus(x2.device))
+    if split < 2:
+        return _mfma_linear(x2, w, bias, act, r2, out, preact, variant=1 if nj == 3 else 0)
+    epi = ACTS[act]
+    if bias is not None:
+        epi |= EPI_BIAS
+    if r2 is not None:
+        epi |= EPI_RESIDUAL
+    ws = torch.empty(split * M * N, dtype=torch.float32, device=x2.device)
+    check(_lib.lib().dlbb_gemm_bf16_nt_sk(
+        x2.data_ptr(), x2.stride(0), w.data_ptr(), w.stride(0), out.data_ptr(), out.stride(0),
+        M, N, K, _lib.ptr(bias), _lib.ptr(r2), r2.stride(0) if r2 is not None else 0,
+        _lib.ptr(preact), epi, 1 if out.dtype == torch.float32 else 0, int(nj), int(split),
+        ws.data_ptr(), _lib.stream(x2.device)), "gemm_bf16_nt_sk")
+    return out
+
+
+def _mfma192_sk_linear(x2, w, bias, act, r2, out, preact):
+    return _mfma_sk_linear(x2, w, bias, act, r2, out, preact, nj=3)
+
+
+def mfma_sk_ok(x2, w, r2, out, preact, nj: int) -> bool:
+    """Contract of the split-K candidates (host-checked again in C) and a split >= 2 plan."""
+    M, K = x2.shape
+    N = w.shape[0]
+    if nj == 3 and not mfma192_ok(M, N):
+        return False
+    if nj == 4 and (N % 64 or M % 8):
+        return False
+    al = lambda t: t is None or t.data_ptr() % 16 == 0  # noqa: E731
+    if not (al(out) and al(preact) and al(r2) and out.stride(0) % 4 == 0
+            and (r2 is None or r2.stride(0) % 4 == 0)):
+        return False
+    if (x2.stride(0) * 512 + K * 2) >= 2 ** 31 or (w.stride(0) * 512 + K * 2) >= 2 ** 31:
+        return False
+    return nt_split_plan(M, N, K, nj, _num_cus(x2.device)) >= 2
+
+
 _APPROX = {"gelu": 0, "gelu_erf": 0, "gelu_tanh": 1}
 
 
@@ -260,8 +335,12 @@ def _blas_linear(x2, w, bias, act, r2, out, preact):
     return out
 
 
-CHOICES = {}          # (M, N, K, epi-signature) -> "mfma" | "mfma192" | "blas"
+CHOICES = {}          # (M, N, K, epi-signature) -> "mfma" | "mfma192" | "mfma_sk" | ... | "blas"
 CALLS = {}            # ("linear" | "wgrad", key) -> calls since import (kernel-mix accounting)
+# Split-K (_mfma_sk_linear) is NOT an autotune candidate: measured 1.1-1.7x slower than the
+# ping-pong on every sub-round TP shape (7B P = 8: qkv 0.102 / 0.065 ms split on 256² / 256 x 192
+# vs 0.059 unsplit; profiles/r04_gemm/gemm_table.jsonl) — a workgroup's fixed cost (prologue,
+# C store, launch: ~10 us) is paid per slice, and the partial slabs add a pass. Kept for A/B.
 _IMPLS = {"mfma": _mfma_linear, "mfma192": _mfma192_linear, "blas": _blas_linear}
 
 

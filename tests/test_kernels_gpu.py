@@ -846,3 +846,54 @@ def test_gemm_autotune_beside_comm_keeps_to_hand_written_kernels(monkeypatch):
     ref = x.float() @ w.float().t()
     torch.testing.assert_close(y, ref, rtol=2e-3, atol=2e-3 * 512 ** 0.5)
     assert gemm._CONCURRENT[0] == 0
+
+
+@pytest.mark.parametrize("M,N,K,nj", [(4096, 1536, 4096, 4), (4096, 1536, 4096, 3),
+                                      (4096, 2048, 4096, 4), (520, 384, 2048, 3),
+                                      (1000, 640, 1024, 4)])
+@pytest.mark.parametrize("epi", ["plain_f32", "bias_gelu_pre_res", "plain_bf16"])
+def test_gemm_nt_split_k_matches_fp32(M, N, K, nj, epi):
+    """Split-K NT ping-pong (fp32 partial slabs + one fused reduce / epilogue pass) for grids
+    well below one round of the CUs, against fp32: ragged M, 256² and 256 x 192 tiles, the
+    whole epilogue chain."""
+    from distributed_llm_backend_benchmark_amd.ops import gemm
+
+    x = _randn(M, K, seed=51, scale=0.3)
+    w = _randn(N, K, seed=52, scale=0.3)
+    b = _randn(N, seed=53)
+    r = _randn(M, N, seed=54)
+    ncu = torch.cuda.get_device_properties(0).multi_processor_count
+    assert gemm.nt_split_plan(M, N, K, nj, ncu) >= 2
+    u = x.float() @ w.float().t()
+    if epi == "plain_f32":
+        y = torch.empty(M, N, dtype=torch.float32, device=DEV)
+        assert gemm.mfma_sk_ok(x, w, None, y, None, nj)
+        gemm._mfma_sk_linear(x, w, None, None, None, y, None, nj=nj)
+        torch.testing.assert_close(y, u, rtol=2e-3, atol=2e-3 * K ** 0.5)
+    elif epi == "plain_bf16":
+        y = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+        gemm._mfma_sk_linear(x, w, None, None, None, y, None, nj=nj)
+        torch.testing.assert_close(y.float(), u, rtol=2e-2, atol=2e-2 * K ** 0.5)
+    else:
+        y = torch.empty(M, N, dtype=torch.float32, device=DEV)
+        pre = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+        gemm._mfma_sk_linear(x, w, b, "gelu", r, y, pre, nj=nj)
+        ub = u + b.float()
+        torch.testing.assert_close(y, F.gelu(ub) + r.float(), rtol=2e-3, atol=2e-3 * K ** 0.5)
+        torch.testing.assert_close(pre.float(), ub, rtol=2e-2, atol=2e-2 * K ** 0.5)
+    torch.cuda.synchronize()
+
+
+def test_gemm_autotune_offers_tile_variants(monkeypatch):
+    """The linear autotuner times the 256 x 192 candidate where its contract holds, and records
+    whichever it picks."""
+    from distributed_llm_backend_benchmark_amd.ops import gemm, linear
+
+    monkeypatch.setenv("DLBB_GEMM", "auto")
+    x = _randn(4096, 4096, seed=61, scale=0.3)
+    w = _randn(1536, 4096, seed=62, scale=0.3)
+    y = linear(x, w)
+    torch.testing.assert_close(y.float(), x.float() @ w.float().t(), rtol=2e-2, atol=1.5)
+    kind, key, times, best = gemm.TUNE_LOG[-1]
+    assert set(times) == {"mfma", "mfma192", "blas"}, times
+    assert gemm.CHOICES[key] == best

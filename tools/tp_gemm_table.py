@@ -6,7 +6,8 @@ interleaved rounds, uniform random operands (CDNA guide §5.4 rules 24/25). One 
 
 ``--modes``: comma list of our-kernel variants to time: ``auto`` = the library dispatch
 (``DLBB_GEMM=mfma``), ``t128`` / ``t256`` force the tile, ``s<N>`` = set_stagger(N), ``v192`` =
-the 256 x 192 tile variant (N % 192 == 0 shapes only). ``--gpt2`` adds the GPT-2 forward GEMMs.
+the 256 x 192 tile variant (N % 192 == 0 shapes only), ``sk`` / ``sk192`` = split-K on 256² /
+256 x 192 tiles (grids well below one round only). ``--gpt2`` adds the GPT-2 forward GEMMs.
 """
 import argparse
 import json
@@ -49,7 +50,7 @@ def set_mode(m):
         gemm.set_tile(128)
     elif m == "t256":
         gemm.set_tile(256)
-    elif m.startswith("s"):
+    elif m.startswith("s") and m[1:].isdigit():
         gemm.set_stagger(int(m[1:]))
 
 
@@ -85,12 +86,18 @@ def main():
         w = (torch.rand(N, K, device="cuda", generator=g) * 2 - 1).to(torch.bfloat16)
         ref = (x.float() @ w.float().t())
         errs = {}
-        ms = [m for m in modes if m != "v192" or gemm.mfma192_ok(M, N)]
         out = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+        ok = {"v192": gemm.mfma192_ok(M, N),
+              "sk": gemm.mfma_sk_ok(x, w, None, out, None, 4),
+              "sk192": gemm.mfma_sk_ok(x, w, None, out, None, 3)}
+        ms = [m for m in modes if ok.get(m, True)]
 
         def run(m):
             if m == "v192":      # 256 x 192 tiles (variant 1)
                 return gemm._mfma192_linear(x, w, None, None, None, out, None)
+            if m in ("sk", "sk192"):      # split-K ping-pong + fused reduce / epilogue
+                return gemm._mfma_sk_linear(x, w, None, None, None, out, None,
+                                            nj=3 if m == "sk192" else 4)
             return ops.linear(x, w)
         for m in ms:
             set_mode(m)
