@@ -10,7 +10,8 @@ change:
   ``collectives/3d/openmpi.py:55-70`` / ``3d/dsccl.py:60-70``), through RCCL (torch process
   group), our native C++ RCCL engine and the direct one-hop IPC kernels (P > 1).
 * **config 4** — MoE-shaped uneven all-to-all (expert-parallel dispatch; the reference only has
-  the equal-split ``alltoall``, ``collectives/1d/openmpi.py:154-171``) at two token payloads.
+  the equal-split ``alltoall``, ``collectives/1d/openmpi.py:154-171``) at two token payloads,
+  through RCCL, the native engine and our one-hop IPC all-to-all-v kernel.
 * **config 5** — a GPT-2-small DDP training step, B16 x T1024 per GPU (the reference's only
   data-parallel step is ``test/ccl.py:92-115``), once per bucket all-reduce path
   (``auto`` / ``rccl`` / ``native`` / ``custom``), the fastest on rank-max ms/step reported.
@@ -261,7 +262,7 @@ def moe_alltoall(comm: Comm, budget: Budget, payloads: Sequence[Tuple[int, int]]
         shape = (tokens, hidden)
         data = local_step(comm, lambda: make_data(shape, torch.bfloat16, comm.rank, comm.device))
         cells = {label: _measure(comm, "alltoall_moe", shape, data, label, opts, iters)
-                 for label, opts in _candidates(comm, direct=False)}
+                 for label, opts in _candidates(comm)}
         best = _best(cells)
         rows.append({"tokens_per_rank": tokens, "hidden": hidden,
                      "bytes_per_rank": data.numel() * data.element_size(),

@@ -68,6 +68,11 @@ struct CarKernelArgs {
   int rank;
   int world;
   uint64_t timeout_ticks;       // wait bound, s_memrealtime ticks (dlbb_car_set_timeout_ms)
+  // uneven all-to-all (K_A2AV, MoE dispatch): bytes this rank pulls from peer p, at v_src[p] in
+  // p's registered input, landing at v_dst[p] in out (all multiples of 16)
+  int64_t v_src[kMaxRanks];
+  int64_t v_cnt[kMaxRanks];
+  int64_t v_dst[kMaxRanks];
 };
 
 // Every kernel body takes its workgroup index `bid` and workgroup count `nb` explicitly instead of
@@ -501,6 +506,41 @@ __device__ __forceinline__ void a2a_body(const CarKernelArgs& a, unsigned bid, u
   pull_body<W, true>(a, bid, nb);
 }
 
+//   uneven all-to-all (MoE expert-parallel dispatch, top-k router splits): from every peer p
+//   out[v_dst[p] .. + v_cnt[p]) = in_p[v_src[p] .. + v_cnt[p]) — each GPU pulls its own tokens
+//   from all 7 peers at once, one hop per link (RCCL's all-to-all-v moves them peer by peer).
+//   Peers are visited from rank + 1 on so the 7 links start loaded evenly; 4 independent 16-B
+//   loads per thread and peer keep enough bytes in flight per link.
+template <int DT, int W>
+__device__ __forceinline__ void a2av_body(const CarKernelArgs& a, unsigned bid, unsigned nb) {
+  const uint32_t e = begin_epoch(a, bid, nb);
+  char* out = static_cast<char*>(a.out);
+  signal_peers(a, 0, e, bid);
+  if (!wait_peers(a, 0, e, bid)) return;
+  const int world = W > 0 ? W : a.world;
+#pragma unroll
+  for (int k = 0; k < (W > 0 ? W : kMaxRanks); ++k) {
+    if (W == 0 && k >= world) break;
+    const int p = W > 0 ? (a.rank + k) & (W - 1) : (a.rank + k) % world;
+    int64_t v0, v1;
+    split_range(a.v_cnt[p] / 16, bid, nb, v0, v1);
+    const u16x8* src = reinterpret_cast<const u16x8*>(a.data[p] + a.v_src[p]);
+    u16x8* dst = reinterpret_cast<u16x8*>(out + a.v_dst[p]);
+    const int64_t bs = blockDim.x;
+    int64_t v = v0 + threadIdx.x;
+    for (; v + 3 * bs < v1; v += 4 * bs) {
+      const u16x8 t0 = src[v], t1 = src[v + bs], t2 = src[v + 2 * bs], t3 = src[v + 3 * bs];
+      dst[v] = t0;
+      dst[v + bs] = t1;
+      dst[v + 2 * bs] = t2;
+      dst[v + 3 * bs] = t3;
+    }
+    for (; v < v1; v += bs) dst[v] = src[v];
+  }
+  signal_peers(a, 2, e, bid);
+  wait_peers(a, 2, e, bid);
+}
+
 //   reduce-scatter : out[0 .. n/P) = sum_p in_p[rank * n/P .. ]   (fp32 accumulation)
 template <int DT, int W>
 __device__ __forceinline__ void rs_body(const CarKernelArgs& a, unsigned bid, unsigned nb) {
@@ -546,10 +586,11 @@ DLBB_CAR_KERNELS(car_twoshot_push_kernel, twoshot_push_body)
 DLBB_CAR_KERNELS(car_ag_kernel, ag_body)
 DLBB_CAR_KERNELS(car_a2a_kernel, a2a_body)
 DLBB_CAR_KERNELS(car_rs_kernel, rs_body)
+DLBB_CAR_KERNELS(car_a2av_kernel, a2av_body)
 #undef DLBB_CAR_KERNELS
 
 enum CarKind : int {
-  K_ONESHOT = 1, K_TWOSHOT = 2, K_REG = 3, K_PUSH = 4, K_AG = 5, K_A2A = 6, K_RS = 7
+  K_ONESHOT = 1, K_TWOSHOT = 2, K_REG = 3, K_PUSH = 4, K_AG = 5, K_A2A = 6, K_RS = 7, K_A2AV = 8
 };
 
 // Resolves (kind, DT, W) to the kernel symbol: per-rank form (VR = false) or virtual form.
@@ -569,6 +610,7 @@ const void* car_kernel_ptr(int kind) {
   if constexpr (DT == DT_BF16) {     // byte movers: one instantiation (dtype-free)
     if (kind == K_AG) return DLBB_CAR_PTR(car_ag_kernel);
     if (kind == K_A2A) return DLBB_CAR_PTR(car_a2a_kernel);
+    if (kind == K_A2AV) return DLBB_CAR_PTR(car_a2av_kernel);
   }
 #undef DLBB_CAR_PTR
   return nullptr;
@@ -576,7 +618,7 @@ const void* car_kernel_ptr(int kind) {
 
 template <bool VR>
 const void* car_kernel(int kind, int dtype, int world) {
-  if (kind == K_AG || kind == K_A2A) dtype = DT_BF16;
+  if (kind == K_AG || kind == K_A2A || kind == K_A2AV) dtype = DT_BF16;
   const int w = world == 2 || world == 4 || world == 8 ? world : 0;
 #define DLBB_CAR_W(D)                                        \
   switch (w) {                                               \
@@ -982,6 +1024,42 @@ DLBB_API int dlbb_car_allreduce_reg_push(void* h, int id, int64_t n, int dtype, 
                                          hipStream_t stream) {
   return car_launch_rank(static_cast<CarState*>(h), K_PUSH, nullptr, nullptr, n, dtype, id,
                          nblocks, stream);
+}
+
+// Uneven all-to-all on registration `id` (every rank registered its input, the same number of
+// bytes everywhere): pull cnt[p] bytes at src_off[p] of peer p's input into out + dst_off[p],
+// for every p (all multiples of 16, within the registration). Collective, like every direct kind.
+DLBB_API int dlbb_car_alltoallv_reg(void* h, int id, const int64_t* src_off, const int64_t* cnt,
+                                    const int64_t* dst_off, void* out, int nblocks,
+                                    hipStream_t stream) {
+  CarState* s = static_cast<CarState*>(h);
+  if (!s || !s->opened || !out || !src_off || !cnt || !dst_off) return hipErrorInvalidValue;
+  const RegBuf* r = car_reg(s, id);
+  if (!r) return hipErrorInvalidValue;
+  CarKernelArgs a = s->args;
+  a.timeout_ticks = g_car_timeout_ticks;
+  for (int p = 0; p < kMaxRanks; ++p) {
+    a.data[p] = r->ptr[p];
+    a.v_src[p] = a.v_cnt[p] = a.v_dst[p] = 0;
+  }
+  int64_t total = 0;
+  for (int p = 0; p < s->world; ++p) {
+    if (cnt[p] < 0 || src_off[p] < 0 || dst_off[p] < 0 || cnt[p] % 16 || src_off[p] % 16 ||
+        dst_off[p] % 16 || src_off[p] + cnt[p] > r->bytes)
+      return hipErrorInvalidValue;
+    a.v_src[p] = src_off[p];
+    a.v_cnt[p] = cnt[p];
+    a.v_dst[p] = dst_off[p];
+    total += cnt[p];
+  }
+  a.inp = r->ptr[s->rank];
+  a.out = out;
+  a.nbytes = total;
+  const void* fn = car_kernel<false>(K_A2AV, DT_BF16, s->world);
+  if (!fn) return hipErrorInvalidValue;
+  void* args[] = {&a};
+  CAR_CHECK(hipLaunchKernel(fn, dim3(clamp_blocks(nblocks)), dim3(kCarThreads), args, 0, stream));
+  return hipSuccess;
 }
 
 // Direct collectives on registration `id` (this rank's registered input; out is local).

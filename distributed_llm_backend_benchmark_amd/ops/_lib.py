@@ -138,6 +138,9 @@ _SIGS = {
     "dlbb_car_allreduce_reg_push": (c_int, [c_void_p, c_int, c_int64, c_int, c_int, c_void_p]),
     "dlbb_car_direct_reg": (c_int, [c_void_p, c_int, c_int, c_int64, c_int, c_void_p, c_int,
                                     c_void_p]),
+    "dlbb_car_alltoallv_reg": (c_int, [c_void_p, c_int, ctypes.POINTER(c_int64),
+                                       ctypes.POINTER(c_int64), ctypes.POINTER(c_int64), c_void_p,
+                                       c_int, c_void_p]),
     "dlbb_car_reg_close": (c_int, [c_void_p, c_int]),
     "dlbb_car_reg_counts": (c_int, [c_void_p, ctypes.POINTER(c_int), ctypes.POINTER(c_int)]),
     "dlbb_car_open_local": (c_int, [ctypes.POINTER(c_void_p), c_int]),

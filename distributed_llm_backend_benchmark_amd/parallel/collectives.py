@@ -16,7 +16,8 @@ reduce           ``1d/openmpi.py:148``, ``1d/dsccl.py:129`` ``dist.reduce`` root
 gather           ``1d/openmpi.py:113``, ``1d/dsccl.py:102`` ``dist.gather`` root 0
 scatter          ``1d/openmpi.py:134``, ``1d/dsccl.py:118`` ``dist.scatter`` root 0 (P copies of N)
 alltoall         ``1d/openmpi.py:167``, ``1d/dsccl.py:143`` ``all_to_all_single``, equal N/P splits
-alltoall_moe     —                                      uneven token splits (top-k router shaped)
+alltoall_moe     —                                      uneven token splits (top-k router shaped);
+                                                          ``direct`` = one-hop IPC pulls
 sendrecv         ``1d/openmpi.py:189-193``                ring ``batch_isend_irecv``
 ================ ====================================== =========================================
 
@@ -427,8 +428,25 @@ class AllToAllMoE(CollectiveOp):
         self.inp = self.data.reshape(-1)
         self.out = torch.empty(sum(self.out_splits), dtype=self.data.dtype,
                                device=self.data.device)
+        self._car = None
+        if self.opts.get("direct"):
+            # one-hop pulls over xGMI: this rank's tokens from every peer's registered input at
+            # once (parallel/custom_allreduce.py all_to_allv_registered)
+            if (hidden * self.data.element_size()) % 16:
+                raise RuntimeError("direct MoE all-to-all needs 16-byte token rows")
+            self._car, self._rid = _direct_ipc(self.comm, self.inp, 16 // self.data.element_size())
+            self._reg_owner = (self._car, self._rid)
+            me = self.rank
+            self._src = [sum(self.mat[p][:me]) for p in range(self.P)]
+            self._dst = [sum(self.out_splits[:p]) for p in range(self.P)]
+            self.impl = "custom"
 
     def run(self):
+        if self._car is not None:
+            self._car.all_to_allv_registered(self.inp, self._rid, self.out, self._src,
+                                             self.out_splits, self._dst,
+                                             nblocks=self.opts.get("nblocks"))
+            return
         dist.all_to_all_single(self.out, self.inp, output_split_sizes=self.out_splits,
                                input_split_sizes=self.in_splits)
 

@@ -258,6 +258,28 @@ class CustomAllReduce:
             raise ValueError("all_to_all_registered: in/out of world x chunk elements")
         return self._direct(DIRECT_A2A, t, rid, out, t.numel() // W * t.element_size(), nblocks)
 
+    def all_to_allv_registered(self, t: torch.Tensor, rid: int, out: torch.Tensor, src_off,
+                               counts, dst_off, nblocks: Optional[int] = None) -> torch.Tensor:
+        """Uneven all-to-all (MoE dispatch) on registration ``rid``: from every peer p,
+        ``out[dst_off[p] : + counts[p]] = t_p[src_off[p] : + counts[p]]`` (ELEMENTS, every
+        offset / count a multiple of 16 bytes). Collective; t registered with the same size on
+        every rank."""
+        W = self.comm.world_size
+        esz = t.element_size()
+        if not out.is_contiguous() or out.dtype != t.dtype or len(counts) != W:
+            raise ValueError("all_to_allv_registered: contiguous out of t's dtype, W counts")
+        if max(d + c for d, c in zip(dst_off, counts)) > out.numel():
+            raise ValueError("all_to_allv_registered: out too small for the receive layout")
+
+        def arr(vals):
+            return (ctypes.c_int64 * W)(*[int(v) * esz for v in vals])
+        total = sum(int(c) for c in counts) * esz
+        nb = nblocks or self.nblocks or int(min(256, max(8, total // (256 << 10))))
+        _lib.check(self.lib.dlbb_car_alltoallv_reg(self.h, rid, arr(src_off), arr(counts),
+                                                   arr(dst_off), out.data_ptr(), nb,
+                                                   _lib.stream(t.device)), "car_alltoallv_reg")
+        return out
+
     def reduce_scatter_registered(self, t: torch.Tensor, rid: int, out: torch.Tensor,
                                   nblocks: Optional[int] = None) -> torch.Tensor:
         """out = shard ``rank`` of sum_p t_p (fp32 accumulation; out n / world)."""

@@ -285,6 +285,18 @@ def _direct_worker(rank, world, n):
                     op.run()
                 torch.cuda.synchronize()
                 res.append((name, str(dt), nb, op.impl, op.check(ins)))
+    # uneven MoE all-to-all (one-hop pulls of this rank's tokens from every peer), tokens x hidden
+    for hidden in (1024, 8):
+        ins = [make_data((2000, hidden), torch.bfloat16, r, torch.device("cuda"))
+               for r in range(world)]
+        for nb in (None, 5, 256):
+            op = make_op("alltoall_moe", comm, ins[rank], direct=True, nblocks=nb)
+            for _ in range(3):
+                op.run()
+            torch.cuda.synchronize()
+            exact = torch.equal(op.result().float(), op.expected(ins))
+            res.append(("alltoall_moe", f"h{hidden}", nb, op.impl, exact))
+            op.close()
     comm.barrier()
     comm.destroy()
     return res
@@ -293,7 +305,8 @@ def _direct_worker(rank, world, n):
 @pytest.mark.parametrize("world", [2, 4, 8])
 def test_direct_ipc_collectives_ranks_on_one_gpu(world):
     """One-hop IPC all-gather / reduce-scatter / all-to-all (registered inputs, entry + exit
-    flag barriers) against closed forms, 2/4/8 ranks sharing one GPU, bf16 and fp32."""
+    flag barriers) and the uneven MoE all-to-all-v against closed forms (the all-to-alls bit
+    exact), 2/4/8 ranks sharing one GPU, bf16 and fp32."""
     res = run_multiprocess(_direct_worker, world, args=(world * 8 * 1000,), timeout=600)
     for r in res:
         for name, dt, nb, impl, ok in r:
@@ -632,6 +645,7 @@ def test_bench_py_two_ranks_rehearsal():
             assert row[op]["busbw_GBps"] > 0
     c4 = cfgs["config4_moe_alltoall"]
     assert "error" not in c4 and c4["rows"][0]["busbw_GBps"] > 0, c4
+    assert "ms" in c4["rows"][0]["by_impl"]["direct_ipc"], c4     # our all-to-all-v kernel
     c5 = cfgs["config5_gpt2_ddp"]
     assert "error" not in c5 and c5["best"] in ("auto", "rccl", "custom"), c5
     # native RCCL refuses two ranks on one GPU: recorded as an error for that path only

@@ -71,6 +71,7 @@ def test_bench_py_across_gpus():
             assert 0 < row[op]["busbw_GBps"] < 7 * 160, row
     c4 = cfgs["config4_moe_alltoall"]
     assert "error" not in c4 and all(0 < r["busbw_GBps"] < 7 * 160 for r in c4["rows"]), c4
+    assert all("ms" in r["by_impl"]["direct_ipc"] for r in c4["rows"]), c4
     c5 = cfgs["config5_gpt2_ddp"]
     assert "error" not in c5 and c5["global_batch"] == 16 * n, c5
     assert all("ms_per_step" in v for v in c5["by_allreduce"].values()), c5
