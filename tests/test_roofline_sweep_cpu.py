@@ -77,3 +77,33 @@ def test_reference_rows_pass_the_guard():
             seen += 1
             assert stats1d.refused(d) is None, f
     assert seen > 0
+
+
+def test_no_committed_csv_row_beats_the_roofline():
+    """every committed stats row (results/**) is physically possible. The
+    virtual-rank dataset (results/vr_custom: W ranks on ONE GPU) is bounded by the W ranks'
+    combined traffic on that device (colocated)."""
+    import csv
+    import glob
+
+    from distributed_llm_backend_benchmark_amd.stats.bandwidth import (KNOWN_OPS,
+                                                                        roofline_violation)
+
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    rows = 0
+    for path in glob.glob(os.path.join(repo, "results", "**", "*_ext.csv"), recursive=True):
+        coloc = "vr_custom" in path
+        for r in csv.DictReader(open(path)):
+            op = r["operation"]
+            if op not in KNOWN_OPS:
+                continue
+            if "median_time_ms" in r:
+                t = float(r["median_time_ms"]) / 1e3
+                nbytes = float(r.get("wire_bytes") or r["tensor_size_bytes"])
+            else:
+                t = float(r["median_time_us"]) / 1e6
+                nbytes = float(r["bytes"])
+            why = roofline_violation(op, nbytes, t, int(r["num_ranks"]), coloc)
+            assert why is None, (path, why)
+            rows += 1
+    assert rows > 100
