@@ -1965,6 +1965,7 @@ DLBB_API void dlbb_gemm_set_stagger(int on) { dlbb_gemm_stagger = on; }
 DLBB_API int dlbb_gemm_get_stagger() { return dlbb_gemm_stagger; }
 DLBB_API void dlbb_gemm_set_persist_epi(int on) { dlbb_persist_epi = on ? 1 : 0; }
 DLBB_API void dlbb_gemm_set_concurrent(int on) { dlbb_gemm_concurrent = on; }
+DLBB_API int dlbb_gemm_get_concurrent() { return dlbb_gemm_concurrent; }
 DLBB_API void dlbb_gemm_set_bal(int mode) { dlbb_gemm_bal = mode >= 0 && mode <= 2 ? mode : 2; }
 
 // ---------------------------------------------------------------------------------------

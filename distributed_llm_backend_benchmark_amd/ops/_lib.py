@@ -79,6 +79,7 @@ _SIGS = {
     "dlbb_gemm_set_bal": (None, [c_int]),
     "dlbb_gemm_set_persist_epi": (None, [c_int]),
     "dlbb_gemm_set_concurrent": (None, [c_int]),
+    "dlbb_gemm_get_concurrent": (c_int, []),
     "dlbb_gemm_wgrad_set_stages": (None, [c_int]),
     "dlbb_attn_set_xcd": (None, [c_int]),
     "dlbb_attn_set_concurrent": (None, [c_int]),

@@ -97,3 +97,19 @@ def test_wgrad_pingpong_tail_plan():
         if split > 1:
             kt = -(-nkt // split)
             assert (split - 1) * kt < nkt, (shape, split, kt)
+
+
+def test_concurrent_comm_switches_off_persistent_forms_in_the_library():
+    """inside gemm.concurrent_comm() (GEMMs beside comm kernels) the library's
+    persistent GEMM forms (grid = num CUs, all workgroups assumed resident) are off, nested
+    contexts included, and back on after."""
+    from distributed_llm_backend_benchmark_amd.ops import _lib, gemm
+
+    lib = _lib.lib()
+    assert lib.dlbb_gemm_get_concurrent() == 0
+    with gemm.concurrent_comm():
+        assert lib.dlbb_gemm_get_concurrent() == 1
+        with gemm.concurrent_comm():
+            assert lib.dlbb_gemm_get_concurrent() == 1
+        assert lib.dlbb_gemm_get_concurrent() == 1
+    assert lib.dlbb_gemm_get_concurrent() == 0
