@@ -279,7 +279,8 @@ def moe_alltoall(comm: Comm, budget: Budget, payloads: Sequence[Tuple[int, int]]
 def ddp_candidates(comm: Comm) -> List[str]:
     if comm.world_size == 1 or not comm.is_gpu:
         return ["rccl"]                     # world 1 / CPU: the process-group path only
-    return ["auto", "rccl", "native", "custom"]
+    # most likely fastest first: the time box may cut the tail of this list at P = 8
+    return ["auto", "native", "custom", "rccl"]
 
 
 def gpt2_ddp(comm: Comm, budget: Budget, steps: int = 10, warmup: int = 3,

@@ -1242,7 +1242,12 @@ __device__ __forceinline__ void pingpong_body(GemmArgs a, char* smem, uint64_t* 
     __syncthreads();
     if (threadIdx.x == 0) {
       uint64_t* r = st + 4 * (blockIdx.x + static_cast<uint64_t>(blockIdx.y) * gridDim.x);
-      r[0] = t_start;
+      // s_memrealtime (100 MHz) needs < 48 bits for days: the XCD id and HW_ID ride in the
+      // top 16 bits of the start stamp (xcc << 13 | se << 10 | cu << 6)
+      const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);     // HW_REG_HW_ID
+      const uint32_t xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20);   // HW_REG_XCC_ID
+      const uint64_t tag = ((xcc & 7u) << 13) | (((hw >> 13) & 7u) << 10) | (((hw >> 8) & 15u) << 6);
+      r[0] = (t_start & ((1ull << 48) - 1)) | (tag << 48);
       r[1] = t_first;
       r[2] = t_loop;
       r[3] = stamp_now();

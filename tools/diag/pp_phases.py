@@ -47,15 +47,28 @@ def main():
             for _ in range(5):
                 run()
                 torch.cuda.synchronize()
-                r = rec.view(-1, 4).cpu().double() * 10.0 / 1e3      # us
+                raw = rec.view(-1, 4).cpu()
+                tag = (raw[:, 0] >> 48) & 0xFFFF
+                raw = raw.clone()
+                raw[:, 0] &= (1 << 48) - 1
+                r = raw.double() * 10.0 / 1e3      # us
                 t0 = r[:, 0].min()
+                xcc = (tag >> 13) & 7
+                loop = r[:, 2] - r[:, 1]
+                per_xcc = {int(x): round(float(loop[xcc == x].median()), 2) for x in range(8)
+                           if bool((xcc == x).any())}
+                # loop time by tile position: workgroup b -> tile (XCD-aware remap in tile_of)
                 rows.append({"span": float(r[:, 3].max() - t0),
                              "skew": float(r[:, 0].max() - t0),
                              "pro": float((r[:, 1] - r[:, 0]).median()),
                              "loop": float((r[:, 2] - r[:, 1]).median()),
                              "epi": float((r[:, 3] - r[:, 2]).median()),
                              "loop_max": float((r[:, 2] - r[:, 1]).max()),
-                             "end_spread": float(r[:, 3].max() - r[:, 3].min())})
+                             "end_spread": float(r[:, 3].max() - r[:, 3].min()),
+                             "loop_median_by_xcc": per_xcc,
+                             "loop_spread_in_xcc": {int(x): round(float(
+                                 loop[xcc == x].max() - loop[xcc == x].min()), 2)
+                                 for x in per_xcc}})
             best = min(rows, key=lambda d: d["span"])
             ref = (torch.rand(1, device=dev))
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -69,7 +82,8 @@ def main():
             blas = e0.elapsed_time(e1) / 20 * 1e3
             del ref
             print(json.dumps({"M": M, "N": N, "K": K, "nj": nj, "tiles": tiles,
-                              **{k: round(v, 2) for k, v in best.items()},
+                              **{k: (round(v, 2) if isinstance(v, float) else v)
+                                 for k, v in best.items()},
                               "loop_per_ktile_us": round(best["loop"] / (K // 64), 4),
                               "blas_us": round(blas, 2)}), flush=True)
 

@@ -28,7 +28,9 @@ for P in 2 4 8; do
 done
 step tp7b_shard4_ov 300 $TP --shard-as 4 --emulate-busbw 300 --overlap-chunks 2 --output-dir $O/tp_shard4_ov
 step gpt2 300 python -m distributed_llm_backend_benchmark_amd.cli.train_ddp --steps 30 --warmup 5 --output $O/gpt2.json
+step gpt2_emu100 300 python -m distributed_llm_backend_benchmark_amd.cli.train_ddp --steps 30 --warmup 5 --emulate-comm 100 --comm-timeline --output $O/gpt2_emu100.json
 cd /tmp && export TMPDIR=/tmp PYTHONPATH=$R
 step prof_tp7b 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/$O/prof_tp7b" -o tp7b -- python3 -m distributed_llm_backend_benchmark_amd.cli.run_tp --config "$R/config/7b_config.yaml" --backend rccl --output-dir "$R/$O/tp_prof"
 step prof_gpt2 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/$O/prof_gpt2" -o gpt2 -- python3 -m distributed_llm_backend_benchmark_amd.cli.train_ddp --steps 8 --warmup 3
+step pp_phases 200 python3 "$R/tools/diag/pp_phases.py" --nj 4 --shapes 4096x4096x4096,4096x4096x16384
 echo done
