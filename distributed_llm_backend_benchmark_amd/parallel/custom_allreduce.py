@@ -273,8 +273,11 @@ class CustomAllReduce:
 
         def arr(vals):
             return (ctypes.c_int64 * W)(*[int(v) * esz for v in vals])
-        total = sum(int(c) for c in counts) * esz
-        nb = nblocks or self.nblocks or int(min(256, max(8, total // (256 << 10))))
+        # the grid must be the same on every rank (workgroup b of each rank meets workgroup b of
+        # its peers at the flag barriers): size it from the registered input, equal everywhere,
+        # never from this rank's own (uneven) receive total
+        size = t.numel() * esz
+        nb = nblocks or self.nblocks or int(min(256, max(8, size // (256 << 10))))
         _lib.check(self.lib.dlbb_car_alltoallv_reg(self.h, rid, arr(src_off), arr(counts),
                                                    arr(dst_off), out.data_ptr(), nb,
                                                    _lib.stream(t.device)), "car_alltoallv_reg")
