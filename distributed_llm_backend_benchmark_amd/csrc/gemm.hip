@@ -65,6 +65,7 @@ struct GemmArgs {
   int vec_ok;              // 16-B aligned C / residual / preact / bias rows (vector epilogue)
   int kt_split;            // NN split-K (gridDim.y > 1): K-tiles per split; split s writes fp32
                            // partials to C + s * M * ldc
+  int group_m = 0;         // tile_of's GROUP_M (0 = kGroupM; A/B only, dlbb_gemm_set_group_m)
 };
 
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
@@ -220,10 +221,11 @@ __device__ __forceinline__ Tile256 tile_of(const GemmArgs& a, int vb) {
   const int nwg = tiles_m * tiles_n;
   const int q = nwg >> 3, r = nwg & 7, x = vb & 7;
   const int wid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (vb >> 3);
-  const int group_size = kGroupM * tiles_n;
+  const int gmx = a.group_m > 0 ? a.group_m : kGroupM;
+  const int group_size = gmx * tiles_n;
   const int group = wid / group_size;
-  const int first_m = group * kGroupM;
-  const int gm = (tiles_m - first_m) < kGroupM ? (tiles_m - first_m) : kGroupM;
+  const int first_m = group * gmx;
+  const int gm = (tiles_m - first_m) < gmx ? (tiles_m - first_m) : gmx;
   const int in_group = wid - group * group_size;
   return Tile256{static_cast<int64_t>(first_m + in_group % gm) * BM2,
                  static_cast<int64_t>(in_group / gm) * BNT};
@@ -1659,6 +1661,287 @@ __global__ void __launch_bounds__(kThreads2, 1) gemm_bf16_nn_256_pp_persist_bal(
 }
 
 // ---------------------------------------------------------------------------------------
+// Persistent 256 x 192 ping-pong with the C stores SPREAD under the next tile's K-loop (plain
+// bf16 output; the GPT-2 LM head 16384 x 50304 x 768: 262 x 192 columns exactly).
+// pp_persist_body flushes a finished tile in one burst at the next tile's first memory interval;
+// stores and DMA loads share vmcnt (in order), so the next counted DMA wait also waits for every
+// store: a tile's 128 KiB of C drains serially (LM head: 1.65 GB of logits = ~0.3 ms of a ~1.1 ms
+// kernel, profiles/r04_gemm/SUMMARY.md). Here the finished accumulators are packed to bf16 (48
+// VGPRs: the 192-wide tile's 96 fp32 accumulators leave room at 2 waves per SIMD), zeroed, and
+// the 24 8-byte stores of a lane go out kSpi per iteration over the next tile's first iterations,
+// each batch AFTER that iteration's DMA issues. Every counted wait of iteration g then adds the
+// stores of iterations g - 1 and g (younger than any load it retires); a batch is retired one
+// iteration later, by which time it has had two memory intervals and an MFMA phase to drain.
+// Host contract: N % 192 == 0, M % 16 == 0, K / 64 > kSpreadIters (every spread window inside
+// one tile).
+// EARLY (12 or 18): stores issued at the boundary itself, before that iteration's loads; the rest
+// (24 / 12 parked VGPRs) go out kSpi per iteration after the loads. 6 or 0 early (36 / 48 parked)
+// spill once the spread iterations are unrolled (249 VGPRs at 12).
+constexpr int kSpi = 3;
+constexpr int spread_iters(int early) { return (24 - early) / kSpi; }
+
+template <int B, int E, typename F>
+__device__ __forceinline__ void static_for(F&& f) {   // f(integral_constant<int, B .. E-1>)
+  if constexpr (B < E) {
+    f(std::integral_constant<int, B>{});
+    static_for<B + 1, E>(f);
+  }
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vmc() {   // any compile-time count
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <bool BAL, int kEarly>
+__device__ __forceinline__ void pp192_spread_body(GemmArgs a, char* smem) {
+  constexpr int kSpreadIters = spread_iters(kEarly);
+  constexpr int NJ = 3, NBI = 6;
+  constexpr int NBx = BAL ? NBI / 2 : NBI;      // B instructions of wave row 0 per iteration
+  constexpr int kTileB = NJ * 64 * BK * 2;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = wave >> 2, wc = wave & 3;
+  const int fr = lane & 15, fq = lane >> 4;
+  const int nk = static_cast<int>(a.K / BK);
+  const int tiles = static_cast<int>(((a.M + BM2 - 1) / BM2) * (a.N / 192));
+  const int nwg = static_cast<int>(gridDim.x), wg = static_cast<int>(blockIdx.x);
+  const int mine = wg < tiles ? (tiles - wg + nwg - 1) / nwg : 0;
+  if (mine == 0) return;
+  const int G = mine * nk;
+  char* const abuf0 = smem;
+  char* const bbuf0 = smem + 2 * kTile2Bytes;
+
+  f32x4 acc[8][NJ];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 af[2][8], bf[2][NJ];
+  const int r_in = lane >> 3, chunk = (lane & 7) ^ (lane >> 3);
+  const uint32_t lda2 = static_cast<uint32_t>(a.lda) * 2, ldb2 = static_cast<uint32_t>(a.ldb) * 2;
+  const uint32_t aoff = static_cast<uint32_t>(r_in) * lda2 + chunk * 16;
+  const uint32_t boff = static_cast<uint32_t>(g48_lane(r_in)) * ldb2 + chunk * 16;
+  constexpr uint32_t kStep = BK * 2;
+#define DLBB_RSRC(P) \
+  __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(P), 0, 0x7fffffff, 0x00020000)
+  Tile256 tc = tile_of<192>(a, wg);
+  Tile256 tp = tc;                              // the tile whose C is in pk
+  Tile256 tprev = tc;                           // the tile finished last
+  {
+    const __amdgpu_buffer_rsrc_t ra = DLBB_RSRC(a.A + tc.m0 * a.lda);
+    const __amdgpu_buffer_rsrc_t rb = DLBB_RSRC(a.B + tc.n0 * a.ldb);
+    const int rows_a = static_cast<int>(a.M - tc.m0);
+    if (wr == 0) {                              // prologue: A-lo(0), B(0), B(1)
+      stage_a_half(ra, lda2, rows_a, 0, abuf0, 0, wc, aoff);
+      stage_b192(rb, ldb2, 0, bbuf0, wc, boff);
+      stage_b192(rb, ldb2, kStep, bbuf0 + kTileB, wc, boff);
+      wait_vm<NBI>();
+      __builtin_amdgcn_s_barrier();
+    } else {                                    // A-hi(0), A-lo(1)
+      stage_a_half(ra, lda2, rows_a, 0, abuf0, 1, wc, aoff);
+      stage_a_half(ra, lda2, rows_a, kStep, abuf0 + kTile2Bytes, 0, wc, aoff);
+      __builtin_amdgcn_s_barrier();
+      DLBB_WAIT_VM(4);
+      __builtin_amdgcn_s_barrier();             // end of interval 0
+    }
+  }
+  // lane's C rows / columns within a tile: rows wr*128 + 16 i + fr, columns wc*48 + 12 fq + 4 j;
+  // buffer stores from the tile origin: lane offset in one VGPR, the (i, j) part in SGPRs, and a
+  // wave-uniform row-block guard (host contract M % 16 == 0)
+  const uint32_t ldc2 = static_cast<uint32_t>(a.ldc) * 2;
+  const uint32_t c_lane = static_cast<uint32_t>(wr * 128 + fr) * ldc2 + (wc * 48 + fq * 12) * 2;
+  typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+  // per batch: the tile's resource and the row pitch are re-derived behind empty asm, so the
+  // compiler cannot hoist 24 per-store offsets out of the K-loop (that spilled)
+  struct CDst { __amdgpu_buffer_rsrc_t rc; uint32_t ld, cl; int64_t rows; };
+  auto cdst = [&]() {
+    CDst d;
+    uint16_t* base = static_cast<uint16_t*>(a.C) + tp.m0 * a.ldc + tp.n0;
+    asm volatile("" : "+s"(base));
+    d.rc = __builtin_amdgcn_make_buffer_rsrc(base, 0, 0x7fffffff, 0x00020000);
+    d.ld = ldc2;
+    asm volatile("" : "+s"(d.ld));
+    d.cl = c_lane;
+    d.rows = a.M - tp.m0 - wr * 128;
+    return d;
+  };
+  auto store_q = [&](const CDst& d, int q, u32x2 v) {   // q compile-time after unrolling
+    const int i = q / 3, j = q % 3;
+    if (i * 16 < d.rows)
+      __builtin_amdgcn_raw_buffer_store_b64(v, d.rc, d.cl + static_cast<uint32_t>(i * 16) * d.ld + j * 8,
+                                            0, 0);
+  };
+  auto pack = [&](int i, int j) {
+    return u32x2{static_cast<uint32_t>(f32_to_bf16(acc[i][j][0])) |
+                     (static_cast<uint32_t>(f32_to_bf16(acc[i][j][1])) << 16),
+                 static_cast<uint32_t>(f32_to_bf16(acc[i][j][2])) |
+                     (static_cast<uint32_t>(f32_to_bf16(acc[i][j][3])) << 16)};
+  };
+  u32x2 pk[24 - kEarly];                        // the previous tile's spread part, bf16 pairs
+  // finished tile tp: store its first kEarly fragments now, park the rest in pk, zero acc
+  auto park = [&]() {
+    const CDst d = cdst();
+#pragma unroll
+    for (int q = 0; q < 24; ++q) {
+      const u32x2 v = pack(q / 3, q % 3);
+      if (q < kEarly) store_q(d, q, v);
+      else pk[q - kEarly] = v;
+      acc[q / 3][q % 3] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  };
+  auto store_batch = [&](int it) {              // it: a constant after inlining
+    const CDst d = cdst();
+#pragma unroll
+    for (int q = kEarly; q < 24; ++q)
+      if ((q - kEarly) / kSpi == it) store_q(d, q, pk[q - kEarly]);
+  };
+  auto mfma_all = [&]() {
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int x = 0; x < 8; ++x)
+#pragma unroll
+        for (int j = 0; j < 3; ++j)
+          acc[x][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[ks][j], af[ks][x], acc[x][j], 0,
+                                                              0, 0);
+  };
+  // One K-loop per wave row (as pp_persist_body: a row test inside the loop keeps both rows'
+  // temporaries live together and spills). Every store count is a template argument of the
+  // iteration, so each counted wait is one immediate (a runtime count measured 13-17 % slower:
+  // the compare-and-branch chain sits between the ds_reads and the barrier):
+  //   E  = boundary stores issued at the top of this iteration (older than its loads)
+  //   SP = spread stores issued in the previous iteration (after its loads)
+  //   SC = spread stores issued in this iteration (after its loads), batch IT
+  using std::integral_constant;
+  auto run = [&](auto row_c) {
+    constexpr int ROW = decltype(row_c)::value;
+    int cb = 0;
+    for (int i = 0; i < mine; ++i) {
+      const Tile256 tn = i + 1 < mine ? tile_of<192>(a, wg + (i + 1) * nwg) : tc;
+      const __amdgpu_buffer_rsrc_t ra = DLBB_RSRC(a.A + tc.m0 * a.lda);
+      const __amdgpu_buffer_rsrc_t rb = DLBB_RSRC(a.B + tc.n0 * a.ldb);
+      const __amdgpu_buffer_rsrc_t ran = DLBB_RSRC(a.A + tn.m0 * a.lda);
+      const __amdgpu_buffer_rsrc_t rbn = DLBB_RSRC(a.B + tn.n0 * a.ldb);
+      const int rows_a = static_cast<int>(a.M - tc.m0), rows_an = static_cast<int>(a.M - tn.m0);
+      auto iter = [&](int k, auto e_c, auto sp_c, auto sc_c, auto it_c) {
+        constexpr int E = decltype(e_c)::value, SP = decltype(sp_c)::value;
+        constexpr int SC = decltype(sc_c)::value, IT = decltype(it_c)::value;
+        constexpr int X = E + SP + SC;          // stores younger than every awaited load
+        const int g = i * nk + k;
+        {
+          const char* ab = abuf0 + (g & 1) * kTile2Bytes;
+          const char* bb = bbuf0 + cb * kTileB;
+#pragma unroll
+          for (int ks = 0; ks < 2; ++ks) {
+#pragma unroll
+            for (int x = 0; x < 8; ++x)
+              af[ks][x] = read_frag(ab, ROW * 128 + x * 16 + fr, ks * 4 + fq);
+#pragma unroll
+            for (int j = 0; j < 3; ++j) bf[ks][j] = read_frag(bb, wc * 48 + j * 16 + fr, ks * 4 + fq);
+          }
+        }
+        if constexpr (ROW == 0) {
+          const bool h1 = g + 1 < G, b2 = g + 2 < G;
+          if (h1) {                             // A-hi(g+1)
+            char* const an = abuf0 + ((g + 1) & 1) * kTile2Bytes;
+            if (k + 1 < nk) stage_a_half(ra, lda2, rows_a, (k + 1) * kStep, an, 1, wc, aoff);
+            else stage_a_half(ran, lda2, rows_an, 0, an, 1, wc, aoff);
+          }
+          if (b2) {                             // B(g+2) (BAL: its first half)
+            char* const bn = bbuf0 + (cb == 0 ? 2 : cb - 1) * kTileB;
+            const bool here = k + 2 < nk;
+            const uint32_t k2 = static_cast<uint32_t>(here ? k + 2 : k + 2 - nk) * kStep;
+            if (BAL) stage_b192<0, 3>(here ? rb : rbn, ldb2, k2, bn, wc, boff);
+            else stage_b192<0, 6>(here ? rb : rbn, ldb2, k2, bn, wc, boff);
+          }
+          if constexpr (SC > 0) store_batch(IT);   // after the loads: younger than all of them
+          // retire A-hi(g): younger = B(g+1), the stores, A-hi(g+1), B(g+2) (g = 0: B(1) is
+          // whole, so BAL over-retires its second half there, as pingpong_body)
+          if (b2) wait_vmc<2 * NBx + 4 + X>();
+          else if (h1) wait_vmc<NBx + 4 + X>();
+          else wait_vmc<X>();
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          __builtin_amdgcn_sched_barrier(0);
+          __builtin_amdgcn_s_barrier();         // end of interval 2g
+          __builtin_amdgcn_sched_barrier(0);
+          mfma_all();
+          __builtin_amdgcn_sched_barrier(0);
+          if (h1) {                             // retire B(g+1) (BAL: its first half)
+            if (b2) wait_vmc<4 + NBx + X>();
+            else wait_vmc<4 + X>();
+          }
+          __builtin_amdgcn_s_barrier();         // end of interval 2g+1
+        } else {
+          const bool l2 = g + 2 < G;
+          if (l2) {                             // A-lo(g+2) (BAL: and B1(g+2))
+            const bool here = k + 2 < nk;
+            const int ub = here ? k + 2 : k + 2 - nk;
+            stage_a_half(here ? ra : ran, lda2, here ? rows_a : rows_an,
+                         static_cast<uint32_t>(ub) * kStep, abuf0 + (g & 1) * kTile2Bytes, 0, wc,
+                         aoff);
+            if (BAL)
+              stage_b192<3, 6>(here ? rb : rbn, ldb2, static_cast<uint32_t>(ub) * kStep,
+                               bbuf0 + (cb == 0 ? 2 : cb - 1) * kTileB, wc, boff);
+          }
+          if constexpr (SC > 0) store_batch(IT);
+          if (g + 1 < G) {                      // retire A-lo(g+1) (BAL: and B1(g+1))
+            if (l2) wait_vmc<4 + (BAL ? NBI / 2 : 0) + X>();
+            else wait_vmc<X>();
+          }
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          __builtin_amdgcn_sched_barrier(0);
+          __builtin_amdgcn_s_barrier();         // end of interval 2g+1
+          __builtin_amdgcn_sched_barrier(0);
+          mfma_all();
+          __builtin_amdgcn_sched_barrier(0);
+          if (g + 1 < G) __builtin_amdgcn_s_barrier();   // end of interval 2g+2
+        }
+        cb = cb == 2 ? 0 : cb + 1;
+      };
+      using Z = integral_constant<int, 0>;
+      using S = integral_constant<int, kSpi>;
+      int k = 0;
+      if (i > 0) {                              // boundary + spread iterations (host: nk > them)
+        tp = tprev;                             // the finished tile: E early stores,
+        __builtin_amdgcn_sched_barrier(0);      // the rest parked in pk (fenced: the next
+        park();                                 // ds_reads must not rise above the packing)
+        __builtin_amdgcn_sched_barrier(0);
+        iter(0, integral_constant<int, kEarly>{}, Z{}, S{}, Z{});
+        static_for<1, kSpreadIters>([&](auto it_c) {
+          iter(decltype(it_c)::value, Z{}, S{}, S{}, it_c);
+        });
+        iter(kSpreadIters, Z{}, S{}, Z{}, Z{});
+        k = kSpreadIters + 1;
+      }
+      for (; k < nk; ++k) iter(k, Z{}, Z{}, Z{}, Z{});
+      tprev = tc;
+      tc = tn;
+    }
+  };
+  if (wr == 0) run(integral_constant<int, 0>{});
+  else run(integral_constant<int, 1>{});
+  // the last tile: plain epilogue (nothing left to hide it under)
+  DLBB_WAIT_VM(0);
+  tp = tprev;
+  park();
+#pragma unroll
+  for (int it = 0; it < kSpreadIters; ++it) store_batch(it);
+#undef DLBB_RSRC
+}
+
+template <int EARLY>
+__global__ void __launch_bounds__(kThreads2, 1) gemm_bf16_nt_192_pp_spread(GemmArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  pp192_spread_body<false, EARLY>(a, smem);
+}
+template <int EARLY>
+__global__ void __launch_bounds__(kThreads2, 1) gemm_bf16_nt_192_pp_spread_bal(GemmArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  pp192_spread_body<true, EARLY>(a, smem);
+}
+
+// ---------------------------------------------------------------------------------------
 // One wave per SIMD (A/B only, set_stagger(9); profiles/r03_gemm/w4_experiment.md): 256 x 256
 // tile, 256 threads = 4 waves as 2 (M) x 2 (N), each wave 128 x 128 outputs = 64 accumulators of
 // 16x16 held in AGPRs — hipBLASLt's MT256x256x64 MI16x16 structure. The MFMAs are inline asm
@@ -1971,6 +2254,12 @@ DLBB_API int dlbb_gemm_get_stagger() { return dlbb_gemm_stagger; }
 DLBB_API void dlbb_gemm_set_persist_epi(int on) { dlbb_persist_epi = on ? 1 : 0; }
 DLBB_API void dlbb_gemm_set_concurrent(int on) { dlbb_gemm_concurrent = on; }
 DLBB_API int dlbb_gemm_get_concurrent() { return dlbb_gemm_concurrent; }
+// spread-store persistent 192 kernel (variant 2): stores issued at the tile boundary, 12 or 18
+static int dlbb_spread_early = 12;
+DLBB_API void dlbb_gemm_set_spread_early(int n) { dlbb_spread_early = n == 18 ? 18 : 12; }
+// tile order experiment: GROUP_M of tile_of for the NT forward launches (0 = kGroupM)
+static int dlbb_group_m = 0;
+DLBB_API void dlbb_gemm_set_group_m(int g) { dlbb_group_m = g > 0 ? g : 0; }
 DLBB_API void dlbb_gemm_set_bal(int mode) { dlbb_gemm_bal = mode >= 0 && mode <= 2 ? mode : 2; }
 
 // ---------------------------------------------------------------------------------------
@@ -2091,6 +2380,8 @@ DLBB_API int dlbb_gemm_nt_phase_probe(const void* A, int64_t lda, const void* B,
 // NT GEMM with an explicit kernel variant (the autotuner's candidates, ops/gemm.py):
 //   0 = the size heuristic below (256² ping-pong / persistent / 128² small grids)
 //   1 = 256 x 192 ping-pong tiles (N % 192 == 0, M % 8 == 0; otherwise variant 0)
+//   2 = persistent 256 x 192 with the C stores spread under the next tile (plain bf16 output;
+//       otherwise variant 1)
 DLBB_API int dlbb_gemm_bf16_nt_v(const void* A, int64_t lda, const void* B, int64_t ldb, void* C,
                                  int64_t ldc, int64_t M, int64_t N, int64_t K, const void* bias,
                                  const void* residual, int64_t ldr, void* preact, int epi,
@@ -2123,7 +2414,27 @@ DLBB_API int dlbb_gemm_bf16_nt_v(const void* A, int64_t lda, const void* B, int6
              static_cast<const uint16_t*>(bias), static_cast<const uint16_t*>(residual),
              static_cast<uint16_t*>(preact), M, N, K, lda, ldb, ldc, ldr, epi, out_f32,
              vec_ok, 0};
+  a.group_m = dlbb_group_m;
   const int64_t tiles256 = ((M + BM2 - 1) / BM2) * ((N + BN2 - 1) / BN2);
+  // variant 2: persistent 256 x 192 with spread C stores (plain bf16 output only, >= 9 K-tiles,
+  // 8-byte aligned rows; pp192_spread_body); anything else falls back to variant 1
+  if (variant == 2 && epi == 0 && !preact && !out_f32 && vec_ok && persist_enabled() &&
+      N % 192 == 0 && M % 16 == 0 && M >= 16 && K / BK >= spread_iters(12) + 2 &&
+      lda * 2 * 256 + K * 2 < (1LL << 31) && ldb * 2 * 192 + K * 2 < (1LL << 31)) {
+    const int64_t tiles = ((M + BM2 - 1) / BM2) * (N / 192);
+    const int64_t grid = tiles < num_cus() ? tiles : num_cus();
+    const dim3 g(static_cast<unsigned>(grid)), b(kThreads2);
+    const bool bal = use_bal(K / BK, false);
+    if (dlbb_spread_early == 18) {
+      if (bal) hipLaunchKernelGGL(gemm_bf16_nt_192_pp_spread_bal<18>, g, b, kPP192Lds, stream, a);
+      else hipLaunchKernelGGL(gemm_bf16_nt_192_pp_spread<18>, g, b, kPP192Lds, stream, a);
+    } else {
+      if (bal) hipLaunchKernelGGL(gemm_bf16_nt_192_pp_spread_bal<12>, g, b, kPP192Lds, stream, a);
+      else hipLaunchKernelGGL(gemm_bf16_nt_192_pp_spread<12>, g, b, kPP192Lds, stream, a);
+    }
+    return hipGetLastError();
+  }
+  if (variant == 2) variant = 1;
   if (variant == 1 && N % 192 == 0 && M % 8 == 0 && M >= 8 &&
       lda * 2 * 256 + K * 2 < (1LL << 31) && ldb * 2 * 192 + K * 2 < (1LL << 31)) {
     const dim3 g(static_cast<unsigned>(((M + BM2 - 1) / BM2) * (N / 192))), b(kThreads2);

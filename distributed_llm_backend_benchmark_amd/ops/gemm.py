@@ -226,6 +226,18 @@ def mfma192_ok(M: int, N: int) -> bool:
     return N % 192 == 0 and M % 8 == 0 and M >= 8
 
 
+def _mfma192p_linear(x2, w, bias, act, r2, out, preact):
+    """Persistent 256 x 192 tiles with the C stores spread under the next tile's K-loop
+    (``csrc/gemm.hip`` ``pp192_spread_body``): plain bf16 output on multi-round grids — the GPT-2
+    LM-head forward 16384 x 50304 x 768, whose 1.65 GB of logits otherwise drain serially at every
+    tile boundary. Outside its contract the library runs variant 1."""
+    return _mfma_linear(x2, w, bias, act, r2, out, preact, variant=2)
+
+
+def mfma192p_ok(M: int, N: int, K: int, plain: bool) -> bool:
+    return plain and N % 192 == 0 and M % 16 == 0 and M >= 16 and K // 64 >= 6
+
+
 _NCU = {}
 
 
@@ -341,7 +353,8 @@ CALLS = {}            # ("linear" | "wgrad", key) -> calls since import (kernel-
 # ping-pong on every sub-round TP shape (7B P = 8: qkv 0.102 / 0.065 ms split on 256² / 256 x 192
 # vs 0.059 unsplit; profiles/r04_gemm/gemm_table.jsonl) — a workgroup's fixed cost (prologue,
 # C store, launch: ~10 us) is paid per slice, and the partial slabs add a pass. Kept for A/B.
-_IMPLS = {"mfma": _mfma_linear, "mfma192": _mfma192_linear, "blas": _blas_linear}
+_IMPLS = {"mfma": _mfma_linear, "mfma192": _mfma192_linear, "mfma192p": _mfma192p_linear,
+          "blas": _blas_linear}
 
 
 # > 0 while GEMMs share the chip with communication kernels on another stream (the overlapped
@@ -384,6 +397,11 @@ def _autotune(key, args) -> str:
         del impls["blas"]
     if not mfma192_ok(key[0], key[1]):
         del impls["mfma192"]
+    # key: (M, N, K, lda, act, bias, residual, out dtype, preact[, "concurrent"])
+    plain = (key[4] is None and not key[5] and not key[6] and key[7] == torch.bfloat16
+             and not key[8] and key[-1] != "concurrent")
+    if not mfma192p_ok(key[0], key[1], key[2], plain):
+        del impls["mfma192p"]
     times = _time_interleaved({n: (lambda f=f: f(*args)) for n, f in impls.items()})
     best, times = _choose(times, "linear", key)
     CHOICES[key] = best

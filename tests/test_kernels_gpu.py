@@ -895,5 +895,36 @@ def test_gemm_autotune_offers_tile_variants(monkeypatch):
     y = linear(x, w)
     torch.testing.assert_close(y.float(), x.float() @ w.float().t(), rtol=2e-2, atol=1.5)
     kind, key, times, best = gemm.TUNE_LOG[-1]
-    assert set(times) == {"mfma", "mfma192", "blas"}, times
+    assert set(times) == {"mfma", "mfma192", "mfma192p", "blas"}, times
     assert gemm.CHOICES[key] == best
+
+
+@pytest.mark.parametrize("M,N,K", [(4096, 9600, 768), (2000, 19200, 640), (1040, 1536, 1024),
+                                   (16384, 3840, 384)])
+@pytest.mark.parametrize("early", [12, 18])
+@pytest.mark.parametrize("bal", [0, 1])
+def test_gemm_nt_192_spread_matches_fp32(M, N, K, early, bal):
+    """Persistent 256 x 192 NT GEMM with the C stores spread under the next tile's K-loop
+    (variant 2): multi-round grids (several tiles per workgroup), ragged M, the shortest
+    reduction it accepts (6 K-tiles), both boundary-store counts and both DMA schedules — against
+    fp32, and bit-identical to the non-persistent 256 x 192 kernel (same MFMA order)."""
+    from distributed_llm_backend_benchmark_amd.ops import _lib, gemm
+
+    lib = _lib.lib()
+    x = _randn(M, K, seed=71, scale=0.3)
+    w = _randn(N, K, seed=72, scale=0.3)
+    y = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+    y1 = torch.empty_like(y)
+    try:
+        lib.dlbb_gemm_set_spread_early(early)
+        lib.dlbb_gemm_set_bal(bal)
+        y.fill_(7.0)
+        gemm._mfma192p_linear(x, w, None, None, None, y, None)
+        gemm._mfma192_linear(x, w, None, None, None, y1, None)
+        torch.cuda.synchronize()
+    finally:
+        lib.dlbb_gemm_set_spread_early(12)
+        lib.dlbb_gemm_set_bal(2)
+    torch.testing.assert_close(y.float(), x.float() @ w.float().t(), rtol=2e-2,
+                               atol=2e-2 * K ** 0.5)
+    assert torch.equal(y, y1)

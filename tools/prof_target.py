@@ -1,5 +1,5 @@
 """Tiny driver for PMC-counter profiling: runs ONE op a few times (no timing logic).
-usage: prof_target.py gemm256|gemm256s6|gemm256s7|gemm128|blas|nn|nnplain|tn|tnplain|wgrad128|
+usage: prof_target.py lmhead|lmhead192|lmhead192p|lmheadblas|gemm256|gemm256s6|gemm256s7|gemm128|blas|nn|nnplain|tn|tnplain|wgrad128|
 blastn|reduce8|ln|xent|xentfused|embbwd"""
 import os
 import sys
@@ -13,7 +13,18 @@ from distributed_llm_backend_benchmark_amd.ops.gemm import set_tile  # noqa: E40
 what = sys.argv[1]
 dev = "cuda"
 g = torch.Generator(device=dev).manual_seed(0)
-if what.startswith("gemm") or what == "blas":
+if what.startswith("lmhead"):    # GPT-2 LM-head forward 16384 x 50304 x 768: lmhead (library
+    # dispatch: 256² persistent), lmhead192 / lmhead192p (256 x 192 ping-pong / persistent spread
+    # stores), lmheadblas (hipBLASLt)
+    from distributed_llm_backend_benchmark_amd.ops import gemm as G
+
+    x = torch.randn(16384, 768, device=dev, generator=g).to(torch.bfloat16)
+    w = torch.randn(50304, 768, device=dev, generator=g).to(torch.bfloat16)
+    out = torch.empty(16384, 50304, device=dev, dtype=torch.bfloat16)
+    impl = {"lmhead": G._mfma_linear, "lmhead192": G._mfma192_linear,
+            "lmhead192p": G._mfma192p_linear, "lmheadblas": G._blas_linear}[what]
+    fn = lambda: impl(x, w, None, None, None, out, None)  # noqa: E731
+elif what.startswith("gemm") or what == "blas":
     M = N = K = 8192
     x = torch.randn(M, K, device=dev, generator=g).to(torch.bfloat16)
     w = torch.randn(N, K, device=dev, generator=g).to(torch.bfloat16)

@@ -6,7 +6,8 @@ interleaved rounds, uniform random operands (CDNA guide §5.4 rules 24/25). One 
 
 ``--modes``: comma list of our-kernel variants to time: ``auto`` = the library dispatch
 (``DLBB_GEMM=mfma``), ``t128`` / ``t256`` force the tile, ``s<N>`` = set_stagger(N), ``v192`` =
-the 256 x 192 tile variant (N % 192 == 0 shapes only), ``sk`` / ``sk192`` = split-K on 256² /
+the 256 x 192 tile variant (N % 192 == 0 shapes only), ``v192p`` / ``v192p18`` = its persistent
+spread-store form (variant 2; 12 / 18 stores at the tile boundary), ``sk`` / ``sk192`` = split-K on 256² /
 256 x 192 tiles (grids well below one round only). ``--gpt2`` adds the GPT-2 forward GEMMs.
 """
 import argparse
@@ -18,7 +19,7 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from distributed_llm_backend_benchmark_amd import ops  # noqa: E402
-from distributed_llm_backend_benchmark_amd.ops import gemm  # noqa: E402
+from distributed_llm_backend_benchmark_amd.ops import _lib, gemm  # noqa: E402
 
 CFG = {"1B": (2048, 8192), "7B": (4096, 16384), "13B": (5120, 20480)}
 
@@ -88,6 +89,8 @@ def main():
         errs = {}
         out = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
         ok = {"v192": gemm.mfma192_ok(M, N),
+              "v192p": gemm.mfma192p_ok(M, N, K, True),
+              "v192p18": gemm.mfma192p_ok(M, N, K, True),
               "sk": gemm.mfma_sk_ok(x, w, None, out, None, 4),
               "sk192": gemm.mfma_sk_ok(x, w, None, out, None, 3)}
         ms = [m for m in modes if ok.get(m, True)]
@@ -95,6 +98,9 @@ def main():
         def run(m):
             if m == "v192":      # 256 x 192 tiles (variant 1)
                 return gemm._mfma192_linear(x, w, None, None, None, out, None)
+            if m in ("v192p", "v192p18"):   # persistent, spread C stores (variant 2)
+                _lib.lib().dlbb_gemm_set_spread_early(18 if m == "v192p18" else 12)
+                return gemm._mfma192p_linear(x, w, None, None, None, out, None)
             if m in ("sk", "sk192"):      # split-K ping-pong + fused reduce / epilogue
                 return gemm._mfma_sk_linear(x, w, None, None, None, out, None,
                                             nj=3 if m == "sk192" else 4)
