@@ -1357,6 +1357,7 @@ DLBB_PP_STAMPED(gemm_bf16_tn_256_pingpong3_bal, true, true, true)
 enum PpLean : int {
   PP_PLAIN = 0, PP_BIAS = 1, PP_BIAS_GELU_TANH = 2, PP_BIAS_GELU_ERF = 3,
   PP_DGELU_TANH = 4, PP_DGELU_ERF = 5,
+  PP_NOSTORE = 99,   // diagnostic: no C output (dlbb_gemm_set_diag_nostore)
 };
 
 // What the epilogue reads (the bias of the lane's 16 columns, or its 8 x 16 values of u) is loaded
@@ -1536,8 +1537,9 @@ __device__ __forceinline__ void pp_persist_body(GemmArgs a, char* smem) {
     __builtin_amdgcn_sched_barrier(0);                                             \
     int ln_ = lane;                                                                \
     asm volatile("" : "+v"(ln_));                                                  \
-    store_lean_bf16<NN, LEAN>(a, acc, (T).m0 + (wave >> 2) * 128, (T).n0 + (wave & 3) * 64,  \
-                              ln_, pre_);                                          \
+    if (LEAN != PP_NOSTORE || a.out_f32 == 77)  /* (no-store: never; keeps the MFMAs) */ \
+      store_lean_bf16<NN, LEAN == PP_NOSTORE ? PP_PLAIN : LEAN>(                   \
+          a, acc, (T).m0 + (wave >> 2) * 128, (T).n0 + (wave & 3) * 64, ln_, pre_);  \
     _Pragma("unroll") for (int x_ = 0; x_ < 8; ++x_)                                \
       _Pragma("unroll") for (int y_ = 0; y_ < 4; ++y_)                              \
         acc[x_][y_] = f32x4{0.f, 0.f, 0.f, 0.f};                                    \
@@ -1693,8 +1695,13 @@ __device__ __forceinline__ void wait_vmc() {   // any compile-time count
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-template <bool BAL, int kEarly>
+// EARLY_ = kNoStores (diagnostic, dlbb_gemm_set_diag_nostore(1)): no C stores at all — the
+// loop's own time for the same tile sequence.
+constexpr int kNoStores = 99;
+template <bool BAL, int EARLY_>
 __device__ __forceinline__ void pp192_spread_body(GemmArgs a, char* smem) {
+  constexpr bool kNoStore = EARLY_ == kNoStores;
+  constexpr int kEarly = kNoStore ? 12 : EARLY_;
   constexpr int kSpreadIters = spread_iters(kEarly);
   constexpr int NJ = 3, NBI = 6;
   constexpr int NBx = BAL ? NBI / 2 : NBI;      // B instructions of wave row 0 per iteration
@@ -1902,7 +1909,7 @@ __device__ __forceinline__ void pp192_spread_body(GemmArgs a, char* smem) {
       using Z = integral_constant<int, 0>;
       using S = integral_constant<int, kSpi>;
       int k = 0;
-      if (i > 0) {                              // boundary + spread iterations (host: nk > them)
+      if (i > 0 && !kNoStore) {                 // boundary + spread iterations (host: nk > them)
         tp = tprev;                             // the finished tile: E early stores,
         __builtin_amdgcn_sched_barrier(0);      // the rest parked in pk (fenced: the next
         park();                                 // ds_reads must not rise above the packing)
@@ -1923,6 +1930,7 @@ __device__ __forceinline__ void pp192_spread_body(GemmArgs a, char* smem) {
   else run(integral_constant<int, 1>{});
   // the last tile: plain epilogue (nothing left to hide it under)
   DLBB_WAIT_VM(0);
+  if (kNoStore && a.out_f32 != 77) return;      // (never 77: the accumulators stay live)
   tp = tprev;
   park();
 #pragma unroll
@@ -2257,6 +2265,10 @@ DLBB_API int dlbb_gemm_get_concurrent() { return dlbb_gemm_concurrent; }
 // spread-store persistent 192 kernel (variant 2): stores issued at the tile boundary, 12 or 18
 static int dlbb_spread_early = 12;
 DLBB_API void dlbb_gemm_set_spread_early(int n) { dlbb_spread_early = n == 18 ? 18 : 12; }
+// diagnostic: the plain persistent kernels (256² mode 10, 256 x 192 variant 2) skip their C
+// stores — the K-loop's own time over the same tile sequence (C is left unwritten)
+static int dlbb_diag_nostore = 0;
+DLBB_API void dlbb_gemm_set_diag_nostore(int on) { dlbb_diag_nostore = on ? 1 : 0; }
 // tile order experiment: GROUP_M of tile_of for the NT forward launches (0 = kGroupM)
 static int dlbb_group_m = 0;
 DLBB_API void dlbb_gemm_set_group_m(int g) { dlbb_group_m = g > 0 ? g : 0; }
@@ -2425,7 +2437,10 @@ DLBB_API int dlbb_gemm_bf16_nt_v(const void* A, int64_t lda, const void* B, int6
     const int64_t grid = tiles < num_cus() ? tiles : num_cus();
     const dim3 g(static_cast<unsigned>(grid)), b(kThreads2);
     const bool bal = use_bal(K / BK, false);
-    if (dlbb_spread_early == 18) {
+    if (dlbb_diag_nostore) {                // diagnostic: no C output
+      if (bal) hipLaunchKernelGGL(gemm_bf16_nt_192_pp_spread_bal<kNoStores>, g, b, kPP192Lds, stream, a);
+      else hipLaunchKernelGGL(gemm_bf16_nt_192_pp_spread<kNoStores>, g, b, kPP192Lds, stream, a);
+    } else if (dlbb_spread_early == 18) {
       if (bal) hipLaunchKernelGGL(gemm_bf16_nt_192_pp_spread_bal<18>, g, b, kPP192Lds, stream, a);
       else hipLaunchKernelGGL(gemm_bf16_nt_192_pp_spread<18>, g, b, kPP192Lds, stream, a);
     } else {
@@ -2488,7 +2503,9 @@ DLBB_API int dlbb_gemm_bf16_nt_v(const void* A, int64_t lda, const void* B, int6
     if (bal) hipLaunchKernelGGL(gemm_bf16_nt_256_pp_persist_bal<L>, gp, bp, kPP6Lds, stream, a); \
     else hipLaunchKernelGGL(gemm_bf16_nt_256_pp_persist<L>, gp, bp, kPP6Lds, stream, a);   \
   } while (0)
+      if (lean == PP_PLAIN && dlbb_diag_nostore) lean = PP_NOSTORE;
       switch (lean) {
+        case PP_NOSTORE: DLBB_PP_PERSIST_LAUNCH(PP_NOSTORE); break;
         case PP_BIAS: DLBB_PP_PERSIST_LAUNCH(PP_BIAS); break;
         case PP_BIAS_GELU_TANH: DLBB_PP_PERSIST_LAUNCH(PP_BIAS_GELU_TANH); break;
         case PP_BIAS_GELU_ERF: DLBB_PP_PERSIST_LAUNCH(PP_BIAS_GELU_ERF); break;

@@ -79,6 +79,7 @@ _SIGS = {
     "dlbb_gemm_set_bal": (None, [c_int]),
     "dlbb_gemm_set_spread_early": (None, [c_int]),
     "dlbb_gemm_set_group_m": (None, [c_int]),
+    "dlbb_gemm_set_diag_nostore": (None, [c_int]),
     "dlbb_gemm_set_persist_epi": (None, [c_int]),
     "dlbb_gemm_set_concurrent": (None, [c_int]),
     "dlbb_gemm_get_concurrent": (c_int, []),

@@ -1,5 +1,5 @@
 """Diagnostic: does the GPT-2 LM-head forward (16384 x 50304 x 768) depend on the order tiles are
-handed out? Times our 256² persistent kernel (``mfma``) and the 256 x 192 spread-store persistent
+handed out, and what do its C stores cost? Times our 256² persistent kernel (``mfma``) and the 256 x 192 spread-store persistent
 kernel (``mfma192p``) for several GROUP_M values of ``tile_of`` (csrc/gemm.hip,
 dlbb_gemm_set_group_m), against hipBLASLt. One JSON line per (kernel, group_m)."""
 import json
@@ -39,4 +39,14 @@ for name, fn in (("mfma", gemm._mfma_linear), ("mfma192p", gemm._mfma192p_linear
         lib.dlbb_gemm_set_group_m(gm)
         ms = timed(lambda: fn(x, w, None, None, None, out, None))
         print(json.dumps({"kernel": name, "group_m": gm, "ms": round(ms, 4)}), flush=True)
+lib.dlbb_gemm_set_group_m(0)
+# the same kernels with their C stores compiled out: the K-loop's own time over the same tiles
+lib.dlbb_gemm_set_diag_nostore(1)
+for name, fn in (("mfma", gemm._mfma_linear), ("mfma192p", gemm._mfma192p_linear)):
+    for gm in (1, 8):
+        lib.dlbb_gemm_set_group_m(gm)
+        ms = timed(lambda: fn(x, w, None, None, None, out, None))
+        print(json.dumps({"kernel": name, "group_m": gm, "no_stores": True, "ms": round(ms, 4)}),
+              flush=True)
+lib.dlbb_gemm_set_diag_nostore(0)
 lib.dlbb_gemm_set_group_m(0)
