@@ -273,7 +273,8 @@ struct AttnBwdArgs {
   const uint16_t* qkv;     // [B, T, 3, H, D]
   const uint16_t* dout;    // [B, T, H, D] (row stride ldo)
   const float* lse;        // [B, H, T] natural log
-  const float* delta;      // [B, H, T]
+  const float* delta;      // [B, H, T]: -rowsum(dO * O) (negated: the dP accumulator's start)
+  const float* nl2;        // [B, H, T]: -LSE * log2(e) (p = exp2(S * scale_log2 + nl2))
   uint16_t* dqkv;          // [B, T, 3, H, D] (row stride ld)
   int64_t ld, ldo;
   int B, T, H;
@@ -282,10 +283,15 @@ struct AttnBwdArgs {
   int xcd;                 // see head_block
 };
 
-// delta[b, h, t] = sum_d dO[b, t, h, d] * O[b, t, h, d]; one thread per (b, t, h) row of 64
+// ndelta[b, h, t] = -sum_d dO[b, t, h, d] * O[b, t, h, d] and nl2[b, h, t] = -LSE * log2(e): the
+// row constants of the backward, pre-negated / pre-scaled once per row here so the dK/dV loop
+// starts its dP accumulator at -delta (dS = P * dP' with no subtraction) and forms
+// p = exp2(S * scale_log2 + nl2) in one fma; one thread per (b, t, h) row of 64
 __global__ void __launch_bounds__(256) attn_bwd_delta_kernel(const uint16_t* __restrict__ dout,
                                                              const uint16_t* __restrict__ out,
-                                                             int64_t ldo, float* __restrict__ delta,
+                                                             int64_t ldo, const float* __restrict__ lse,
+                                                             float* __restrict__ delta,
+                                                             float* __restrict__ nl2,
                                                              int B, int T, int H) {
   const int64_t row = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   const int64_t nrows = static_cast<int64_t>(B) * T * H;
@@ -304,7 +310,9 @@ __global__ void __launch_bounds__(256) attn_bwd_delta_kernel(const uint16_t* __r
     for (int j = 0; j < 8; ++j) acc += x[j] * y[j];
   }
   const int64_t b = bt / T, t = bt % T;
-  delta[(b * H + h) * T + t] = acc;
+  const int64_t i = (b * H + h) * T + t;
+  delta[i] = -acc;
+  nl2[i] = -lse[i] * 1.4426950408889634f;
 }
 
 // transposed operand read of a [rows][64] bf16 image (bswz): A operand of a 32x32x16 MFMA whose
@@ -370,8 +378,8 @@ __global__ void __launch_bounds__(kAttnThreads, 2) attn_bwd_dkdv_d64_kernel(Attn
   const uint16_t* dout_bt = a.dout + static_cast<int64_t>(b) * a.T * a.ldo;
   const int hoff = h * kAttnD;
   const int64_t bh = static_cast<int64_t>(b) * a.H + h;
-  const float* lrow = a.lse + bh * a.T;
-  const float* drow = a.delta + bh * a.T;
+  const float* lrow = a.nl2 + bh * a.T;            // -LSE * log2(e)
+  const float* drow = a.delta + bh * a.T;          // -delta
 
   bf16x8 kf[4], vf[4];
   {
@@ -426,19 +434,20 @@ __global__ void __launch_bounds__(kAttnThreads, 2) attn_bwd_dkdv_d64_kernel(Attn
       const int qsub = qs + 32 * sub;
       if (qsub + 31 < kw) continue;                 // wave-uniform: every query < every key
       const int rb = 32 * sub;                      // image row base of this 32-query block
-      // per-row constants for rows q = qsub + 8 g + 4 hi + u (register e = 4 g + u)
-      float l2[16], dl[16];
+      // per-row constants for rows q = qsub + 8 g + 4 hi + u (register e = 4 g + u): -LSE log2e
+      // and -delta, the latter as the dP accumulator's starting value (dP' = dO V^T - delta)
+      float l2[16];
+      f32x16 s, dp;
 #pragma unroll
       for (int g4 = 0; g4 < 4; ++g4) {
         const float4 lv = *reinterpret_cast<const float4*>(rv + rb + 8 * g4 + 4 * hi);
         const float4 dv4 = *reinterpret_cast<const float4*>(rv + 64 + rb + 8 * g4 + 4 * hi);
         l2[4 * g4 + 0] = lv.x; l2[4 * g4 + 1] = lv.y; l2[4 * g4 + 2] = lv.z; l2[4 * g4 + 3] = lv.w;
-        dl[4 * g4 + 0] = dv4.x; dl[4 * g4 + 1] = dv4.y; dl[4 * g4 + 2] = dv4.z;
-        dl[4 * g4 + 3] = dv4.w;
+        dp[4 * g4 + 0] = dv4.x; dp[4 * g4 + 1] = dv4.y; dp[4 * g4 + 2] = dv4.z;
+        dp[4 * g4 + 3] = dv4.w;
       }
-      f32x16 s, dp;
 #pragma unroll
-      for (int e = 0; e < 16; ++e) { s[e] = 0.f; dp[e] = 0.f; }
+      for (int e = 0; e < 16; ++e) s[e] = 0.f;
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) {
         s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_operand(iq, rb + r, 2 * ks + hi), kf[ks],
@@ -446,15 +455,22 @@ __global__ void __launch_bounds__(kAttnThreads, 2) attn_bwd_dkdv_d64_kernel(Attn
         dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_operand(ig, rb + r, 2 * ks + hi), vf[ks],
                                                      dp, 0, 0, 0);
       }
+      // mask the raw scores (exp2(-inf) = 0) only where a query of the block can precede a key
+      // of the wave (the diagonal) or lies past T: a wave-uniform branch, so interior blocks run
+      // no per-element index compares
       const bool diag = qsub < kw + 31;
+      if (diag || qsub + 31 >= a.T) {
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int q = qsub + (e & 3) + 8 * (e >> 2) + 4 * hi;
+          if ((diag && mykey > q) || q >= a.T) s[e] = -INFINITY;
+        }
+      }
 #pragma unroll
       for (int e = 0; e < 16; ++e) {
-        const int q = qsub + (e & 3) + 8 * (e >> 2) + 4 * hi;
-        float p = __builtin_amdgcn_exp2f(
-            __builtin_fmaf(s[e], a.scale_log2, -l2[e] * 1.4426950408889634f));
-        if ((diag && mykey > q) || q >= a.T) p = 0.f;
+        const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(s[e], a.scale_log2, l2[e]));
         s[e] = p;
-        dp[e] = p * (dp[e] - dl[e]);
+        dp[e] = p * dp[e];
       }
 #pragma unroll
       for (int st = 0; st < 2; ++st) {
@@ -531,8 +547,8 @@ __global__ void __launch_bounds__(kAttnThreads, 2) attn_bwd_dq_d64_kernel(AttnBw
       gf[ks] = *reinterpret_cast<const bf16x8*>(gp + 16 * ks);
     }
   }
-  const float l2 = a.lse[bh * a.T + qc] * 1.4426950408889634f;
-  const float dl = a.delta[bh * a.T + qc];
+  const float nl2 = a.nl2[bh * a.T + qc];          // -LSE * log2(e)
+  const float nd = a.delta[bh * a.T + qc];         // -delta
   f32x16 dq[2];
 #pragma unroll
   for (int dt = 0; dt < 2; ++dt)
@@ -554,7 +570,7 @@ __global__ void __launch_bounds__(kAttnThreads, 2) attn_bwd_dq_d64_kernel(AttnBw
     if (k0 <= q_hi) {
       const char* tk = tileK(cur);
       const char* tv = tileV(cur);
-      const bool diag = k0 + kKB - 1 > qw;
+      const bool diag = k0 + kKB - 1 > qw;           // wave-uniform: a key beyond a query
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk) {
         f32x16 s, dp;
@@ -567,12 +583,19 @@ __global__ void __launch_bounds__(kAttnThreads, 2) attn_bwd_dq_d64_kernel(AttnBw
           dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_operand(tv, kk * 32 + r, 2 * ks + hi),
                                                        gf[ks], dp, 0, 0, 0);
         }
+        // causal mask on the raw scores of diagonal tiles only (a branch, as in the forward:
+        // exp2 of -inf is the zero probability); interior tiles run no per-element compares
+        if (diag) {
+#pragma unroll
+          for (int e = 0; e < 16; ++e) {
+            const int key = k0 + kk * 32 + (e & 3) + 8 * (e >> 2) + 4 * hi;
+            if (key > qme) s[e] = -INFINITY;
+          }
+        }
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
-          const int key = k0 + kk * 32 + (e & 3) + 8 * (e >> 2) + 4 * hi;
-          float p = __builtin_amdgcn_exp2f(s[e] * a.scale_log2 - l2);
-          if (diag && key > qme) p = 0.f;
-          dp[e] = p * (dp[e] - dl);
+          const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(s[e], a.scale_log2, nl2));
+          dp[e] = p * (dp[e] + nd);
         }
 #pragma unroll
         for (int st = 0; st < 2; ++st) {
@@ -656,7 +679,8 @@ DLBB_API int dlbb_attn_fwd(const void* qkv, int64_t ld, void* out, int64_t ldo, 
 }
 
 // Backward of dlbb_attn_fwd. dout / out: [B, T, H, 64] (row stride ldo); lse: forward's;
-// delta: [B, H, T] fp32 workspace; dqkv: [B, T, 3, H, 64] (row stride ld, written fully).
+// delta: [2, B, H, T] fp32 workspace (-delta, -LSE log2 e); dqkv: [B, T, 3, H, 64] (row stride
+// ld, written fully).
 DLBB_API int dlbb_attn_bwd(const void* qkv, int64_t ld, const void* out, const void* dout,
                            int64_t ldo, const float* lse, float* delta, void* dqkv, int B, int T,
                            int H, int D, float scale, hipStream_t stream) {
@@ -665,12 +689,13 @@ DLBB_API int dlbb_attn_bwd(const void* qkv, int64_t ld, const void* out, const v
   if (ld % 8 || ldo % 8 || ld < 3 * H * D || ldo < H * D) return hipErrorInvalidValue;
   auto mis16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) != 0; };
   if (mis16(qkv) || mis16(out) || mis16(dout) || mis16(dqkv)) return hipErrorInvalidValue;
+  if (!lse || !delta) return hipErrorInvalidValue;
   const int64_t rows = static_cast<int64_t>(B) * T * H;
   hipLaunchKernelGGL(attn_bwd_delta_kernel, dim3(static_cast<unsigned>((rows + 255) / 256)),
                      dim3(256), 0, stream, static_cast<const uint16_t*>(dout),
-                     static_cast<const uint16_t*>(out), ldo, delta, B, T, H);
+                     static_cast<const uint16_t*>(out), ldo, lse, delta, delta + rows, B, T, H);
   AttnBwdArgs a{static_cast<const uint16_t*>(qkv), static_cast<const uint16_t*>(dout), lse, delta,
-                static_cast<uint16_t*>(dqkv), ld, ldo, B, T, H,
+                delta + rows, static_cast<uint16_t*>(dqkv), ld, ldo, B, T, H,
                 scale * 1.4426950408889634f, scale, g_attn_xcd};
   // dK/dV and dQ are independent (both read Q/K/V/dO/LSE/delta, write disjoint dQKV columns):
   // dQ runs on a side stream forked after the delta kernel and joined back, so each kernel's
