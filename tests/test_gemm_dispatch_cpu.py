@@ -113,3 +113,22 @@ def test_concurrent_comm_switches_off_persistent_forms_in_the_library():
             assert lib.dlbb_gemm_get_concurrent() == 1
         assert lib.dlbb_gemm_get_concurrent() == 1
     assert lib.dlbb_gemm_get_concurrent() == 0
+
+
+def test_library_candidate_needs_margin(monkeypatch):
+    """The autotuners pick hipBLASLt only when it beats the fastest hand-written candidate by
+    more than ``library_margin()`` (host setup cost and co-residency hazards are invisible to
+    device-time tuning); DLBB_LIB_MARGIN=0 is plain fastest-wins."""
+    from distributed_llm_backend_benchmark_amd.ops import gemm
+
+    monkeypatch.delenv("DLBB_LIB_MARGIN", raising=False)
+    assert gemm.library_margin() == 0.03
+    assert gemm._choose({"mfma": 1.02, "blas": 1.0})[0] == "mfma"
+    assert gemm._choose({"mfma": 1.05, "mfma192": 1.029, "blas": 1.0})[0] == "mfma192"
+    assert gemm._choose({"mfma": 1.05, "blas": 1.0})[0] == "blas"
+    assert gemm._choose({"mfma": 0.9, "blas": 1.0})[0] == "mfma"
+    assert gemm._choose({"blas": 1.0})[0] == "blas"
+    monkeypatch.setenv("DLBB_LIB_MARGIN", "0")
+    assert gemm._choose({"mfma": 1.02, "blas": 1.0})[0] == "blas"
+    monkeypatch.setenv("DLBB_LIB_MARGIN", "bogus")
+    assert gemm.library_margin() == 0.03
