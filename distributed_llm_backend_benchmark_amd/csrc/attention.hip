@@ -274,7 +274,8 @@ struct AttnBwdArgs {
   const uint16_t* dout;    // [B, T, H, D] (row stride ldo)
   const float* lse;        // [B, H, T] natural log
   const float* delta;      // [B, H, T]: -rowsum(dO * O) (negated: the dP accumulator's start)
-  const float* nl2;        // [B, H, T]: -LSE * log2(e) (p = exp2(S * scale_log2 + nl2))
+  const float* nls;        // [B, H, T]: -LSE * sqrt(D) (the S accumulator's start: S' = S - LSE
+                           // sqrt(D), p = exp2(S' * scale_log2))
   uint16_t* dqkv;          // [B, T, 3, H, D] (row stride ld)
   int64_t ld, ldo;
   int B, T, H;
@@ -283,16 +284,17 @@ struct AttnBwdArgs {
   int xcd;                 // see head_block
 };
 
-// ndelta[b, h, t] = -sum_d dO[b, t, h, d] * O[b, t, h, d] and nl2[b, h, t] = -LSE * log2(e): the
+// ndelta[b, h, t] = -sum_d dO[b, t, h, d] * O[b, t, h, d] and nls[b, h, t] = -LSE * sqrt(D): the
 // row constants of the backward, pre-negated / pre-scaled once per row here so the dK/dV loop
-// starts its dP accumulator at -delta (dS = P * dP' with no subtraction) and forms
-// p = exp2(S * scale_log2 + nl2) in one fma; one thread per (b, t, h) row of 64
+// starts its S and dP accumulators at them (guide: 'row constants as the initial accumulator'):
+// p = exp2(S' * scale_log2) and dS = P * dP' with no subtraction, and no constant held in
+// registers across the MFMA chains; one thread per (b, t, h) row of 64
 __global__ void __launch_bounds__(256) attn_bwd_delta_kernel(const uint16_t* __restrict__ dout,
                                                              const uint16_t* __restrict__ out,
                                                              int64_t ldo, const float* __restrict__ lse,
                                                              float* __restrict__ delta,
-                                                             float* __restrict__ nl2,
-                                                             int B, int T, int H) {
+                                                             float* __restrict__ nls,
+                                                             float sqrt_d, int B, int T, int H) {
   const int64_t row = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   const int64_t nrows = static_cast<int64_t>(B) * T * H;
   if (row >= nrows) return;
@@ -312,7 +314,7 @@ __global__ void __launch_bounds__(256) attn_bwd_delta_kernel(const uint16_t* __r
   const int64_t b = bt / T, t = bt % T;
   const int64_t i = (b * H + h) * T + t;
   delta[i] = -acc;
-  nl2[i] = -lse[i] * 1.4426950408889634f;
+  nls[i] = -lse[i] * sqrt_d;
 }
 
 // transposed operand read of a [rows][64] bf16 image (bswz): A operand of a 32x32x16 MFMA whose
@@ -378,7 +380,7 @@ __global__ void __launch_bounds__(kAttnThreads, 2) attn_bwd_dkdv_d64_kernel(Attn
   const uint16_t* dout_bt = a.dout + static_cast<int64_t>(b) * a.T * a.ldo;
   const int hoff = h * kAttnD;
   const int64_t bh = static_cast<int64_t>(b) * a.H + h;
-  const float* lrow = a.nl2 + bh * a.T;            // -LSE * log2(e)
+  const float* lrow = a.nls + bh * a.T;            // -LSE * sqrt(D)
   const float* drow = a.delta + bh * a.T;          // -delta
 
   bf16x8 kf[4], vf[4];
@@ -434,20 +436,17 @@ __global__ void __launch_bounds__(kAttnThreads, 2) attn_bwd_dkdv_d64_kernel(Attn
       const int qsub = qs + 32 * sub;
       if (qsub + 31 < kw) continue;                 // wave-uniform: every query < every key
       const int rb = 32 * sub;                      // image row base of this 32-query block
-      // per-row constants for rows q = qsub + 8 g + 4 hi + u (register e = 4 g + u): -LSE log2e
-      // and -delta, the latter as the dP accumulator's starting value (dP' = dO V^T - delta)
-      float l2[16];
+      // per-row constants for rows q = qsub + 8 g + 4 hi + u (register e = 4 g + u) as the
+      // accumulators' starting values: S' = Q K^T - LSE sqrt(D), dP' = dO V^T - delta
       f32x16 s, dp;
 #pragma unroll
       for (int g4 = 0; g4 < 4; ++g4) {
         const float4 lv = *reinterpret_cast<const float4*>(rv + rb + 8 * g4 + 4 * hi);
         const float4 dv4 = *reinterpret_cast<const float4*>(rv + 64 + rb + 8 * g4 + 4 * hi);
-        l2[4 * g4 + 0] = lv.x; l2[4 * g4 + 1] = lv.y; l2[4 * g4 + 2] = lv.z; l2[4 * g4 + 3] = lv.w;
+        s[4 * g4 + 0] = lv.x; s[4 * g4 + 1] = lv.y; s[4 * g4 + 2] = lv.z; s[4 * g4 + 3] = lv.w;
         dp[4 * g4 + 0] = dv4.x; dp[4 * g4 + 1] = dv4.y; dp[4 * g4 + 2] = dv4.z;
         dp[4 * g4 + 3] = dv4.w;
       }
-#pragma unroll
-      for (int e = 0; e < 16; ++e) s[e] = 0.f;
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) {
         s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_operand(iq, rb + r, 2 * ks + hi), kf[ks],
@@ -468,7 +467,7 @@ __global__ void __launch_bounds__(kAttnThreads, 2) attn_bwd_dkdv_d64_kernel(Attn
       }
 #pragma unroll
       for (int e = 0; e < 16; ++e) {
-        const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(s[e], a.scale_log2, l2[e]));
+        const float p = __builtin_amdgcn_exp2f(s[e] * a.scale_log2);
         s[e] = p;
         dp[e] = p * dp[e];
       }
@@ -547,7 +546,7 @@ __global__ void __launch_bounds__(kAttnThreads, 2) attn_bwd_dq_d64_kernel(AttnBw
       gf[ks] = *reinterpret_cast<const bf16x8*>(gp + 16 * ks);
     }
   }
-  const float nl2 = a.nl2[bh * a.T + qc];          // -LSE * log2(e)
+  const float nl2 = a.nls[bh * a.T + qc] * a.scale_log2;   // -LSE * log2(e)
   const float nd = a.delta[bh * a.T + qc];         // -delta
   f32x16 dq[2];
 #pragma unroll
@@ -679,7 +678,7 @@ DLBB_API int dlbb_attn_fwd(const void* qkv, int64_t ld, void* out, int64_t ldo, 
 }
 
 // Backward of dlbb_attn_fwd. dout / out: [B, T, H, 64] (row stride ldo); lse: forward's;
-// delta: [2, B, H, T] fp32 workspace (-delta, -LSE log2 e); dqkv: [B, T, 3, H, 64] (row stride
+// delta: [2, B, H, T] fp32 workspace (-delta, -LSE sqrt(D)); dqkv: [B, T, 3, H, 64] (row stride
 // ld, written fully).
 DLBB_API int dlbb_attn_bwd(const void* qkv, int64_t ld, const void* out, const void* dout,
                            int64_t ldo, const float* lse, float* delta, void* dqkv, int B, int T,
@@ -693,7 +692,8 @@ DLBB_API int dlbb_attn_bwd(const void* qkv, int64_t ld, const void* out, const v
   const int64_t rows = static_cast<int64_t>(B) * T * H;
   hipLaunchKernelGGL(attn_bwd_delta_kernel, dim3(static_cast<unsigned>((rows + 255) / 256)),
                      dim3(256), 0, stream, static_cast<const uint16_t*>(dout),
-                     static_cast<const uint16_t*>(out), ldo, lse, delta, delta + rows, B, T, H);
+                     static_cast<const uint16_t*>(out), ldo, lse, delta, delta + rows,
+                     1.0f / scale, B, T, H);
   AttnBwdArgs a{static_cast<const uint16_t*>(qkv), static_cast<const uint16_t*>(dout), lse, delta,
                 delta + rows, static_cast<uint16_t*>(dqkv), ld, ldo, B, T, H,
                 scale * 1.4426950408889634f, scale, g_attn_xcd};

@@ -77,7 +77,7 @@ def attn_bwd(qkv: torch.Tensor, out: torch.Tensor, lse: torch.Tensor, gout: torc
     D = C // n_head
     gout = gout.contiguous()
     dqkv = torch.empty_like(qkv)
-    # workspace: -rowsum(dO * O) and -LSE * log2(e), [2, B, H, T] (csrc/attention.hip)
+    # workspace: -rowsum(dO * O) and -LSE * sqrt(D), [2, B, H, T] (csrc/attention.hip)
     delta = torch.empty(2, B, n_head, T, dtype=torch.float32, device=qkv.device)
     check(_lib.lib().dlbb_attn_bwd(qkv.data_ptr(), C3, out.data_ptr(), gout.data_ptr(), C,
                                    lse.data_ptr(), delta.data_ptr(), dqkv.data_ptr(), B, T, n_head,

@@ -62,16 +62,17 @@ def _agree_names(kind: str, key, names) -> list:
 
 def library_margin() -> float:
     """Fraction by which the library GEMM (``blas``) must beat the fastest hand-written candidate
-    to be chosen (``DLBB_LIB_MARGIN``, default 0.03). The autotuners time device work only; a
+    to be chosen (``DLBB_LIB_MARGIN``, default 0.05). The autotuners time device work only; a
     hipBLASLt call also pays ~15 us of host-side setup per call (round-3 measurement, invisible
     to device-time tuning but exposed whenever the host is the bottleneck, e.g. the eager TP
     forward), is a persistent Stream-K grid that stalls beside comm kernels, and keeps the
     kernel mix off our own code. Inside the margin the hand-written kernel runs: at the GPT-2
-    LM-head forward that costs 0.03 ms per step (1.11 vs 1.08 ms). 0 = pure fastest-wins (A/B)."""
+    LM-head forward (ours 2.8-3.3 % behind by box) that costs ~0.03 ms per step; the A/B against
+    ``DLBB_LIB_MARGIN=0`` is recorded in profiles/r04_final. 0 = pure fastest-wins."""
     try:
-        return max(0.0, float(os.environ.get("DLBB_LIB_MARGIN", "0.03")))
+        return max(0.0, float(os.environ.get("DLBB_LIB_MARGIN", "0.05")))
     except ValueError:
-        return 0.03
+        return 0.05
 
 
 def _choose(times: dict, kind: str = "", key=()):

@@ -122,13 +122,13 @@ def test_library_candidate_needs_margin(monkeypatch):
     from distributed_llm_backend_benchmark_amd.ops import gemm
 
     monkeypatch.delenv("DLBB_LIB_MARGIN", raising=False)
-    assert gemm.library_margin() == 0.03
-    assert gemm._choose({"mfma": 1.02, "blas": 1.0})[0] == "mfma"
-    assert gemm._choose({"mfma": 1.05, "mfma192": 1.029, "blas": 1.0})[0] == "mfma192"
-    assert gemm._choose({"mfma": 1.05, "blas": 1.0})[0] == "blas"
+    assert gemm.library_margin() == 0.05
+    assert gemm._choose({"mfma": 1.04, "blas": 1.0})[0] == "mfma"
+    assert gemm._choose({"mfma": 1.07, "mfma192": 1.049, "blas": 1.0})[0] == "mfma192"
+    assert gemm._choose({"mfma": 1.07, "blas": 1.0})[0] == "blas"
     assert gemm._choose({"mfma": 0.9, "blas": 1.0})[0] == "mfma"
     assert gemm._choose({"blas": 1.0})[0] == "blas"
     monkeypatch.setenv("DLBB_LIB_MARGIN", "0")
     assert gemm._choose({"mfma": 1.02, "blas": 1.0})[0] == "blas"
     monkeypatch.setenv("DLBB_LIB_MARGIN", "bogus")
-    assert gemm.library_margin() == 0.03
+    assert gemm.library_margin() == 0.05
