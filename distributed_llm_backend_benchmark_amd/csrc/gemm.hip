@@ -1664,21 +1664,18 @@ __global__ void __launch_bounds__(kThreads2, 1) gemm_bf16_nn_256_pp_persist_bal(
 
 // ---------------------------------------------------------------------------------------
 // Persistent 256 x 192 ping-pong with the C stores SPREAD under the next tile's K-loop (plain
-// bf16 output; the GPT-2 LM head 16384 x 50304 x 768: 262 x 192 columns exactly).
-// pp_persist_body flushes a finished tile in one burst at the next tile's first memory interval;
-// stores and DMA loads share vmcnt (in order), so the next counted DMA wait also waits for every
-// store: a tile's 128 KiB of C drains serially (LM head: 1.65 GB of logits = ~0.3 ms of a ~1.1 ms
-// kernel, profiles/r04_gemm/SUMMARY.md). Here the finished accumulators are packed to bf16 (48
-// VGPRs: the 192-wide tile's 96 fp32 accumulators leave room at 2 waves per SIMD), zeroed, and
-// the 24 8-byte stores of a lane go out kSpi per iteration over the next tile's first iterations,
-// each batch AFTER that iteration's DMA issues. Every counted wait of iteration g then adds the
-// stores of iterations g - 1 and g (younger than any load it retires); a batch is retired one
-// iteration later, by which time it has had two memory intervals and an MFMA phase to drain.
-// Host contract: N % 192 == 0, M % 16 == 0, K / 64 > kSpreadIters (every spread window inside
-// one tile).
-// EARLY (12 or 18): stores issued at the boundary itself, before that iteration's loads; the rest
-// (24 / 12 parked VGPRs) go out kSpi per iteration after the loads. 6 or 0 early (36 / 48 parked)
-// spill once the spread iterations are unrolled (249 VGPRs at 12).
+// bf16 output; autotune candidate `mfma192p`). Built to test whether a tile's C stores, flushed in
+// one burst by pp_persist_body at the next tile's first memory interval, cost the GPT-2 LM head
+// (16384 x 50304 x 768: 1.65 GB of logits) because they serialise with the counted DMA waits
+// (stores and loads share vmcnt). They do not: the K-loop alone takes 0.83 ms and the stores add
+// 0.25 ms burst or spread alike (profiles/r04_gemm/SUMMARY.md) — kept as a correct candidate.
+// At a tile boundary each lane packs its 96 fp32 accumulators to bf16 pairs and zeroes them;
+// EARLY (12 or 18) of its 24 eight-byte stores go out right there (before that iteration's
+// loads), the rest (24 / 12 parked VGPRs) kSpi per iteration AFTER that iteration's DMA. Every
+// counted wait adds the stores younger than the load it retires (template arguments: one
+// immediate per wait; a runtime count measured 13-17 % slower); a spread batch is retired one
+// iteration later. 6 or 0 early (36 / 48 parked) spill once the spread iterations are unrolled
+// (249 VGPRs at 12). Host contract: N % 192 == 0, M % 16 == 0, K / 64 > the spread iterations.
 constexpr int kSpi = 3;
 constexpr int spread_iters(int early) { return (24 - early) / kSpi; }
 
