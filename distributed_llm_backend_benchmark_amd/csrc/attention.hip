@@ -273,9 +273,12 @@ struct AttnBwdArgs {
   const uint16_t* qkv;     // [B, T, 3, H, D]
   const uint16_t* dout;    // [B, T, H, D] (row stride ldo)
   const float* lse;        // [B, H, T] natural log
-  const float* delta;      // [B, H, T]: -rowsum(dO * O) (negated: the dP accumulator's start)
-  const float* nls;        // [B, H, T]: -LSE * sqrt(D) (the S accumulator's start: S' = S - LSE
+  float* delta;            // [B, H, T]: -rowsum(dO * O) (negated: the dP accumulator's start)
+  float* nls;              // [B, H, T]: -LSE * sqrt(D) (the S accumulator's start: S' = S - LSE
                            // sqrt(D), p = exp2(S' * scale_log2))
+  const uint16_t* out;     // [B, T, H, D] forward output O (row stride ldo): fuse_delta only
+  int fuse_delta;          // 1: the dQ kernel computes delta / nls for its queries and writes
+                           // them for the dK/dV kernel launched after it (no delta kernel)
   uint16_t* dqkv;          // [B, T, 3, H, D] (row stride ld)
   int64_t ld, ldo;
   int B, T, H;
@@ -294,7 +297,7 @@ __global__ void __launch_bounds__(256) attn_bwd_delta_kernel(const uint16_t* __r
                                                              int64_t ldo, const float* __restrict__ lse,
                                                              float* __restrict__ delta,
                                                              float* __restrict__ nls,
-                                                             float sqrt_d, int B, int T, int H) {
+                                                             float scale, int B, int T, int H) {
   const int64_t row = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   const int64_t nrows = static_cast<int64_t>(B) * T * H;
   if (row >= nrows) return;
@@ -302,19 +305,21 @@ __global__ void __launch_bounds__(256) attn_bwd_delta_kernel(const uint16_t* __r
   const int64_t bt = row / H;
   const uint16_t* g = dout + bt * ldo + h * kAttnD;
   const uint16_t* o = out + bt * ldo + h * kAttnD;
-  float acc = 0.f;
+  // even / odd 8-dim chunks summed separately, then added: the order of the dQ kernel's fused
+  // form (lane halves hi = 0 / 1, joined by lane ^ 32), so both give bitwise the same constants
+  float acc2[2] = {0.f, 0.f};
 #pragma unroll
   for (int c = 0; c < kAttnD / 8; ++c) {
     float x[8], y[8];
     load8<DT_BF16>(g, c, x);
     load8<DT_BF16>(o, c, y);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) acc += x[j] * y[j];
+    for (int j = 0; j < 8; ++j) acc2[c & 1] += x[j] * y[j];
   }
   const int64_t b = bt / T, t = bt % T;
   const int64_t i = (b * H + h) * T + t;
-  delta[i] = -acc;
-  nls[i] = -lse[i] * sqrt_d;
+  delta[i] = -(acc2[0] + acc2[1]);
+  nls[i] = -lse[i] / scale;
 }
 
 // transposed operand read of a [rows][64] bf16 image (bswz): A operand of a 32x32x16 MFMA whose
@@ -546,8 +551,32 @@ __global__ void __launch_bounds__(kAttnThreads, 2) attn_bwd_dq_d64_kernel(AttnBw
       gf[ks] = *reinterpret_cast<const bf16x8*>(gp + 16 * ks);
     }
   }
-  const float nl2 = a.nls[bh * a.T + qc] * a.scale_log2;   // -LSE * log2(e)
-  const float nd = a.delta[bh * a.T + qc];         // -delta
+  float nl2, nd;                                   // -LSE * log2(e), -delta
+  if (a.fuse_delta) {
+    // the row constants of this lane's query, here instead of a separate pass over dO and O:
+    // delta = dO . O over the 64 dims (8 per (ks, hi) fragment, halves joined by lane ^ 32)
+    const uint16_t* op = a.out + (static_cast<int64_t>(b) * a.T + qc) * a.ldo + hoff + 8 * hi;
+    float acc = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const bf16x8 of = *reinterpret_cast<const bf16x8*>(op + 16 * ks);
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        acc += bf16_to_f32(static_cast<uint16_t>(gf[ks][j])) *
+               bf16_to_f32(static_cast<uint16_t>(of[j]));
+    }
+    const float other = __shfl_xor(acc, 32, 64);
+    nd = -(hi == 0 ? acc + other : other + acc);   // (even chunks) + (odd chunks), as the kernel
+    const float nls = -a.lse[bh * a.T + qc] / a.scale;   // -LSE * sqrt(D)
+    nl2 = nls * a.scale_log2;
+    if (hi == 0 && qme < a.T) {
+      a.delta[bh * a.T + qme] = nd;
+      a.nls[bh * a.T + qme] = nls;
+    }
+  } else {
+    nl2 = a.nls[bh * a.T + qc] * a.scale_log2;
+    nd = a.delta[bh * a.T + qc];
+  }
   f32x16 dq[2];
 #pragma unroll
   for (int dt = 0; dt < 2; ++dt)
@@ -690,12 +719,17 @@ DLBB_API int dlbb_attn_bwd(const void* qkv, int64_t ld, const void* out, const v
   if (mis16(qkv) || mis16(out) || mis16(dout) || mis16(dqkv)) return hipErrorInvalidValue;
   if (!lse || !delta) return hipErrorInvalidValue;
   const int64_t rows = static_cast<int64_t>(B) * T * H;
-  hipLaunchKernelGGL(attn_bwd_delta_kernel, dim3(static_cast<unsigned>((rows + 255) / 256)),
-                     dim3(256), 0, stream, static_cast<const uint16_t*>(dout),
-                     static_cast<const uint16_t*>(out), ldo, lse, delta, delta + rows,
-                     1.0f / scale, B, T, H);
+  // sequential (default): the dQ kernel produces delta / nls for the dK/dV kernel after it;
+  // concurrent: both read them, so the separate delta kernel runs first
+  const int fuse = g_attn_concurrent ? 0 : 1;
+  if (!fuse)
+    hipLaunchKernelGGL(attn_bwd_delta_kernel, dim3(static_cast<unsigned>((rows + 255) / 256)),
+                       dim3(256), 0, stream, static_cast<const uint16_t*>(dout),
+                       static_cast<const uint16_t*>(out), ldo, lse, delta, delta + rows,
+                       scale, B, T, H);
   AttnBwdArgs a{static_cast<const uint16_t*>(qkv), static_cast<const uint16_t*>(dout), lse, delta,
-                delta + rows, static_cast<uint16_t*>(dqkv), ld, ldo, B, T, H,
+                delta + rows, static_cast<const uint16_t*>(out), fuse,
+                static_cast<uint16_t*>(dqkv), ld, ldo, B, T, H,
                 scale * 1.4426950408889634f, scale, g_attn_xcd};
   // dK/dV and dQ are independent (both read Q/K/V/dO/LSE/delta, write disjoint dQKV columns):
   // dQ runs on a side stream forked after the delta kernel and joined back, so each kernel's

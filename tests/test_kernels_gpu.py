@@ -427,10 +427,15 @@ def test_layernorm_fwd(cols, with_res):
         torch.testing.assert_close(h.float(), hin, rtol=0, atol=0)
 
 
-@pytest.mark.parametrize("cols", [768, 1024, 4096])
+@pytest.mark.parametrize("cols", [768, 1024, 4096, 128, 200])
 @pytest.mark.parametrize("with_res", [False, True])
 def test_layernorm_bwd(cols, with_res):
+    """Fused backward at the instantiated widths; at others (128, 200: toy models) the same math
+    in fp32 torch ops, counted in ``LN_FALLBACKS``."""
     from distributed_llm_backend_benchmark_amd.ops import layernorm
+    from distributed_llm_backend_benchmark_amd.ops import norm_act
+
+    fb0 = norm_act.LN_FALLBACKS["count"]
 
     rows = 520
     x = _randn(rows, cols, seed=15).requires_grad_(True)
@@ -458,6 +463,7 @@ def test_layernorm_bwd(cols, with_res):
     torch.testing.assert_close(b.grad.float(), bf.grad, rtol=3e-2, atol=0.5)
     if with_res:
         torch.testing.assert_close(r.grad.float(), rf.grad, rtol=3e-2, atol=3e-2)
+    assert norm_act.LN_FALLBACKS["count"] - fb0 == (0 if cols % 256 == 0 else 1)
 
 
 @pytest.mark.parametrize("approx", ["none", "tanh"])
