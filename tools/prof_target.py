@@ -1,5 +1,5 @@
 """Tiny driver for PMC-counter profiling: runs ONE op a few times (no timing logic).
-usage: prof_target.py lmhead|lmhead192|lmhead192p|lmheadblas|gemm256|gemm256s6|gemm256s7|gemm128|blas|nn|nnplain|tn|tnplain|wgrad128|
+usage: prof_target.py attnfwd|attnbwd|lmhead|lmhead192|lmhead192p|lmheadblas|gemm256|gemm256s6|gemm256s7|gemm128|blas|nn|nnplain|tn|tnplain|wgrad128|
 blastn|reduce8|ln|xent|xentfused|embbwd"""
 import os
 import sys
@@ -13,7 +13,15 @@ from distributed_llm_backend_benchmark_amd.ops.gemm import set_tile  # noqa: E40
 what = sys.argv[1]
 dev = "cuda"
 g = torch.Generator(device=dev).manual_seed(0)
-if what.startswith("lmhead"):    # GPT-2 LM-head forward 16384 x 50304 x 768: lmhead (library
+if what in ("attnfwd", "attnbwd"):   # causal attention at the GPT-2 step shape (B16 T1024 H12)
+    from distributed_llm_backend_benchmark_amd.ops.attention import attn_bwd, attn_fwd
+
+    qkv = torch.randn(16, 1024, 3 * 12 * 64, device=dev, generator=g).to(torch.bfloat16)
+    gout = torch.randn(16, 1024, 12 * 64, device=dev, generator=g).to(torch.bfloat16)
+    o, lse = attn_fwd(qkv, 12)
+    fn = ((lambda: attn_fwd(qkv, 12)) if what == "attnfwd"  # noqa: E731
+          else (lambda: attn_bwd(qkv, o, lse, gout, 12)))
+elif what.startswith("lmhead"):    # GPT-2 LM-head forward 16384 x 50304 x 768: lmhead (library
     # dispatch: 256² persistent), lmhead192 / lmhead192p (256 x 192 ping-pong / persistent spread
     # stores), lmheadblas (hipBLASLt)
     from distributed_llm_backend_benchmark_amd.ops import gemm as G
