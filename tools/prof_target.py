@@ -1,5 +1,5 @@
 """Tiny driver for PMC-counter profiling: runs ONE op a few times (no timing logic).
-usage: prof_target.py attnfwd|attnbwd|lmhead|lmhead192|lmhead192p|lmheadblas|gemm256|gemm256s6|gemm256s7|gemm128|blas|nn|nnplain|tn|tnplain|wgrad128|
+usage: prof_target.py longk|longkblas|attnfwd|attnbwd|lmhead|lmhead192|lmhead192p|lmheadblas|gemm256|gemm256s6|gemm256s7|gemm128|blas|nn|nnplain|tn|tnplain|wgrad128|
 blastn|reduce8|ln|xent|xentfused|embbwd"""
 import os
 import sys
@@ -32,6 +32,11 @@ elif what.startswith("lmhead"):    # GPT-2 LM-head forward 16384 x 50304 x 768: 
     impl = {"lmhead": G._mfma_linear, "lmhead192": G._mfma192_linear,
             "lmhead192p": G._mfma192p_linear, "lmheadblas": G._blas_linear}[what]
     fn = lambda: impl(x, w, None, None, None, out, None)  # noqa: E731
+elif what in ("longk", "longkblas"):   # single-round long-K NT GEMM 4096 x 4096 x 16384
+    x = torch.randn(4096, 16384, device=dev, generator=g).to(torch.bfloat16)
+    w = torch.randn(4096, 16384, device=dev, generator=g).to(torch.bfloat16)
+    os.environ["DLBB_GEMM"] = "blas" if what == "longkblas" else "mfma"
+    fn = lambda: ops.linear(x, w)  # noqa: E731
 elif what.startswith("gemm") or what == "blas":
     M = N = K = 8192
     x = torch.randn(M, K, device=dev, generator=g).to(torch.bfloat16)
