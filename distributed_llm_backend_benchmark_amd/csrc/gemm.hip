@@ -1002,18 +1002,8 @@ __device__ __forceinline__ void store_tile12(const GemmArgs& a, const f32x4 (&ac
 // counted LDS-DMA wait with a compile-time count (the 192-wide tile changes every count)
 template <int N>
 __device__ __forceinline__ void wait_vm() {
-  static_assert(N >= 0 && N <= 24, "vmcnt range");
-  if constexpr (N == 0) DLBB_WAIT_VM(0);
-  else if constexpr (N == 3) DLBB_WAIT_VM(3);
-  else if constexpr (N == 4) DLBB_WAIT_VM(4);
-  else if constexpr (N == 6) DLBB_WAIT_VM(6);
-  else if constexpr (N == 7) DLBB_WAIT_VM(7);
-  else if constexpr (N == 8) DLBB_WAIT_VM(8);
-  else if constexpr (N == 10) DLBB_WAIT_VM(10);
-  else if constexpr (N == 12) DLBB_WAIT_VM(12);
-  else if constexpr (N == 16) DLBB_WAIT_VM(16);
-  else if constexpr (N == 20) DLBB_WAIT_VM(20);
-  else static_assert(N < 0, "add this count to wait_vm");
+  static_assert(N >= 0 && N <= 63, "vmcnt range");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
 // The ping-pong schedule, for B stored [N][K] (NT: forward, C = A · B^T) or [K][N] (NN: dgrad).
@@ -1036,9 +1026,15 @@ __device__ __forceinline__ void wait_vm() {
 // below is written in it (NJ = 4 gives the original literals).
 // PHASES (diagnostic only, dlbb_gemm_nt_phase_probe): thread 0 stamps start / first MFMA (after
 // the prologue waits) / end of the K-loop / end of the stores: 4 u64 per workgroup into `st`.
+// MOVEB (A/B, set_stagger(11); NT 256² only): wave row 0 issues B(u+2) between the two k-halves
+// of its MFMA phase instead of in its memory interval — the memory interval (24 ds_reads + 8
+// LDS-DMA pieces at 60-185 issue cycles each) outlasts the MFMA phase (PMC: MFMA busy 82 % on
+// the single-round long-K case, profiles/r04_gemm/SUMMARY.md). Its first counted wait then has
+// B(u+2) not yet issued: NBx fewer younger loads.
 template <bool NN, bool BAL = false, bool TN = false, bool STAMP = false, int NJ = 4,
-          bool PHASES = false>
+          bool PHASES = false, bool MOVEB = false>
 __device__ __forceinline__ void pingpong_body(GemmArgs a, char* smem, uint64_t* st = nullptr) {
+  static_assert(!MOVEB || (NJ == 4 && !NN && !TN), "MOVEB: NT 256² only");
   static_assert(NJ == 4 || (NJ == 3 && !NN && !TN), "192-wide tiles: NT only");
   constexpr int NBI = 2 * NJ;                 // B DMA instructions per staging wave per K-tile
   constexpr int kTileB = NJ * 64 * BK * 2;    // bytes of one B tile buffer
@@ -1165,20 +1161,22 @@ __device__ __forceinline__ void pingpong_body(GemmArgs a, char* smem, uint64_t* 
         DLBB_STAGE_A(u + 1, abuf0 + ((u + 1) & 1) * kTile2Bytes, 1,
                      stage_a_half(ra, lda2, rows_a, (u + 1) * kStep,
                                   abuf0 + ((u + 1) & 1) * kTile2Bytes, 1, wc, aoff));
-      if (b2) {
+      auto stage_b2 = [&]() {
         const int cb2 = cb == 0 ? 2 : cb - 1;         // (u + 2) % 3
         if (BAL)
           stage_bt(Z{}, H{}, u + 2, bbuf0 + cb2 * kTileB);
         else
           stage_bt(Z{}, F{}, u + 2, bbuf0 + cb2 * kTileB);
-      }
+      };
+      if (!MOVEB && b2) stage_b2();
       // retire A-hi(u) (issued two intervals ago; tile 0's came from row 1)
-      if (BAL) {
-        if (b2) wait_vm<NBI + 4>();
+      constexpr int kB2 = MOVEB ? 0 : (BAL ? NBI / 2 : NBI);   // B(u+2) instructions issued
+      if constexpr (BAL) {
+        if (b2) wait_vm<NBI / 2 + 4 + kB2>();
         else if (h1) wait_vm<NBI / 2 + 4>();
         else wait_vm<0>();
       } else {
-        if (b2) wait_vm<2 * NBI + 4>();
+        if (b2) wait_vm<NBI + 4 + kB2>();
         else if (h1) wait_vm<NBI + 4>();
         else wait_vm<0>();
       }
@@ -1186,7 +1184,25 @@ __device__ __forceinline__ void pingpong_body(GemmArgs a, char* smem, uint64_t* 
       __builtin_amdgcn_sched_barrier(0);
       __builtin_amdgcn_s_barrier();                   // end of interval 2u
       __builtin_amdgcn_sched_barrier(0);
-      mfma_all();
+      if constexpr (MOVEB) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[0][j], af[0][i], acc[i][j],
+                                                                0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        if (b2) stage_b2();                           // buffer (u+2)%3 free since 2u-1
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[1][j], af[1][i], acc[i][j],
+                                                                0, 0, 0);
+      } else {
+        mfma_all();
+      }
       __builtin_amdgcn_sched_barrier(0);
       if (h1) {                                       // retire B(u+1) (BAL: its first half)
         if (b2) { if (BAL) wait_vm<4 + NBI / 2>(); else wait_vm<4 + NBI>(); }
@@ -1267,6 +1283,11 @@ __global__ void __launch_bounds__(kThreads2, 1) gemm_bf16_nt_256_pingpong3(GemmA
 __global__ void __launch_bounds__(kThreads2, 1) gemm_bf16_nt_256_pingpong3_bal(GemmArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   pingpong_body<false, true>(a, smem);
+}
+// A/B variant (set_stagger(11)): BAL with wave row 0's B DMA inside its MFMA phase (MOVEB)
+__global__ void __launch_bounds__(kThreads2, 1) gemm_bf16_nt_256_pingpong3_bal_mb(GemmArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  pingpong_body<false, true, false, false, 4, false, true>(a, smem);
 }
 
 // 256 x 192 tiles (N % 192 == 0): grids that end in a partial round of 256² tiles
@@ -2487,10 +2508,10 @@ DLBB_API int dlbb_gemm_bf16_nt_v(const void* A, int64_t lda, const void* B, int6
     if (mode == 10 && (K < 2 * BK || lean < 0)) mode = 6;
     // ping-pong contract: 8-row A groups and 64-row B blocks wholly in or out (uniform clamps),
     // 32-bit buffer offsets within a 256-row panel
-    if ((mode == 6 || mode == 7 || mode == 10) && !(M % 8 == 0 && N % 64 == 0 && M >= 8 && lda * 2 * 256 + K * 2 < (1LL << 31) &&
+    if ((mode == 6 || mode == 7 || mode == 10 || mode == 11) && !(M % 8 == 0 && N % 64 == 0 && M >= 8 && lda * 2 * 256 + K * 2 < (1LL << 31) &&
                        ldb * 2 * 256 + K * 2 < (1LL << 31)))
       mode = 3;
-    if (mode == 5 || mode == 8 || mode > 10) mode = 3;
+    if (mode == 5 || mode == 8 || mode > 11) mode = 3;
     if (mode == 10) {
       const int64_t grid = tiles256 < num_cus() ? tiles256 : num_cus();
       const dim3 gp(static_cast<unsigned>(grid)), bp(kThreads2);
@@ -2528,6 +2549,8 @@ DLBB_API int dlbb_gemm_bf16_nt_v(const void* A, int64_t lda, const void* B, int6
                          2 * kBuf2Bytes, stream, a);
     } else if (mode == 9)
       launch_w4d(g, a, stream);
+    else if (mode == 11)                  // A/B: BAL + row 0's B DMA inside its MFMA phase
+      hipLaunchKernelGGL(gemm_bf16_nt_256_pingpong3_bal_mb, g, dim3(kThreads2), kPP6Lds, stream, a);
     else if (mode == 7 || (mode == 6 && use_bal(K / BK, false)))
       DLBB_PP_LAUNCH(gemm_bf16_nt_256_pingpong3_bal, STAMP_GEMM_NT, g, a);
     else if (mode == 6)

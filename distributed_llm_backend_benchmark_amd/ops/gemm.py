@@ -168,7 +168,8 @@ def set_stagger(mode: int) -> None:
     persistent kernel (next tile's prologue overlaps this tile's epilogue), 6 ping-pong (the
     two waves of each SIMD alternate whole-K-tile MFMA clusters and fragment loads, 160 KiB of
     LDS; M % 8 == 0 and N % 64 == 0, else 3 — the default; balanced DMA issue per
-    :func:`set_bal`), 7 ping-pong with the balanced DMA issue forced. For A/B benchmarking; the
+    :func:`set_bal`), 7 ping-pong with the balanced DMA issue forced, 11 = 7 with wave row 0's B
+    DMA issued inside its MFMA phase (NT only). For A/B benchmarking; the
     library default is the measured fastest (profiles/r02_gemm)."""
     _lib.lib().dlbb_gemm_set_stagger(int(mode))
 
