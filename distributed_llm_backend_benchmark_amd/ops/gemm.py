@@ -826,4 +826,6 @@ def kernel_mix() -> dict:
     # True: every choice above was made on rank-max timings agreed by all ranks
     out["agreed_across_ranks"] = _AGREE is not None
     out["contract_fallbacks"] = FALLBACKS["count"]
+    from .norm_act import LN_FALLBACKS                # LayerNorm backward at unfused widths
+    out["layernorm_bwd_fallbacks"] = LN_FALLBACKS["count"]
     return out
