@@ -717,7 +717,7 @@ DLBB_API int dlbb_attn_bwd(const void* qkv, int64_t ld, const void* out, const v
   if (ld % 8 || ldo % 8 || ld < 3 * H * D || ldo < H * D) return hipErrorInvalidValue;
   auto mis16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) != 0; };
   if (mis16(qkv) || mis16(out) || mis16(dout) || mis16(dqkv)) return hipErrorInvalidValue;
-  if (!lse || !delta) return hipErrorInvalidValue;
+  if (!lse || !delta || !out || !dout) return hipErrorInvalidValue;
   const int64_t rows = static_cast<int64_t>(B) * T * H;
   // sequential (default): the dQ kernel produces delta / nls for the dK/dV kernel after it;
   // concurrent: both read them, so the separate delta kernel runs first
