@@ -20,6 +20,11 @@ B16 x T1024 per GPU) as isolated, validated, roofline-guarded, time-boxed sectio
 (``bench/baseline_configs.py``) — a failing section records ``{"error": ...}`` and never costs
 the headline.
 
+Whole-run deadline (``--deadline-s``, default 420 s, rank-agreed): the headline all-reduce is
+always measured and printed; every later part (remaining headline candidates, side runs, each
+sweep size, each BASELINE config section) first checks the deadline and, once it has passed, is
+recorded as ``skipped_deadline`` instead of run. ``wall_s`` in the JSON is the whole run.
+
 Usage: ``python bench.py [--gpus N] [--steps K] [--warmup W]``; for N>1 launch with
 ``python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py``.
 """
@@ -70,16 +75,40 @@ def parse(argv=None):
                     metavar="LAYERS,HEADS,EMBD,VOCAB,BATCH,SEQ",
                     help="config 5 model (default: GPT-2 small, B16 x T1024 per GPU)")
     ap.add_argument("--ddp-steps", type=int, default=10)
+    ap.add_argument("--deadline-s", type=float, default=420.0,
+                    help="whole-run deadline (rank-agreed): parts after the headline are skipped "
+                         "and recorded as skipped_deadline once it has passed")
     return ap.parse_args(argv)
+
+
+class Deadline:
+    """Rank-agreed whole-run deadline: every check is collective (max elapsed over ranks), so
+    all ranks take the same skip decision at the same point and no rank is left alone in a
+    collective."""
+
+    def __init__(self, comm, seconds: float, t0: float):
+        self.comm, self.seconds, self.t0 = comm, float(seconds), t0
+        self.skipped = []
+
+    def remaining(self) -> float:
+        return self.seconds - self.comm.allreduce_max(time.perf_counter() - self.t0)
+
+    def expired(self, what: str = "") -> bool:
+        gone = self.remaining() <= 0
+        if gone and what:
+            self.skipped.append(what)
+        return gone
 
 
 def _shapes(spec):
     return [tuple(int(v) for v in part.split(",")) for part in spec.split(";") if part.strip()]
 
 
-def _baseline_configs(comm, args) -> dict:
+def _baseline_configs(comm, args, deadline=None) -> dict:
     """BASELINE configs 3/4/5 as isolated, validated, roofline-guarded, time-boxed sections
-    (bench/baseline_configs.py): a failure is recorded as {"error": ...} for its section only."""
+    (bench/baseline_configs.py): a failure is recorded as {"error": ...} for its section only;
+    each section's time box is cut to what is left of the whole-run ``deadline`` and a section
+    that starts after it is recorded as skipped."""
     from distributed_llm_backend_benchmark_amd.bench import baseline_configs as bc
 
     comm.cpu_group()        # host side channel for the sections' failure agreement (collective)
@@ -93,22 +122,31 @@ def _baseline_configs(comm, args) -> dict:
     if args.ddp_model:
         keys = ("n_layer", "n_head", "n_embd", "vocab", "batch", "seq")
         model = dict(zip(keys, (int(v) for v in args.ddp_model.split(","))))
-    budget = args.config_budget_s
-    return {
-        "config3_3d_allgather_reduce_scatter": bc.run_section(
-            comm, "config3", lambda c, b: bc.grid_3d(c, b, shapes=grid), budget),
-        "config4_moe_alltoall": bc.run_section(
-            comm, "config4", lambda c, b: bc.moe_alltoall(c, b, payloads=moe), budget),
-        "config5_gpt2_ddp": bc.run_section(
-            comm, "config5", lambda c, b: bc.gpt2_ddp(c, b, steps=args.ddp_steps, model=model),
-            budget),
-    }
+    sections = [
+        ("config3_3d_allgather_reduce_scatter", "config3",
+         lambda c, b: bc.grid_3d(c, b, shapes=grid)),
+        ("config4_moe_alltoall", "config4", lambda c, b: bc.moe_alltoall(c, b, payloads=moe)),
+        ("config5_gpt2_ddp", "config5",
+         lambda c, b: bc.gpt2_ddp(c, b, steps=args.ddp_steps, model=model)),
+    ]
+    out = {}
+    for key, name, fn in sections:
+        budget = args.config_budget_s
+        if deadline is not None:
+            left = deadline.remaining()
+            if left <= 0:
+                deadline.skipped.append(key)
+                out[key] = {"skipped_deadline": True}
+                continue
+            budget = min(budget, left)
+        out[key] = bc.run_section(comm, name, fn, budget)
+    return out
 
 
 SWEEP_BYTES = [1 << 10, 8 << 10, 64 << 10, 512 << 10, 4 << 20, 32 << 20, 256 << 20, 1 << 30]
 
 
-def _allreduce_sweep(comm, max_mib: int):
+def _allreduce_sweep(comm, max_mib: int, deadline=None):
     """Mean time per call (back to back, rank max) of a bf16 SUM all-reduce per message size and
     implementation; per size the fastest VALIDATED one (one extra call on fresh data checked
     against an fp32 reference sum on every rank) is reported with busBW / algBW. Candidates: RCCL via
@@ -131,6 +169,9 @@ def _allreduce_sweep(comm, max_mib: int):
     for nbytes in SWEEP_BYTES:
         if nbytes > max_mib << 20:
             break
+        if deadline is not None and deadline.expired(f"allreduce_sweep/{nbytes}"):
+            out.append({"bytes": nbytes, "impl": None, "skipped_deadline": True})
+            continue
         data = make_data((nbytes // 2,), torch.bfloat16, comm.rank, comm.device)
         flat = data.reshape(-1)
         if P == 1 and comm.is_gpu:
@@ -225,6 +266,7 @@ def _timed_steps(comm, op, steps: int) -> float:
 
 
 def main(argv=None) -> int:
+    t_start = time.perf_counter()
     args = parse(argv)
     import torch
 
@@ -244,6 +286,7 @@ def main(argv=None) -> int:
     else:
         comm = init_distributed(backend, timeout_s=900)
     P = comm.world_size
+    deadline = Deadline(comm, args.deadline_s, t_start)
     if args.gpus != P and comm.rank == 0:
         print(f"note: --gpus {args.gpus} but world size is {P}; using {P}", file=sys.stderr)
 
@@ -292,6 +335,8 @@ def main(argv=None) -> int:
 
         dist.all_reduce(ref)
     for label, impl, opts in cands:
+        if op is not None and deadline.expired(f"headline_candidate/{label}"):
+            continue                        # keep the best candidate timed so far
         try:
             cand = make_op("allreduce", comm, data, impl=impl, **opts)
         except RuntimeError as e:      # e.g. native engine init failed (agreed on all ranks)
@@ -333,7 +378,9 @@ def main(argv=None) -> int:
         raise SystemExit(f"{why}: {op_label} timed an empty call, refusing to report it")
 
     side = {}
-    if not args.no_side:
+    if not args.no_side and deadline.expired("side_512B_8MiB"):
+        side = {"side_skipped_deadline": True}
+    elif not args.no_side:
         small_opts = ({"impl": "native", "out_of_place": True} if P == 1 and comm.is_gpu
                       else {"impl": "auto"})
         # 512 B latency candidates: the size policy (IPC one-shot below the crossover, else RCCL)
@@ -412,13 +459,16 @@ def main(argv=None) -> int:
     # runs carries the whole curve
     sweep = []
     if not args.no_side and not args.no_sweep:
-        sweep = _allreduce_sweep(comm, args.sweep_max_mib)
+        sweep = _allreduce_sweep(comm, args.sweep_max_mib, deadline)
 
     # BASELINE configs 3/4 on the same [B,S,H] message at P > 1: all-gather, reduce-scatter and
     # all-to-all through RCCL and through the direct one-hop IPC kernels (side measurements)
     coll = {}
     if not args.no_side and P > 1:
         for name in ("allgather", "reduce_scatter", "alltoall"):
+            if deadline.expired(f"collectives_same_message/{name}"):
+                coll[name] = {"skipped_deadline": True}
+                continue
             res = {}
             for label, opts in (("rccl", {}), ("direct_ipc", {"direct": True})):
                 if label == "direct_ipc" and not comm.is_gpu:
@@ -445,7 +495,10 @@ def main(argv=None) -> int:
     # (parallel/virtual_ranks.py) — protocol latency and in-place two-shot time on one HBM,
     # validated against an fp32 sum first; NOT inter-GPU numbers (never used for "value")
     emulation = None
-    if P == 1 and comm.is_gpu and not args.no_side:
+    if (P == 1 and comm.is_gpu and not args.no_side
+            and deadline.expired("virtual_rank_emulation")):
+        emulation = {"skipped_deadline": True}
+    elif P == 1 and comm.is_gpu and not args.no_side:
         try:
             from distributed_llm_backend_benchmark_amd.parallel.virtual_ranks import (
                 emulation_summary)
@@ -457,8 +510,9 @@ def main(argv=None) -> int:
     # BASELINE configs 3-5 at this N (the driver's scaling run measures every config)
     configs = {}
     if not args.no_configs:
-        configs = _baseline_configs(comm, args)
+        configs = _baseline_configs(comm, args, deadline)
     affinity = comm.affinity_all_ranks() if comm.is_gpu else None   # collective
+    wall = comm.allreduce_max(time.perf_counter() - t_start)
 
     if comm.rank == 0:
         rec = {
@@ -493,6 +547,9 @@ def main(argv=None) -> int:
                       "message: real GPU work, algBW = copy throughput); in-place candidates "
                       "enqueue nothing at one rank and are excluded" if P == 1 else "")),
             **side,
+            "wall_s": round(wall, 2),
+            "deadline_s": args.deadline_s,
+            "skipped_deadline": deadline.skipped,
         }
         if calibration:
             rec["allreduce_calibration"] = calibration

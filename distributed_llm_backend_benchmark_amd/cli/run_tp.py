@@ -210,27 +210,46 @@ def main(argv=None) -> int:
     # forward host-bound and GEMM tuning depend on the caller) is gone; --eager keeps the
     # reference's host-timed semantics
     use_graph = (not args.eager) and bool(ex.get("graph", True)) and gpu
-    if use_graph and world > 1 and ex.get("allreduce") not in ("custom", "native", "auto"):
-        if rank == 0 and (args.graph or ex.get("graph")):
-            print("note: --graph needs world 1 or execution.allreduce custom|native|auto; "
-                  "running eagerly")
-        use_graph = False
+    graph_note = None
+    if use_graph and world > 1:
+        # a layer whose all-reduce would go through ProcessGroup all_reduce (e.g.
+        # allreduce=auto when the native engine could not be created on some rank) cannot be
+        # captured; the decision is agreed, so every rank takes the same path
+        if not all(comm.all_gather_object(_all_reduces_capturable(model))):
+            graph_note = ("an all-reduce path is not capturable on some rank (no native engine "
+                          "/ custom kernel)")
+            use_graph = False
     if use_graph:
         # HIP graph: one replay launches the whole forward (all GEMM / LN / all-reduce kernels);
-        # the autotuned GEMM choices were fixed by the eager warmup above.
+        # the autotuned GEMM choices were fixed by the eager warmup above. Any capture failure
+        # on any rank -> every rank runs eagerly (agreed over the host side channel BEFORE the
+        # first replay, so no rank replays collectives its peers never enqueue)
         static_in = dataset.get_batch()
-        side = torch.cuda.Stream(comm.device)
-        side.wait_stream(torch.cuda.current_stream(comm.device))
-        with torch.cuda.stream(side):
-            model(static_in)
-        torch.cuda.current_stream(comm.device).wait_stream(side)
-        comm.sync()
-        graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph, capture_error_mode="thread_local"):
-            model(static_in)
-        graph.replay()
-        comm.sync()
-        run_forward = graph.replay
+        graph, err = None, None
+        try:
+            side = torch.cuda.Stream(comm.device)
+            side.wait_stream(torch.cuda.current_stream(comm.device))
+            with torch.cuda.stream(side):
+                model(static_in)
+            torch.cuda.current_stream(comm.device).wait_stream(side)
+            comm.sync()
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph, capture_error_mode="thread_local"):
+                model(static_in)
+        except Exception as e:  # noqa: BLE001 - agreed below, then eager
+            err = f"{type(e).__name__}: {e}"[:500]
+            graph = None
+        torch.cuda.synchronize(comm.device)
+        errs = _agree_host(comm, err)
+        if errs:
+            graph_note = f"capture failed on rank(s) {sorted(errs)}: {errs[min(errs)]}"
+            use_graph = False
+        else:
+            graph.replay()
+            comm.sync()
+            run_forward = graph.replay
+    if graph_note and rank == 0:
+        print(f"note: HIP graph replay off, running eagerly: {graph_note}")
 
     from ..utils import tracing
 
@@ -264,6 +283,9 @@ def main(argv=None) -> int:
         metrics.metrics["forward_device_times"] = ev
 
     summary = metrics.get_summary()
+    # next to forward_mean: the reference host-times EAGER forwards
+    # (run_mpi.py:173-185); a graph-replayed forward is not the same quantity
+    summary["timing_mode"] = "hip_graph_replay" if use_graph else "eager"
     means = comm.all_gather_object(summary["forward_mean"])
     affinity = comm.affinity_all_ranks()
     if rank == 0:
@@ -278,6 +300,7 @@ def main(argv=None) -> int:
             "forward_device_mean": float(np.mean(ev)) if ev else None,
             "kernels": ex.get("kernels"),
             "hip_graph": use_graph,
+            "hip_graph_note": graph_note,
             "timing_mode": "hip_graph_replay" if use_graph else "eager",
             "gemm_tune_timing": __import__(
                 "distributed_llm_backend_benchmark_amd.ops.gemm", fromlist=["x"]).tune_timing(),
@@ -326,6 +349,34 @@ def main(argv=None) -> int:
     comm.barrier()
     comm.destroy()
     return 0
+
+
+def _all_reduces_capturable(model) -> bool:
+    """Every row-parallel layer's all-reduce can be captured in a HIP graph: our native RCCL
+    engine exists on the layer, or it is forced to the IPC kernel (``allreduce=custom``);
+    ``emulate`` is local work. Otherwise ``RowParallelLinear._all_reduce`` may fall through to
+    ProcessGroup ``all_reduce``."""
+    from ..parallel.tensor_parallel import RowParallelLinear
+
+    for m in model.modules():
+        if isinstance(m, RowParallelLinear):
+            if m.allreduce == "emulate":
+                continue
+            if m._native is None and not (m.allreduce == "custom" and m._car is not None):
+                return False
+    return True
+
+
+def _agree_host(comm, err):
+    """Every rank's error string (None = ok), gathered over the host side channel (a failed
+    capture may leave the device communicator unusable); returns {rank: error} of the failed."""
+    import torch.distributed as dist
+
+    if comm.world_size == 1:
+        return {0: err} if err else {}
+    out = [None] * comm.world_size
+    dist.all_gather_object(out, err, group=comm.cpu_group())
+    return {r: e for r, e in enumerate(out) if e}
 
 
 def _check_against_dense(config, comm, model, batch) -> dict:

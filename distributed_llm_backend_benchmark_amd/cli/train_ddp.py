@@ -81,6 +81,10 @@ def parse_args(argv=None):
                     help="emit roctx ranges (record with rocprofv3 --marker-trace)")
     ap.add_argument("--torch-profile", default=None, metavar="DIR",
                     help="torch.profiler Chrome trace per rank into DIR")
+    ap.add_argument("--main-stream-priority", type=int, default=0, choices=[0, -1],
+                    help="-1: run the step on a HIGH-priority stream, so the critical-path "
+                         "kernels are dispatched ahead of the side-stream weight gradients / "
+                         "bucket reductions (A/B)")
     ap.add_argument("--output", default=None, help="write the result JSON here (rank 0)")
     return ap.parse_args(argv)
 
@@ -96,7 +100,6 @@ def _path_counts(tr) -> dict:
 def run(args, comm, overlap: bool):
     import torch
 
-    from ..data import SyntheticTokenDataset
     from ..models.gpt2 import GPT2, GPT2Config
     from ..parallel.ddp import FlatParamTrainer
 
@@ -114,6 +117,21 @@ def run(args, comm, overlap: bool):
                               emulate_comm=args.emulate_comm, emulate_world=args.emulate_world,
                               late_bucket=not args.no_late_bucket,
                               split_optimizer=not args.no_split_optimizer)
+    # everything after the trainer registered its buckets runs under try/finally, so
+    # a failure (an agreed one: check_comm_errors, a section's candidate) still releases the IPC
+    # registrations and gradient buffers before the caller moves on to the next candidate
+    try:
+        return _train(args, comm, tr, model, cfg)
+    finally:
+        tr.close()
+        del tr, model
+        if comm.is_gpu:
+            torch.cuda.empty_cache()
+
+
+def _train(args, comm, tr, model, cfg):
+    from ..data import SyntheticTokenDataset
+
     data = SyntheticTokenDataset(args.batch, args.seq, cfg.vocab_size, rank=comm.rank,
                                  device=comm.device)
     if args.resume_from:
@@ -176,10 +194,6 @@ def run(args, comm, overlap: bool):
         tr.save_checkpoint(args.save_checkpoint)
         res["checkpoint"] = args.save_checkpoint
     res["step_count"] = tr.step_count
-    tr.close()
-    del tr, model
-    if comm.is_gpu:
-        torch.cuda.empty_cache()
     return res
 
 
@@ -194,7 +208,15 @@ def main(argv=None) -> int:
     affinity = comm.affinity_all_ranks()    # host threads on the GPU's NUMA node (collective)
     if args.trace:
         tracing.enable()
-    with tracing.torch_profile(args.torch_profile, comm.rank):
+    import contextlib
+
+    import torch
+
+    main_ctx = contextlib.nullcontext()
+    if args.main_stream_priority and comm.is_gpu:
+        main_ctx = torch.cuda.stream(torch.cuda.Stream(comm.device,
+                                                       priority=args.main_stream_priority))
+    with tracing.torch_profile(args.torch_profile, comm.rank), main_ctx:
         main_res = run(args, comm, overlap=not args.no_overlap)
     out = {"metric": "gpt2_ddp_tokens_per_s", "value": main_res["tokens_per_s"],
            "n_gpus": comm.world_size, "overlap": not args.no_overlap, **main_res,
@@ -204,7 +226,8 @@ def main(argv=None) -> int:
                                                     "allreduce", "zero", "comm_blocks",
                                                     "emulate_comm", "emulate_world",
                                                     "no_late_bucket",
-                                                    "no_split_optimizer")}}
+                                                    "no_split_optimizer",
+                                                    "main_stream_priority")}}
     if args.compare_overlap:
         alt = run(args, comm, overlap=args.no_overlap)
         out["other_overlap_setting"] = alt

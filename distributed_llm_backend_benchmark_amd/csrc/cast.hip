@@ -36,6 +36,104 @@ __global__ void __launch_bounds__(256) cast_kernel(const void* __restrict__ src,
   }
 }
 
+// Cast v2 (default). The kernel above measured 4.10 TB/s bf16 -> fp32 against 5.49 for torch's
+// copy (profiles/r01_initial/kernel_microbench.jsonl:14): it moves 8 elements per lane, so
+// one of its two sides is a 32-B-per-lane access split over two instructions that each touch
+// every other 16 B of a wave's span. Here a lane moves E elements with E chosen so the WIDER side
+// is exactly one 16-B access per lane (bf16 <-> fp32: 8 B in, 16 B out; 16-bit <-> 16-bit: 16 B
+// both): every wave instruction covers one contiguous 512 B / 1 KiB span. U such vectors per
+// lane are loaded before any is stored (U x 16 B in flight per lane), block-contiguous tiles of
+// 256 x U vectors, grid-stride over tiles. NT: non-temporal stores (a streaming destination is
+// not re-read by this kernel; A/B via dlbb_cast_set_variant).
+template <int DT, int E>
+struct VecIO;
+template <>
+struct VecIO<DT_F32, 4> {
+  __device__ __forceinline__ static void ld(const void* p, int64_t i, float (&v)[4]) {
+    const f32x4 t = reinterpret_cast<const f32x4*>(p)[i];
+    v[0] = t[0]; v[1] = t[1]; v[2] = t[2]; v[3] = t[3];
+  }
+  template <bool NT>
+  __device__ __forceinline__ static void st(void* p, int64_t i, const float (&v)[4]) {
+    const f32x4 t = {v[0], v[1], v[2], v[3]};
+    f32x4* q = reinterpret_cast<f32x4*>(p) + i;
+    if constexpr (NT) __builtin_nontemporal_store(t, q); else *q = t;
+  }
+};
+template <int DT>
+struct VecIO16_4 {
+  __device__ __forceinline__ static void ld(const void* p, int64_t i, float (&v)[4]) {
+    const u16x4 t = reinterpret_cast<const u16x4*>(p)[i];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = DT == DT_BF16 ? bf16_to_f32(t[j]) : f16_to_f32(t[j]);
+  }
+  template <bool NT>
+  __device__ __forceinline__ static void st(void* p, int64_t i, const float (&v)[4]) {
+    u16x4 t;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) t[j] = DT == DT_BF16 ? f32_to_bf16(v[j]) : f32_to_f16(v[j]);
+    u16x4* q = reinterpret_cast<u16x4*>(p) + i;
+    if constexpr (NT) __builtin_nontemporal_store(t, q); else *q = t;
+  }
+};
+template <int DT>
+struct VecIO16_8 {
+  __device__ __forceinline__ static void ld(const void* p, int64_t i, float (&v)[8]) {
+    const u16x8 t = reinterpret_cast<const u16x8*>(p)[i];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = DT == DT_BF16 ? bf16_to_f32(t[j]) : f16_to_f32(t[j]);
+  }
+  template <bool NT>
+  __device__ __forceinline__ static void st(void* p, int64_t i, const float (&v)[8]) {
+    u16x8 t;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) t[j] = DT == DT_BF16 ? f32_to_bf16(v[j]) : f32_to_f16(v[j]);
+    u16x8* q = reinterpret_cast<u16x8*>(p) + i;
+    if constexpr (NT) __builtin_nontemporal_store(t, q); else *q = t;
+  }
+};
+template <> struct VecIO<DT_BF16, 4> : VecIO16_4<DT_BF16> {};
+template <> struct VecIO<DT_F16, 4> : VecIO16_4<DT_F16> {};
+template <> struct VecIO<DT_BF16, 8> : VecIO16_8<DT_BF16> {};
+template <> struct VecIO<DT_F16, 8> : VecIO16_8<DT_F16> {};
+
+template <int DTI, int DTO>
+constexpr int cast_vec() {   // elements per lane-vector: the wider side is one 16-B access
+  return (Elem<DTI>::kBytes == 4 || Elem<DTO>::kBytes == 4) ? 4 : 8;
+}
+
+template <int DTI, int DTO, int U, bool NT>
+__global__ void __launch_bounds__(256) cast2_kernel(const void* __restrict__ src,
+                                                    void* __restrict__ dst, int64_t n) {
+  constexpr int E = cast_vec<DTI, DTO>();
+  const int64_t nvec = n / E;
+  const int64_t tile = 256 * U;
+  for (int64_t base = static_cast<int64_t>(blockIdx.x) * tile; base < nvec;
+       base += static_cast<int64_t>(gridDim.x) * tile) {
+    float v[U][E];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t i = base + u * 256 + threadIdx.x;
+      if (i < nvec) VecIO<DTI, E>::ld(src, i, v[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t i = base + u * 256 + threadIdx.x;
+      if (i < nvec) VecIO<DTO, E>::template st<NT>(dst, i, v[u]);
+    }
+  }
+  if (blockIdx.x == 0) {
+    const int64_t t = nvec * E + threadIdx.x;
+    if (t < n)
+      Elem<DTO>::st(static_cast<typename Elem<DTO>::T*>(dst), t,
+                    Elem<DTI>::ld(static_cast<const typename Elem<DTI>::T*>(src), t));
+  }
+}
+
+// 0: 8-element kernel above, 1: cast2, 2: cast2 + nt stores, 3: 2 with one tile per block,
+// 4: 1 with one tile per block
+static int g_cast_variant = 1;
+
 // One wave-row loop: rows x cols, source row stride ld_src (elements), dense-or-strided dest.
 template <int DTI, int DTO>
 __global__ void __launch_bounds__(256) pack_rows_kernel(const void* __restrict__ src,
@@ -64,8 +162,21 @@ __global__ void __launch_bounds__(256) pack_rows_kernel(const void* __restrict__
 template <int DTI, int DTO>
 static hipError_t launch_cast(const void* s, void* d, int64_t n, hipStream_t st) {
   const int block = 256;
-  hipLaunchKernelGGL((cast_kernel<DTI, DTO>), dim3(stream_grid((n + 7) / 8, block)),
-                     dim3(block), 0, st, s, d, n);
+  constexpr int E = cast_vec<DTI, DTO>(), U = 8;
+  const uintptr_t align = reinterpret_cast<uintptr_t>(s) | reinterpret_cast<uintptr_t>(d);
+  if (g_cast_variant == 0 || (align & 15)) {
+    hipLaunchKernelGGL((cast_kernel<DTI, DTO>), dim3(stream_grid((n + 7) / 8, block)),
+                       dim3(block), 0, st, s, d, n);
+    return hipGetLastError();
+  }
+  int64_t g = (n / E + 256 * U - 1) / (256 * U);
+  // variants 3/4: one tile per block (no grid-stride loop), as torch's elementwise launch
+  const int64_t cap = g_cast_variant >= 3 ? (int64_t{1} << 30) : 4096;
+  g = g < 1 ? 1 : (g > cap ? cap : g);
+  if (g_cast_variant == 2 || g_cast_variant == 3)
+    hipLaunchKernelGGL((cast2_kernel<DTI, DTO, U, true>), dim3(g), dim3(block), 0, st, s, d, n);
+  else
+    hipLaunchKernelGGL((cast2_kernel<DTI, DTO, U, false>), dim3(g), dim3(block), 0, st, s, d, n);
   return hipGetLastError();
 }
 
@@ -87,6 +198,10 @@ static hipError_t launch_pack(const void* s, void* d, int64_t rows, int64_t cols
 
 using namespace dlbb;
 
+
+// A/B switch: 0 = 8-element kernel, 1 = one 16-B wide side per lane (default), 2 = 1 + nt stores,
+// 3 = 2 without the grid-stride cap, 4 = 1 without it
+DLBB_API void dlbb_cast_set_variant(int v) { g_cast_variant = v < 0 || v > 4 ? 1 : v; }
 
 DLBB_API int dlbb_cast(const void* src, int dtype_in, void* dst, int dtype_out, int64_t n,
                        hipStream_t stream) {

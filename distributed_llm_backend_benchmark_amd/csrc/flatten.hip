@@ -18,6 +18,7 @@ struct CopyChunk {
   uint64_t nbytes;
 };
 
+template <bool NT>
 __global__ void __launch_bounds__(256) chunk_copy_kernel(const CopyChunk* __restrict__ table,
                                                          int64_t nchunks) {
   for (int64_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
@@ -27,9 +28,21 @@ __global__ void __launch_bounds__(256) chunk_copy_kernel(const CopyChunk* __rest
     const uint64_t nb = ch.nbytes;
     if (((ch.src | ch.dst) & 15) == 0) {
       const uint64_t nv = nb >> 4;
-      const uint4* s4 = reinterpret_cast<const uint4*>(s);
-      uint4* d4 = reinterpret_cast<uint4*>(d);
-      for (uint64_t i = threadIdx.x; i < nv; i += blockDim.x) d4[i] = s4[i];
+      typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+      const u32x4* __restrict__ s4 = reinterpret_cast<const u32x4*>(s);
+      u32x4* __restrict__ d4 = reinterpret_cast<u32x4*>(d);
+      uint64_t i = threadIdx.x;
+      for (; i + 3 * 256 < nv; i += 4 * 256) {   // 4 x 16 B in flight per lane before a store
+        u32x4 t[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) t[u] = s4[i + u * 256];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          if constexpr (NT) __builtin_nontemporal_store(t[u], d4 + i + u * 256);
+          else d4[i + u * 256] = t[u];
+        }
+      }
+      for (; i < nv; i += blockDim.x) d4[i] = s4[i];
       for (uint64_t i = (nv << 4) + threadIdx.x; i < nb; i += blockDim.x) d[i] = s[i];
     } else if (((ch.src | ch.dst | nb) & 1) == 0) {
       const uint16_t* s2 = reinterpret_cast<const uint16_t*>(s);
@@ -81,10 +94,18 @@ static int grid_for(int64_t nchunks) {
 using namespace dlbb;
 
 // table: DEVICE pointer to nchunks CopyChunk entries (3 x uint64 each).
+static int g_chunk_nt = 0;   // 1: non-temporal destination stores (A/B)
+
+DLBB_API void dlbb_chunk_copy_set_nt(int nt) { g_chunk_nt = nt ? 1 : 0; }
+
 DLBB_API int dlbb_chunk_copy(const void* table, int64_t nchunks, hipStream_t stream) {
   if (nchunks <= 0) return hipSuccess;
-  hipLaunchKernelGGL(chunk_copy_kernel, dim3(grid_for(nchunks)), dim3(256), 0, stream,
-                     static_cast<const CopyChunk*>(table), nchunks);
+  if (g_chunk_nt)
+    hipLaunchKernelGGL(chunk_copy_kernel<true>, dim3(grid_for(nchunks)), dim3(256), 0, stream,
+                       static_cast<const CopyChunk*>(table), nchunks);
+  else
+    hipLaunchKernelGGL(chunk_copy_kernel<false>, dim3(grid_for(nchunks)), dim3(256), 0, stream,
+                       static_cast<const CopyChunk*>(table), nchunks);
   return hipGetLastError();
 }
 

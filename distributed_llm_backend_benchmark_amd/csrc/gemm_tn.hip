@@ -41,8 +41,79 @@ struct Args {
   int m_per_split;
   int nsplit;          // fused db partials (BIAS) at ws + nsplit * N * K (tk == 0 blocks)
   void* direct;        // nsplit == 1, no accumulate, no bias: store dW here (no ws, no reduce)
-  int direct_bf16;     // direct store dtype: bf16 (1) or fp32 (0)
+  int direct_bf16;     // direct / fused-reduce store dtype: bf16 (1) or fp32 (0)
+  // in-launch split-K reduce (cnt != null): per-tile arrival counters (zero on entry; the last
+  // arriver resets its own), the final dW / db and whether to add into them
+  int* cnt;
+  void* out;
+  void* out_bias;
+  int accumulate;
+  int tile_major;      // workgroup order: 0 = split-major, 1 = a tile's splits adjacent
 };
+
+// The last-arriving workgroup of a tile sums the `nsplit` fp32 slabs of that tile (+ the fused
+// bias partials of column block 0) and writes the final bf16 / fp32 dW — replaces the separate
+// split_reduce_kernel pass (profiles/r04_final/gpt2_kernel_stats_steady.csv:5: 40 us x 50 calls
+// per GPT-2 step). Slab reads are 16-B, coalesced along K, 8 independent loads per thread per
+// slab; NT threads cover the BNxTBK tile in TBK / 8 float4 per thread, 8 at a time.
+template <int NT, int BN, int TBK>
+__device__ __forceinline__ void wgrad_tile_reduce(const Args& a, int n0, int k0, bool bias) {
+  constexpr int C4 = TBK / 4;                      // float4 per tile row
+  constexpr int PER = BN * C4 / NT;                // float4 per thread
+  static_assert(PER % 8 == 0, "tile must split into 8-float4 chunks per thread");
+  const int64_t slab = static_cast<int64_t>(a.N) * a.K;
+#pragma unroll 1
+  for (int ch = 0; ch < PER / 8; ++ch) {
+    f32x4 acc[8];
+    int64_t off[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int f = (ch * 8 + u) * NT + static_cast<int>(threadIdx.x);
+      off[u] = static_cast<int64_t>(n0 + f / C4) * a.K + k0 + (f % C4) * 4;
+      acc[u] = *reinterpret_cast<const f32x4*>(a.ws + off[u]);
+    }
+#pragma unroll 2
+    for (int s = 1; s < a.nsplit; ++s) {
+      f32x4 t[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) t[u] = *reinterpret_cast<const f32x4*>(a.ws + s * slab + off[u]);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc[u] += t[u];
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      if (a.direct_bf16) {
+        uint16_t* o = static_cast<uint16_t*>(a.out) + off[u];
+        float v[4] = {acc[u][0], acc[u][1], acc[u][2], acc[u][3]};
+        if (a.accumulate) {
+          const u16x4 p = *reinterpret_cast<const u16x4*>(o);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) v[j] += bf16_to_f32(p[j]);
+        }
+        u16x4 r;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) r[j] = f32_to_bf16(v[j]);
+        *reinterpret_cast<u16x4*>(o) = r;
+      } else {
+        f32x4* o = reinterpret_cast<f32x4*>(static_cast<float*>(a.out) + off[u]);
+        *o = a.accumulate ? *o + acc[u] : acc[u];
+      }
+    }
+  }
+  if (bias && static_cast<int>(threadIdx.x) < BN) {
+    const float* wb = a.ws + static_cast<int64_t>(a.nsplit) * slab + n0 + threadIdx.x;
+    float s0 = 0.f;
+    for (int s = 0; s < a.nsplit; ++s) s0 += wb[static_cast<int64_t>(s) * a.N];
+    const int n = n0 + threadIdx.x;
+    if (a.direct_bf16) {
+      uint16_t* o = static_cast<uint16_t*>(a.out_bias) + n;
+      *o = f32_to_bf16(a.accumulate ? s0 + bf16_to_f32(*o) : s0);
+    } else {
+      float* o = static_cast<float*>(a.out_bias) + n;
+      *o = a.accumulate ? s0 + *o : s0;
+    }
+  }
+}
 
 // MFMA 16x16x32 operand from a [64 m][128 col] image: lane l gets column colbase + (l & 15),
 // rows kbase + 8 (l >> 4) + j, j = 0..7 (two transposed reads of 4 rows each).
@@ -116,7 +187,10 @@ __global__ void __launch_bounds__(128 * WM, WJ == 8 ? 2 : (WM == 2 ? 3 : 2))
   const int tiles = (a.N / (64 * WM)) * tiles_k;
   const int nwg = gridDim.x, xcd = blockIdx.x % 8, q = nwg / 8, r = nwg % 8;
   const int wid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + blockIdx.x / 8;
-  const int split = wid / tiles, t = wid % tiles;
+  // tile_major: a tile's nsplit slices are adjacent ids, i.e. mostly on one XCD, so the
+  // in-launch reducer reads its slabs from its own L2 (guide: 104-122 vs 62-70 GB/s per block)
+  const int split = a.tile_major ? wid % a.nsplit : wid / tiles;
+  const int t = a.tile_major ? wid / a.nsplit : wid % tiles;
   const int tn = t / tiles_k, tk = t % tiles_k;
   const int n0 = tn * 64 * WM, k0 = tk * TBK;
   const int mb = split * a.m_per_split;
@@ -224,6 +298,31 @@ __global__ void __launch_bounds__(128 * WM, WJ == 8 ? 2 : (WM == 2 ? 3 : 2))
 #pragma unroll
       for (int r = 0; r < 4; ++r) wb[n0 + wm * 64 + (2 * wn + h) * 16 + fq * 4 + r] = bacc[h][r];
   }
+  if (!a.cnt) return;
+  // in-launch split-K combine (guide §5 "In-launch split-K reduction", counter form): every
+  // wave's slab stores retired -> barrier -> ONE agent release -> ticket; the workgroup drawing
+  // nsplit - 1 acquires once and reduces. The explicit waits after the fences are kept on
+  // purpose (ROCm 7.2 may drop the fence's own wait).
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  int* last = reinterpret_cast<int*>(smem);        // LDS is free: the k-loop is over
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int prev = __hip_atomic_fetch_add(a.cnt + t, 1, __ATOMIC_RELAXED,
+                                            __HIP_MEMORY_SCOPE_AGENT);
+    const int is_last = prev == a.nsplit - 1;
+    if (is_last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      // re-arm for the next launch on this stream (kernel boundary orders it)
+      __hip_atomic_store(a.cnt + t, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    last[0] = is_last;
+  }
+  __syncthreads();
+  if (!last[0]) return;
+  wgrad_tile_reduce<128 * WM, 64 * WM, TBK>(a, n0, k0, BIAS && tk == 0);
 }
 
 // out[i] = sum_s ws[s][i] (+ out[i] if accumulate), bf16 or fp32 output; 8 elements / thread.
@@ -275,10 +374,20 @@ DLBB_API void dlbb_gemm_wgrad_set_stages(int nb) { g_wgrad_stages = nb >= 2 && n
 // split * (N * K + N) floats. out: bf16 (dt_out 1) or fp32 (0), dense [N][K]. out_bias
 // (optional, same dtype as out, N elements): fused db = column sums of A.
 // bk: output columns (K) per tile, 128 or 256 (the latter with bn = 128 only: 64 x 128 per wave).
-DLBB_API int dlbb_gemm_wgrad_tile2(const void* A, int64_t lda, const void* B, int64_t ldb,
-                                   void* out, int dt_out, int accumulate, float* ws, int M, int N,
-                                   int K, int split, void* out_bias, int bn, int bk,
-                                   hipStream_t stream) {
+// workgroup order of the fused-reduce launches (A/B: dlbb_gemm_wgrad_set_order)
+static int g_wgrad_tile_major = 1;
+
+DLBB_API void dlbb_gemm_wgrad_set_order(int tile_major) { g_wgrad_tile_major = tile_major ? 1 : 0; }
+
+// Number of per-tile arrival counters a fused-reduce launch of this shape needs.
+DLBB_API int dlbb_gemm_wgrad_counters(int N, int K, int bn, int bk) {
+  return bn > 0 && bk > 0 ? (N / bn) * (K / bk) : 0;
+}
+
+static int wgrad_launch(const void* A, int64_t lda, const void* B, int64_t ldb, void* out,
+                        int dt_out, int accumulate, float* ws, int M, int N, int K, int split,
+                        void* out_bias, int bn, int bk, int* counters, int ncounters,
+                        hipStream_t stream) {
   using namespace dlbb::tn;
   if (M <= 0 || N <= 0 || K <= 0) return hipSuccess;
   if (bn != 128 && bn != 256) return hipErrorInvalidValue;
@@ -293,8 +402,16 @@ DLBB_API int dlbb_gemm_wgrad_tile2(const void* A, int64_t lda, const void* B, in
   // one split, plain store, no bias: the kernel writes dW itself (ws may be null)
   const bool direct = split == 1 && !accumulate && !out_bias;
   if (!direct && !ws) return hipErrorInvalidValue;
+  const int ntiles = (N / bn) * (K / bk);
+  // in-launch combine: needs one zeroed counter per tile and 16-B aligned outputs
+  const bool fused = !direct && counters && ncounters >= ntiles &&
+                     !((reinterpret_cast<uintptr_t>(out) |
+                        reinterpret_cast<uintptr_t>(counters)) & 15);
+  if (counters && !direct && !fused) return hipErrorInvalidValue;
   Args a{static_cast<const uint16_t*>(A), static_cast<const uint16_t*>(B), ws, lda, ldb, M, N, K,
-         per, split, direct ? out : nullptr, dt_out == DT_BF16 ? 1 : 0};
+         per, split, direct ? out : nullptr, dt_out == DT_BF16 ? 1 : 0,
+         fused ? counters : nullptr, out, out_bias, accumulate,
+         fused ? g_wgrad_tile_major : 0};
   const dim3 grid((N / bn) * (K / bk) * split);
   const int stages = g_wgrad_stages;
 #define WG_LAUNCH(BIASV, NBV, WMV, WJV)                                                     \
@@ -313,7 +430,7 @@ DLBB_API int dlbb_gemm_wgrad_tile2(const void* A, int64_t lda, const void* B, in
   }
 #undef WG_STAGES
 #undef WG_LAUNCH
-  if (direct) return hipGetLastError();
+  if (direct || fused) return hipGetLastError();
   const int64_t n = static_cast<int64_t>(N) * K;
   const int64_t nb = out_bias ? N : 0;
   const int g = stream_grid((n + nb) / 8, 256);
@@ -324,6 +441,27 @@ DLBB_API int dlbb_gemm_wgrad_tile2(const void* A, int64_t lda, const void* B, in
     hipLaunchKernelGGL(split_reduce_kernel<DT_F32>, dim3(g), dim3(256), 0, stream, ws, out, n,
                        out_bias, nb, split, accumulate);
   return hipGetLastError();
+}
+
+DLBB_API int dlbb_gemm_wgrad_tile2(const void* A, int64_t lda, const void* B, int64_t ldb,
+                                   void* out, int dt_out, int accumulate, float* ws, int M, int N,
+                                   int K, int split, void* out_bias, int bn, int bk,
+                                   hipStream_t stream) {
+  return wgrad_launch(A, lda, B, ldb, out, dt_out, accumulate, ws, M, N, K, split, out_bias, bn,
+                      bk, nullptr, 0, stream);
+}
+
+// As tile2, with the split-K combine done inside the launch by each tile's last-arriving
+// workgroup: `counters` = dlbb_gemm_wgrad_counters(N, K, bn, bk) ints, ZERO on entry (the
+// launch leaves them zero again), owned by one stream at a time. A one-split plain store still
+// takes the direct path (no counters touched).
+DLBB_API int dlbb_gemm_wgrad_fused(const void* A, int64_t lda, const void* B, int64_t ldb,
+                                   void* out, int dt_out, int accumulate, float* ws, int M, int N,
+                                   int K, int split, void* out_bias, int bn, int bk,
+                                   int* counters, int ncounters, hipStream_t stream) {
+  if (!counters) return hipErrorInvalidValue;
+  return wgrad_launch(A, lda, B, ldb, out, dt_out, accumulate, ws, M, N, K, split, out_bias, bn,
+                      bk, counters, ncounters, stream);
 }
 
 DLBB_API int dlbb_gemm_wgrad_tile(const void* A, int64_t lda, const void* B, int64_t ldb,

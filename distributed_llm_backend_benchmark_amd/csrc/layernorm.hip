@@ -244,6 +244,114 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(LnBwdArgs a) {
   }
 }
 
+// Backward, pipelined (default). The kernel above is latency-bound at the GPT-2 shape (16384 x
+// 768: 59 us per call, ~1.7 TB/s; profiles/r04_final/gpt2_kernel_stats_steady.csv:6): each wave
+// owns 8 rows in sequence and every row is load -> wait -> two wave reductions -> store, with
+// only 2 waves per SIMD to hide it. Here:
+//   * WPB = 8 waves per block, so the same 512 partial rows of dgamma/dbeta come with twice the
+//     resident waves (rows up to 1024 wide: wider rows keep the kernel above, whose register
+//     footprint already limits it to 1-2 waves / SIMD);
+//   * a two-deep register pipeline per wave: row r + stride's h / dy / dres / mean / rstd loads
+//     are issued BEFORE row r's reductions and stores, so one row is always in flight while the
+//     previous one is reduced (restrict pointers: the dx store of row r cannot alias them);
+//   * the cross-wave dgamma / dbeta reduction reuses ONE [WPB][cols] LDS array (dgamma, then
+//     dbeta); operands stay packed bf16 in registers until used (2 rows in flight <= 128 VGPRs).
+template <int NV>
+struct LnRow {                    // one row's operands, still packed bf16 (2 VGPRs per 4 values)
+  u16x4 h[NV], dy[NV], dr[NV];
+  float mu, rs;
+};
+
+template <int NV>
+__device__ __forceinline__ void ln_row_load(const LnBwdArgs& a, const uint16_t* __restrict__ hp,
+                                            const uint16_t* __restrict__ dyp,
+                                            const uint16_t* __restrict__ drp, int64_t row,
+                                            int lane, LnRow<NV>& r) {
+  const int64_t base4 = row * (a.cols / 4);
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    r.h[i] = reinterpret_cast<const u16x4*>(hp)[base4 + i * 64 + lane];
+    r.dy[i] = reinterpret_cast<const u16x4*>(dyp)[base4 + i * 64 + lane];
+  }
+  if (drp) {
+#pragma unroll
+    for (int i = 0; i < NV; ++i) r.dr[i] = reinterpret_cast<const u16x4*>(drp)[base4 + i * 64 + lane];
+  }
+  r.mu = a.mean[row];
+  r.rs = a.rstd[row];
+}
+
+template <int NV, int PDT, int WPB>
+__global__ void __launch_bounds__(64 * WPB) ln_bwd_pipe_kernel(LnBwdArgs a) {
+  __shared__ float red[WPB][NV * 256];
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  float dg[NV][4], db[NV][4], gam[NV][4];
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    ldp4<PDT>(a.gamma, i * 64 + lane, gam[i]);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) dg[i][j] = db[i][j] = 0.f;
+  }
+  const float inv_c = 1.0f / static_cast<float>(a.cols);
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * WPB;
+  const uint16_t* __restrict__ hp = a.h;
+  const uint16_t* __restrict__ dyp = a.dy;
+  const uint16_t* __restrict__ drp = a.dres;
+  uint16_t* __restrict__ dxp = a.dx;
+  int64_t row = static_cast<int64_t>(blockIdx.x) * WPB + w;
+  LnRow<NV> cur;
+  if (row < a.rows) ln_row_load<NV>(a, hp, dyp, drp, row, lane, cur);
+  for (; row < a.rows; row += stride) {
+    LnRow<NV> nxt;
+    const bool more = row + stride < a.rows;
+    if (more) ln_row_load<NV>(a, hp, dyp, drp, row + stride, lane, nxt);
+    float xh[NV][4], g[NV][4];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < NV; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float dyv = bf16_to_f32(cur.dy[i][j]);
+        xh[i][j] = (bf16_to_f32(cur.h[i][j]) - cur.mu) * cur.rs;
+        g[i][j] = dyv * gam[i][j];
+        s1 += g[i][j] * xh[i][j];
+        s2 += g[i][j];
+        dg[i][j] += dyv * xh[i][j];
+        db[i][j] += dyv;
+      }
+    const float c1 = wave_sum(s1) * inv_c, c2 = wave_sum(s2) * inv_c;
+    const int64_t base4 = row * (a.cols / 4);
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      float o[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        o[j] = cur.rs * (g[i][j] - xh[i][j] * c1 - c2) + (drp ? bf16_to_f32(cur.dr[i][j]) : 0.f);
+      st4(dxp, base4 + i * 64 + lane, o);
+    }
+    if (more) cur = nxt;
+  }
+  // cross-wave reduction of the partials: dgamma, then dbeta through the same LDS array
+#pragma unroll
+  for (int pass = 0; pass < 2; ++pass) {
+    if (pass == 1 && !a.dbeta_part) break;
+    if (pass == 1) __syncthreads();          // every wave has read the dgamma pass
+#pragma unroll
+    for (int i = 0; i < NV; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) red[w][(i * 64 + lane) * 4 + j] = pass ? db[i][j] : dg[i][j];
+    __syncthreads();
+    float* dst = (pass ? a.dbeta_part : a.dgamma_part) + static_cast<int64_t>(blockIdx.x) * a.cols;
+    for (int c = threadIdx.x; c < a.cols; c += 64 * WPB) {
+      float s = 0.f;
+#pragma unroll
+      for (int k = 0; k < WPB; ++k) s += red[k][c];
+      dst[c] = s;
+    }
+  }
+}
+
 // out[c] = sum_b part[b, c]  (fp32 accumulate, out in bf16 or fp32).
 // 256 threads = 8 row groups x 32 columns: every wave reads 2 x 128 contiguous bytes per
 // partial row, and each thread keeps 8 independent loads in flight (the naive
@@ -404,8 +512,24 @@ static hipError_t fwd_dispatch(const LnFwdArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
+// Partial rows of the pipelined backward: one block per WPB rows, at most 512 blocks (one
+// resident round at <= 128 VGPRs: 4 waves / SIMD).
+static inline int bwd_pipe_grid(int64_t rows, int wpb) {
+  int64_t g = (rows + wpb - 1) / wpb;
+  if (g > 512) g = 512;
+  return static_cast<int>(g < 1 ? 1 : g);
+}
+
+static int g_ln_bwd_variant = 1;   // 0: wave-per-row-sequence kernel, 1: pipelined (A/B)
+
 template <int NV, int PDT>
 static hipError_t bwd_nv(const LnBwdArgs& a, int grid, hipStream_t s) {
+  if constexpr (NV <= 4) {
+    if (g_ln_bwd_variant != 0) {
+      hipLaunchKernelGGL((ln_bwd_pipe_kernel<NV, PDT, 8>), dim3(grid), dim3(512), 0, s, a);
+      return hipGetLastError();
+    }
+  }
   hipLaunchKernelGGL((ln_bwd_kernel<NV, PDT>), dim3(grid), dim3(256), 0, s, a);
   return hipGetLastError();
 }
@@ -436,13 +560,18 @@ DLBB_API int dlbb_layernorm_bwd_grid(int64_t rows) {
   return static_cast<int>(g < 1 ? 1 : g);
 }
 
+// A/B switch of the backward kernel: 0 = wave-per-row-sequence, 1 = pipelined (default)
+DLBB_API void dlbb_layernorm_bwd_set_variant(int v) { g_ln_bwd_variant = v == 0 ? 0 : 1; }
+
 DLBB_API int dlbb_layernorm_bwd(const void* dy, const void* h, const void* gamma, int param_dtype,
                                 const float* mean, const float* rstd, const void* dres, void* dx,
                                 float* part_ws, void* dgamma, void* dbeta, int64_t rows,
                                 int cols, int accumulate, hipStream_t stream) {
   if (rows <= 0) return hipSuccess;
   if (cols % 256 != 0) return hipErrorInvalidValue;
-  const int grid = dlbb_layernorm_bwd_grid(rows);
+  // partial rows actually used (<= dlbb_layernorm_bwd_grid(rows), the caller's ws size)
+  const int grid = g_ln_bwd_variant != 0 && cols <= 1024 ? bwd_pipe_grid(rows, 8)
+                                                         : dlbb_layernorm_bwd_grid(rows);
   float* pg = part_ws;
   float* pb = dbeta ? part_ws + static_cast<int64_t>(grid) * cols : nullptr;
   LnBwdArgs a{static_cast<const uint16_t*>(dy), static_cast<const uint16_t*>(h), gamma, mean,

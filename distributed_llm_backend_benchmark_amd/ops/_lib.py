@@ -41,14 +41,17 @@ _SIGS = {
     "dlbb_stamps_entry": (c_int, [c_int64, ctypes.POINTER(c_int), ctypes.POINTER(c_int64),
                                   ctypes.POINTER(c_int64)]),
     "dlbb_cast": (c_int, [c_void_p, c_int, c_void_p, c_int, c_int64, c_void_p]),
+    "dlbb_cast_set_variant": (None, [c_int]),
     "dlbb_pack_rows": (c_int, [c_void_p, c_int, c_int64, c_void_p, c_int, c_int64, c_int64,
                                c_int64, c_void_p]),
     "dlbb_chunk_copy": (c_int, [c_void_p, c_int64, c_void_p]),
+    "dlbb_chunk_copy_set_nt": (None, [c_int]),
     "dlbb_chunk_copy_scale": (c_int, [c_void_p, c_int64, c_int, c_int, c_float, c_void_p]),
     "dlbb_layernorm_fwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p,
                                    c_void_p, c_void_p, c_void_p, c_int64, c_int, c_float,
                                    c_void_p]),
     "dlbb_layernorm_bwd_grid": (c_int, [c_int64]),
+    "dlbb_layernorm_bwd_set_variant": (None, [c_int]),
     "dlbb_layernorm_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p,
                                    c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64,
                                    c_int, c_int, c_void_p]),
@@ -107,6 +110,11 @@ _SIGS = {
     "dlbb_gemm_wgrad_tile2": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int,
                                      c_int, c_void_p, c_int, c_int, c_int, c_int, c_void_p,
                                      c_int, c_int, c_void_p]),
+    "dlbb_gemm_wgrad_fused": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int,
+                                      c_int, c_void_p, c_int, c_int, c_int, c_int, c_void_p,
+                                      c_int, c_int, c_void_p, c_int, c_void_p]),
+    "dlbb_gemm_wgrad_counters": (c_int, [c_int, c_int, c_int, c_int]),
+    "dlbb_gemm_wgrad_set_order": (None, [c_int]),
     "dlbb_embedding_fwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int, c_int,
                                    c_int64, c_void_p]),
     "dlbb_embedding_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
@@ -182,6 +190,13 @@ def _load() -> ctypes.CDLL:
                 fn = getattr(lib, name)
                 fn.restype = res
                 fn.argtypes = args
+            # A/B kernel variants selectable per process from the environment
+            for env, setter in (("DLBB_LN_BWD_VARIANT", "dlbb_layernorm_bwd_set_variant"),
+                                ("DLBB_CAST_VARIANT", "dlbb_cast_set_variant"),
+                                ("DLBB_WGRAD_ORDER", "dlbb_gemm_wgrad_set_order"),
+                                ("DLBB_CHUNK_NT", "dlbb_chunk_copy_set_nt")):
+                if os.environ.get(env, "") != "":
+                    getattr(lib, setter)(int(os.environ[env]))
             _lib = lib
             return lib
         except BaseException as e:  # remember and re-raise loudly on every use

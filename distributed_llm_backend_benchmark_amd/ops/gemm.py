@@ -48,7 +48,8 @@ def set_tune_agreement(fn) -> None:
 # ranks started with different settings fail at the first tuned shape instead of "agreeing" on
 # timings of different kernels
 _AGREED_ENV = ("DLBB_GEMM", "DLBB_TUNE_TIMING", "DLBB_WGRAD256", "DLBB_PP_TAIL",
-               "DLBB_GEMM_PERSIST", "DLBB_GEMM_PERSIST_EPI", "DLBB_WGRAD_STREAM")
+               "DLBB_WGRAD_FUSED", "DLBB_GEMM_PERSIST", "DLBB_GEMM_PERSIST_EPI",
+               "DLBB_WGRAD_STREAM")
 
 
 def _agree_names(kind: str, key, names) -> list:
@@ -490,6 +491,31 @@ def wgrad_supported(dy2: torch.Tensor, x2: torch.Tensor) -> bool:
             and dy2.data_ptr() % 16 == 0 and x2.data_ptr() % 16 == 0)
 
 
+_COUNTERS = {}   # (device index, stream handle) -> int32 tile counters, zero between launches
+
+
+def wgrad_fused_reduce() -> bool:
+    """In-launch split-K combine of the weight-gradient kernel (each tile's last-arriving
+    workgroup sums the fp32 slabs; ``DLBB_WGRAD_FUSED=1``). OFF by default: measured 1.3-2.3x
+    SLOWER than the separate reduce pass at every GPT-2 dW shape (profiles/r05_wgrad): a tile's
+    slabs are split x 64 KiB (0.4-1.4 MB), read serially by ONE workgroup at ~0.1 TB/s, i.e.
+    far past the "few tens of KB per tile" where an in-launch combine pays (CDNA guide §5)."""
+    return os.environ.get("DLBB_WGRAD_FUSED", "0") == "1"
+
+
+def _tile_counters(device: torch.device, n: int) -> torch.Tensor:
+    """Arrival counters for ``n`` tiles, private to the current stream: launches on one stream
+    are ordered, and every fused launch leaves its counters zero again, so one zero-filled
+    buffer per stream serves every call on it (grown, never shrunk)."""
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    key = (idx, _lib.stream(device))
+    buf = _COUNTERS.get(key)
+    if buf is None or buf.numel() < n:
+        buf = torch.zeros(max(n, 4096), dtype=torch.int32, device=device)
+        _COUNTERS[key] = buf
+    return buf
+
+
 def _wgrad_hip(dy2, x2, out, accumulate, split=None, bias_out=None, bn=128, bk=128):
     M, N = dy2.shape
     K = x2.shape[1]
@@ -507,6 +533,15 @@ def _wgrad_hip(dy2, x2, out, accumulate, split=None, bias_out=None, bn=128, bk=1
     direct = split == 1 and not accumulate and bias_out is None
     ws = None if direct else torch.empty(split * (N * K + N), dtype=torch.float32,
                                          device=dy2.device)
+    if not direct and wgrad_fused_reduce() and out.data_ptr() % 16 == 0:
+        # split-K partials combined inside the launch by each tile's last-arriving workgroup
+        cnt = _tile_counters(dy2.device, tiles)
+        check(_lib.lib().dlbb_gemm_wgrad_fused(
+            dy2.data_ptr(), dy2.stride(0), x2.data_ptr(), x2.stride(0), out.data_ptr(),
+            _lib.dt(out), int(accumulate), ws.data_ptr(), M, N, K, split, _lib.ptr(bias_out),
+            int(bn), int(bk), cnt.data_ptr(), cnt.numel(), _lib.stream(dy2.device)),
+            "gemm_wgrad_fused")
+        return
     check(_lib.lib().dlbb_gemm_wgrad_tile2(dy2.data_ptr(), dy2.stride(0), x2.data_ptr(),
                                            x2.stride(0), out.data_ptr(), _lib.dt(out),
                                            int(accumulate), _lib.ptr(ws), M, N, K, split,

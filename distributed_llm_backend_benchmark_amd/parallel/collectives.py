@@ -37,6 +37,7 @@ from typing import Callable, Dict, List, Optional
 import torch
 import torch.distributed as dist
 
+from ..ops.elementwise import ChunkTable
 from .comm import Comm
 
 DTYPES = {
@@ -204,7 +205,15 @@ class AllGather(CollectiveOp):
         n = self.data.numel()
         self._car = None
         if self.form == "list":
+            # reference: dist.all_gather into a Python list (collectives/1d/dsccl.py:72-76). Here
+            # ONE all_gather_into_tensor into a flat staging buffer, then the list unpack is one
+            # chunk-copy launch over a (flat slice -> list entry) table (csrc/flatten.hip)
             self.outs = [torch.empty_like(self.data) for _ in range(self.P)]
+            self.flat = self.data.reshape(-1)
+            self.stage = torch.empty(self.P * n, dtype=self.data.dtype, device=self.data.device)
+            self._unpack = ChunkTable([(self.stage[i * n:(i + 1) * n], o.reshape(-1))
+                                       for i, o in enumerate(self.outs)])
+            self._tensor_ok = True
         else:
             self.out = torch.empty(self.P * n, dtype=self.data.dtype, device=self.data.device)
             self.flat = self.data.reshape(-1)
@@ -221,6 +230,13 @@ class AllGather(CollectiveOp):
                                             nblocks=self.opts.get("nblocks"))
             return
         if self.form == "list":
+            if self._tensor_ok:
+                try:
+                    dist.all_gather_into_tensor(self.stage, self.flat)
+                    self._unpack.run()
+                    return
+                except (RuntimeError, NotImplementedError, ValueError):
+                    self._tensor_ok = False    # backend without _allgather_base
             dist.all_gather(self.outs, self.data)
             return
         if self._tensor_ok:

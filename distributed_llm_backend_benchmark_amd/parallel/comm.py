@@ -293,7 +293,25 @@ def init_distributed(backend: str = "auto", timeout_s: float = 600.0,
     if dev.type == "cuda":
         from ..utils.affinity import bind_to_device
 
-        comm._extra["affinity"] = bind_to_device(dev.index, local_rank,
-                                                 local_world or min(world, 64),
-                                                 cores_per_rank=cores_per_rank)
+        lw = local_world or min(world, 64)
+        comm._extra["affinity"] = bind_to_device(dev.index, local_rank, lw,
+                                                 cores_per_rank=cores_per_rank,
+                                                 peers_allowed=_local_masks(comm, lw))
     return comm
+
+
+def _local_masks(comm: "Comm", local_world: int):
+    """Every local rank's CPU mask before binding (host name + local rank over the process
+    group; collective), for the launcher-pinned rule of ``utils.affinity.plan``; None at one
+    rank or when unavailable."""
+    if comm.world_size == 1 or not hasattr(os, "sched_getaffinity"):
+        return None
+
+    host = socket.gethostname()
+    mine = (host, comm.local_rank, sorted(os.sched_getaffinity(0)))
+    try:
+        allv = comm.all_gather_object(mine)
+    except RuntimeError:
+        return None
+    masks = {lr: m for h, lr, m in allv if h == host}
+    return [masks.get(r) for r in range(local_world)]

@@ -39,6 +39,14 @@ def _elem_bytes(row: Dict[str, str], default: int) -> int:
     return default
 
 
+def _impl(row: Dict[str, str], col: str) -> str:
+    """Row label: the run's impl name, plus what actually ran when the stats ext CSV records it
+    and it differs (``rccl[native_oop]``: the P = 1 out-of-place substitute)."""
+    impl = row.get(col) or "?"
+    op_impl = row.get("op_impl") or ""
+    return f"{impl}[{op_impl}]" if op_impl and op_impl != impl else impl
+
+
 def load_1d(paths: Iterable[str], default_elem_bytes: int = 2) -> Dict[Key, Dict[str, object]]:
     """Best (lowest p50) row per 1D key across the given stats CSVs."""
     best: Dict[Key, Dict[str, object]] = {}
@@ -48,7 +56,7 @@ def load_1d(paths: Iterable[str], default_elem_bytes: int = 2) -> Dict[Key, Dict
             p50_us = float(r["median_time_us"])
             nbytes = int(r.get("bytes") or 0) or int(r["num_elements"]) * _elem_bytes(
                 r, default_elem_bytes)
-            rec = {"impl": r.get("mpi_implementation", "?"), "p50_us": p50_us, "bytes": nbytes}
+            rec = {"impl": _impl(r, "mpi_implementation"), "p50_us": p50_us, "bytes": nbytes}
             if key not in best or p50_us < best[key]["p50_us"]:
                 best[key] = rec
     return best
@@ -62,7 +70,7 @@ def load_3d(paths: Iterable[str]) -> Dict[Key, Dict[str, object]]:
                    int(r["hidden_dim"]))
             p50_us = float(r["median_time_ms"]) * 1e3
             nbytes = int(r.get("tensor_size_bytes") or 0) or int(r["num_elements"]) * 2
-            rec = {"impl": r.get("implementation", "?"), "p50_us": p50_us, "bytes": nbytes}
+            rec = {"impl": _impl(r, "implementation"), "p50_us": p50_us, "bytes": nbytes}
             if key not in best or p50_us < best[key]["p50_us"]:
                 best[key] = rec
     return best

@@ -22,7 +22,7 @@ import numpy as np
 
 from ..utils.io import load_json, save_json
 from .bandwidth import algbw_gbps, busbw_gbps
-from .stats1d import rank_max_p50, refused
+from .stats1d import op_impl_label, rank_max_p50, refused
 
 STANDARD_COLUMNS = [
     "implementation", "operation", "num_ranks", "hidden_dim", "seq_len", "batch",
@@ -31,7 +31,7 @@ STANDARD_COLUMNS = [
 ]
 EXT_COLUMNS = STANDARD_COLUMNS + [
     "tensor_size_bytes", "dtype", "wire_dtype", "wire_bytes", "rank_max_p50_ms",
-    "algbw_gbps", "busbw_gbps", "timing_method",
+    "algbw_gbps", "busbw_gbps", "timing_method", "op_impl",
 ]
 _METRICS = ["mean_time_ms", "median_time_ms", "min_time_ms", "max_time_ms"]
 
@@ -73,6 +73,7 @@ def stats_for_result(data: Dict[str, object]) -> Dict[str, object]:
         "algbw_gbps": algbw_gbps(op, wire_bytes, p50, p),
         "busbw_gbps": busbw_gbps(op, wire_bytes, p50, p),
         "timing_method": data.get("timing_method"),
+        "op_impl": op_impl_label(data),
     }
 
 

@@ -15,8 +15,13 @@ Done in-process at ``init_distributed`` — no ``numactl`` relaunch and no exec 
 2. ``/sys/bus/pci/devices/<bdf>/numa_node`` and ``local_cpulist``,
 3. the local ranks whose GPUs share that CPU list split it into disjoint slices
    (``cores_per_rank`` each when given, else an even share), intersected with the CPUs this
-   process may use (cgroup / launcher mask), then ``os.sched_setaffinity``;
-4. with an explicit ``cores_per_rank``, ``torch.set_num_threads`` / ``OMP_NUM_THREADS`` /
+   process may use (cgroup / launcher mask) — unless the launcher already pinned this rank to
+   part of the list (its mask differs from its peers'), which is then kept as is;
+4. the mask is applied to EVERY thread of the process (``/proc/self/task``: the HIP runtime,
+   RCCL proxy, process-group watchdog and OpenMP threads created before this point, not only
+   the caller — Linux ``sched_setaffinity(0, …)`` binds one thread), as the reference's
+   launchers bind the whole process; threads created later inherit it;
+5. with an explicit ``cores_per_rank``, ``torch.set_num_threads`` / ``OMP_NUM_THREADS`` /
    ``MKL_NUM_THREADS`` follow the slice (otherwise the launcher's thread settings stand).
 
 ``DLBB_BIND=0`` disables it. The applied binding is recorded in result JSONs.
@@ -97,19 +102,34 @@ def numa_of(bdf: str, sysfs: str = "/sys") -> Dict:
 
 def plan(local_rank: int, local_cpus: Sequence[Sequence[int]],
          cores_per_rank: Optional[int] = None,
-         allowed: Optional[Sequence[int]] = None) -> List[int]:
+         allowed: Optional[Sequence[int]] = None,
+         peers_allowed: Optional[Sequence[Optional[Sequence[int]]]] = None) -> List[int]:
     """The CPU set of ``local_rank`` given every local rank's GPU-local CPU list
     (``local_cpus[r]``). Ranks with the same list share it in disjoint slices, in local-rank
     order: ``cores_per_rank`` cores each when given (reference ``--map-by socket:PE=14``), else
     an even split. ``allowed`` (the process's current mask) is applied first. Falls back to the
-    whole (allowed) list when the slice would be empty."""
-    mine = list(local_cpus[local_rank])
+    whole (allowed) list when the slice would be empty.
+
+    Launcher-pinned ranks: without ``cores_per_rank``, when ``allowed`` already
+    leaves out part of the GPU-local list, the launcher (``mpirun --map-by socket:PE=14``,
+    Slurm) or a cgroup placed this rank — its mask is kept as is instead of being cut into a
+    1/peers slice of itself. The even split still applies when ``peers_allowed`` (every local
+    rank's mask) shows all ranks sharing the list were given the SAME mask (nothing placed them
+    apart)."""
+    full = list(local_cpus[local_rank])
+    mine = full
     if allowed is not None:
         allow = set(allowed)
         mine = [c for c in mine if c in allow]
     if not mine:
         return []
-    peers = [r for r in range(len(local_cpus)) if list(local_cpus[r]) == list(local_cpus[local_rank])]
+    peers = [r for r in range(len(local_cpus)) if list(local_cpus[r]) == full]
+    if cores_per_rank is None and len(mine) < len(full) and len(peers) > 1:
+        same = peers_allowed is not None and all(
+            peers_allowed[r] is not None and sorted(peers_allowed[r]) == sorted(allowed)
+            for r in peers if r < len(peers_allowed))
+        if not same:
+            return mine
     slot = peers.index(local_rank)
     n = int(cores_per_rank) if cores_per_rank else max(1, len(mine) // len(peers))
     chunk = mine[slot * n:(slot + 1) * n]
@@ -120,14 +140,46 @@ def _local_device_indices(local_world: int, ndev: int) -> List[int]:
     return [r % max(1, ndev) for r in range(local_world)]
 
 
+def thread_ids() -> List[int]:
+    """Every thread (task) id of this process (``/proc/self/task``); empty where unavailable."""
+    try:
+        return sorted(int(t) for t in os.listdir("/proc/self/task"))
+    except (OSError, ValueError):
+        return []
+
+
+def apply_to_all_threads(cpus: Sequence[int]) -> Dict:
+    """Set the affinity of EVERY thread of the process to ``cpus`` (threads that exit meanwhile
+    are skipped) and read each back: ``{"threads": n, "threads_bound": k, "threads_outside":
+    [tids still outside]}``. Also binds the calling thread first, so threads it creates later
+    inherit the mask."""
+    want = set(cpus)
+    os.sched_setaffinity(0, cpus)
+    bound, outside, seen = 0, [], 0
+    for tid in thread_ids():
+        try:
+            os.sched_setaffinity(tid, cpus)
+            got = os.sched_getaffinity(tid)
+        except OSError:          # the thread exited between listing and binding
+            continue
+        seen += 1
+        if set(got) <= want:
+            bound += 1
+        else:
+            outside.append(tid)
+    return {"threads": seen, "threads_bound": bound, "threads_outside": outside}
+
+
 def bind_to_device(device_index: int, local_rank: int, local_world: int,
                    cores_per_rank: Optional[int] = None, sysfs: str = "/sys",
                    bdf_of=None, apply: bool = True,
-                   allowed: Optional[Sequence[int]] = None) -> Dict:
-    """Bind this process's threads to its GPU's NUMA-local cores (see module doc). Returns the
-    record written into result JSONs; never raises (``{"bound": False, "reason": ...}``).
-    ``bdf_of`` / ``apply=False`` / ``allowed``: test hooks (a fake device -> PCI map, plan
-    without binding, a fake process mask)."""
+                   allowed: Optional[Sequence[int]] = None,
+                   peers_allowed: Optional[Sequence[Optional[Sequence[int]]]] = None) -> Dict:
+    """Bind this process (every thread) to its GPU's NUMA-local cores (see module doc). Returns
+    the record written into result JSONs; never raises (``{"bound": False, "reason": ...}``).
+    ``peers_allowed``: every local rank's CPU mask before binding (gathered at init), for the
+    launcher-pinned rule of :func:`plan`. ``bdf_of`` / ``apply=False`` / ``allowed``: test
+    hooks (a fake device -> PCI map, plan without binding, a fake process mask)."""
     rec: Dict = {"bound": False, "local_rank": local_rank, "device": device_index}
     bdf_of = bdf_of or device_bdf
     if os.environ.get("DLBB_BIND", "1") == "0":
@@ -161,14 +213,17 @@ def bind_to_device(device_index: int, local_rank: int, local_world: int,
         return rec
     if allowed is None:
         allowed = sorted(os.sched_getaffinity(0))
-    cpus = plan(local_rank, [infos[d]["cpus"] for d in devs], cores_per_rank, allowed)
+    if peers_allowed is not None and len(peers_allowed) != len(devs):
+        peers_allowed = None                  # one GPU per process: peers not visible here
+    cpus = plan(local_rank, [infos[d]["cpus"] for d in devs], cores_per_rank, allowed,
+                peers_allowed)
     if not cpus:
         rec["reason"] = "no GPU-local CPU in this process's allowed set"
         return rec
     if not apply:
         return dict(rec, planned=format_cpulist(cpus), ncpus=len(cpus))
     try:
-        os.sched_setaffinity(0, cpus)
+        threads = apply_to_all_threads(cpus)
     except OSError as e:
         rec["reason"] = f"sched_setaffinity: {e}"
         return rec
@@ -183,14 +238,21 @@ def bind_to_device(device_index: int, local_rank: int, local_world: int,
         except RuntimeError:
             pass
     rec.update(bound=True, cpus=format_cpulist(cpus), ncpus=n,
-               cores_per_rank=cores_per_rank)
+               cores_per_rank=cores_per_rank, **threads)
     return rec
 
 
 def current() -> Dict:
-    """This process's CPU mask (for result JSONs)."""
+    """This process's CPU mask — the union over its threads, and how many threads it has (for
+    result JSONs)."""
     try:
-        cpus = sorted(os.sched_getaffinity(0))
+        cpus = set(os.sched_getaffinity(0))
     except (AttributeError, OSError):
         return {}
-    return {"cpus": format_cpulist(cpus), "ncpus": len(cpus)}
+    tids = thread_ids()
+    for tid in tids:
+        try:
+            cpus |= set(os.sched_getaffinity(tid))
+        except OSError:
+            pass
+    return {"cpus": format_cpulist(sorted(cpus)), "ncpus": len(cpus), "threads": len(tids)}

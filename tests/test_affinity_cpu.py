@@ -80,3 +80,69 @@ def test_local_env_launchers(monkeypatch):
     monkeypatch.setenv("SLURM_LOCALID", "3")
     monkeypatch.setenv("SLURM_NTASKS_PER_NODE", "8(x2)")
     assert local_env(11) == (3, 8)
+
+
+def test_launcher_pinned_mask_is_kept_unless_all_peers_share_it():
+    """a rank the launcher already pinned inside its GPU-local list (mpirun
+    --map-by socket:PE=14) keeps that mask instead of a 1/peers slice of it; identical masks
+    on every peer (nothing placed them apart) are still split evenly."""
+    local = [A.parse_cpulist("0-55")] * 4
+    pinned = [list(range(14 * r, 14 * r + 14)) for r in range(4)]
+    for r in range(4):
+        assert A.plan(r, local, allowed=pinned[r], peers_allowed=pinned) == pinned[r]
+        assert A.plan(r, local, allowed=pinned[r]) == pinned[r]      # peers unknown: keep
+    shared = list(range(0, 40))                                      # cgroup, same for all
+    got = [A.plan(r, local, allowed=shared, peers_allowed=[shared] * 4) for r in range(4)]
+    assert [len(g) for g in got] == [10] * 4
+    assert len(set().union(*map(set, got))) == 40
+    full = list(range(224))                                          # unrestricted: split
+    assert A.plan(1, local, allowed=full) == list(range(14, 28))
+
+
+def test_binding_applies_to_every_thread(tmp_path):
+    """threads that exist BEFORE bind_to_device (HIP runtime, RCCL proxy,
+    PG watchdog in a real run) end up inside the planned set too, not only the caller; the
+    original mask is restored afterwards."""
+    import threading
+
+    orig = sorted(os.sched_getaffinity(0))
+    if len(orig) < 2:
+        pytest.skip("needs at least 2 CPUs")
+    half = orig[: len(orig) // 2]
+    base = tmp_path / "bus" / "pci" / "devices" / "0000:11:00.0"
+    base.mkdir(parents=True)
+    (base / "numa_node").write_text("0\n")
+    (base / "local_cpulist").write_text(A.format_cpulist(half) + "\n")
+    stop = threading.Event()
+    tids = []
+    ready = threading.Barrier(4)
+
+    def worker():
+        tids.append(threading.get_native_id())
+        ready.wait()
+        stop.wait(30)
+
+    ths = [threading.Thread(target=worker, daemon=True) for _ in range(3)]
+    for t in ths:
+        t.start()
+    ready.wait()
+    try:
+        rec = A.bind_to_device(0, 0, 1, sysfs=str(tmp_path), bdf_of={0: "0000:11:00.0"}.get)
+        assert rec["bound"] is True, rec
+        planned = set(A.parse_cpulist(rec["cpus"]))
+        assert planned == set(half)
+        assert rec["threads"] >= 4 and rec["threads_bound"] == rec["threads"]
+        assert rec["threads_outside"] == []
+        for tid in tids:                                  # created before the binding
+            assert set(os.sched_getaffinity(tid)) <= planned, tid
+        t_new = threading.Thread(target=lambda: tids.append(-threading.get_native_id()))
+        t_new.start()
+        t_new.join()
+        cur = A.current()
+        assert A.parse_cpulist(cur["cpus"]) == sorted(planned)
+    finally:
+        stop.set()
+        for t in ths:
+            t.join()
+        A.apply_to_all_threads(orig)
+    assert sorted(os.sched_getaffinity(0)) == orig

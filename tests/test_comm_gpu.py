@@ -811,3 +811,26 @@ def test_collectives_sweep_pipeline_ranks_on_one_gpu(tmp_path):
 
     res = run_pipeline(tmp_path, 2, backend="gloo", device="cuda", direct_ipc=True, timeout=600)
     check_pipeline(res, 2)
+
+
+def test_allgather_list_form_unpack_bit_exact_world1():
+    """List-form all-gather (reference collectives/1d/dsccl.py:72-76) on RCCL: one
+    all_gather_into_tensor into a staging buffer, then the list unpack as ONE chunk-copy launch
+    (csrc/flatten.hip) — bit-exact at 16-B aligned and unaligned slice offsets."""
+    from distributed_llm_backend_benchmark_amd.parallel.collectives import make_data, make_op
+    from distributed_llm_backend_benchmark_amd.parallel.comm import init_distributed
+
+    comm = init_distributed("rccl")
+    try:
+        for n in (1, 7, 4096, 1000003, 1 << 24):
+            x = make_data((n,), torch.bfloat16, 0, comm.device)
+            op = make_op("allgather", comm, x, form="list")
+            for o in op.outs:
+                o.fill_(float("nan"))
+            op.run()
+            torch.cuda.synchronize()
+            assert op._tensor_ok                 # staged + chunk-copy path, not the list call
+            assert len(op.outs) == 1 and torch.equal(op.outs[0], x), n
+            assert torch.equal(op.result(), x.reshape(-1))
+    finally:
+        comm.destroy()

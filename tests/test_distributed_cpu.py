@@ -262,6 +262,64 @@ def test_fault_injection_records_error_and_continues(tmp_path, spec):
     assert "injected fault" in rec["error"]
 
 
+def _corrupt_worker(rank, world, outdir, spec):
+    os.environ["DLBB_FAULT_INJECT"] = spec
+    from distributed_llm_backend_benchmark_amd.bench.sweep import run_1d_sweep, run_3d_sweep
+    from distributed_llm_backend_benchmark_amd.parallel.comm import init_distributed
+
+    comm = init_distributed("gloo")
+    w1 = run_1d_sweep(comm, ops=["allreduce", "allgather"], sizes={"1KB": 256, "4KiB": 2048},
+                      dtype="fp32", warmup=1, iters=2, output_dir=outdir + "/1d",
+                      impl_name="gloo", validate=True)
+    w3 = run_3d_sweep(comm, ops=["allreduce"], batch_sizes=[1], seq_lengths=[4, 8],
+                      hidden_dims=[64], dtype="fp32", warmup=1, iters=2,
+                      output_dir=outdir + "/3d", impl_name="gloo", validate=True)
+    comm.destroy()
+    return [os.path.basename(w) for w in w1 + w3]
+
+
+def test_wrong_result_never_becomes_a_statistic(tmp_path):
+    """a collective whose output fails validation (injected on rank 1 with
+    DLBB_FAULT_INJECT stage=corrupt) is written as <stem>.error.json with invalid=wrong_result,
+    no result file; and a raw record carrying validated=false is refused by BOTH stats stages."""
+    from distributed_llm_backend_benchmark_amd.stats import stats1d, stats3d
+
+    out = str(tmp_path / "c")
+    spec = "op=allreduce,rank=1,stage=corrupt"
+    written = run_multiprocess(_corrupt_worker, 2, args=(out, spec), timeout=300)[0]
+    assert sorted(written) == ["gloo_allgather_ranks2_1KB.json",
+                               "gloo_allgather_ranks2_4KiB.json"], written
+    for sub, n in (("1d", 2), ("3d", 2)):
+        errs = [f for f in os.listdir(f"{out}/{sub}") if f.endswith(".error.json")]
+        assert len(errs) == n, errs
+        for f in errs:
+            rec = json.load(open(f"{out}/{sub}/{f}"))
+            assert rec["invalid"] == "wrong_result" and rec["validated"] is False
+            assert not os.path.exists(f"{out}/{sub}/{f[:-len('.error.json')]}.json")
+    # the stats stages refuse a raw record whose validation failed, even if someone wrote one
+    good = json.load(open(f"{out}/1d/gloo_allgather_ranks2_1KB.json"))
+    assert good["validated"] is True
+    assert stats1d.refused(good) is None
+    bad = dict(good, operation="allreduce", validated=False)
+    assert stats1d.refused(bad) == "wrong_result"
+    os.makedirs(f"{out}/raw1", exist_ok=True)
+    json.dump(bad, open(f"{out}/raw1/gloo_allreduce_ranks2_1KB.json", "w"))
+    json.dump(good, open(f"{out}/raw1/gloo_allgather_ranks2_1KB.json", "w"))
+    rows = stats1d.process_directory(f"{out}/raw1", f"{out}/s1", verbose=False)
+    assert [r["operation"] for r in rows] == ["allgather"]
+    os.makedirs(f"{out}/raw3", exist_ok=True)
+    rec3 = {"implementation": "gloo", "operation": "allreduce", "num_ranks": 2,
+            "tensor_shape": {"batch": 1, "seq_len": 4, "hidden_dim": 64}, "num_elements": 256,
+            "tensor_size_bytes": 1024, "tensor_size_mb": 0.001, "dtype": "float32",
+            "timings": [[1e-3, 1e-3], [1e-3, 1e-3]], "validated": False}
+    json.dump(rec3, open(f"{out}/raw3/gloo_allreduce_ranks2_b1_s4_h64.json", "w"))
+    json.dump(dict(rec3, validated=True, num_elements=512, tensor_size_bytes=2048,
+                   tensor_shape={"batch": 1, "seq_len": 8, "hidden_dim": 64}),
+              open(f"{out}/raw3/gloo_allreduce_ranks2_b1_s8_h64.json", "w"))
+    rows3 = stats3d.process_directory(f"{out}/raw3", f"{out}/s3", "gloo", verbose=False)
+    assert [r["seq_len"] for r in rows3] == [8]
+
+
 def _experiment_worker(rank, world):
     from distributed_llm_backend_benchmark_amd.data import create_dataset_from_config
     from distributed_llm_backend_benchmark_amd.models.tp_transformer import create_model_from_config
@@ -349,6 +407,36 @@ def test_bench_py_gloo_world2_contract():
     assert rec["higher_is_better"] is True and rec["scaling"] == "weak"
     assert [e["bytes"] for e in rec["allreduce_sweep"]] == [1 << 10, 8 << 10, 64 << 10, 512 << 10]
     assert all(e["impl"] == "rccl" and e["busbw_GBps"] > 0 for e in rec["allreduce_sweep"])
+
+
+def test_bench_py_deadline_keeps_the_headline():
+    """with a whole-run deadline that has already passed, bench.py (gloo,
+    world 2) still measures and prints the one valid headline line; everything after it is
+    recorded as skipped_deadline, and the run's wall time is in the record."""
+    import json
+    import subprocess
+    import sys
+
+    from conftest import free_port
+
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
+           os.path.join(repo, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "1",
+           "--shape", "1,64,256", "--sweep-max-mib", "1", "--deadline-s", "0"]
+    env = {k: v for k, v in os.environ.items() if k not in ("CUDA_VISIBLE_DEVICES",)}
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=repo, env=env)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    rec = json.loads(lines[0])
+    assert rec["metric"] == "all-reduce bus BW (GB/s)" and rec["value"] > 0
+    assert rec["steps"] == 3 and rec["deadline_s"] == 0 and rec["wall_s"] > 0
+    assert rec["side_skipped_deadline"] is True
+    assert all(e.get("skipped_deadline") for e in rec["allreduce_sweep"])
+    assert all(v == {"skipped_deadline": True} for v in rec["baseline_configs"].values())
+    assert "config5_gpt2_ddp" in rec["skipped_deadline"]
+    assert any(k.startswith("allreduce_sweep/") for k in rec["skipped_deadline"])
 
 
 def _precision_worker(rank, world, grad_dtype_name):
@@ -598,3 +686,32 @@ def test_high_priority_comm_stream_is_fenced(monkeypatch):
     assert ddp.comm_stream_priority() == -1
     monkeypatch.setattr(ddp, "_COMM_PRIORITY", 0)
     assert ddp.comm_stream_priority() == 0
+
+
+def _list_allgather_worker(rank, world):
+    import torch
+
+    from distributed_llm_backend_benchmark_amd.parallel.collectives import make_data, make_op
+    from distributed_llm_backend_benchmark_amd.parallel.comm import init_distributed
+
+    comm = init_distributed("gloo")
+    try:
+        res = []
+        for n in (1, 7, 4096, 100003):
+            x = make_data((n,), torch.bfloat16, rank, comm.device)
+            op = make_op("allgather", comm, x, form="list")
+            op.run()
+            ins = [make_data((n,), torch.bfloat16, r, comm.device) for r in range(world)]
+            exact = all(torch.equal(o, i) for o, i in zip(op.outs, ins))
+            res.append((n, exact, op._tensor_ok))
+        return res
+    finally:
+        comm.destroy()
+
+
+def test_allgather_list_form_unpack_bit_exact():
+    """Reference list form (collectives/1d/dsccl.py:72-76): gathered once into a flat staging
+    buffer, unpacked into the list by one chunk-copy table; every entry bit-exact."""
+    for rank, res in enumerate(run_multiprocess(_list_allgather_worker, 2, timeout=300)):
+        for n, exact, _ in res:
+            assert exact, (rank, n)

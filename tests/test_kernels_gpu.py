@@ -40,12 +40,22 @@ def test_reduce_sum(dtype, nsrc, n):
 @pytest.mark.parametrize("src,dst", [(torch.bfloat16, torch.float32), (torch.float32, torch.bfloat16),
                                      (torch.float16, torch.float32), (torch.float32, torch.float16),
                                      (torch.bfloat16, torch.float16)])
-@pytest.mark.parametrize("n", [1, 13, 65536 + 5])
-def test_cast(src, dst, n):
-    from distributed_llm_backend_benchmark_amd.ops import cast
+@pytest.mark.parametrize("n", [1, 13, 65536 + 5, 3 * 2048 * 256 + 3])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4])
+def test_cast(src, dst, n, variant):
+    """Every cast kernel variant (8-element, one-16-B-side, + non-temporal stores) bit-exact
+    against torch's conversion, with ragged tails and multi-tile grids."""
+    from distributed_llm_backend_benchmark_amd.ops import _lib, cast
 
     x = _randn(n, dtype=src, seed=3)
-    torch.testing.assert_close(cast(x, dst), x.to(dst), rtol=0, atol=0)
+    _lib.lib().dlbb_cast_set_variant(variant)
+    try:
+        torch.testing.assert_close(cast(x, dst), x.to(dst), rtol=0, atol=0)
+        # unaligned source (16-B alignment lost): the 8-element kernel takes it
+        if n > 1:
+            torch.testing.assert_close(cast(x[1:], dst), x[1:].to(dst), rtol=0, atol=0)
+    finally:
+        _lib.lib().dlbb_cast_set_variant(1)
 
 
 def test_cast_nan_inf_preserved():
@@ -66,8 +76,11 @@ def test_pack_rows(cols, ld):
     torch.testing.assert_close(out, view.float(), rtol=0, atol=0)
 
 
-def test_chunk_copy_and_scale():
-    from distributed_llm_backend_benchmark_amd.ops import ChunkTable, ScaleTable, flatten_into
+@pytest.mark.parametrize("nt", [0, 1])
+def test_chunk_copy_and_scale(nt):
+    from distributed_llm_backend_benchmark_amd.ops import ChunkTable, ScaleTable, _lib, flatten_into
+
+    _lib.lib().dlbb_chunk_copy_set_nt(nt)
 
     ts = [_randn(n, seed=i) for i, n in enumerate([1, 7, 1024, 300001, 64])]
     flat = torch.zeros(sum(t.numel() for t in ts), dtype=torch.bfloat16, device=DEV)
@@ -87,6 +100,7 @@ def test_chunk_copy_and_scale():
     ScaleTable(list(zip(views, outs)), scale=0.125).run()
     for t, o in zip(ts, outs):
         torch.testing.assert_close(o, t.float() * 0.125, rtol=1e-6, atol=1e-6)
+    _lib.lib().dlbb_chunk_copy_set_nt(0)
 
 
 @pytest.fixture(params=[("mfma", 0, 1), ("mfma", 128, 1), ("mfma", 256, 1), ("mfma", 256, 0),
@@ -467,6 +481,47 @@ def test_layernorm_bwd(cols, with_res):
     assert norm_act.LN_FALLBACKS["count"] - fb0 == (0 if cols % 256 == 0 else 1)
 
 
+@pytest.mark.parametrize("rows,cols", [(16384, 768), (520, 768), (4099, 1024), (7, 256)])
+@pytest.mark.parametrize("with_res", [False, True])
+def test_layernorm_bwd_pipelined_matches_sequential(rows, cols, with_res):
+    """The pipelined LN backward (8 waves / block, next row's loads in flight) against the
+    wave-per-row-sequence kernel: dx BITWISE equal (same per-row math), dgamma / dbeta equal to
+    fp32 summation-order noise, and both against the fp32 torch reference."""
+    from distributed_llm_backend_benchmark_amd.ops import _lib
+    from distributed_llm_backend_benchmark_amd.ops.norm_act import _ln_bwd_reference
+
+    L = _lib.lib()
+    h, dy = _randn(rows, cols, seed=31), _randn(rows, cols, seed=32)
+    dres = _randn(rows, cols, seed=33) if with_res else None
+    gam = _randn(cols, seed=34)
+    mean = h.float().mean(1)
+    rstd = torch.rsqrt(h.float().var(1, unbiased=False) + 1e-5)
+    grid = L.dlbb_layernorm_bwd_grid(rows)
+    outs = {}
+    for var in (0, 1):
+        L.dlbb_layernorm_bwd_set_variant(var)
+        dx = torch.empty_like(h)
+        ws = torch.full((2 * grid * cols,), float("nan"), device=DEV)
+        # dgamma / dbeta come out in the parameter dtype (bf16 here)
+        dg = torch.empty(cols, device=DEV, dtype=torch.bfloat16)
+        db = torch.empty(cols, device=DEV, dtype=torch.bfloat16)
+        _lib.check(L.dlbb_layernorm_bwd(
+            dy.data_ptr(), h.data_ptr(), gam.data_ptr(), 1, mean.data_ptr(), rstd.data_ptr(),
+            _lib.ptr(dres), dx.data_ptr(), ws.data_ptr(), dg.data_ptr(), db.data_ptr(), rows,
+            cols, 0, _lib.stream(h.device)), "ln_bwd")
+        outs[var] = (dx, dg, db)
+    L.dlbb_layernorm_bwd_set_variant(1)
+    assert torch.equal(outs[0][0], outs[1][0])
+    # fp32 sums in a different order, then one bf16 rounding: at most an ulp apart
+    torch.testing.assert_close(outs[1][1].float(), outs[0][1].float(), rtol=8e-3, atol=1e-2)
+    torch.testing.assert_close(outs[1][2].float(), outs[0][2].float(), rtol=8e-3, atol=1e-2)
+    rdg, rdb = torch.empty(cols, device=DEV), torch.empty(cols, device=DEV)
+    rdx = _ln_bwd_reference(dy, h, gam, mean, rstd, dres, rdg, rdb, False)
+    torch.testing.assert_close(outs[1][0].float(), rdx.float(), rtol=2e-2, atol=2e-2)
+    torch.testing.assert_close(outs[1][1].float(), rdg, rtol=1e-2, atol=1e-2 * rows ** 0.5)
+    torch.testing.assert_close(outs[1][2].float(), rdb, rtol=1e-2, atol=1e-2 * rows ** 0.5)
+
+
 @pytest.mark.parametrize("approx", ["none", "tanh"])
 def test_bias_gelu_fwd_bwd(approx):
     from distributed_llm_backend_benchmark_amd.ops import bias_gelu
@@ -734,6 +789,77 @@ def test_wgrad_256_tile_matches_fp32(M, N, K, split):
     wb = torch.empty(N, K, device=DEV, dtype=torch.bfloat16)
     _wgrad_hip256(dy, x, wb, False, split, None)
     torch.testing.assert_close(wb.float(), ref, rtol=2e-2, atol=2e-2 * (M ** 0.5))
+
+
+@pytest.mark.parametrize("impl", ["mfma", "mfma256", "mfma_wide"])
+@pytest.mark.parametrize("M,N,K", [(16384, 768, 768), (16384, 3072, 768), (4096, 2304, 768),
+                                   (512, 768, 3072)])
+@pytest.mark.parametrize("order", [0, 1])
+def test_wgrad_fused_reduce_bitwise(monkeypatch, impl, M, N, K, order):
+    """In-launch split-K combine (last-arriving workgroup per tile) against the separate reduce
+    pass: same fp32 summation order, so dW / db / accumulate results must be BITWISE equal, for
+    both workgroup orders (a tile's slices on one XCD, or spread over all of them)."""
+    from distributed_llm_backend_benchmark_amd.ops import _lib, gemm
+
+    fn = {"mfma": gemm._wgrad_hip, "mfma256": gemm._wgrad_hip256,
+          "mfma_wide": gemm._wgrad_hip_wide}[impl]
+    if impl == "mfma256" and N % 256 or impl == "mfma_wide" and K % 256:
+        pytest.skip("tile does not divide the shape")
+    dy = _randn(M, N, seed=61, scale=0.5)
+    x = _randn(M, K, seed=62, scale=0.5)
+    _lib.lib().dlbb_gemm_wgrad_set_order(order)
+    try:
+        outs = {}
+        for fused in ("0", "1"):
+            monkeypatch.setenv("DLBB_WGRAD_FUSED", fused)
+            w32, b32 = torch.empty(N, K, device=DEV), torch.empty(N, device=DEV)
+            fn(dy, x, w32, False, None, b32)
+            wacc, bacc = torch.full((N, K), 0.25, device=DEV), torch.full((N,), 0.5, device=DEV)
+            fn(dy, x, wacc, True, None, bacc)
+            wb = torch.empty(N, K, device=DEV, dtype=torch.bfloat16)
+            bb = torch.empty(N, device=DEV, dtype=torch.bfloat16)
+            fn(dy, x, wb, False, None, bb)
+            outs[fused] = (w32, b32, wacc, bacc, wb, bb)
+        for a, b in zip(outs["0"], outs["1"]):
+            assert torch.equal(a, b)
+        ref = dy.float().t() @ x.float()
+        torch.testing.assert_close(outs["1"][0], ref, rtol=2e-3, atol=2e-3 * (M ** 0.5))
+        torch.testing.assert_close(outs["1"][1], dy.float().sum(0), rtol=2e-3,
+                                   atol=2e-3 * (M ** 0.5))
+    finally:
+        _lib.lib().dlbb_gemm_wgrad_set_order(1)
+
+
+def test_wgrad_fused_reduce_repeated_under_load(monkeypatch):
+    """20 back-to-back fused launches on one stream with different inputs while a second stream
+    streams HBM (uneven load, reducer L1 warm from the previous launch): every result must equal
+    the separate-pass result, and the per-stream tile counters end at zero (re-armed)."""
+    from distributed_llm_backend_benchmark_amd.ops import gemm
+
+    M, N, K = 16384, 768, 768
+    xs = [_randn(M, K, seed=70 + i, scale=0.5) for i in range(4)]
+    dys = [_randn(M, N, seed=80 + i, scale=0.5) for i in range(4)]
+    monkeypatch.setenv("DLBB_WGRAD_FUSED", "0")
+    refs = []
+    for i in range(4):
+        o = torch.empty(N, K, device=DEV)
+        gemm._wgrad_hip(dys[i], xs[i], o, False, None, None)
+        refs.append(o)
+    monkeypatch.setenv("DLBB_WGRAD_FUSED", "1")
+    side = torch.cuda.Stream()
+    big = torch.empty(256 << 20, dtype=torch.uint8, device=DEV)
+    outs = [torch.empty(N, K, device=DEV) for _ in range(20)]
+    torch.cuda.synchronize()
+    with torch.cuda.stream(side):
+        for _ in range(8):
+            big.add_(1)
+    for i in range(20):
+        gemm._wgrad_hip(dys[i % 4], xs[i % 4], outs[i], False, None, None)
+    torch.cuda.synchronize()
+    for i in range(20):
+        assert torch.equal(outs[i], refs[i % 4]), i
+    cnt = gemm._tile_counters(torch.device(DEV), 1)
+    assert int(cnt.abs().sum()) == 0
 
 
 def test_wgrad_256_tile_asymmetric():

@@ -13,7 +13,7 @@ GIB = 1 << 30
 
 
 def _fake_bench_one(comm, op_name, data, warmup, iters, timing, batched, graph, validate, seed,
-                    op_opts):
+                    op_opts, label=""):
     return {"op_impl": "rccl", "timings": [[14e-6] * iters], "host_timings": [[20e-6] * iters],
             "timing_method": "hip_event", "message_bytes": GIB, "num_elements": GIB // 2}
 

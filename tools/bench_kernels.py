@@ -206,3 +206,111 @@ if "gelu" in which:
                                                     ws.data_ptr(), 16384, 3072, 1, L.stream(a.device)), iters=30)
     out(kernel="bias_gelu_tanh", fwd_us=t_f * 1e6, fwd_TBps=a.numel() * 4 / t_f / 1e12,
         bwd_us=t_b * 1e6, bwd_db_us=t_bd * 1e6, bwd_TBps=a.numel() * 6 / t_b / 1e12)
+if "lnab" in which:
+    # LayerNorm backward, wave-per-row-sequence (variant 0) vs pipelined (1), raw launcher
+    # (kernel + dgamma/dbeta column reduce); bytes = h + dy (+ dres) read + dx written
+    from distributed_llm_backend_benchmark_amd.ops import _lib as L
+    for rows, cols in ((16384, 768), (16384, 1024), (4096, 768)):
+        h, dy, dres = rnd(rows, cols), rnd(rows, cols), rnd(rows, cols)
+        gam = rnd(cols)
+        mean = torch.randn(rows, device="cuda")
+        rstd = torch.rand(rows, device="cuda") + 0.5
+        dx = torch.empty_like(h)
+        grid = L.lib().dlbb_layernorm_bwd_grid(rows)
+        ws = torch.empty(2 * grid * cols, device="cuda")
+        dg, db = torch.empty(cols, device="cuda", dtype=torch.bfloat16), \
+            torch.empty(cols, device="cuda", dtype=torch.bfloat16)
+        res = {}
+        for var in (0, 1):
+            L.lib().dlbb_layernorm_bwd_set_variant(var)
+            for with_res in (False, True):
+                def run():
+                    L.check(L.lib().dlbb_layernorm_bwd(
+                        dy.data_ptr(), h.data_ptr(), gam.data_ptr(), 1, mean.data_ptr(),
+                        rstd.data_ptr(), dres.data_ptr() if with_res else None, dx.data_ptr(),
+                        ws.data_ptr(), dg.data_ptr(), db.data_ptr(), rows, cols, 0,
+                        L.stream(h.device)), "ln_bwd")
+                t = t_med(run, iters=50)
+                nb = rows * cols * 2 * (4 if with_res else 3)
+                res[f"v{var}_{'res' if with_res else 'nores'}"] = {
+                    "us": round(t * 1e6, 2), "TBps": round(nb / t / 1e12, 3)}
+        L.lib().dlbb_layernorm_bwd_set_variant(1)
+        out(kernel="layernorm_bwd_ab", rows=rows, cols=cols, res=res)
+if "wgradfused" in which:
+    # weight gradient at the GPT-2 shapes: separate split-K reduce pass vs in-launch combine
+    # (both workgroup orders), accumulate into bf16 + fused bias (the training-step call)
+    from distributed_llm_backend_benchmark_amd.ops import _lib as L
+    from distributed_llm_backend_benchmark_amd.ops.gemm import (_wgrad_hip, _wgrad_hip256,
+                                                                _wgrad_hip_wide)
+    for N, K in ((2304, 768), (768, 768), (3072, 768), (768, 3072)):
+        M = 16384
+        dy, x = rnd(M, N), rnd(M, K)
+        w_out = torch.zeros(N, K, device="cuda", dtype=torch.bfloat16)
+        b_out = torch.zeros(N, device="cuda", dtype=torch.bfloat16)
+        res = {}
+        for name, fn in (("t128", _wgrad_hip), ("t256", _wgrad_hip256), ("wide", _wgrad_hip_wide)):
+            if name == "t256" and N % 256 or name == "wide" and K % 256:
+                continue
+            for mode in ("sep", "fused_split_major", "fused_tile_major"):
+                os.environ["DLBB_WGRAD_FUSED"] = "0" if mode == "sep" else "1"
+                L.lib().dlbb_gemm_wgrad_set_order(1 if mode == "fused_tile_major" else 0)
+                res[f"{name}_{mode}"] = round(t_med(
+                    lambda: fn(dy, x, w_out, True, None, b_out), iters=30) * 1e6, 1)
+        os.environ["DLBB_WGRAD_FUSED"] = "1"
+        L.lib().dlbb_gemm_wgrad_set_order(1)
+        out(kernel="wgrad_fused_reduce_ab", M=M, N=N, K=K, us=res,
+            tflops={k: round(2 * M * N * K / v / 1e6, 1) for k, v in res.items()})
+if "memroof" in which:
+    # collective-path memory kernels against the HBM roofline: cast (every
+    # dtype pair, 3 variants) vs torch's copy, strided pack, chunk-copy flatten / list unpack,
+    # chunk-copy with scale, n-way reduce — 64 MiB .. 1 GiB of source
+    from distributed_llm_backend_benchmark_amd.ops import _lib as L
+    from distributed_llm_backend_benchmark_amd.ops.elementwise import ChunkTable, ScaleTable
+    dts = {"bf16": torch.bfloat16, "fp16": torch.float16, "fp32": torch.float32}
+    for mib in (64, 256, 1024):
+        for si, so in (("bf16", "fp32"), ("fp32", "bf16"), ("fp16", "fp32"), ("fp32", "fp16"),
+                       ("bf16", "fp16"), ("bf16", "bf16"), ("fp32", "fp32")):
+            n = (mib << 20) // dts[si].itemsize
+            x = rnd(n, dt=dts[si])
+            y = torch.empty(n, device="cuda", dtype=dts[so])
+            nb = n * (dts[si].itemsize + dts[so].itemsize)
+            res = {}
+            for var in (0, 1, 2, 3, 4):
+                L.lib().dlbb_cast_set_variant(var)
+                res[f"v{var}"] = t_med(lambda: ops.cast(x, dts[so], out=y), iters=20)
+            L.lib().dlbb_cast_set_variant(1)
+            tt = t_med(lambda: y.copy_(x), iters=20)
+            out(kernel="cast", src=si, dst=so, src_MiB=mib,
+                TBps={k: round(nb / v / 1e12, 3) for k, v in res.items()},
+                torch_copy_TBps=round(nb / tt / 1e12, 3))
+        # strided pack: the QKV column slice [rows, 3H] -> [rows, H] bf16
+        cols = 4096
+        rows = (mib << 20) // (2 * cols)
+        src = rnd(rows, 3 * cols)
+        dst = torch.empty(rows, cols, device="cuda", dtype=torch.bfloat16)
+        t = t_med(lambda: ops.pack_rows(src[:, :cols], out=dst), iters=20)
+        tt = t_med(lambda: dst.copy_(src[:, :cols]), iters=20)
+        nb = rows * cols * 4
+        out(kernel="pack_rows", src_MiB=mib, TBps=round(nb / t / 1e12, 3),
+            torch_copy_TBps=round(nb / tt / 1e12, 3))
+        # chunk-copy: the list unpack of an 8-rank all-gather (8 equal slices -> 8 tensors)
+        n = (mib << 20) // 2
+        flat = rnd(n)
+        outs = [torch.empty(n // 8, device="cuda", dtype=torch.bfloat16) for _ in range(8)]
+        tab = ChunkTable([(flat[i * (n // 8):(i + 1) * (n // 8)], outs[i]) for i in range(8)])
+        t = t_med(tab.run, iters=20)
+        L.lib().dlbb_chunk_copy_set_nt(1)
+        tnt = t_med(tab.run, iters=20)
+        L.lib().dlbb_chunk_copy_set_nt(0)
+        tt = t_med(lambda: [o.copy_(flat[i * (n // 8):(i + 1) * (n // 8)])
+                            for i, o in enumerate(outs)], iters=20)
+        out(kernel="chunk_copy", src_MiB=mib, chunks=tab.nchunks,
+            TBps=round(2 * n * 2 / t / 1e12, 3), nt_TBps=round(2 * n * 2 / tnt / 1e12, 3),
+            torch_8copies_TBps=round(2 * n * 2 / tt / 1e12, 3))
+        g32 = torch.empty(n, device="cuda")
+        st = ScaleTable([(flat, g32)], 0.125)
+        t = t_med(st.run, iters=20)
+        out(kernel="chunk_copy_scale_bf16_fp32", src_MiB=mib, TBps=round(n * 6 / t / 1e12, 3))
+        srcs = [rnd(n // 8) for _ in range(8)]
+        t = t_med(lambda: ops.reduce_sum(srcs), iters=20)
+        out(kernel="reduce_sum_8src", src_MiB=mib, TBps=round(9 * (n // 8) * 2 / t / 1e12, 3))
