@@ -327,12 +327,44 @@ __global__ void __launch_bounds__(128 * WM, WJ == 8 ? 2 : (WM == 2 ? 3 : 2))
 
 // out[i] = sum_s ws[s][i] (+ out[i] if accumulate), bf16 or fp32 output; 8 elements / thread.
 // Vectors past n / 8 reduce the bias partials ([split][nb] after the weight partials) into outb.
-template <int DTO>
+// Sum of `split` fp32 slabs (+ optional existing output), one 16-byte float4 per thread per
+// item. S > 0: the split count is a template constant, so all S slab loads of an item are
+// issued before the first add (S x 16 B in flight per lane); S == 0: runtime split, 8 slabs per
+// load batch. The previous form (8 floats per thread, one slab per loop trip) waited for every
+// slab in turn: 40 us per GPT-2 dW call, ~2 TB/s (profiles/r04_final/gpt2_kernel_stats_steady.csv:5).
+template <int S>
+__device__ __forceinline__ f32x4 sum_slabs(const float* __restrict__ src, int64_t ld, int64_t vi,
+                                           int split) {
+  const f32x4* p = reinterpret_cast<const f32x4*>(src) + vi;
+  const int64_t ld4 = ld / 4;
+  if constexpr (S > 0) {
+    f32x4 t[S];
+#pragma unroll
+    for (int s = 0; s < S; ++s) t[s] = __builtin_nontemporal_load(p + s * ld4);
+#pragma unroll
+    for (int s = 1; s < S; ++s) t[0] += t[s];
+    return t[0];
+  } else {
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    int s = 0;
+    for (; s + 8 <= split; s += 8) {
+      f32x4 t[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) t[u] = __builtin_nontemporal_load(p + (s + u) * ld4);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc += t[u];
+    }
+    for (; s < split; ++s) acc += __builtin_nontemporal_load(p + s * ld4);
+    return acc;
+  }
+}
+
+template <int DTO, int S>
 __global__ void __launch_bounds__(256) split_reduce_kernel(const float* __restrict__ ws,
                                                            void* __restrict__ out, int64_t n,
                                                            void* __restrict__ outb, int64_t nb,
                                                            int split, int accumulate) {
-  const int64_t nv = n / 8, nvb = nb / 8;
+  const int64_t nv = n / 4, nvb = nb / 4;
   const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
   for (int64_t v = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; v < nv + nvb;
        v += stride) {
@@ -340,22 +372,41 @@ __global__ void __launch_bounds__(256) split_reduce_kernel(const float* __restri
     const float* src = is_b ? ws + split * n : ws;
     const int64_t ld = is_b ? nb : n, vi = is_b ? v - nv : v;
     void* dst = is_b ? outb : out;
-    float acc[8];
-    load8<DT_F32>(src, vi, acc);
-    for (int s = 1; s < split; ++s) {
-      float t[8];
-      load8<DT_F32>(src + static_cast<int64_t>(s) * ld, vi, t);
+    f32x4 acc = sum_slabs<S>(src, ld, vi, split);
+    if constexpr (DTO == DT_F32) {
+      f32x4* o = static_cast<f32x4*>(dst) + vi;
+      *o = accumulate ? *o + acc : acc;
+    } else {
+      u16x4* o = static_cast<u16x4*>(dst) + vi;
+      if (accumulate) {
+        const u16x4 p = *o;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) acc[j] += t[j];
-    }
-    if (accumulate) {
-      float o[8];
-      load8<DTO>(dst, vi, o);
+        for (int j = 0; j < 4; ++j) acc[j] += bf16_to_f32(p[j]);
+      }
+      u16x4 r;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) acc[j] += o[j];
+      for (int j = 0; j < 4; ++j) r[j] = f32_to_bf16(acc[j]);
+      *o = r;
     }
-    store8<DTO>(dst, vi, acc);
   }
+}
+
+template <int DTO>
+static void split_reduce_dispatch(const float* ws, void* out, int64_t n, void* outb, int64_t nb,
+                                  int split, int accumulate, hipStream_t stream) {
+  const int g = stream_grid((n + nb) / 4, 256);
+#define SR(SV)                                                                               \
+  case SV:                                                                                   \
+    hipLaunchKernelGGL((split_reduce_kernel<DTO, SV>), dim3(g), dim3(256), 0, stream, ws, out, \
+                       n, outb, nb, split, accumulate);                                      \
+    return;
+  switch (split) {
+    SR(1) SR(2) SR(3) SR(4) SR(5) SR(6) SR(7) SR(8) SR(9) SR(10) SR(11) SR(12) SR(16)
+    default:
+      hipLaunchKernelGGL((split_reduce_kernel<DTO, 0>), dim3(g), dim3(256), 0, stream, ws, out, n,
+                         outb, nb, split, accumulate);
+  }
+#undef SR
 }
 
 }  // namespace tn
@@ -433,13 +484,10 @@ static int wgrad_launch(const void* A, int64_t lda, const void* B, int64_t ldb, 
   if (direct || fused) return hipGetLastError();
   const int64_t n = static_cast<int64_t>(N) * K;
   const int64_t nb = out_bias ? N : 0;
-  const int g = stream_grid((n + nb) / 8, 256);
   if (dt_out == DT_BF16)
-    hipLaunchKernelGGL(split_reduce_kernel<DT_BF16>, dim3(g), dim3(256), 0, stream, ws, out, n,
-                       out_bias, nb, split, accumulate);
+    split_reduce_dispatch<DT_BF16>(ws, out, n, out_bias, nb, split, accumulate, stream);
   else
-    hipLaunchKernelGGL(split_reduce_kernel<DT_F32>, dim3(g), dim3(256), 0, stream, ws, out, n,
-                       out_bias, nb, split, accumulate);
+    split_reduce_dispatch<DT_F32>(ws, out, n, out_bias, nb, split, accumulate, stream);
   return hipGetLastError();
 }
 
@@ -476,13 +524,10 @@ DLBB_API int dlbb_gemm_wgrad_tile(const void* A, int64_t lda, const void* B, int
 int dlbb_split_reduce_launch(const float* ws, void* out, int dt_f32, int64_t n, int split,
                              hipStream_t stream) {
   if (n % 8 != 0) return hipErrorInvalidValue;
-  const int g = stream_grid(n / 8, 256);
   if (dt_f32)
-    hipLaunchKernelGGL(tn::split_reduce_kernel<DT_F32>, dim3(g), dim3(256), 0, stream, ws, out,
-                       n, nullptr, int64_t{0}, split, 0);
+    tn::split_reduce_dispatch<DT_F32>(ws, out, n, nullptr, 0, split, 0, stream);
   else
-    hipLaunchKernelGGL(tn::split_reduce_kernel<DT_BF16>, dim3(g), dim3(256), 0, stream, ws, out,
-                       n, nullptr, int64_t{0}, split, 0);
+    tn::split_reduce_dispatch<DT_BF16>(ws, out, n, nullptr, 0, split, 0, stream);
   return hipGetLastError();
 }
 

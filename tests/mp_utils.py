@@ -16,8 +16,9 @@ def _entry(rank, world, port, fn, args, q):
         q.put((rank, "err", f"{type(e).__name__}: {e}\n{traceback.format_exc()}"))
 
 
-def run_multiprocess(fn, world, args=(), timeout=240):
-    """Run ``fn(rank, world, *args)`` in ``world`` spawned processes; returns results by rank."""
+def run_multiprocess(fn, world, args=(), timeout=240, hw_queues="auto"):
+    """Run ``fn(rank, world, *args)`` in ``world`` spawned processes; returns results by rank.
+    ``hw_queues``: "auto" = the 8+-rank queue cap below, None = inherit the environment."""
     from conftest import free_port
 
     ctx = mp.get_context("spawn")
@@ -29,13 +30,14 @@ def run_multiprocess(fn, world, args=(), timeout=240):
     # until a time slice comes round (one such run stalled past the box's silence limit) —
     # 2 queues per rank keep all ranks' queues mapped (children inherit the environment)
     old_q = os.environ.get("GPU_MAX_HW_QUEUES")
-    if world >= 8 and old_q is None:
+    cap = hw_queues == "auto" and world >= 8 and old_q is None
+    if cap:
         os.environ["GPU_MAX_HW_QUEUES"] = "2"
     try:
         for p in procs:
             p.start()
     finally:
-        if world >= 8 and old_q is None:
+        if cap:
             os.environ.pop("GPU_MAX_HW_QUEUES", None)
     out = {}
     try:
