@@ -34,9 +34,6 @@ constexpr int kAttnThreads = 256;
 constexpr int kTileKV = kKB * kAttnD * 2;   // 8 KiB
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
-typedef short i16x4 __attribute__((ext_vector_type(4)));
-typedef __attribute__((address_space(3))) void* lds_vptr_t;
-typedef __attribute__((address_space(3))) i16x4* lds_i16x4_ptr;
 
 // 16-B chunk c (0..7) of LDS row r is stored in slot c ^ swz(r)
 __device__ __forceinline__ int kswz(int r) { return (r >> 1) & 7; }
@@ -206,24 +203,28 @@ __global__ void __launch_bounds__(kAttnThreads, 2) attn_fwd_d64_kernel(AttnArgs 
       for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
         for (int st = 0; st < 2; ++st) {
-          bf16x8 pf;
+          // V^T fragments by asm transposed reads (common.h ds_read_tr16: the builtin made the
+          // compiler drain the next tile's DMA here), waited for before their MFMAs
+          bf16x8 vf[2];
 #pragma unroll
-          for (int j = 0; j < 8; ++j)
-            pf[j] = __builtin_bit_cast(short, static_cast<__bf16>(s[kk][8 * st + j]));
-#pragma unroll
-          for (int dt = 0; dt < 2; ++dt) {
-            bf16x8 vf;
+          for (int dt = 0; dt < 2; ++dt)
 #pragma unroll
             for (int half = 0; half < 2; ++half) {
               const int row = kk * 32 + 16 * st + 8 * half + 4 * (g >> 1) + tq;
               const int col = dt * 32 + 16 * (g & 1) + 4 * tp;
               const int off = row * 128 + (((col >> 3) ^ vswz(row)) << 4) + (col & 7) * 2;
-              const i16x4 t = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4_ptr)(tv + off));
+              const i16x4 t = ds_read_tr16(tv + off);
 #pragma unroll
-              for (int u = 0; u < 4; ++u) vf[4 * half + u] = t[u];
+              for (int u = 0; u < 4; ++u) vf[dt][4 * half + u] = t[u];
             }
-            o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf, o[dt], 0, 0, 0);
-          }
+          bf16x8 pf;
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            pf[j] = __builtin_bit_cast(short, static_cast<__bf16>(s[kk][8 * st + j]));
+          tr_wait(vf[0], vf[1]);
+#pragma unroll
+          for (int dt = 0; dt < 2; ++dt)
+            o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[dt], pf, o[dt], 0, 0, 0);
         }
     }
   }
@@ -334,7 +335,7 @@ __device__ __forceinline__ bf16x8 tr_operand(const char* img, int rowbase, int c
     const int row = rowbase + 8 * half + 4 * (g >> 1) + tq;
     const int col = colbase + 16 * (g & 1) + 4 * tp;
     const int off = row * 128 + (((col >> 3) ^ bswz(row)) << 4) + (col & 7) * 2;
-    const i16x4 t = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4_ptr)(img + off));
+    const i16x4 t = ds_read_tr16(img + off);   // asm read: the caller waits (tr_wait)
 #pragma unroll
     for (int u = 0; u < 4; ++u) f[4 * half + u] = t[u];
   }
@@ -443,15 +444,23 @@ __global__ void __launch_bounds__(kAttnThreads, 2) attn_bwd_dkdv_d64_kernel(Attn
       const int rb = 32 * sub;                      // image row base of this 32-query block
       // per-row constants for rows q = qsub + 8 g + 4 hi + u (register e = 4 g + u) as the
       // accumulators' starting values: S' = Q K^T - LSE sqrt(D), dP' = dO V^T - delta
+      // (asm reads: rowv is filled by LDS-DMA, and a compiler-visible read of it drained every
+      // DMA in flight — the next slice's Q / dO included; common.h ds_read_b128_asm)
       f32x16 s, dp;
+      f32x4 lv[4], dv4[4];
 #pragma unroll
       for (int g4 = 0; g4 < 4; ++g4) {
-        const float4 lv = *reinterpret_cast<const float4*>(rv + rb + 8 * g4 + 4 * hi);
-        const float4 dv4 = *reinterpret_cast<const float4*>(rv + 64 + rb + 8 * g4 + 4 * hi);
-        s[4 * g4 + 0] = lv.x; s[4 * g4 + 1] = lv.y; s[4 * g4 + 2] = lv.z; s[4 * g4 + 3] = lv.w;
-        dp[4 * g4 + 0] = dv4.x; dp[4 * g4 + 1] = dv4.y; dp[4 * g4 + 2] = dv4.z;
-        dp[4 * g4 + 3] = dv4.w;
+        lv[g4] = ds_read_b128_asm(rv + rb + 8 * g4 + 4 * hi);
+        dv4[g4] = ds_read_b128_asm(rv + 64 + rb + 8 * g4 + 4 * hi);
       }
+      tr_wait(lv[0], lv[1], lv[2], lv[3], dv4[0], dv4[1], dv4[2], dv4[3]);
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4)
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          s[4 * g4 + u] = lv[g4][u];
+          dp[4 * g4 + u] = dv4[g4][u];
+        }
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) {
         s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_operand(iq, rb + r, 2 * ks + hi), kf[ks],
@@ -482,10 +491,11 @@ __global__ void __launch_bounds__(kAttnThreads, 2) attn_bwd_dkdv_d64_kernel(Attn
         const bf16x8 db = acc_to_bf16(dp, st);
 #pragma unroll
         for (int dt = 0; dt < 2; ++dt) {
-          dv[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
-              tr_operand(ig, rb + 16 * st, 32 * dt, lane), pb, dv[dt], 0, 0, 0);
-          dk[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
-              tr_operand(iq, rb + 16 * st, 32 * dt, lane), db, dk[dt], 0, 0, 0);
+          bf16x8 gt = tr_operand(ig, rb + 16 * st, 32 * dt, lane);   // dO^T, Q^T (asm reads)
+          bf16x8 qt = tr_operand(iq, rb + 16 * st, 32 * dt, lane);
+          tr_wait(gt, qt);
+          dv[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(gt, pb, dv[dt], 0, 0, 0);
+          dk[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qt, db, dk[dt], 0, 0, 0);
         }
       }
     }
@@ -627,11 +637,14 @@ __global__ void __launch_bounds__(kAttnThreads, 2) attn_bwd_dq_d64_kernel(AttnBw
         }
 #pragma unroll
         for (int st = 0; st < 2; ++st) {
+          bf16x8 kt2[2];                            // K^T operands (asm reads)
+#pragma unroll
+          for (int dt = 0; dt < 2; ++dt) kt2[dt] = tr_operand(tk, kk * 32 + 16 * st, 32 * dt, lane);
           const bf16x8 db = acc_to_bf16(dp, st);
+          tr_wait(kt2[0], kt2[1]);
 #pragma unroll
           for (int dt = 0; dt < 2; ++dt)
-            dq[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
-                tr_operand(tk, kk * 32 + 16 * st, 32 * dt, lane), db, dq[dt], 0, 0, 0);
+            dq[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kt2[dt], db, dq[dt], 0, 0, 0);
         }
       }
     }
@@ -662,7 +675,12 @@ static int g_attn_concurrent = [] {
   return (v && v[0] == '1') ? 1 : 0;
 }();
 
+// delta / nls computed inside the dQ kernel (1, default) or by the separate row kernel first (0);
+// the concurrent form always uses the separate kernel (A/B: dlbb_attn_set_fuse_delta)
+static int g_attn_fuse_delta = 1;
+
 DLBB_API void dlbb_attn_set_xcd(int on) { g_attn_xcd = on ? 1 : 0; }
+DLBB_API void dlbb_attn_set_fuse_delta(int on) { g_attn_fuse_delta = on ? 1 : 0; }
 DLBB_API void dlbb_attn_set_concurrent(int on) { g_attn_concurrent = on ? 1 : 0; }
 
 // Per-device side stream + fork/join events for the concurrent backward (created once; a fork
@@ -721,7 +739,7 @@ DLBB_API int dlbb_attn_bwd(const void* qkv, int64_t ld, const void* out, const v
   const int64_t rows = static_cast<int64_t>(B) * T * H;
   // sequential (default): the dQ kernel produces delta / nls for the dK/dV kernel after it;
   // concurrent: both read them, so the separate delta kernel runs first
-  const int fuse = g_attn_concurrent ? 0 : 1;
+  const int fuse = g_attn_concurrent ? 0 : g_attn_fuse_delta;
   if (!fuse)
     hipLaunchKernelGGL(attn_bwd_delta_kernel, dim3(static_cast<unsigned>((rows + 255) / 256)),
                        dim3(256), 0, stream, static_cast<const uint16_t*>(dout),

@@ -131,8 +131,10 @@ __global__ void __launch_bounds__(256) cast2_kernel(const void* __restrict__ src
 }
 
 // 0: 8-element kernel above, 1: cast2, 2: cast2 + nt stores, 3: 2 with one tile per block,
-// 4: 1 with one tile per block
-static int g_cast_variant = 1;
+// 4: 1 with one tile per block, 5 (default): 1 while source + destination fit the 256 MiB MALL,
+// else 2 — measured (profiles/r05_kernels/memroof_pass1.jsonl, TB/s v1 / v2): bf16->fp32 64 MiB
+// 5.54 / 5.43, 256 MiB 5.15 / 6.56, 1 GiB 5.36 / 5.49; fp32->bf16 256 MiB 4.65 / 5.72
+static int g_cast_variant = 5;
 
 // One wave-row loop: rows x cols, source row stride ld_src (elements), dense-or-strided dest.
 template <int DTI, int DTO>
@@ -169,11 +171,14 @@ static hipError_t launch_cast(const void* s, void* d, int64_t n, hipStream_t st)
                        dim3(block), 0, st, s, d, n);
     return hipGetLastError();
   }
+  int v = g_cast_variant;
+  if (v == 5)
+    v = n * (Elem<DTI>::kBytes + Elem<DTO>::kBytes) > (int64_t{256} << 20) ? 2 : 1;
   int64_t g = (n / E + 256 * U - 1) / (256 * U);
   // variants 3/4: one tile per block (no grid-stride loop), as torch's elementwise launch
-  const int64_t cap = g_cast_variant >= 3 ? (int64_t{1} << 30) : 4096;
+  const int64_t cap = v >= 3 ? (int64_t{1} << 30) : 4096;
   g = g < 1 ? 1 : (g > cap ? cap : g);
-  if (g_cast_variant == 2 || g_cast_variant == 3)
+  if (v == 2 || v == 3)
     hipLaunchKernelGGL((cast2_kernel<DTI, DTO, U, true>), dim3(g), dim3(block), 0, st, s, d, n);
   else
     hipLaunchKernelGGL((cast2_kernel<DTI, DTO, U, false>), dim3(g), dim3(block), 0, st, s, d, n);
@@ -199,9 +204,9 @@ static hipError_t launch_pack(const void* s, void* d, int64_t rows, int64_t cols
 using namespace dlbb;
 
 
-// A/B switch: 0 = 8-element kernel, 1 = one 16-B wide side per lane (default), 2 = 1 + nt stores,
-// 3 = 2 without the grid-stride cap, 4 = 1 without it
-DLBB_API void dlbb_cast_set_variant(int v) { g_cast_variant = v < 0 || v > 4 ? 1 : v; }
+// A/B switch: 0 = 8-element kernel, 1 = one 16-B wide side per lane, 2 = 1 + nt stores,
+// 3 = 2 without the grid-stride cap, 4 = 1 without it, 5 = 1 or 2 by size (default)
+DLBB_API void dlbb_cast_set_variant(int v) { g_cast_variant = v < 0 || v > 5 ? 5 : v; }
 
 DLBB_API int dlbb_cast(const void* src, int dtype_in, void* dst, int dtype_out, int64_t n,
                        hipStream_t stream) {

@@ -25,6 +25,52 @@ typedef uint16_t u16x8 __attribute__((ext_vector_type(8)));
 typedef uint16_t u16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef short bf16x8 __attribute__((ext_vector_type(8)));   // MFMA operand fragment
+typedef short i16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) void* lds_vptr_t;
+typedef __attribute__((address_space(3))) i16x4* lds_i16x4_ptr;
+
+// Transposed LDS read (ds_read_b64_tr_b16) issued through inline asm, at byte address
+// `lds` + OFF (OFF: the instruction's 16-bit immediate). The builtin form carries an LDS memory
+// operand that the compiler's wait-count pass cannot separate from LDS-DMA still in flight into
+// ANOTHER buffer of a multi-buffered loop, so it put `s_waitcnt vmcnt(0)` before the first such
+// read of every iteration — draining the very prefetch the loop overlaps (NN / TN ping-pong
+// GEMMs, the weight-gradient kernel, all attention kernels; tools/isa_check.py reports it).
+// The asm read is invisible to that pass in both directions: the compiler never waits for its
+// RESULT either, so every caller issues `s_waitcnt lgkmcnt(0)` before any use of the returned
+// registers (tr_wait below ties the wait to them). tools/isa_check.py checks the compiled code:
+// no instruction may touch a destination register of such a read before an lgkmcnt(0).
+template <int OFF = 0>
+__device__ __forceinline__ i16x4 ds_read_tr16(const void* lds) {
+  static_assert(OFF >= 0 && OFF < 65536, "ds offset is a 16-bit immediate");
+  i16x4 t;
+  const uint32_t addr = static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lds_i16x4_ptr)(lds)));
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(t) : "v"(addr), "n"(OFF));
+  return t;
+}
+
+// 16-byte LDS read through inline asm at `lds` + OFF, for reads of a region that LDS-DMA also
+// fills (same reason and same contract as ds_read_tr16: wait lgkmcnt(0) before use)
+template <int OFF = 0>
+__device__ __forceinline__ f32x4 ds_read_b128_asm(const void* lds) {
+  static_assert(OFF >= 0 && OFF < 65536, "ds offset is a 16-bit immediate");
+  f32x4 t;
+  const uint32_t addr = static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lds_vptr_t)(lds)));
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(t) : "v"(addr), "n"(OFF));
+  return t;
+}
+
+// s_waitcnt lgkmcnt(0) that the fragments passed in depend on, so no use of them can be
+// scheduled before it (see ds_read_tr16); later arguments are tied by empty asm statements
+// ordered after the wait
+template <typename F>
+__device__ __forceinline__ void tr_tie(F& f) {
+  asm volatile("" : "+v"(f));
+}
+template <typename F, typename... R>
+__device__ __forceinline__ void tr_wait(F& f, R&... r) {
+  asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(f));
+  (tr_tie(r), ...);
+}
 
 __device__ __forceinline__ float bf16_to_f32(uint16_t v) {
   return __uint_as_float(static_cast<uint32_t>(v) << 16);

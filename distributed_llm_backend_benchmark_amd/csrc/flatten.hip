@@ -94,19 +94,31 @@ static int grid_for(int64_t nchunks) {
 using namespace dlbb;
 
 // table: DEVICE pointer to nchunks CopyChunk entries (3 x uint64 each).
-static int g_chunk_nt = 0;   // 1: non-temporal destination stores (A/B)
+// Destination stores: 0 plain, 1 non-temporal, 2 auto (default) = non-temporal once the copy's
+// source + destination bytes exceed the 256 MiB MALL — measured (profiles/r05_kernels/
+// memroof_pass1.jsonl): 8-way list unpack of 256 MiB 4.82 -> 6.12 TB/s with nt stores, 64 MiB
+// (everything cache-resident) 4.89 plain vs 4.86 nt.
+static int g_chunk_nt = 2;
+constexpr int64_t kNtBytes = int64_t{256} << 20;
 
-DLBB_API void dlbb_chunk_copy_set_nt(int nt) { g_chunk_nt = nt ? 1 : 0; }
+DLBB_API void dlbb_chunk_copy_set_nt(int nt) { g_chunk_nt = nt < 0 || nt > 2 ? 2 : nt; }
 
-DLBB_API int dlbb_chunk_copy(const void* table, int64_t nchunks, hipStream_t stream) {
+// total_bytes: bytes the table moves (0 = unknown: plain stores under auto)
+DLBB_API int dlbb_chunk_copy2(const void* table, int64_t nchunks, int64_t total_bytes,
+                              hipStream_t stream) {
   if (nchunks <= 0) return hipSuccess;
-  if (g_chunk_nt)
+  const bool nt = g_chunk_nt == 1 || (g_chunk_nt == 2 && 2 * total_bytes > kNtBytes);
+  if (nt)
     hipLaunchKernelGGL(chunk_copy_kernel<true>, dim3(grid_for(nchunks)), dim3(256), 0, stream,
                        static_cast<const CopyChunk*>(table), nchunks);
   else
     hipLaunchKernelGGL(chunk_copy_kernel<false>, dim3(grid_for(nchunks)), dim3(256), 0, stream,
                        static_cast<const CopyChunk*>(table), nchunks);
   return hipGetLastError();
+}
+
+DLBB_API int dlbb_chunk_copy(const void* table, int64_t nchunks, hipStream_t stream) {
+  return dlbb_chunk_copy2(table, nchunks, 0, stream);
 }
 
 DLBB_API int dlbb_chunk_copy_scale(const void* table, int64_t nchunks, int dtype_in,

@@ -785,26 +785,28 @@ __device__ __forceinline__ void stage_b_nn(__amdgpu_buffer_rsrc_t rb, uint32_t l
   }
 }
 
-typedef short i16x4 __attribute__((ext_vector_type(4)));
-typedef __attribute__((address_space(3))) i16x4* lds_i16x4_ptr;
 
 __device__ __forceinline__ void read_b_nn(const char* bbuf, int wc, int fr, int fq,
                                           bf16x8 (&bf)[2][4]) {
   const int q = fr >> 2, p = fr & 3;
   const char* img = bbuf + (wc >> 1) * (kTile2Bytes / 2);
+  // rows ks * 32 + 8 fq + 4 h + q all have nnf(row) = nnf(8 fq + q): the address is a per-lane
+  // base per column block j plus the immediate (ks * 32 + 4 h) * 256 (asm reads: common.h)
+  const int r0 = 8 * fq + q;
 #pragma unroll
-  for (int ks = 0; ks < 2; ++ks)
+  for (int j = 0; j < 4; ++j) {
+    const int col = (wc & 1) * 64 + 16 * p + 4 * (j ^ (p & 1));
+    const char* base = img + r0 * 256 + (((col >> 3) ^ nnf(r0)) << 4) + (col & 7) * 2;
+    const i16x4 t00 = ds_read_tr16<0>(base), t01 = ds_read_tr16<1024>(base);
+    const i16x4 t10 = ds_read_tr16<8192>(base), t11 = ds_read_tr16<9216>(base);
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int row = ks * 32 + 8 * fq + 4 * h + q;
-        const int col = (wc & 1) * 64 + 16 * p + 4 * (j ^ (p & 1));
-        const int off = row * 256 + (((col >> 3) ^ nnf(row)) << 4) + (col & 7) * 2;
-        const i16x4 t = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4_ptr)(img + off));
-#pragma unroll
-        for (int e = 0; e < 4; ++e) bf[ks][j][4 * h + e] = t[e];
-      }
+    for (int e = 0; e < 4; ++e) {
+      bf[0][j][e] = t00[e];
+      bf[0][j][4 + e] = t01[e];
+      bf[1][j][e] = t10[e];
+      bf[1][j][4 + e] = t11[e];
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -849,15 +851,16 @@ __device__ __forceinline__ void read_a_tn(const char* abuf, int wr, int fr, int 
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     const char* ai = lb + (sx ^ (32 * i));
+    // rows (ks * 32 + 4 h): immediates (asm reads, common.h)
+    const i16x4 t00 = ds_read_tr16<0>(ai), t01 = ds_read_tr16<1024>(ai);
+    const i16x4 t10 = ds_read_tr16<8192>(ai), t11 = ds_read_tr16<9216>(ai);
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const i16x4 t = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-            (lds_i16x4_ptr)(ai + (ks * 32 + 4 * h) * 256));
-#pragma unroll
-        for (int e = 0; e < 4; ++e) af[ks][i][4 * h + e] = t[e];
-      }
+    for (int e = 0; e < 4; ++e) {
+      af[0][i][e] = t00[e];
+      af[0][i][4 + e] = t01[e];
+      af[1][i][e] = t10[e];
+      af[1][i][4 + e] = t11[e];
+    }
   }
 }
 

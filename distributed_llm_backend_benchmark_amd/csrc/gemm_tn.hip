@@ -19,6 +19,8 @@
 // BM = 32 rows of m per stage, two LDS buffers (32 KiB: three workgroups per CU).
 #include "common.h"
 
+#include <type_traits>
+
 namespace dlbb {
 
 namespace tn {
@@ -26,9 +28,6 @@ namespace tn {
 constexpr int BKO = 128, BM = 32;                 // output cols (K) per tile, reduction rows/stage
 constexpr int kTile = BM * 128 * 2;               // 8 KiB per [BM][128] image
 
-typedef short i16x4 __attribute__((ext_vector_type(4)));
-typedef __attribute__((address_space(3))) void* lds_vptr_t;
-typedef __attribute__((address_space(3))) i16x4* lds_i16x4_ptr;
 
 __device__ __forceinline__ int swz(int m) { return ((m & 3) | (((m >> 3) & 1) << 2)) << 1; }
 
@@ -116,19 +115,23 @@ __device__ __forceinline__ void wgrad_tile_reduce(const Args& a, int n0, int k0,
 }
 
 // MFMA 16x16x32 operand from a [64 m][128 col] image: lane l gets column colbase + (l & 15),
-// rows kbase + 8 (l >> 4) + j, j = 0..7 (two transposed reads of 4 rows each).
-__device__ __forceinline__ bf16x8 frag(const char* img, int kbase, int colbase, int lane) {
+// rows 32 KS + 8 (l >> 4) + j, j = 0..7 (two transposed reads of 4 rows each). swz(row) is the
+// same for every (KS, half) (row & 3 = q, bit 3 = g & 1), so the rows' offset (32 KS + 4 half)
+// x 256 is the reads' immediate. Asm reads (common.h ds_read_tr16): the caller waits lgkmcnt(0)
+// before using the fragment.
+template <int KS>
+__device__ __forceinline__ bf16x8 frag(const char* img, int colbase, int lane) {
   const int g = lane >> 4, i16 = lane & 15;
   const int q = i16 >> 2, p = i16 & 3;
+  const int r0 = 8 * g + q;
+  const int col = colbase + 4 * p;
+  const char* base = img + r0 * 256 + (((col >> 3) ^ swz(r0)) << 4) + (col & 7) * 2;
+  const i16x4 t0 = ds_read_tr16<KS * 8192>(base), t1 = ds_read_tr16<KS * 8192 + 1024>(base);
   bf16x8 f;
 #pragma unroll
-  for (int half = 0; half < 2; ++half) {
-    const int row = kbase + 8 * g + 4 * half + q;
-    const int col = colbase + 4 * p;
-    const int off = row * 256 + (((col >> 3) ^ swz(row)) << 4) + (col & 7) * 2;
-    const i16x4 t = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4_ptr)(img + off));
-#pragma unroll
-    for (int u = 0; u < 4; ++u) f[4 * half + u] = t[u];
+  for (int u = 0; u < 4; ++u) {
+    f[u] = t0[u];
+    f[4 + u] = t1[u];
   }
   return f;
 }
@@ -235,13 +238,18 @@ __global__ void __launch_bounds__(128 * WM, WJ == 8 ? 2 : (WM == 2 ? 3 : 2))
       stage_all<WM, WJ>(a, mb + (s + NB - 1) * BM, n0, k0, stg((s + NB - 1) % NB), wave, lane);
     const char* ia = stg(cur) + asub * kTile;
     const char* ib = stg(cur) + bsub * kTile;
-#pragma unroll
-    for (int ks = 0; ks < BM / 32; ++ks) {
+    auto kstep = [&](auto ksc) {
+      constexpr int ks = decltype(ksc)::value;
       bf16x8 af[4], bfr[WJ];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) af[i] = frag(ia, 32 * ks, acol + i * 16, lane);
+      for (int i = 0; i < 4; ++i) af[i] = frag<ks>(ia, acol + i * 16, lane);
 #pragma unroll
-      for (int j = 0; j < WJ; ++j) bfr[j] = frag(ib, 32 * ks, bcol + j * 16, lane);
+      for (int j = 0; j < WJ; ++j) bfr[j] = frag<ks>(ib, bcol + j * 16, lane);
+      tr_wait(af[0]);                    // the asm reads' results (frag)
+#pragma unroll
+      for (int i = 1; i < 4; ++i) tr_tie(af[i]);
+#pragma unroll
+      for (int j = 0; j < WJ; ++j) tr_tie(bfr[j]);
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int i = 0; i < 4; ++i)
@@ -259,7 +267,9 @@ __global__ void __launch_bounds__(128 * WM, WJ == 8 ? 2 : (WM == 2 ? 3 : 2))
         }
       }
       __builtin_amdgcn_s_setprio(0);
-    }
+    };
+    static_assert(BM == 32, "one 32-deep k-step per stage");
+    kstep(std::integral_constant<int, 0>{});
   }
   // D map: col = lane & 15 (output k), row = 4 (lane >> 4) + r (output n)
   const int fr = lane & 15, fq = lane >> 4;
@@ -332,7 +342,12 @@ __global__ void __launch_bounds__(128 * WM, WJ == 8 ? 2 : (WM == 2 ? 3 : 2))
 // issued before the first add (S x 16 B in flight per lane); S == 0: runtime split, 8 slabs per
 // load batch. The previous form (8 floats per thread, one slab per loop trip) waited for every
 // slab in turn: 40 us per GPT-2 dW call, ~2 TB/s (profiles/r04_final/gpt2_kernel_stats_steady.csv:5).
-template <int S>
+template <int S, bool NT>
+__device__ __forceinline__ f32x4 ld_slab(const f32x4* p) {
+  if constexpr (NT) return __builtin_nontemporal_load(p);
+  else return *p;
+}
+template <int S, bool NT>
 __device__ __forceinline__ f32x4 sum_slabs(const float* __restrict__ src, int64_t ld, int64_t vi,
                                            int split) {
   const f32x4* p = reinterpret_cast<const f32x4*>(src) + vi;
@@ -340,7 +355,7 @@ __device__ __forceinline__ f32x4 sum_slabs(const float* __restrict__ src, int64_
   if constexpr (S > 0) {
     f32x4 t[S];
 #pragma unroll
-    for (int s = 0; s < S; ++s) t[s] = __builtin_nontemporal_load(p + s * ld4);
+    for (int s = 0; s < S; ++s) t[s] = ld_slab<S, NT>(p + s * ld4);
 #pragma unroll
     for (int s = 1; s < S; ++s) t[0] += t[s];
     return t[0];
@@ -350,16 +365,16 @@ __device__ __forceinline__ f32x4 sum_slabs(const float* __restrict__ src, int64_
     for (; s + 8 <= split; s += 8) {
       f32x4 t[8];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) t[u] = __builtin_nontemporal_load(p + (s + u) * ld4);
+      for (int u = 0; u < 8; ++u) t[u] = ld_slab<S, NT>(p + (s + u) * ld4);
 #pragma unroll
       for (int u = 0; u < 8; ++u) acc += t[u];
     }
-    for (; s < split; ++s) acc += __builtin_nontemporal_load(p + s * ld4);
+    for (; s < split; ++s) acc += ld_slab<S, NT>(p + s * ld4);
     return acc;
   }
 }
 
-template <int DTO, int S>
+template <int DTO, int S, bool NT>
 __global__ void __launch_bounds__(256) split_reduce_kernel(const float* __restrict__ ws,
                                                            void* __restrict__ out, int64_t n,
                                                            void* __restrict__ outb, int64_t nb,
@@ -372,7 +387,7 @@ __global__ void __launch_bounds__(256) split_reduce_kernel(const float* __restri
     const float* src = is_b ? ws + split * n : ws;
     const int64_t ld = is_b ? nb : n, vi = is_b ? v - nv : v;
     void* dst = is_b ? outb : out;
-    f32x4 acc = sum_slabs<S>(src, ld, vi, split);
+    f32x4 acc = sum_slabs<S, NT>(src, ld, vi, split);
     if constexpr (DTO == DT_F32) {
       f32x4* o = static_cast<f32x4*>(dst) + vi;
       *o = accumulate ? *o + acc : acc;
@@ -391,22 +406,72 @@ __global__ void __launch_bounds__(256) split_reduce_kernel(const float* __restri
   }
 }
 
+// Round-4 form (A/B variant 0): 8 floats per thread, one slab per loop trip.
 template <int DTO>
-static void split_reduce_dispatch(const float* ws, void* out, int64_t n, void* outb, int64_t nb,
-                                  int split, int accumulate, hipStream_t stream) {
+__global__ void __launch_bounds__(256) split_reduce8_kernel(const float* __restrict__ ws,
+                                                            void* __restrict__ out, int64_t n,
+                                                            void* __restrict__ outb, int64_t nb,
+                                                            int split, int accumulate) {
+  const int64_t nv = n / 8, nvb = nb / 8;
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
+  for (int64_t v = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; v < nv + nvb;
+       v += stride) {
+    const bool is_b = v >= nv;
+    const float* src = is_b ? ws + split * n : ws;
+    const int64_t ld = is_b ? nb : n, vi = is_b ? v - nv : v;
+    void* dst = is_b ? outb : out;
+    float acc[8];
+    load8<DT_F32>(src, vi, acc);
+    for (int s = 1; s < split; ++s) {
+      float t[8];
+      load8<DT_F32>(src + static_cast<int64_t>(s) * ld, vi, t);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += t[j];
+    }
+    if (accumulate) {
+      float o[8];
+      load8<DTO>(dst, vi, o);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += o[j];
+    }
+    store8<DTO>(dst, vi, acc);
+  }
+}
+
+// split-reduce form (A/B: dlbb_split_reduce_set_variant): 0 = round-4 8-float form, 1 = all
+// slab loads in flight, non-temporal loads, 2 = all slab loads in flight, plain loads
+static int g_split_reduce_variant = 2;
+
+template <int DTO, bool NT>
+static void split_reduce_dispatch_v(const float* ws, void* out, int64_t n, void* outb, int64_t nb,
+                                    int split, int accumulate, hipStream_t stream) {
   const int g = stream_grid((n + nb) / 4, 256);
-#define SR(SV)                                                                               \
-  case SV:                                                                                   \
-    hipLaunchKernelGGL((split_reduce_kernel<DTO, SV>), dim3(g), dim3(256), 0, stream, ws, out, \
-                       n, outb, nb, split, accumulate);                                      \
+#define SR(SV)                                                                                   \
+  case SV:                                                                                       \
+    hipLaunchKernelGGL((split_reduce_kernel<DTO, SV, NT>), dim3(g), dim3(256), 0, stream, ws, out, \
+                       n, outb, nb, split, accumulate);                                          \
     return;
   switch (split) {
     SR(1) SR(2) SR(3) SR(4) SR(5) SR(6) SR(7) SR(8) SR(9) SR(10) SR(11) SR(12) SR(16)
     default:
-      hipLaunchKernelGGL((split_reduce_kernel<DTO, 0>), dim3(g), dim3(256), 0, stream, ws, out, n,
-                         outb, nb, split, accumulate);
+      hipLaunchKernelGGL((split_reduce_kernel<DTO, 0, NT>), dim3(g), dim3(256), 0, stream, ws, out,
+                         n, outb, nb, split, accumulate);
   }
 #undef SR
+}
+
+template <int DTO>
+static void split_reduce_dispatch(const float* ws, void* out, int64_t n, void* outb, int64_t nb,
+                                  int split, int accumulate, hipStream_t stream) {
+  if (g_split_reduce_variant == 0) {
+    const int g = stream_grid((n + nb) / 8, 256);
+    hipLaunchKernelGGL(split_reduce8_kernel<DTO>, dim3(g), dim3(256), 0, stream, ws, out, n, outb,
+                       nb, split, accumulate);
+  } else if (g_split_reduce_variant == 1) {
+    split_reduce_dispatch_v<DTO, true>(ws, out, n, outb, nb, split, accumulate, stream);
+  } else {
+    split_reduce_dispatch_v<DTO, false>(ws, out, n, outb, nb, split, accumulate, stream);
+  }
 }
 
 }  // namespace tn
@@ -488,6 +553,22 @@ static int wgrad_launch(const void* A, int64_t lda, const void* B, int64_t ldb, 
     split_reduce_dispatch<DT_BF16>(ws, out, n, out_bias, nb, split, accumulate, stream);
   else
     split_reduce_dispatch<DT_F32>(ws, out, n, out_bias, nb, split, accumulate, stream);
+  return hipGetLastError();
+}
+
+DLBB_API void dlbb_split_reduce_set_variant(int v) {
+  tn::g_split_reduce_variant = v >= 0 && v <= 2 ? v : 2;
+}
+
+// The weight-gradient split-K reduce alone (microbenchmarks): out[n] (+ outb[nb]) = sum of the
+// `split` fp32 slabs of ws laid out as the wgrad kernel writes them (n slabs, then nb slabs).
+DLBB_API int dlbb_split_reduce(const float* ws, void* out, int dt_out, int64_t n, void* outb,
+                               int64_t nb, int split, int accumulate, hipStream_t stream) {
+  if (n % 8 || nb % 8 || split < 1) return hipErrorInvalidValue;
+  if (dt_out == DT_BF16)
+    tn::split_reduce_dispatch<DT_BF16>(ws, out, n, outb, nb, split, accumulate, stream);
+  else
+    tn::split_reduce_dispatch<DT_F32>(ws, out, n, outb, nb, split, accumulate, stream);
   return hipGetLastError();
 }
 

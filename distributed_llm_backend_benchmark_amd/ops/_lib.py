@@ -45,6 +45,7 @@ _SIGS = {
     "dlbb_pack_rows": (c_int, [c_void_p, c_int, c_int64, c_void_p, c_int, c_int64, c_int64,
                                c_int64, c_void_p]),
     "dlbb_chunk_copy": (c_int, [c_void_p, c_int64, c_void_p]),
+    "dlbb_chunk_copy2": (c_int, [c_void_p, c_int64, c_int64, c_void_p]),
     "dlbb_chunk_copy_set_nt": (None, [c_int]),
     "dlbb_chunk_copy_scale": (c_int, [c_void_p, c_int64, c_int, c_int, c_float, c_void_p]),
     "dlbb_layernorm_fwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p,
@@ -115,6 +116,10 @@ _SIGS = {
                                       c_int, c_int, c_void_p, c_int, c_void_p]),
     "dlbb_gemm_wgrad_counters": (c_int, [c_int, c_int, c_int, c_int]),
     "dlbb_gemm_wgrad_set_order": (None, [c_int]),
+    "dlbb_split_reduce_set_variant": (None, [c_int]),
+    "dlbb_attn_set_fuse_delta": (None, [c_int]),
+    "dlbb_split_reduce": (c_int, [c_void_p, c_void_p, c_int, c_int64, c_void_p, c_int64, c_int,
+                                  c_int, c_void_p]),
     "dlbb_embedding_fwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int, c_int,
                                    c_int64, c_void_p]),
     "dlbb_embedding_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
@@ -194,7 +199,9 @@ def _load() -> ctypes.CDLL:
             for env, setter in (("DLBB_LN_BWD_VARIANT", "dlbb_layernorm_bwd_set_variant"),
                                 ("DLBB_CAST_VARIANT", "dlbb_cast_set_variant"),
                                 ("DLBB_WGRAD_ORDER", "dlbb_gemm_wgrad_set_order"),
-                                ("DLBB_CHUNK_NT", "dlbb_chunk_copy_set_nt")):
+                                ("DLBB_CHUNK_NT", "dlbb_chunk_copy_set_nt"),
+                                ("DLBB_SPLIT_REDUCE_VARIANT", "dlbb_split_reduce_set_variant"),
+                                ("DLBB_ATTN_FUSE_DELTA", "dlbb_attn_set_fuse_delta")):
                 if os.environ.get(env, "") != "":
                     getattr(lib, setter)(int(os.environ[env]))
             _lib = lib

@@ -114,6 +114,7 @@ class ChunkTable:
                 rows.append((s + off, d + off, c))
                 off += c
         self.nchunks = len(rows)
+        self.nbytes = sum(r[2] for r in rows)
         arr = np.asarray(rows if rows else [(0, 0, 0)], dtype=np.uint64)
         host = torch.from_numpy(arr.view(np.int64).copy())
         self.device = dev or torch.device("cpu")
@@ -124,8 +125,8 @@ class ChunkTable:
         if self.nchunks == 0:
             return
         if use_hip(self.table):
-            check(_lib.lib().dlbb_chunk_copy(self.table.data_ptr(), self.nchunks,
-                                             stream(self.device)), "chunk_copy")
+            check(_lib.lib().dlbb_chunk_copy2(self.table.data_ptr(), self.nchunks, self.nbytes,
+                                              stream(self.device)), "chunk_copy")
             return
         for s, d in self.pairs:
             d.view(-1).view(torch.uint8).copy_(s.reshape(-1).view(torch.uint8))
@@ -178,6 +179,7 @@ class ScaleTable(ChunkTable):
                 rows.append((src.data_ptr() + off * es, dst.data_ptr() + off * ed, c * es))
                 off += c
         self.nchunks = len(rows)
+        self.nbytes = sum(r[2] for r in rows)
         arr = np.asarray(rows if rows else [(0, 0, 0)], dtype=np.uint64)
         host = torch.from_numpy(arr.view(np.int64).copy())
         self.device = dev or torch.device("cpu")

@@ -41,7 +41,7 @@ def test_reduce_sum(dtype, nsrc, n):
                                      (torch.float16, torch.float32), (torch.float32, torch.float16),
                                      (torch.bfloat16, torch.float16)])
 @pytest.mark.parametrize("n", [1, 13, 65536 + 5, 3 * 2048 * 256 + 3])
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5])
 def test_cast(src, dst, n, variant):
     """Every cast kernel variant (8-element, one-16-B-side, + non-temporal stores) bit-exact
     against torch's conversion, with ragged tails and multi-tile grids."""
@@ -55,7 +55,7 @@ def test_cast(src, dst, n, variant):
         if n > 1:
             torch.testing.assert_close(cast(x[1:], dst), x[1:].to(dst), rtol=0, atol=0)
     finally:
-        _lib.lib().dlbb_cast_set_variant(1)
+        _lib.lib().dlbb_cast_set_variant(5)
 
 
 def test_cast_nan_inf_preserved():
@@ -76,7 +76,7 @@ def test_pack_rows(cols, ld):
     torch.testing.assert_close(out, view.float(), rtol=0, atol=0)
 
 
-@pytest.mark.parametrize("nt", [0, 1])
+@pytest.mark.parametrize("nt", [0, 1, 2])
 def test_chunk_copy_and_scale(nt):
     from distributed_llm_backend_benchmark_amd.ops import ChunkTable, ScaleTable, _lib, flatten_into
 
@@ -100,7 +100,12 @@ def test_chunk_copy_and_scale(nt):
     ScaleTable(list(zip(views, outs)), scale=0.125).run()
     for t, o in zip(ts, outs):
         torch.testing.assert_close(o, t.float() * 0.125, rtol=1e-6, atol=1e-6)
-    _lib.lib().dlbb_chunk_copy_set_nt(0)
+    if nt == 2:       # auto: a copy past the MALL size takes the non-temporal stores
+        big = _randn(80 << 20, seed=9)
+        dst = torch.empty_like(big)
+        ChunkTable([(big, dst)]).run()
+        assert torch.equal(dst, big)
+    _lib.lib().dlbb_chunk_copy_set_nt(2)
 
 
 @pytest.fixture(params=[("mfma", 0, 1), ("mfma", 128, 1), ("mfma", 256, 1), ("mfma", 256, 0),

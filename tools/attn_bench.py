@@ -41,6 +41,9 @@ for B, T, H in ((16, 1024, 12), (8, 2048, 12), (4, 4096, 16)):
     L.lib().dlbb_attn_set_concurrent(1)
     t_bwd_conc = t_best(lambda: attn_bwd(qkv, o, lse, go, H), iters=10, rounds=3)
     L.lib().dlbb_attn_set_concurrent(0)
+    L.lib().dlbb_attn_set_fuse_delta(0)
+    t_bwd_unfused = t_best(lambda: attn_bwd(qkv, o, lse, go, H), iters=10, rounds=3)
+    L.lib().dlbb_attn_set_fuse_delta(1)
     t_bwd = t_best(lambda: attn_bwd(qkv, o, lse, go, H), iters=10, rounds=3)
     t_bwd_lib = t_best(lambda: attn_bwd_library(qkv, o, lse, go, H), iters=10, rounds=3)
     print(json.dumps({"B": B, "T": T, "H": H, "D": 64, "fwd_us_ours": t_ours * 1e6,
@@ -48,6 +51,7 @@ for B, T, H in ((16, 1024, 12), (8, 2048, 12), (4, 4096, 16)):
                       "fwd_tflops_torch": fl / t_torch / 1e12,
                       "fwd_bwd_us_ours": t_fb_ours * 1e6, "fwd_bwd_us_torch": t_fb_torch * 1e6,
                       "bwd_us_ours": t_bwd * 1e6, "bwd_us_ours_concurrent": t_bwd_conc * 1e6,
+                      "bwd_us_ours_separate_delta": t_bwd_unfused * 1e6,
                       "bwd_us_library": t_bwd_lib * 1e6,
                       "bwd_tflops_ours": 2.5 * fl / t_bwd / 1e12}),
           flush=True)

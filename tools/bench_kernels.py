@@ -275,10 +275,10 @@ if "memroof" in which:
             y = torch.empty(n, device="cuda", dtype=dts[so])
             nb = n * (dts[si].itemsize + dts[so].itemsize)
             res = {}
-            for var in (0, 1, 2, 3, 4):
+            for var in (0, 1, 2, 3, 4, 5):
                 L.lib().dlbb_cast_set_variant(var)
                 res[f"v{var}"] = t_med(lambda: ops.cast(x, dts[so], out=y), iters=20)
-            L.lib().dlbb_cast_set_variant(1)
+            L.lib().dlbb_cast_set_variant(5)
             tt = t_med(lambda: y.copy_(x), iters=20)
             out(kernel="cast", src=si, dst=so, src_MiB=mib,
                 TBps={k: round(nb / v / 1e12, 3) for k, v in res.items()},
@@ -298,14 +298,17 @@ if "memroof" in which:
         flat = rnd(n)
         outs = [torch.empty(n // 8, device="cuda", dtype=torch.bfloat16) for _ in range(8)]
         tab = ChunkTable([(flat[i * (n // 8):(i + 1) * (n // 8)], outs[i]) for i in range(8)])
+        L.lib().dlbb_chunk_copy_set_nt(0)
         t = t_med(tab.run, iters=20)
         L.lib().dlbb_chunk_copy_set_nt(1)
         tnt = t_med(tab.run, iters=20)
-        L.lib().dlbb_chunk_copy_set_nt(0)
+        L.lib().dlbb_chunk_copy_set_nt(2)
+        tauto = t_med(tab.run, iters=20)
         tt = t_med(lambda: [o.copy_(flat[i * (n // 8):(i + 1) * (n // 8)])
                             for i, o in enumerate(outs)], iters=20)
         out(kernel="chunk_copy", src_MiB=mib, chunks=tab.nchunks,
             TBps=round(2 * n * 2 / t / 1e12, 3), nt_TBps=round(2 * n * 2 / tnt / 1e12, 3),
+            auto_TBps=round(2 * n * 2 / tauto / 1e12, 3),
             torch_8copies_TBps=round(2 * n * 2 / tt / 1e12, 3))
         g32 = torch.empty(n, device="cuda")
         st = ScaleTable([(flat, g32)], 0.125)
@@ -314,3 +317,25 @@ if "memroof" in which:
         srcs = [rnd(n // 8) for _ in range(8)]
         t = t_med(lambda: ops.reduce_sum(srcs), iters=20)
         out(kernel="reduce_sum_8src", src_MiB=mib, TBps=round(9 * (n // 8) * 2 / t / 1e12, 3))
+if "splitred" in which:
+    # the weight-gradient split-K reduce alone (fp32 slabs -> bf16 dW += sum, + bias slabs), by
+    # variant (0 round-4 8-float form, 1 all slabs in flight + nt loads, 2 all in flight, plain)
+    # at the GPT-2 dW shapes and the splits the step uses; bytes = slabs read + dW read + written
+    from distributed_llm_backend_benchmark_amd.ops import _lib as L
+    for N, K, splits in ((2304, 768, (8, 9)), (768, 768, (6, 16)), (3072, 768, (6, 7, 9)),
+                         (768, 3072, (6, 7))):
+        n, nb = N * K, N
+        for sp in splits:
+            ws = torch.randn(sp * (n + nb), device="cuda")
+            o = torch.zeros(n, device="cuda", dtype=torch.bfloat16)
+            ob = torch.zeros(nb, device="cuda", dtype=torch.bfloat16)
+            res = {}
+            for var in (0, 1, 2):
+                L.lib().dlbb_split_reduce_set_variant(var)
+                t = t_med(lambda: L.check(L.lib().dlbb_split_reduce(
+                    ws.data_ptr(), o.data_ptr(), 1, n, ob.data_ptr(), nb, sp, 1,
+                    L.stream(ws.device)), "split_reduce"), iters=50)
+                nbytes = sp * (n + nb) * 4 + 2 * (n + nb) * 2
+                res[f"v{var}"] = {"us": round(t * 1e6, 2), "TBps": round(nbytes / t / 1e12, 3)}
+            L.lib().dlbb_split_reduce_set_variant(2)
+            out(kernel="split_reduce", N=N, K=K, split=sp, res=res)
