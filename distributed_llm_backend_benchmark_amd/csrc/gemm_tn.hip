@@ -439,8 +439,12 @@ __global__ void __launch_bounds__(256) split_reduce8_kernel(const float* __restr
 }
 
 // split-reduce form (A/B: dlbb_split_reduce_set_variant): 0 = round-4 8-float form, 1 = all
-// slab loads in flight, non-temporal loads, 2 = all slab loads in flight, plain loads
-static int g_split_reduce_variant = 2;
+// slab loads in flight, non-temporal loads (default), 2 = all slab loads in flight, plain loads.
+// Isolated at the GPT-2 dW shapes all three run at 4.5-5.4 TB/s (11-18 us; v1 fastest by 2-5 %,
+// profiles/r05_kernels/split_reduce.jsonl): the 40-118 us seen inside the training step is
+// contention with the main stream's kernels, not the pass itself. The slabs are read once, so
+// v1's streaming loads also keep them from displacing the main stream's L2 lines.
+static int g_split_reduce_variant = 1;
 
 template <int DTO, bool NT>
 static void split_reduce_dispatch_v(const float* ws, void* out, int64_t n, void* outb, int64_t nb,
@@ -557,7 +561,7 @@ static int wgrad_launch(const void* A, int64_t lda, const void* B, int64_t ldb, 
 }
 
 DLBB_API void dlbb_split_reduce_set_variant(int v) {
-  tn::g_split_reduce_variant = v >= 0 && v <= 2 ? v : 2;
+  tn::g_split_reduce_variant = v >= 0 && v <= 2 ? v : 1;
 }
 
 // The weight-gradient split-K reduce alone (microbenchmarks): out[n] (+ outb[nb]) = sum of the

@@ -542,9 +542,19 @@ def get_custom_allreduce(comm: Comm, self_test: bool = True) -> Optional[CustomA
             inst = CustomAllReduce(comm, capacity_bytes=cap)
             if self_test:
                 inst.self_test()
-                if (comm.world_size > 1 and inst.healthy
+                # the calibration's reference leg is the process group's all-reduce: only an
+                # RCCL group gives the IPC-vs-RCCL crossover it is for. On a gloo group (ranks
+                # sharing one GPU: tests, rehearsals) that leg is a host-staged CPU all-reduce of
+                # up to 64 MiB x 20 iterations per rank — at 8 ranks 34.5 of a 38.8 s test
+                # (round-5 probe, tools/diag/ipc8_probe.py), and the silent minutes that got an
+                # 8-rank test killed in round 4 — and its crossovers would be meaningless
+                if (comm.world_size > 1 and inst.healthy and comm.backend == "nccl"
                         and os.environ.get("DLBB_CUSTOM_AR_CALIBRATE", "1") != "0"):
                     inst.calibrate()
+                elif comm.world_size > 1 and comm.backend != "nccl":
+                    inst.calibration = {"world": comm.world_size, "skipped":
+                                        f"process group is {comm.backend}, not RCCL: no "
+                                        "crossover to measure (default thresholds)"}
         except RuntimeError as e:   # agreed on all ranks: fall back to RCCL everywhere
             if comm.rank == 0:
                 print(f"[custom all-reduce disabled] {e}", flush=True)

@@ -16,19 +16,17 @@ def _entry(rank, world, port, fn, args, q):
         q.put((rank, "err", f"{type(e).__name__}: {e}\n{traceback.format_exc()}"))
 
 
-def run_multiprocess(fn, world, args=(), timeout=240, hw_queues="auto"):
+def run_multiprocess(fn, world, args=(), timeout=240, hw_queues=None):
     """Run ``fn(rank, world, *args)`` in ``world`` spawned processes; returns results by rank.
-    ``hw_queues``: "auto" = the 8+-rank queue cap below, None = inherit the environment."""
+    ``hw_queues``: None = inherit the environment (HIP's default 4 hardware queues per process);
+    "auto" = the round-4 cap of 2 queues per rank at 8+ ranks (kept only for A/B runs: the
+    8-rank slowness it was added for was the gloo-leg calibration, see custom_allreduce)."""
     from conftest import free_port
 
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = free_port()
     procs = [ctx.Process(target=_entry, args=(r, world, port, fn, args, q)) for r in range(world)]
-    # 8+ ranks sharing one GPU: at HIP's default 4 hardware queues per process the ranks' queues
-    # oversubscribe the scheduler, and a rank's spinning IPC kernel can sit in an unmapped queue
-    # until a time slice comes round (one such run stalled past the box's silence limit) —
-    # 2 queues per rank keep all ranks' queues mapped (children inherit the environment)
     old_q = os.environ.get("GPU_MAX_HW_QUEUES")
     cap = hw_queues == "auto" and world >= 8 and old_q is None
     if cap:

@@ -337,5 +337,28 @@ if "splitred" in which:
                     L.stream(ws.device)), "split_reduce"), iters=50)
                 nbytes = sp * (n + nb) * 4 + 2 * (n + nb) * 2
                 res[f"v{var}"] = {"us": round(t * 1e6, 2), "TBps": round(nbytes / t / 1e12, 3)}
-            L.lib().dlbb_split_reduce_set_variant(2)
+            L.lib().dlbb_split_reduce_set_variant(1)
             out(kernel="split_reduce", N=N, K=K, split=sp, res=res)
+if "wgradstages" in which:
+    # weight-gradient LDS ring depth (2 / 3 stages) x split at the GPT-2 dW shapes, whole call
+    # (GEMM + reduce, fused bias, accumulate): the asm transposed reads keep the DMA prefetch in
+    # flight, so a deeper ring can now pay
+    from distributed_llm_backend_benchmark_amd.ops import _lib as L
+    from distributed_llm_backend_benchmark_amd.ops.gemm import _wgrad_hip, _wgrad_hip256
+    for N, K in ((2304, 768), (768, 768), (3072, 768), (768, 3072)):
+        M = 16384
+        dy, x = rnd(M, N), rnd(M, K)
+        w_out, b_out = torch.zeros(N, K, device="cuda", dtype=torch.bfloat16), \
+            torch.zeros(N, device="cuda", dtype=torch.bfloat16)
+        res = {}
+        for nb in (2, 3):
+            L.lib().dlbb_gemm_wgrad_set_stages(nb)
+            for sp in (None, 4, 6, 8, 12):
+                res[f"t128_nb{nb}_s{sp}"] = round(t_med(
+                    lambda: _wgrad_hip(dy, x, w_out, True, sp, b_out), iters=30) * 1e6, 1)
+                if N % 256 == 0:
+                    res[f"t256_nb{nb}_s{sp}"] = round(t_med(
+                        lambda: _wgrad_hip256(dy, x, w_out, True, sp, b_out), iters=30) * 1e6, 1)
+        L.lib().dlbb_gemm_wgrad_set_stages(2)
+        best = min(res, key=res.get)
+        out(kernel="wgrad_stages", M=M, N=N, K=K, best=best, us=res)

@@ -1,0 +1,74 @@
+"""Diagnostic: does HIP-graph replay run the parallel branches of a captured
+fork / join concurrently? Two independent chains of spin kernels (``torch.cuda._sleep``), one on
+the current stream and one on a side stream forked / joined by events — the pattern of the
+DDP step's side-stream weight gradients — timed eager and as one replayed graph. Concurrent
+branches take ~one chain's time, serialised branches ~two. Also the same with two streams of
+small GEMM chains (work that occupies only part of the GPU, like the wgrad kernels).
+
+Prints one JSON line: eager / graph ms for both workloads, the ratio to one chain's time, and the
+HIP graph env knobs in force (DEBUG_HIP_FORCE_GRAPH_QUEUES, DEBUG_CLR_GRAPH_PACKET_CAPTURE).
+"""
+import json
+import os
+
+import torch
+
+
+def timed(fn, iters=10):
+    fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    e.synchronize()
+    return s.elapsed_time(e) / iters
+
+
+def main():
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    side = torch.cuda.Stream(dev)
+    out = {"env": {k: os.environ.get(k) for k in ("DEBUG_HIP_FORCE_GRAPH_QUEUES",
+                                                   "DEBUG_CLR_GRAPH_PACKET_CAPTURE",
+                                                   "GPU_MAX_HW_QUEUES")}}
+    a = torch.randn(2048, 2048, device=dev, dtype=torch.bfloat16)
+    b = torch.randn(2048, 2048, device=dev, dtype=torch.bfloat16)
+    c1 = torch.empty_like(a)
+    c2 = torch.empty_like(a)
+    cyc = 200_000
+    work = {"sleep": (lambda: torch.cuda._sleep(cyc), lambda: torch.cuda._sleep(cyc)),
+            "gemm": (lambda: torch.matmul(a, b, out=c1), lambda: torch.matmul(b, a, out=c2))}
+    for name, (w1, w2) in work.items():
+        n = 8
+        one = timed(lambda: [w1() for _ in range(n)])
+
+        def step():
+            cur = torch.cuda.current_stream()
+            side.wait_stream(cur)
+            for _ in range(n):
+                w1()
+            with torch.cuda.stream(side):
+                for _ in range(n):
+                    w2()
+            cur.wait_stream(side)
+        eager = timed(step)
+        cap = torch.cuda.Stream(dev)
+        cap.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(cap):
+            step()
+        torch.cuda.current_stream().wait_stream(cap)
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            step()
+        graph = timed(g.replay)
+        out[name] = {"one_chain_ms": round(one, 4), "eager_ms": round(eager, 4),
+                     "graph_ms": round(graph, 4), "eager_over_one": round(eager / one, 3),
+                     "graph_over_one": round(graph / one, 3)}
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()
