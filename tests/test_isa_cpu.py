@@ -48,3 +48,34 @@ _Z1kv:                                  ; @_Z1kv
     rep = isa_check.check_asm(asm)["_Z1kv"]
     assert rep["tr_reads"] == 1
     assert len(rep["violations"]) == 1 and "v4" in rep["violations"][0][1]
+
+
+def test_compiler_drains_lds_dma_before_builtin_transposed_read():
+    """The reason for the asm reads, pinned: with the builtin the compiler waits vmcnt(0) for
+    the other buffer's LDS-DMA before the read; a plain LDS load and the asm read do not wait
+    (tools/diag/lds_dma_wait.hip). If a future compiler stops doing it, this test says so."""
+    import re
+
+    import isa_check
+
+    asm = isa_check.device_asm(os.path.join(REPO, "tools", "diag", "lds_dma_wait.hip"))
+    funcs = {}
+    cur = None
+    for line in asm.split("\n"):
+        m = re.match(r"^(k_\w+):", line)
+        if m:
+            cur = m.group(1)
+            funcs[cur] = []
+        elif cur:
+            funcs[cur].append(line.strip())
+
+    def vmcnt0_before_lds_read(lines):
+        for i, s in enumerate(lines):
+            if s.startswith("ds_read"):
+                prev = [x for x in lines[max(0, i - 3):i] if x.startswith("s_waitcnt")]
+                return any("vmcnt(0)" in x for x in prev)
+        raise AssertionError("no LDS read found")
+
+    assert vmcnt0_before_lds_read(funcs["k_builtin"])
+    assert not vmcnt0_before_lds_read(funcs["k_plain"])
+    assert not vmcnt0_before_lds_read(funcs["k_asm"])
