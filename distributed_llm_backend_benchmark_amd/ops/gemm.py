@@ -49,7 +49,7 @@ def set_tune_agreement(fn) -> None:
 # timings of different kernels
 _AGREED_ENV = ("DLBB_GEMM", "DLBB_TUNE_TIMING", "DLBB_WGRAD256", "DLBB_PP_TAIL",
                "DLBB_WGRAD_FUSED", "DLBB_GEMM_PERSIST", "DLBB_GEMM_PERSIST_EPI",
-               "DLBB_WGRAD_STREAM")
+               "DLBB_WGRAD_STREAM", "DLBB_WGRAD_SLOTS")
 
 
 def _agree_names(kind: str, key, names) -> list:
@@ -492,6 +492,7 @@ def wgrad_supported(dy2: torch.Tensor, x2: torch.Tensor) -> bool:
 
 
 _COUNTERS = {}   # (device index, stream handle) -> int32 tile counters, zero between launches
+_WGRAD_SLOTS_SCALE = float(os.environ.get("DLBB_WGRAD_SLOTS", "1.0"))
 
 
 def wgrad_fused_reduce() -> bool:
@@ -526,8 +527,13 @@ def _wgrad_hip(dy2, x2, out, accumulate, split=None, bias_out=None, bn=128, bk=1
         # (profiles/r01_gpt2/wgrad_split_xcd.jsonl)
         # (two-per-CU tiles: at most the 512 resident slots — a 2nd partial round costs a
         # whole workgroup time)
-        split = max(1, min(M // 256, (-(-768 // tiles)) if bn == bk == 128
-                           else max(1, 512 // tiles)))
+        # DLBB_WGRAD_SLOTS scales the workgroup budget (A/B: the weight gradients run on the
+        # side stream beside the main stream's kernels, where fewer, longer workgroups may
+        # leave more of the GPU to the critical path; round-5 asm reads made long K-loops
+        # 25-30 % cheaper per workgroup)
+        slots = _WGRAD_SLOTS_SCALE
+        split = max(1, min(M // 256, (-(-int(768 * slots) // tiles)) if bn == bk == 128
+                           else max(1, int(512 * slots) // tiles)))
     # one split, plain store, no bias: the kernel stores dW itself (no fp32 partials, no
     # reduce pass — the LM-head dW)
     direct = split == 1 and not accumulate and bias_out is None

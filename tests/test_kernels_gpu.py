@@ -1066,3 +1066,35 @@ def test_gemm_nt_192_spread_matches_fp32(M, N, K, early, bal):
     torch.testing.assert_close(y.float(), x.float() @ w.float().t(), rtol=2e-2,
                                atol=2e-2 * K ** 0.5)
     assert torch.equal(y, y1)
+
+
+@pytest.mark.parametrize("variant", [0, 1, 2])
+@pytest.mark.parametrize("split", [1, 3, 7, 9, 16, 19])
+@pytest.mark.parametrize("dt_out", ["bf16", "fp32"])
+def test_split_reduce_variants_match_fp32(variant, split, dt_out):
+    """The weight-gradient split-K reduce (every form: round-4 8-float loop, all slabs in flight
+    with streaming / plain loads; templated splits and the runtime-split fallback) against an
+    fp32 sum of the slabs, accumulating into an existing output, with the bias slabs."""
+    from distributed_llm_backend_benchmark_amd.ops import _lib
+
+    N, K = 384, 256
+    n, nb = N * K, N
+    g = torch.Generator(device=DEV).manual_seed(split)
+    ws = torch.randn(split * (n + nb), device=DEV, generator=g)
+    dt = torch.bfloat16 if dt_out == "bf16" else torch.float32
+    o = torch.randn(n, device=DEV, generator=g).to(dt)
+    ob = torch.randn(nb, device=DEV, generator=g).to(dt)
+    ref = ws[:split * n].view(split, n).sum(0) + o.float()
+    refb = ws[split * n:].view(split, nb).sum(0) + ob.float()
+    _lib.lib().dlbb_split_reduce_set_variant(variant)
+    try:
+        _lib.check(_lib.lib().dlbb_split_reduce(ws.data_ptr(), o.data_ptr(),
+                                                1 if dt_out == "bf16" else 0, n, ob.data_ptr(),
+                                                nb, split, 1, _lib.stream(ws.device)),
+                   "split_reduce")
+        torch.cuda.synchronize()
+    finally:
+        _lib.lib().dlbb_split_reduce_set_variant(1)
+    tol = dict(rtol=1e-2, atol=1e-2) if dt_out == "bf16" else dict(rtol=1e-5, atol=1e-4)
+    torch.testing.assert_close(o.float(), ref, **tol)
+    torch.testing.assert_close(ob.float(), refb, **tol)

@@ -42,3 +42,18 @@ s=$(date +%s)
 step bench 900 python -u bench.py
 echo "bench wall $(( $(date +%s) - s )) s"
 tail -1 $O/bench.log | cut -c1-600
+# attention: software-pipelined operand reads (ab/attn_pipe: forward V^T groups, dQ K^T pairs)
+# vs the tree's kernels, interleaved, and the variant's kernel tests
+step attn_base 300 python -u tools/attn_bench.py
+(cd ab/attn_pipe && PYTHONPATH=$R/ab/attn_pipe timeout -k 10 300 python -u tools/attn_bench.py > $O/attn_pipe.log 2>&1) && echo "attn_pipe ok"
+step attn_base2 300 python -u tools/attn_bench.py
+(cd ab/attn_pipe && PYTHONPATH=$R/ab/attn_pipe timeout -k 10 300 python -u tools/attn_bench.py > $O/attn_pipe2.log 2>&1) && echo "attn_pipe2 ok"
+(cd ab/attn_pipe && PYTHONPATH=$R/ab/attn_pipe timeout -k 10 300 python -u -m pytest -x -q --timeout 120 -p no:cacheprovider tests/test_attention_gpu.py > $O/attn_pipe_tests.log 2>&1); echo "attn_pipe tests rc=$?"
+# weight-gradient workgroup budget on the side stream (DLBB_WGRAD_SLOTS scale), GPT-2 step
+for rep in a b; do
+  for sl in 1.0 0.5 0.33; do
+    run=slots${sl}_$rep
+    step gpt2_$run 300 env DLBB_WGRAD_SLOTS=$sl $T --output $O/gpt2_$run.json
+    python -c "import json; d=json.load(open('$O/gpt2_$run.json')); print('RESULT $run', round(d['ms_per_step'],3), d['loss'])"
+  done
+done
