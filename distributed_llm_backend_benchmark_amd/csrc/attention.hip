@@ -203,28 +203,31 @@ __global__ void __launch_bounds__(kAttnThreads, 2) attn_fwd_d64_kernel(AttnArgs 
       for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
         for (int st = 0; st < 2; ++st) {
-          // V^T fragments by asm transposed reads (common.h ds_read_tr16: the builtin made the
-          // compiler drain the next tile's DMA here), waited for before their MFMAs
-          bf16x8 vf[2];
+          bf16x8 pf;
 #pragma unroll
-          for (int dt = 0; dt < 2; ++dt)
+          for (int j = 0; j < 8; ++j)
+            pf[j] = __builtin_bit_cast(short, static_cast<__bf16>(s[kk][8 * st + j]));
+#pragma unroll
+          for (int dt = 0; dt < 2; ++dt) {
+            bf16x8 vf;
 #pragma unroll
             for (int half = 0; half < 2; ++half) {
               const int row = kk * 32 + 16 * st + 8 * half + 4 * (g >> 1) + tq;
               const int col = dt * 32 + 16 * (g & 1) + 4 * tp;
               const int off = row * 128 + (((col >> 3) ^ vswz(row)) << 4) + (col & 7) * 2;
-              const i16x4 t = ds_read_tr16(tv + off);
+              // builtin read, kept on purpose: the compiler drains the next tile's K/V DMA
+              // (vmcnt(0)) before the first of these, but that DMA has had the S MFMAs and the
+              // softmax to land, and the builtin lets it interleave the reads with the MFMAs
+              // under counted lgkmcnt waits. The asm form (common.h ds_read_tr16, grouped
+              // waits; also software-pipelined) measured 3-4 % SLOWER here (61-62 vs 58-60 us
+              // at the GPT-2 shape, profiles/r05_attention/), unlike dQ / dK/dV where the
+              // drain sat right behind the DMA issue. tools/isa_check.py allows this kernel.
+              const i16x4 t = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4_ptr)(tv + off));
 #pragma unroll
-              for (int u = 0; u < 4; ++u) vf[dt][4 * half + u] = t[u];
+              for (int u = 0; u < 4; ++u) vf[4 * half + u] = t[u];
             }
-          bf16x8 pf;
-#pragma unroll
-          for (int j = 0; j < 8; ++j)
-            pf[j] = __builtin_bit_cast(short, static_cast<__bf16>(s[kk][8 * st + j]));
-          tr_wait(vf[0], vf[1]);
-#pragma unroll
-          for (int dt = 0; dt < 2; ++dt)
-            o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[dt], pf, o[dt], 0, 0, 0);
+            o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf, o[dt], 0, 0, 0);
+          }
         }
     }
   }

@@ -562,8 +562,13 @@ class FlatParamTrainer:
         cur.wait_stream(side)
         torch.cuda.synchronize(dev)
         graph = torch.cuda.CUDAGraph()
+        dot = os.environ.get("DLBB_GRAPH_DOT")   # diagnostics: dump the captured topology
+        if dot:
+            graph.enable_debug_mode()
         with torch.cuda.graph(graph, capture_error_mode="thread_local"):
             static_loss = self.step(static_idx, static_tgt, sync_loss=False)
+        if dot:
+            graph.debug_dump(dot)
         # capture recorded the step without running it: undo the host-side bookkeeping
         self.step_count -= 1
         self.opt.t -= 1

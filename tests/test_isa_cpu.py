@@ -26,8 +26,12 @@ def test_asm_lds_reads_are_waited_for(src):
     bad = {k: r["violations"][:3] for k, r in rep.items() if r["violations"]}
     assert not bad, bad
     drains = {k: r["vmcnt0_before_lds_read"] for k, r in rep.items()
-              if r["vmcnt0_before_lds_read"]}
+              if r["vmcnt0_before_lds_read"] and not any(a in k for a in ALLOWED_DRAINS)}
     assert not drains, drains
+
+
+# kernels that keep the builtin transposed read on purpose (measured faster, see the source)
+ALLOWED_DRAINS = ("attn_fwd_d64_kernel",)
 
 
 def test_checker_flags_an_early_use():

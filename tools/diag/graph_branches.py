@@ -67,6 +67,35 @@ def main():
         out[name] = {"one_chain_ms": round(one, 4), "eager_ms": round(eager, 4),
                      "graph_ms": round(graph, 4), "eager_over_one": round(eager / one, 3),
                      "graph_over_one": round(graph / one, 3)}
+    # the DDP backward's pattern: every "layer" forks a side-stream kernel off the main chain
+    # mid-graph (side.wait_stream(main) before each), one join at the end
+    for name, (w1, w2) in work.items():
+        L = 8
+
+        def layers():
+            cur = torch.cuda.current_stream()
+            for _ in range(L):
+                w1()
+                side.wait_stream(cur)
+                with torch.cuda.stream(side):
+                    w2()
+            cur.wait_stream(side)
+        one = timed(lambda: [w1() for _ in range(L)])
+        eager = timed(layers)
+        cap = torch.cuda.Stream(dev)
+        cap.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(cap):
+            layers()
+        torch.cuda.current_stream().wait_stream(cap)
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            layers()
+        graph = timed(g.replay)
+        out[name + "_midgraph_forks"] = {"one_chain_ms": round(one, 4), "eager_ms": round(eager, 4),
+                                         "graph_ms": round(graph, 4),
+                                         "eager_over_one": round(eager / one, 3),
+                                         "graph_over_one": round(graph / one, 3)}
     print(json.dumps(out), flush=True)
 
 

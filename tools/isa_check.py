@@ -9,8 +9,8 @@ kernel, all three attention kernels; found in round 5 by reading the ISA). The a
 invisible to that pass, so the compiler also never waits for its RESULT: the kernels wait
 ``lgkmcnt(0)`` themselves before any use. This tool checks that on the compiled code.
 
-Check, per kernel, over the device assembly in program order: after a ``ds_read_b64_tr_b16`` or
-any LDS read written as inline asm (``ds_read_b128_asm``), its destination registers are PENDING until an ``s_waitcnt`` with ``lgkmcnt(0)`` (counted
+Check, per kernel, over the device assembly in program order: after any LDS read written as
+inline asm (``ds_read_tr16``, ``ds_read_b128_asm``), its destination registers are PENDING until an ``s_waitcnt`` with ``lgkmcnt(0)`` (counted
 ``lgkmcnt(N)`` waits do not clear: the compiler cannot have counted the asm reads). Any other
 instruction that reads or writes a pending register is a violation (a use of data that may not
 have landed, or a write the late LDS return would overwrite). Also reports, per kernel, every
@@ -100,7 +100,7 @@ def check_asm(text: str) -> Dict[str, Dict]:
                         res[kern]["vmcnt0_before_lds_read"] += 1
                         break
             continue
-        if op.startswith("ds_read") and (in_asm or op.startswith("ds_read_b64_tr_b16")):
+        if op.startswith("ds_read") and in_asm:   # builtin reads: the compiler counts them
             parts = s[len(op):].split(",")
             dst = regs(parts[0])
             src = regs(",".join(parts[1:]))
