@@ -23,16 +23,22 @@ def _randn(*shape, dtype=torch.bfloat16, seed=0, scale=1.0):
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16, torch.float32])
-@pytest.mark.parametrize("nsrc", [1, 2, 8, 16])
+@pytest.mark.parametrize("nsrc", [1, 2, 3, 4, 5, 8, 16])
 @pytest.mark.parametrize("n", [7, 4096, 1000003])
-def test_reduce_sum(dtype, nsrc, n):
-    from distributed_llm_backend_benchmark_amd.ops import reduce_sum
+@pytest.mark.parametrize("variant", [0, 1])
+def test_reduce_sum(dtype, nsrc, n, variant):
+    """Both forms (templated source counts 2/3/4/8 with every load in flight; runtime loop)."""
+    from distributed_llm_backend_benchmark_amd.ops import _lib, reduce_sum
 
     srcs = [_randn(n, dtype=dtype, seed=i) for i in range(nsrc)]
     ref = sum(s.float() for s in srcs) * 0.5
-    out = reduce_sum(srcs, out_dtype=torch.float32, scale=0.5)
-    torch.testing.assert_close(out, ref, rtol=1e-5, atol=1e-5)
-    out2 = reduce_sum(srcs, scale=0.5)
+    _lib.lib().dlbb_reduce_set_variant(variant)
+    try:
+        out = reduce_sum(srcs, out_dtype=torch.float32, scale=0.5)
+        torch.testing.assert_close(out, ref, rtol=1e-5, atol=1e-5)
+        out2 = reduce_sum(srcs, scale=0.5)
+    finally:
+        _lib.lib().dlbb_reduce_set_variant(1)
     tol = 1e-2 if dtype != torch.float32 else 1e-5
     torch.testing.assert_close(out2.float(), ref, rtol=tol, atol=tol * nsrc)
 

@@ -96,6 +96,39 @@ def main():
                                          "graph_ms": round(graph, 4),
                                          "eager_over_one": round(eager / one, 3),
                                          "graph_over_one": round(graph / one, 3)}
+    # the same with the side kernels dealt round-robin over k side streams: a side node then
+    # depends on the main chain and on the side node k layers back, not the one just before
+    sides = [side] + [torch.cuda.Stream(dev) for _ in range(3)]
+    for k in (2, 4):
+        for name, (w1, w2) in work.items():
+            L = 8
+
+            def layers_rr():
+                cur = torch.cuda.current_stream()
+                for i in range(L):
+                    w1()
+                    sd = sides[i % k]
+                    sd.wait_stream(cur)
+                    with torch.cuda.stream(sd):
+                        w2()
+                for sd in sides[:k]:
+                    cur.wait_stream(sd)
+            one = timed(lambda: [w1() for _ in range(L)])
+            eager = timed(layers_rr)
+            cap = torch.cuda.Stream(dev)
+            cap.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(cap):
+                layers_rr()
+            torch.cuda.current_stream().wait_stream(cap)
+            torch.cuda.synchronize()
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                layers_rr()
+            graph = timed(g.replay)
+            out[f"{name}_midgraph_forks_rr{k}"] = {
+                "one_chain_ms": round(one, 4), "eager_ms": round(eager, 4),
+                "graph_ms": round(graph, 4), "eager_over_one": round(eager / one, 3),
+                "graph_over_one": round(graph / one, 3)}
     print(json.dumps(out), flush=True)
 
 
