@@ -51,6 +51,9 @@ _GRAD_SINKS = os.environ.get("DLBB_GRAD_SINKS", "1") != "0"   # A/B switch for t
 # 18.90 ms, and 19.17 -> 18.58 ms with the interleaved autotune timing
 # (profiles/r03_lean/tune_ab)
 _WGRAD_STREAM = os.environ.get("DLBB_WGRAD_STREAM", "1") == "1"
+# number of side streams the weight gradients are dealt over, round-robin by parameter (A/B;
+# with k > 1 a weight-gradient kernel depends only on its dY and on the one k layers back)
+_WGRAD_STREAMS = max(1, int(os.environ.get("DLBB_WGRAD_STREAMS", "1")))
 # priority of the dedicated bucket-reduction stream: 0 = normal (default, measured), -1 = high
 # (A/B knob; see the module docstring and profiles/r02_overlap/SUMMARY.md)
 _COMM_PRIORITY = int(os.environ.get("DLBB_COMM_STREAM_PRIORITY", "0"))
@@ -158,6 +161,10 @@ class FlatParamTrainer:
         self._wgrad_stream = (concurrent_stream(dev, "ddp_wgrad")
                               if mode == "view" and dev.type == "cuda" and _GRAD_SINKS
                               and _WGRAD_STREAM else None)
+        self._wgrad_streams = ([self._wgrad_stream] + [concurrent_stream(dev, f"ddp_wgrad{i}")
+                                                       for i in range(1, _WGRAD_STREAMS)]
+                               if self._wgrad_stream is not None else [])
+        n_sink = 0
         if mode == "view":
             for p, o in zip(order, offs):
                 p.grad = self.flat_grad[o:o + p.numel()].view_as(p)
@@ -169,7 +176,9 @@ class FlatParamTrainer:
                         or getattr(p, "_dlbb_sink_uses", 0) > 0) and _GRAD_SINKS:
                     p._dlbb_grad_sink = self._on_grad
                     if self._wgrad_stream is not None:
-                        p._dlbb_grad_stream = self._wgrad_stream
+                        p._dlbb_grad_stream = self._wgrad_streams[n_sink % len(
+                            self._wgrad_streams)]
+                        n_sink += 1
         self._hooks = [p.register_post_accumulate_grad_hook(self._on_grad) for p in order]
         self._next = 0
         self._seen = set()
@@ -372,7 +381,7 @@ class FlatParamTrainer:
             cs = self._comm_stream
             cs.wait_stream(torch.cuda.current_stream(buf.device))
             if ws is not None:
-                cs.wait_stream(ws)
+                self._wait_wgrad(cs)
             with torch.cuda.stream(cs):
                 self._tl_mark(b, "start", cs)
                 self._car.all_reduce_registered(buf, self._bucket_reg[b.idx],
@@ -385,7 +394,7 @@ class FlatParamTrainer:
             cs = self._comm_stream
             cs.wait_stream(torch.cuda.current_stream(buf.device))
             if ws is not None:
-                cs.wait_stream(ws)
+                self._wait_wgrad(cs)
             with torch.cuda.stream(cs):
                 self._tl_mark(b, "start", cs)
                 self._car.all_reduce_(buf, nblocks=self.comm_blocks)
@@ -398,7 +407,7 @@ class FlatParamTrainer:
             cs = self._comm_stream
             cs.wait_stream(torch.cuda.current_stream(buf.device))
             if ws is not None:
-                cs.wait_stream(ws)
+                self._wait_wgrad(cs)
             self._tl_mark(b, "start", cs)
             self._native.enqueue("allreduce", buf, buf, buf.numel(), stream=cs.cuda_stream)
             self._tl_mark(b, "end", cs)
@@ -408,10 +417,17 @@ class FlatParamTrainer:
             # ProcessGroupNCCL orders its stream after the CURRENT stream: issue from the side
             # stream once it has joined the main one (covers both producers)
             ws.wait_stream(torch.cuda.current_stream(buf.device))
+            for other in self._wgrad_streams[1:]:
+                ws.wait_stream(other)
             with torch.cuda.stream(ws):
                 b.work = dist.all_reduce(buf, async_op=True)
         else:
             b.work = dist.all_reduce(buf, async_op=True)
+
+    def _wait_wgrad(self, stream) -> None:
+        """Order ``stream`` after every weight-gradient side stream."""
+        for ws in self._wgrad_streams:
+            stream.wait_stream(ws)
 
     def _mark_done(self, b: _Bucket, cs) -> None:
         """Per-bucket completion event on the comm stream (waited per bucket by the split
@@ -449,7 +465,7 @@ class FlatParamTrainer:
         for b in self.buckets:
             self._wait_bucket(b)
         if self._wgrad_stream is not None:      # side-stream weight gradients (and copies)
-            torch.cuda.current_stream(self.flat_grad.device).wait_stream(self._wgrad_stream)
+            self._wait_wgrad(torch.cuda.current_stream(self.flat_grad.device))
 
     def check_comm_errors(self) -> None:
         """Collective: raise on every rank if an IPC all-reduce of any rank timed out since the
@@ -491,8 +507,7 @@ class FlatParamTrainer:
                 for b in head:
                     self._wait_bucket(b)
                 if self._wgrad_stream is not None:
-                    torch.cuda.current_stream(self.flat_grad.device).wait_stream(
-                        self._wgrad_stream)
+                    self._wait_wgrad(torch.cuda.current_stream(self.flat_grad.device))
                 self._optimizer_step(ranges=[(0, tail.start)], advance=True)
                 self._wait_bucket(tail)
                 self._optimizer_step(ranges=[(tail.start, self.numel)], advance=False)

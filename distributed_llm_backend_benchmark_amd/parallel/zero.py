@@ -70,6 +70,8 @@ class ShardedTrainer(FlatParamTrainer):
             # bucket complete on main AND side stream (sink weight gradients): issue from the
             # side stream after it joined the main one; finish() joins it back
             ws.wait_stream(torch.cuda.current_stream(out.device))
+            for other in self._wgrad_streams[1:]:
+                ws.wait_stream(other)
         with torch.cuda.stream(ws) if ws is not None else contextlib.nullcontext():
             if self.world == 1:
                 out.copy_(self.flat_grad[b.start:b.end])
