@@ -15,7 +15,7 @@ step() {  # step <name> <timeout> <cmd...>
   if [ $rc -ne 0 ]; then exit $rc; fi
 }
 step tests 600 python -u -m pytest -x -q --timeout 200 --timeout-method thread -p no:cacheprovider \
-  tests/test_kernels_gpu.py -k "reduce" tests/test_ddp_gpu.py
+  tests/test_kernels_gpu.py tests/test_comm_gpu.py -k "reduce or ddp or graph or capture"
 step gb 180 python -u tools/diag/graph_branches.py
 T="python -u -m distributed_llm_backend_benchmark_amd.cli.train_ddp --steps 30 --warmup 5"
 for rep in a b; do
