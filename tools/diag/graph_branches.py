@@ -129,6 +129,40 @@ def main():
                 "one_chain_ms": round(one, 4), "eager_ms": round(eager, 4),
                 "graph_ms": round(graph, 4), "eager_over_one": round(eager / one, 3),
                 "graph_over_one": round(graph / one, 3)}
+    # does one memcpy / memset node anywhere in the graph change how its branches run? (the
+    # GPT-2 step's graph holds D2D copies and fills besides kernels)
+    src_buf = torch.randn(1 << 20, device=dev)
+    dst_buf = torch.empty_like(src_buf)
+    for extra in ("memcpy", "memset"):
+        def forks_extra():
+            cur = torch.cuda.current_stream()
+            if extra == "memcpy":
+                dst_buf.copy_(src_buf)                 # hipMemcpyAsync D2D -> memcpy node
+            else:
+                torch.cuda.current_stream()            # noqa
+                dst_buf.zero_()                        # fill (kernel or memset node)
+            side.wait_stream(cur)
+            for _ in range(8):
+                torch.cuda._sleep(cyc)
+            with torch.cuda.stream(side):
+                for _ in range(8):
+                    torch.cuda._sleep(cyc)
+            cur.wait_stream(side)
+        one = timed(lambda: [torch.cuda._sleep(cyc) for _ in range(8)])
+        eager = timed(forks_extra)
+        cap = torch.cuda.Stream(dev)
+        cap.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(cap):
+            forks_extra()
+        torch.cuda.current_stream().wait_stream(cap)
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            forks_extra()
+        graph = timed(g.replay)
+        out[f"sleep_forks_with_{extra}"] = {
+            "one_chain_ms": round(one, 4), "eager_ms": round(eager, 4), "graph_ms": round(graph, 4),
+            "eager_over_one": round(eager / one, 3), "graph_over_one": round(graph / one, 3)}
     print(json.dumps(out), flush=True)
 
 
