@@ -17,6 +17,8 @@
 // GPT-2 step (profiles/r01_gpt2/gpt2_step_timeline_787k.txt).
 #include "common.h"
 
+#include <rocprim/block/block_radix_sort.hpp>
+
 namespace dlbb {
 
 constexpr int kEmbThreads = 64;   // one wave per row: C / 8 vectors strided over the lanes
@@ -85,6 +87,39 @@ __global__ void __launch_bounds__(kEmbThreads) emb_bwd_kernel(
   }
 }
 
+// Stable sort of the token ids for the embedding backward, in ONE workgroup (the ids are at
+// most kSortMax and the vocabulary below 2^18): key and position packed into one 32-bit word
+// (id << 14 | position), the blocked layout already in position order, so a radix sort on the
+// id bits alone is the stable sort. Replaces torch.sort (a device memcpy of the keys plus
+// several rocPRIM launches, 50 us per GPT-2 step) with one launch of pure kernel work — the
+// memcpy was the only non-kernel node in the captured training step.
+constexpr int kSortThreads = 1024, kSortItems = 16, kSortMax = kSortThreads * kSortItems;
+constexpr int kSortPosBits = 14;                         // 2^14 = kSortMax
+
+__global__ void __launch_bounds__(kSortThreads) sort_ids_kernel(const int64_t* __restrict__ ids,
+                                                                int64_t* __restrict__ sorted,
+                                                                int64_t* __restrict__ order,
+                                                                int n, int key_bits) {
+  using Sort = rocprim::block_radix_sort<uint32_t, kSortThreads, kSortItems>;
+  __shared__ typename Sort::storage_type storage;
+  uint32_t k[kSortItems];
+#pragma unroll
+  for (int j = 0; j < kSortItems; ++j) {
+    const int i = threadIdx.x * kSortItems + j;           // blocked: position order
+    k[j] = i < n ? (static_cast<uint32_t>(ids[i]) << kSortPosBits) | static_cast<uint32_t>(i)
+                 : 0xFFFFFFFFu;
+  }
+  Sort().sort(k, storage, kSortPosBits, kSortPosBits + key_bits);
+#pragma unroll
+  for (int j = 0; j < kSortItems; ++j) {
+    const int i = threadIdx.x * kSortItems + j;
+    if (i < n) {
+      sorted[i] = static_cast<int64_t>(k[j] >> kSortPosBits);
+      order[i] = static_cast<int64_t>(k[j] & ((1u << kSortPosBits) - 1));
+    }
+  }
+}
+
 }  // namespace dlbb
 
 using namespace dlbb;
@@ -124,5 +159,18 @@ DLBB_API int dlbb_embedding_bwd(const int64_t* sorted_ids, const int64_t* order,
                        order, d, wte_grad, wpe_grad, N, T, C, V);
   else
     return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
+// sorted / order (int64, n each) = the stable ascending sort of ids and the positions it took.
+// hipErrorNotSupported when n > 16384 or vocab > 2^18 (the caller falls back to a library sort).
+DLBB_API int dlbb_sort_ids(const int64_t* ids, int64_t* sorted, int64_t* order, int64_t n,
+                           int vocab, hipStream_t stream) {
+  if (n <= 0) return hipSuccess;
+  if (n > kSortMax || vocab <= 0 || vocab > (1 << 18)) return hipErrorNotSupported;
+  int bits = 1;
+  while ((1 << bits) < vocab) ++bits;
+  hipLaunchKernelGGL(sort_ids_kernel, dim3(1), dim3(kSortThreads), 0, stream, ids, sorted, order,
+                     static_cast<int>(n), bits);
   return hipGetLastError();
 }

@@ -118,6 +118,7 @@ _SIGS = {
     "dlbb_gemm_wgrad_set_order": (None, [c_int]),
     "dlbb_split_reduce_set_variant": (None, [c_int]),
     "dlbb_reduce_set_variant": (None, [c_int]),
+    "dlbb_sort_ids": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int, c_void_p]),
     "dlbb_attn_set_fuse_delta": (None, [c_int]),
     "dlbb_split_reduce": (c_int, [c_void_p, c_void_p, c_int, c_int64, c_void_p, c_int64, c_int,
                                   c_int, c_void_p]),

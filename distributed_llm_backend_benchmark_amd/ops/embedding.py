@@ -64,7 +64,7 @@ class _EmbeddingFn(torch.autograd.Function):
             else [(ge, None), (None, gp)]
         sorted_ids = order = None
         if ge is not None:
-            sorted_ids, order = torch.sort(ids, stable=True)
+            sorted_ids, order = sort_ids(ids, wte.shape[0])
         for e, p in groups:
             g_dt = (e if e is not None else p).dtype
             check(_lib.lib().dlbb_embedding_bwd(
@@ -84,6 +84,22 @@ class _EmbeddingFn(torch.autograd.Function):
             else:
                 out_p = gp.to(wpe.dtype)
         return None, out_e, out_p   # out_p: full wpe shape, rows >= T zero
+
+
+def sort_ids(ids: torch.Tensor, vocab: int):
+    """Stable ascending sort of int64 token ids -> (sorted ids, positions), both int64. One
+    workgroup's block radix sort (``dlbb_sort_ids``: at most 16384 ids, vocabulary < 2^18 —
+    pure kernel work, no device memcpy, so a captured step stays kernel-only); the library sort
+    beyond that."""
+    n = ids.numel()
+    if ids.is_cuda and ids.dtype == torch.int64 and ids.is_contiguous() and n <= 16384 \
+            and vocab <= (1 << 18):
+        s = torch.empty_like(ids)
+        o = torch.empty_like(ids)
+        check(_lib.lib().dlbb_sort_ids(ids.data_ptr(), s.data_ptr(), o.data_ptr(), n, int(vocab),
+                                       _lib.stream(ids.device)), "sort_ids")
+        return s, o
+    return torch.sort(ids, stable=True)
 
 
 def embedding(idx: torch.Tensor, wte: torch.Tensor, wpe: torch.Tensor) -> torch.Tensor:
