@@ -20,3 +20,4 @@ step prof_mem 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/pr
 cd "$R"
 f=$(find $O/prof_mem -name "*kernel_trace.csv" | head -1); rm -f "$f"
 ls $O/prof_mem
+bash tools/runs/gpu_r05n.sh
