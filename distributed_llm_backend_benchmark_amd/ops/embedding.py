@@ -14,6 +14,8 @@ the last one (:func:`.linear_fn.sink_used`).
 
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn.functional as F
 
@@ -93,7 +95,7 @@ def sort_ids(ids: torch.Tensor, vocab: int):
     beyond that."""
     n = ids.numel()
     if ids.is_cuda and ids.dtype == torch.int64 and ids.is_contiguous() and n <= 16384 \
-            and vocab <= (1 << 18):
+            and vocab <= (1 << 18) and os.environ.get("DLBB_SORT_IDS", "hip") != "torch":
         s = torch.empty_like(ids)
         o = torch.empty_like(ids)
         check(_lib.lib().dlbb_sort_ids(ids.data_ptr(), s.data_ptr(), o.data_ptr(), n, int(vocab),
