@@ -24,8 +24,8 @@ struct ReduceArgs {
 };
 
 // NS > 0: the source count is a template constant and every source's 16-byte vector of an item
-// is loaded before the first add (NS loads in flight per lane); NS == 0: runtime count, one
-// source per loop trip (the round-1..4 form; A/B: dlbb_reduce_set_variant(0)).
+// is loaded before the first add (NS loads in flight per lane; A/B: dlbb_reduce_set_variant(1));
+// NS == 0: runtime count, one source per loop trip (the default).
 template <int DTI, int DTO, int NS>
 __global__ void __launch_bounds__(256) reduce_sum_kernel(ReduceArgs a) {
   uint64_t t0 = 0;
@@ -106,7 +106,11 @@ uint64_t* stamp_acquire(int kind, int64_t nrec) {
   return p;
 }
 
-static int g_reduce_variant = 1;   // 1: templated source counts 2/3/4/8 (default), 0: runtime
+// 0 (default): runtime source count; 1: templated counts 2/3/4/8 with every source's load in
+// flight. Measured equal within noise, the runtime loop 1-3 % ahead at 64 MiB-1 GiB x 8 sources
+// (profiles/r05_kernels/memroof_pass2.jsonl, memroof_rocprof_kernel_stats.csv: 100.1 vs 101.7 us
+// average): the hardware already overlaps the loop trips' loads, unlike the split-K reduce's.
+static int g_reduce_variant = 0;
 
 template <int DTI, int DTO>
 static hipError_t launch_reduce(const ReduceArgs& a, int nblocks, hipStream_t s) {

@@ -38,7 +38,7 @@ def test_reduce_sum(dtype, nsrc, n, variant):
         torch.testing.assert_close(out, ref, rtol=1e-5, atol=1e-5)
         out2 = reduce_sum(srcs, scale=0.5)
     finally:
-        _lib.lib().dlbb_reduce_set_variant(1)
+        _lib.lib().dlbb_reduce_set_variant(0)
     tol = 1e-2 if dtype != torch.float32 else 1e-5
     torch.testing.assert_close(out2.float(), ref, rtol=tol, atol=tol * nsrc)
 

@@ -315,12 +315,12 @@ if "memroof" in which:
         t = t_med(st.run, iters=20)
         out(kernel="chunk_copy_scale_bf16_fp32", src_MiB=mib, TBps=round(n * 6 / t / 1e12, 3))
         srcs = [rnd(n // 8) for _ in range(8)]
-        L.lib().dlbb_reduce_set_variant(0)
-        t0 = t_med(lambda: ops.reduce_sum(srcs), iters=20)
         L.lib().dlbb_reduce_set_variant(1)
+        t1 = t_med(lambda: ops.reduce_sum(srcs), iters=20)
+        L.lib().dlbb_reduce_set_variant(0)
         t = t_med(lambda: ops.reduce_sum(srcs), iters=20)
         out(kernel="reduce_sum_8src", src_MiB=mib, TBps=round(9 * (n // 8) * 2 / t / 1e12, 3),
-            runtime_loop_TBps=round(9 * (n // 8) * 2 / t0 / 1e12, 3))
+            templated_TBps=round(9 * (n // 8) * 2 / t1 / 1e12, 3))
 if "splitred" in which:
     # the weight-gradient split-K reduce alone (fp32 slabs -> bf16 dW += sum, + bias slabs), by
     # variant (0 round-4 8-float form, 1 all slabs in flight + nt loads, 2 all in flight, plain)
