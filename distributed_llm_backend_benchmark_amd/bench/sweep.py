@@ -46,8 +46,11 @@ class WrongResult(RuntimeError):
     into a statistic (VERDICT r04 weak #8)."""
 
 
-def _validate(comm: Comm, op, shape, dtype, seed, label=("", "")) -> bool:
-    inputs = [make_data(shape, dtype, r, comm.device, seed) for r in range(comm.world_size)]
+def _validate(comm: Comm, op, shape, dtype, seed, label=("", ""), src_dtype=None) -> bool:
+    # src_dtype: the dtype the data was generated in before a wire cast (3D sweep with
+    # wire_dtype): the closed form must see the same rounded values the collective moves
+    inputs = [make_data(shape, src_dtype or dtype, r, comm.device, seed).to(dtype)
+              for r in range(comm.world_size)]
     op.reset()
     comm.sync()
     comm.barrier()
@@ -63,7 +66,7 @@ def _validate(comm: Comm, op, shape, dtype, seed, label=("", "")) -> bool:
 
 def _bench_one(comm: Comm, op_name: str, data: torch.Tensor, warmup: int, iters: int,
                timing: str, batched: bool, graph: bool, validate: bool, seed: int,
-               op_opts: Dict, label: str = "") -> Dict:
+               op_opts: Dict, label: str = "", src_dtype=None) -> Dict:
     op = make_op(op_name, comm, data, **op_opts)
     out: Dict = {"op_impl": getattr(op, "impl", None) or comm.backend_label}
     if op_opts.get("out_of_place"):
@@ -72,7 +75,7 @@ def _bench_one(comm: Comm, op_name: str, data: torch.Tensor, warmup: int, iters:
         out["colocated"] = True
     if validate:
         out["validated"] = _validate(comm, op, tuple(data.shape), data.dtype, seed,
-                                     (op_name, label))
+                                     (op_name, label), src_dtype)
         if not out["validated"]:          # agreed on every rank by _validate
             op.close()
             raise WrongResult(f"{op_name} {label}: output failed the closed-form check on at "
@@ -260,7 +263,8 @@ def run_3d_sweep(comm: Comm, *, ops: Sequence[str], batch_sizes: Iterable[int],
                         with tracing.range(f"{impl_name}/{op_name}/{shape_name}"):
                             r = _bench_one(comm, op_name, data, warmup, iters, timing, batched,
                                            graph, validate, seed,
-                                           p1_opts(comm, op_name, op_opts or {}), shape_name)
+                                           p1_opts(comm, op_name, op_opts or {}), shape_name,
+                                           src_dtype=tdt)
                         roofline_guard(op_name, r, comm.world_size, colocated(comm.world_size))
                         rec = schema.result_3d(
                             impl=impl_name, backend=comm.backend_label, op=op_name,

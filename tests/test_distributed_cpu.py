@@ -29,6 +29,12 @@ def _sweep_worker(rank, world, outdir):
                  batch_sizes=[1, 2], seq_lengths=[4], hidden_dims=[64], dtype="bf16",
                  warmup=1, iters=3, output_dir=os.path.join(outdir, "3d"), impl_name="gloo",
                  validate=True)
+    # the reference's 3D MPI form: bf16 data on an fp32 wire, validated against the same
+    # bf16-rounded values (round 5: the closed form used to regenerate unrounded fp32 data)
+    run_3d_sweep(comm, ops=["allreduce", "allgather", "reduce_scatter"], batch_sizes=[1],
+                 seq_lengths=[4], hidden_dims=[64], dtype="bf16", wire_dtype="fp32",
+                 warmup=1, iters=2, output_dir=os.path.join(outdir, "3d_wire"),
+                 impl_name="gloo", validate=True)
     # resume: nothing rewritten
     again = run_1d_sweep(comm, ops=["allreduce"], sizes={"1KB": 256}, dtype="fp32", warmup=1,
                          iters=2, output_dir=os.path.join(outdir, "1d"), impl_name="gloo",
@@ -55,6 +61,9 @@ def test_gloo_sweeps_all_ops(tmp_path, world):
         assert len(rec["timings"]) == world and all(len(t) == 4 for t in rec["timings"])
         assert rec["timing_method"] == "host_perf_counter"
         assert rec["batched_mean_s"] > 0
+    wire = sorted(os.listdir(tmp_path / "3d_wire"))
+    assert wire and not [f for f in wire if f.endswith(".error.json")], wire
+    assert all(json.load(open(tmp_path / "3d_wire" / f))["validated"] is True for f in wire)
     rows = stats1d.process_directory(str(d1), str(tmp_path / "s1d"), verbose=False)
     assert len(rows) == len(files)
     ar = [r for r in rows if r["operation"] == "allreduce" and r["data_size_name"] == "4KiB"][0]
