@@ -1035,9 +1035,9 @@ __device__ __forceinline__ void wait_vm() {
 // the single-round long-K case, profiles/r04_gemm/SUMMARY.md). Its first counted wait then has
 // B(u+2) not yet issued: NBx fewer younger loads.
 template <bool NN, bool BAL = false, bool TN = false, bool STAMP = false, int NJ = 4,
-          bool PHASES = false, bool MOVEB = false>
+          bool PHASES = false, int MOVEB = 0>
 __device__ __forceinline__ void pingpong_body(GemmArgs a, char* smem, uint64_t* st = nullptr) {
-  static_assert(!MOVEB || (NJ == 4 && !NN && !TN), "MOVEB: NT 256² only");
+  static_assert(!MOVEB || (NJ == 4 && !NN && !TN && BAL), "MOVEB: NT 256² balanced only");
   static_assert(NJ == 4 || (NJ == 3 && !NN && !TN), "192-wide tiles: NT only");
   constexpr int NBI = 2 * NJ;                 // B DMA instructions per staging wave per K-tile
   constexpr int kTileB = NJ * 64 * BK * 2;    // bytes of one B tile buffer
@@ -1187,7 +1187,7 @@ __device__ __forceinline__ void pingpong_body(GemmArgs a, char* smem, uint64_t* 
       __builtin_amdgcn_sched_barrier(0);
       __builtin_amdgcn_s_barrier();                   // end of interval 2u
       __builtin_amdgcn_sched_barrier(0);
-      if constexpr (MOVEB) {
+      if constexpr (MOVEB == 1) {
 #pragma unroll
         for (int i = 0; i < 8; ++i)
 #pragma unroll
@@ -1203,6 +1203,34 @@ __device__ __forceinline__ void pingpong_body(GemmArgs a, char* smem, uint64_t* 
           for (int j = 0; j < 4; ++j)
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[1][j], af[1][i], acc[i][j],
                                                                 0, 0, 0);
+      } else if constexpr (MOVEB == 2) {
+        // B(u+2)'s four pieces spread one per 16 MFMAs (the guide: a lone LDS-DMA piece among
+        // bare MFMAs costs ~60 issue cycles, within the 8 free issue cycles x 16 MFMAs after it)
+        const int cb2 = cb == 0 ? 2 : cb - 1;
+        auto group = [&](auto ksc, auto i0c) {
+          constexpr int ks = decltype(ksc)::value, i0 = decltype(i0c)::value;
+#pragma unroll
+          for (int i = i0; i < i0 + 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[ks][j], af[ks][i],
+                                                                  acc[i][j], 0, 0, 0);
+        };
+        auto piece = [&](auto pc) {
+          constexpr int pp = decltype(pc)::value;
+          __builtin_amdgcn_sched_barrier(0);
+          if (b2) stage_bt(std::integral_constant<int, pp>{}, std::integral_constant<int, pp + 1>{},
+                           u + 2, bbuf0 + cb2 * kTileB);
+          __builtin_amdgcn_sched_barrier(0);
+        };
+        group(std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{});
+        piece(std::integral_constant<int, 0>{});
+        group(std::integral_constant<int, 0>{}, std::integral_constant<int, 4>{});
+        piece(std::integral_constant<int, 1>{});
+        group(std::integral_constant<int, 1>{}, std::integral_constant<int, 0>{});
+        piece(std::integral_constant<int, 2>{});
+        group(std::integral_constant<int, 1>{}, std::integral_constant<int, 4>{});
+        piece(std::integral_constant<int, 3>{});
       } else {
         mfma_all();
       }
@@ -1290,7 +1318,12 @@ __global__ void __launch_bounds__(kThreads2, 1) gemm_bf16_nt_256_pingpong3_bal(G
 // A/B variant (set_stagger(11)): BAL with wave row 0's B DMA inside its MFMA phase (MOVEB)
 __global__ void __launch_bounds__(kThreads2, 1) gemm_bf16_nt_256_pingpong3_bal_mb(GemmArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  pingpong_body<false, true, false, false, 4, false, true>(a, smem);
+  pingpong_body<false, true, false, false, 4, false, 1>(a, smem);
+}
+// A/B variant (set_stagger(12)): BAL with row 0's B DMA pieces spread one per 16 MFMAs
+__global__ void __launch_bounds__(kThreads2, 1) gemm_bf16_nt_256_pingpong3_bal_mb2(GemmArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  pingpong_body<false, true, false, false, 4, false, 2>(a, smem);
 }
 
 // 256 x 192 tiles (N % 192 == 0): grids that end in a partial round of 256² tiles
@@ -2554,6 +2587,8 @@ DLBB_API int dlbb_gemm_bf16_nt_v(const void* A, int64_t lda, const void* B, int6
       launch_w4d(g, a, stream);
     else if (mode == 11)                  // A/B: BAL + row 0's B DMA inside its MFMA phase
       hipLaunchKernelGGL(gemm_bf16_nt_256_pingpong3_bal_mb, g, dim3(kThreads2), kPP6Lds, stream, a);
+    else if (mode == 12)                  // A/B: same, one piece per 16 MFMAs
+      hipLaunchKernelGGL(gemm_bf16_nt_256_pingpong3_bal_mb2, g, dim3(kThreads2), kPP6Lds, stream, a);
     else if (mode == 7 || (mode == 6 && use_bal(K / BK, false)))
       DLBB_PP_LAUNCH(gemm_bf16_nt_256_pingpong3_bal, STAMP_GEMM_NT, g, a);
     else if (mode == 6)
