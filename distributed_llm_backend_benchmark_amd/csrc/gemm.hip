@@ -716,6 +716,16 @@ __device__ __forceinline__ void stage_a_half(__amdgpu_buffer_rsrc_t ra, uint32_t
   }
 }
 
+// piece I (0..3) of stage_a_half: one wave-instruction (8 rows x 128 B)
+template <int I>
+__device__ __forceinline__ void stage_a_piece(__amdgpu_buffer_rsrc_t ra, uint32_t lda2,
+                                              int rows_a, uint32_t k2, char* abuf, int half,
+                                              int w4, uint32_t aoff) {
+  const int trow = half * 128 + (I * 4 + w4) * 8;
+  const int g = trow < rows_a - 8 ? trow : rows_a - 8;
+  bldsx4(ra, aoff, static_cast<uint32_t>(g) * lda2 + k2, abuf + trow * (BK * 2));
+}
+
 // I0 / I1: the slice [I0, I1) of the 8 instructions (0..3 = tile rows [0, 128), 4..7 = rows
 // [128, 256)) — the balanced ping-pong splits a B tile between the two wave rows
 template <int I0 = 0, int I1 = 8>
@@ -1160,7 +1170,7 @@ __device__ __forceinline__ void pingpong_body(GemmArgs a, char* smem, uint64_t* 
       const char* ab = abuf0 + (u & 1) * kTile2Bytes;
       read_frags(ab, bbuf0 + cb * kTileB, 0);
       const bool h1 = u + 1 < nk, b2 = u + 2 < nk;
-      if (h1)
+      if (MOVEB != 3 && h1)
         DLBB_STAGE_A(u + 1, abuf0 + ((u + 1) & 1) * kTile2Bytes, 1,
                      stage_a_half(ra, lda2, rows_a, (u + 1) * kStep,
                                   abuf0 + ((u + 1) & 1) * kTile2Bytes, 1, wc, aoff));
@@ -1174,7 +1184,12 @@ __device__ __forceinline__ void pingpong_body(GemmArgs a, char* smem, uint64_t* 
       if (!MOVEB && b2) stage_b2();
       // retire A-hi(u) (issued two intervals ago; tile 0's came from row 1)
       constexpr int kB2 = MOVEB ? 0 : (BAL ? NBI / 2 : NBI);   // B(u+2) instructions issued
-      if constexpr (BAL) {
+      if constexpr (MOVEB == 3) {
+        // A-hi(u) and B0(u+1) were both issued in the previous MFMA phase (A-hi first); only
+        // B0(u+1) is younger than A-hi(u) — and nothing of this interval is issued yet
+        if (h1) wait_vm<NBI / 2>();
+        else wait_vm<0>();
+      } else if constexpr (BAL) {
         if (b2) wait_vm<NBI / 2 + 4 + kB2>();
         else if (h1) wait_vm<NBI / 2 + 4>();
         else wait_vm<0>();
@@ -1203,6 +1218,36 @@ __device__ __forceinline__ void pingpong_body(GemmArgs a, char* smem, uint64_t* 
           for (int j = 0; j < 4; ++j)
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[1][j], af[1][i], acc[i][j],
                                                                 0, 0, 0);
+      } else if constexpr (MOVEB == 3) {
+        // A-hi(u+1)'s four pieces, then B0(u+2)'s four, one piece per 8 MFMAs: the memory
+        // interval keeps only its ds_reads and one counted wait
+        const int cb2 = cb == 0 ? 2 : cb - 1;
+        char* const anext = abuf0 + ((u + 1) & 1) * kTile2Bytes;
+        auto group = [&](auto gc) {
+          constexpr int gi = decltype(gc)::value, ks = gi >> 2, i0 = 2 * (gi & 3);
+#pragma unroll
+          for (int i = i0; i < i0 + 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[ks][j], af[ks][i],
+                                                                  acc[i][j], 0, 0, 0);
+          __builtin_amdgcn_sched_barrier(0);
+          if constexpr (gi < 4) {
+            if (h1) stage_a_piece<gi>(ra, lda2, rows_a, (u + 1) * kStep, anext, 1, wc, aoff);
+          } else {
+            if (b2) stage_bt(std::integral_constant<int, gi - 4>{},
+                             std::integral_constant<int, gi - 3>{}, u + 2, bbuf0 + cb2 * kTileB);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        };
+        group(std::integral_constant<int, 0>{});
+        group(std::integral_constant<int, 1>{});
+        group(std::integral_constant<int, 2>{});
+        group(std::integral_constant<int, 3>{});
+        group(std::integral_constant<int, 4>{});
+        group(std::integral_constant<int, 5>{});
+        group(std::integral_constant<int, 6>{});
+        group(std::integral_constant<int, 7>{});
       } else if constexpr (MOVEB == 2) {
         // B(u+2)'s four pieces spread one per 16 MFMAs (the guide: a lone LDS-DMA piece among
         // bare MFMAs costs ~60 issue cycles, within the 8 free issue cycles x 16 MFMAs after it)
@@ -1324,6 +1369,11 @@ __global__ void __launch_bounds__(kThreads2, 1) gemm_bf16_nt_256_pingpong3_bal_m
 __global__ void __launch_bounds__(kThreads2, 1) gemm_bf16_nt_256_pingpong3_bal_mb2(GemmArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   pingpong_body<false, true, false, false, 4, false, 2>(a, smem);
+}
+// A/B variant (set_stagger(13)): row 0's A-hi(u+1) AND B0(u+2) pieces spread one per 8 MFMAs
+__global__ void __launch_bounds__(kThreads2, 1) gemm_bf16_nt_256_pingpong3_bal_mb3(GemmArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  pingpong_body<false, true, false, false, 4, false, 3>(a, smem);
 }
 
 // 256 x 192 tiles (N % 192 == 0): grids that end in a partial round of 256² tiles
@@ -2589,6 +2639,8 @@ DLBB_API int dlbb_gemm_bf16_nt_v(const void* A, int64_t lda, const void* B, int6
       hipLaunchKernelGGL(gemm_bf16_nt_256_pingpong3_bal_mb, g, dim3(kThreads2), kPP6Lds, stream, a);
     else if (mode == 12)                  // A/B: same, one piece per 16 MFMAs
       hipLaunchKernelGGL(gemm_bf16_nt_256_pingpong3_bal_mb2, g, dim3(kThreads2), kPP6Lds, stream, a);
+    else if (mode == 13)                  // A/B: A-hi + B pieces, one per 8 MFMAs
+      hipLaunchKernelGGL(gemm_bf16_nt_256_pingpong3_bal_mb3, g, dim3(kThreads2), kPP6Lds, stream, a);
     else if (mode == 7 || (mode == 6 && use_bal(K / BK, false)))
       DLBB_PP_LAUNCH(gemm_bf16_nt_256_pingpong3_bal, STAMP_GEMM_NT, g, a);
     else if (mode == 6)

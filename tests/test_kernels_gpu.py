@@ -117,12 +117,13 @@ def test_chunk_copy_and_scale(nt):
 @pytest.fixture(params=[("mfma", 0, 1), ("mfma", 128, 1), ("mfma", 256, 1), ("mfma", 256, 0),
                         ("mfma", 256, 2), ("mfma", 256, 3), ("mfma", 256, 4), ("mfma", 256, 6),
                         ("mfma", 256, 6, 0), ("mfma", 256, 7), ("mfma", 256, 9), ("mfma", 256, 10),
-                        ("mfma", 256, 11), ("mfma", 256, 12), ("blas", 0, 1)],
+                        ("mfma", 256, 11), ("mfma", 256, 12), ("mfma", 256, 13), ("blas", 0, 1)],
                 ids=["mfma_auto", "mfma_t128", "mfma_t256", "mfma_t256_lockstep",
                      "mfma_t256_early", "mfma_t256_deep", "mfma_t256_persistent",
                      "mfma_t256_pingpong", "mfma_t256_pingpong_nobal", "mfma_t256_pingpong_bal",
                      "mfma_t256_w4_agpr", "mfma_t256_pp_persistent", "mfma_t256_pingpong_moveb",
-                     "mfma_t256_pingpong_moveb_spread", "blas"])
+                     "mfma_t256_pingpong_moveb_spread", "mfma_t256_pingpong_moveab_spread",
+                     "blas"])
 def gemm_tile(request, monkeypatch):
     from distributed_llm_backend_benchmark_amd.ops.gemm import (get_stagger, set_bal, set_stagger,
                                                                 set_tile)

@@ -17,6 +17,6 @@ step() {  # step <name> <timeout> <cmd...>
 }
 step tests 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread -p no:cacheprovider \
   tests/test_kernels_gpu.py -k "moveb"
-step table 600 python -u tools/tp_gemm_table.py --ps 1,2 --modes s7,s11,s12 --lmhead
+step table 600 python -u tools/tp_gemm_table.py --ps 1,2 --modes s7,s12,s13 --lmhead
 cat $O/table.log | grep '^{' | cut -c1-400
-step table2 600 python -u tools/tp_gemm_table.py --ps 1,2 --modes s12,s7 --lmhead
+step table2 600 python -u tools/tp_gemm_table.py --ps 1,2 --modes s13,s12,s7 --lmhead
