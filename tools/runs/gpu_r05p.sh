@@ -16,7 +16,7 @@ step() {  # step <name> <timeout> <cmd...>
   if [ $rc -ne 0 ]; then exit $rc; fi
 }
 step tests 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread -p no:cacheprovider \
-  tests/test_kernels_gpu.py -k "moveb"
+  tests/test_kernels_gpu.py -k "moveb or moveab"
 step table 600 python -u tools/tp_gemm_table.py --ps 1,2 --modes s7,s12,s13 --lmhead
 cat $O/table.log | grep '^{' | cut -c1-400
 step table2 600 python -u tools/tp_gemm_table.py --ps 1,2 --modes s13,s12,s7 --lmhead
