@@ -57,6 +57,13 @@ _WGRAD_STREAMS = max(1, int(os.environ.get("DLBB_WGRAD_STREAMS", "1")))
 # priority of the dedicated bucket-reduction stream: 0 = normal (default, measured), -1 = high
 # (A/B knob; see the module docstring and profiles/r02_overlap/SUMMARY.md)
 _COMM_PRIORITY = int(os.environ.get("DLBB_COMM_STREAM_PRIORITY", "0"))
+# split optimizer only: AdamW of a head bucket is issued as soon as that bucket is reduced,
+# during backward, on a stream of its own (1) or on the weight-gradient side stream (2, default),
+# instead of for all head buckets after backward (0). GPT-2 step, three interleaved reps in one
+# call: 0 -> 17.45-17.47 ms, 1 -> 17.48-17.52, 2 -> 17.42-17.43 (profiles/r05_step/SUMMARY.md §5):
+# the AdamW ranges slot in behind the side stream's weight gradients instead of competing with
+# the main stream from a fourth queue. Bit-exact in every mode (tests/test_comm_gpu.py).
+_OPT_OVERLAP = int(os.environ.get("DLBB_OPT_OVERLAP", "2"))
 
 
 def comm_stream_priority() -> int:
@@ -234,6 +241,10 @@ class FlatParamTrainer:
         # buckets are reduced, then the last bucket — whose all-reduce (it is ready only at the
         # end of backward) overlaps the first range's AdamW instead of preceding all of it
         self.split_optimizer = split_optimizer
+        self.opt_overlap = _OPT_OVERLAP if dev.type == "cuda" else 0
+        self._opt_stream = None
+        self._opt_issued = 0          # head-bucket AdamW ranges issued in this step's backward
+        self._in_step = False         # only step() (which joins the optimizer stream) overlaps
         self.timeline = False       # record comm events per bucket (comm_tail_report)
         self._tl = None
         self.step_count = 0
@@ -316,6 +327,7 @@ class FlatParamTrainer:
         for b in self.buckets:
             b.ready, b.launched, b.work = 0, False, None
         self._next = 0
+        self._opt_issued = 0
         self._seen.clear()
         for p in self._params:          # per-step use counters of multi-use gradient sinks
             if getattr(p, "_dlbb_sink_count", 0):
@@ -339,6 +351,29 @@ class FlatParamTrainer:
                 return
             self._launch(b)
             self._next += 1
+            self._maybe_opt_bucket(b)
+
+    def _maybe_opt_bucket(self, b: _Bucket) -> None:
+        """Overlapped split optimizer: AdamW of head bucket ``b`` on the optimizer stream, ordered
+        after everything that produced or reads the bucket — the main stream up to now (its
+        dgrads read these weights before the sinks report them ready, ops/linear_fn.py), the
+        weight-gradient side streams, and the bucket's all-reduce. The first range of the step
+        advances the AdamW step count; the tail bucket waits for this stream in ``step``."""
+        if (not self.opt_overlap or not self._in_step or b.idx == len(self.buckets) - 1
+                or not self._split_optimizer_ok()):
+            return
+        dev = self.flat_grad.device
+        if self._opt_stream is None:
+            self._opt_stream = (self._wgrad_stream if self.opt_overlap == 2
+                                and self._wgrad_stream is not None
+                                else concurrent_stream(dev, "ddp_opt"))
+        os_ = self._opt_stream
+        os_.wait_stream(torch.cuda.current_stream(dev))
+        self._wait_wgrad(os_)
+        with torch.cuda.stream(os_):
+            self._wait_bucket(b)
+            self._optimizer_step(ranges=[(b.start, b.end)], advance=self._opt_issued == 0)
+        self._opt_issued += 1
 
     def _launch(self, b: _Bucket) -> None:
         b.launched = True
@@ -425,9 +460,11 @@ class FlatParamTrainer:
             b.work = dist.all_reduce(buf, async_op=True)
 
     def _wait_wgrad(self, stream) -> None:
-        """Order ``stream`` after every weight-gradient side stream."""
+        """Order ``stream`` after every weight-gradient side stream (not after itself: a
+        stream waiting on its own event inside a HIP-graph capture crashes capture_end)."""
         for ws in self._wgrad_streams:
-            stream.wait_stream(ws)
+            if ws != stream:
+                stream.wait_stream(ws)
 
     def _mark_done(self, b: _Bucket, cs) -> None:
         """Per-bucket completion event on the comm stream (waited per bucket by the split
@@ -456,8 +493,10 @@ class FlatParamTrainer:
 
     def _launch_rest(self) -> None:
         while self._next < len(self.buckets):
-            self._launch(self.buckets[self._next])
+            b = self.buckets[self._next]
+            self._launch(b)
             self._next += 1
+            self._maybe_opt_bucket(b)
 
     def finish(self) -> None:
         """Launch what backward did not (e.g. overlap off), then wait every bucket."""
@@ -490,6 +529,7 @@ class FlatParamTrainer:
         """One full training step: forward, backward (+ overlapped all-reduce), AdamW."""
         self.zero_grad()
         self._reset()
+        self._in_step = True
         if self.timeline and not torch.cuda.is_current_stream_capturing():
             self._tl = {"buckets": {}}
         with tracing.range("fwd"):
@@ -504,11 +544,16 @@ class FlatParamTrainer:
             with tracing.range("grad_sync_tail+optimizer"):
                 self._launch_rest()
                 head, tail = self.buckets[:-1], self.buckets[-1]
-                for b in head:
-                    self._wait_bucket(b)
+                if self._opt_issued:
+                    # head AdamW already issued bucket by bucket during backward
+                    torch.cuda.current_stream(self.flat_grad.device).wait_stream(self._opt_stream)
+                else:
+                    for b in head:
+                        self._wait_bucket(b)
                 if self._wgrad_stream is not None:
                     self._wait_wgrad(torch.cuda.current_stream(self.flat_grad.device))
-                self._optimizer_step(ranges=[(0, tail.start)], advance=True)
+                if not self._opt_issued:
+                    self._optimizer_step(ranges=[(0, tail.start)], advance=True)
                 self._wait_bucket(tail)
                 self._optimizer_step(ranges=[(tail.start, self.numel)], advance=False)
         else:
@@ -516,6 +561,7 @@ class FlatParamTrainer:
                 self.finish()
             with tracing.range("optimizer"):
                 self._optimizer_step()
+        self._in_step = False
         if self._tl is not None:
             self._tl["opt_end"] = torch.cuda.Event(enable_timing=True)
             self._tl["opt_end"].record(torch.cuda.current_stream(self.flat_grad.device))

@@ -834,3 +834,34 @@ def test_allgather_list_form_unpack_bit_exact_world1():
             assert torch.equal(op.result(), x.reshape(-1))
     finally:
         comm.destroy()
+
+
+@pytest.mark.parametrize("mode", [1, 2])
+def test_ddp_overlapped_optimizer_is_bit_exact(mode):
+    """Split optimizer with per-bucket AdamW issued during backward (opt_overlap 1: own stream,
+    2: on the weight-gradient side stream) must give the same losses and masters, bit for bit, as
+    the head range updated after backward — eager and as a captured HIP graph; the step count
+    advances once per step."""
+    from distributed_llm_backend_benchmark_amd.models.gpt2 import GPT2, GPT2Config
+    from distributed_llm_backend_benchmark_amd.parallel.ddp import FlatParamTrainer
+
+    dev = torch.device("cuda", 0)
+    cfg = GPT2Config(vocab_size=512, block_size=64, n_layer=3, n_head=4, n_embd=256)
+    g = torch.Generator(device="cuda").manual_seed(3)
+    data = torch.randint(0, cfg.vocab_size, (6, 4, 65), device=dev, generator=g)
+    out = []
+    for ov in (0, mode):
+        tr = FlatParamTrainer(GPT2(cfg, device=dev, seed=6), None, lr=1e-3, bucket_mb=0.3)
+        tr.opt_overlap = ov
+        assert len(tr.buckets) > 2 and tr._split_optimizer_ok()
+        losses = [tr.step(data[s, :, :-1], data[s, :, 1:]) for s in range(3)]
+        if ov:
+            assert tr._opt_issued == len(tr.buckets) - 1 and tr._opt_stream is not None
+        replay = tr.capture_step(data[3, :, :-1], data[3, :, 1:])
+        losses += [float(replay(data[s, :, :-1], data[s, :, 1:]).item()) for s in (4, 5)]
+        torch.cuda.synchronize()
+        assert tr.opt.t == 6 and int(tr.opt.t_dev.item()) == 6
+        out.append((losses, tr.master.clone()))
+        tr.close()
+    assert out[0][0] == out[1][0]
+    assert torch.equal(out[0][1], out[1][1])

@@ -343,6 +343,45 @@ if "splitred" in which:
                 res[f"v{var}"] = {"us": round(t * 1e6, 2), "TBps": round(nbytes / t / 1e12, 3)}
             L.lib().dlbb_split_reduce_set_variant(1)
             out(kernel="split_reduce", N=N, K=K, split=sp, res=res)
+if "wgradpp" in which:
+    # GPT-2 dW shapes on the 256^2 ping-pong TN kernel with split-K over all tokens (fp32 slabs
+    # + the NN split reduce), vs the tuned default (128 x 256 / 256 x 128 wgrad tiles with the
+    # fused bias); the bias column sum the TN path would need is timed on its own
+    from distributed_llm_backend_benchmark_amd.ops import _lib as L
+    from distributed_llm_backend_benchmark_amd.ops.gemm import (_pp_launch, _wgrad_hip,
+                                                                _wgrad_hip256, _wgrad_hip_wide)
+    for N, K in ((2304, 768), (768, 768), (3072, 768), (768, 3072)):
+        M = 16384
+        dy, x = rnd(M, N), rnd(M, K)
+        w_out = torch.zeros(N, K, device="cuda", dtype=torch.bfloat16)
+        b_out = torch.zeros(N, device="cuda", dtype=torch.bfloat16)
+        ref = (dy.float().t() @ x.float())
+        res, err = {}, {}
+        res["t128_bias"] = round(t_med(lambda: _wgrad_hip(dy, x, w_out, False, None, b_out),
+                                       iters=30) * 1e6, 1)
+        if N % 256 == 0:
+            res["t256x128_bias"] = round(t_med(
+                lambda: _wgrad_hip256(dy, x, w_out, False, None, b_out), iters=30) * 1e6, 1)
+        if K % 256 == 0:
+            res["t128x256_bias"] = round(t_med(
+                lambda: _wgrad_hip_wide(dy, x, w_out, False, None, b_out), iters=30) * 1e6, 1)
+            res["t128x256_nobias"] = round(t_med(
+                lambda: _wgrad_hip_wide(dy, x, w_out, False, None, None), iters=30) * 1e6, 1)
+        res["colsum_torch"] = round(t_med(lambda: dy.sum(0, dtype=torch.float32), iters=30)
+                                    * 1e6, 1)
+        for sp in (1, 2, 3, 4, 6, 8, 9, 12, 16):
+            if M // 64 < sp:
+                continue
+            res[f"pp_s{sp}"] = round(t_med(lambda: _pp_launch(dy, x, w_out, False, 0, N, sp),
+                                           iters=30) * 1e6, 1)
+            err[f"pp_s{sp}"] = round(float((w_out.float() - ref).abs().max()
+                                           / ref.abs().max()), 5)
+        fl = 2.0 * M * N * K
+        best = min((k for k in res if k != "colsum_torch"), key=res.get)
+        out(kernel="wgrad_pp_split", M=M, N=N, K=K, best=best, us=res, rel_err=err,
+            tflops={k: round(fl / v / 1e6, 1) for k, v in res.items() if k != "colsum_torch"})
+
+
 if "wgradstages" in which:
     # weight-gradient LDS ring depth (2 / 3 stages) x split at the GPT-2 dW shapes, whole call
     # (GEMM + reduce, fused bias, accumulate): the asm transposed reads keep the DMA prefetch in
