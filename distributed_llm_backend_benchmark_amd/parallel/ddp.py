@@ -63,7 +63,10 @@ _COMM_PRIORITY = int(os.environ.get("DLBB_COMM_STREAM_PRIORITY", "0"))
 # call: 0 -> 17.45-17.47 ms, 1 -> 17.48-17.52, 2 -> 17.42-17.43 (profiles/r05_step/SUMMARY.md §5):
 # the AdamW ranges slot in behind the side stream's weight gradients instead of competing with
 # the main stream from a fourth queue. Bit-exact in every mode (tests/test_comm_gpu.py).
-_OPT_OVERLAP = int(os.environ.get("DLBB_OPT_OVERLAP", "2"))
+# World > 1 keeps 0 unless set: there mode 2 would hold every later weight gradient behind the
+# bucket's all-reduce (the AdamW range waits for it on that stream), and mode 1 is unmeasured
+# across GPUs.
+_OPT_OVERLAP = os.environ.get("DLBB_OPT_OVERLAP")
 
 
 def comm_stream_priority() -> int:
@@ -241,7 +244,9 @@ class FlatParamTrainer:
         # buckets are reduced, then the last bucket — whose all-reduce (it is ready only at the
         # end of backward) overlaps the first range's AdamW instead of preceding all of it
         self.split_optimizer = split_optimizer
-        self.opt_overlap = _OPT_OVERLAP if dev.type == "cuda" else 0
+        self.opt_overlap = ((int(_OPT_OVERLAP) if _OPT_OVERLAP is not None
+                             else (2 if self.world == 1 else 0))
+                            if dev.type == "cuda" else 0)
         self._opt_stream = None
         self._opt_issued = 0          # head-bucket AdamW ranges issued in this step's backward
         self._in_step = False         # only step() (which joins the optimizer stream) overlaps
