@@ -96,6 +96,35 @@ def main():
                                          "graph_ms": round(graph, 4),
                                          "eager_over_one": round(eager / one, 3),
                                          "graph_over_one": round(graph / one, 3)}
+    # how many forks can one graph hold before the replay stops overlapping its branches? (the
+    # GPT-2 step forks the side stream ~50 times; the probes above fork 8 times)
+    if os.environ.get("GB_FORK_SWEEP", "1") == "1":
+        short = 20_000
+        for L in (8, 16, 32, 64, 128):
+            def many():
+                cur = torch.cuda.current_stream()
+                for _ in range(L):
+                    torch.cuda._sleep(short)
+                    side.wait_stream(cur)
+                    with torch.cuda.stream(side):
+                        torch.cuda._sleep(short)
+                cur.wait_stream(side)
+            one = timed(lambda: [torch.cuda._sleep(short) for _ in range(L)])
+            eager = timed(many)
+            cap = torch.cuda.Stream(dev)
+            cap.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(cap):
+                many()
+            torch.cuda.current_stream().wait_stream(cap)
+            torch.cuda.synchronize()
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                many()
+            graph = timed(g.replay)
+            out[f"sleep_forks_L{L}"] = {"one_chain_ms": round(one, 4), "eager_ms": round(eager, 4),
+                                        "graph_ms": round(graph, 4),
+                                        "eager_over_one": round(eager / one, 3),
+                                        "graph_over_one": round(graph / one, 3)}
     # the same with the side kernels dealt round-robin over k side streams: a side node then
     # depends on the main chain and on the side node k layers back, not the one just before
     sides = [side] + [torch.cuda.Stream(dev) for _ in range(3)]
