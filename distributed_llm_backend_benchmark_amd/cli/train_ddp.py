@@ -182,6 +182,8 @@ def _train(args, comm, tr, model, cfg):
         # which all-reduce each bucket took (auto picks per bucket size)
         "bucket_paths": _path_counts(tr),
         "gemm_tune_timing": _gemm.tune_timing(),
+        # per-bucket AdamW during backward (parallel/ddp.py _OPT_OVERLAP; 0 = after backward)
+        "opt_overlap": getattr(tr, "opt_overlap", 0),
     }
     if args.comm_timeline and not args.zero:
         tr.timeline = True

@@ -93,6 +93,22 @@ __device__ __forceinline__ void attn_stage(const AttnArgs& a, const uint16_t* ba
   }
 }
 
+// lane ^ 32 half exchange of a per-lane value by v_permlane32_swap (a VALU op) instead of a
+// ds_bpermute LDS round trip; max over both halves ends in every lane
+__device__ __forceinline__ float xhalf_max(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false,
+                                                  false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+
+// Forward variants (bit mask, A/B via dlbb_attn_set_fwd_variant):
+//   1: the tile's 8 K fragments read up front (asm ds_read_b128, one counted lgkmcnt wait per
+//      32-key half) — the compiler's schedule re-used one register quad and waited for each read
+//      in front of its MFMA (8 LDS round trips per tile);
+//   2: the row-max exchange with the other lane half by v_permlane32_swap (no LDS round trip);
+//   4: K/V DMA sources from per-lane base pointers + one uniform offset per tile (the clamped
+//      per-row 64-bit address arithmetic only on a tile that crosses T).
+template <int V>
 __global__ void __launch_bounds__(kAttnThreads, 2) attn_fwd_d64_kernel(AttnArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = threadIdx.x & 63;
@@ -131,15 +147,41 @@ __global__ void __launch_bounds__(kAttnThreads, 2) attn_fwd_d64_kernel(AttnArgs 
   auto tileK = [&](int c) { return smem + c * 2 * kTileKV; };
   auto tileV = [&](int c) { return smem + c * 2 * kTileKV + kTileKV; };
 
-  attn_stage(a, base_bt, 0, hoff, tileK(0), tileV(0), wave, lane);
+  // V & 4: this lane's 4 DMA sources of key-tile 0 (rows wave * 16 + i * 8 + lane / 8, K and V
+  // sections); tile kt adds kt * 64 rows, uniform
+  const uint16_t* dsrc[4];
+  if constexpr ((V & 4) != 0) {
+    const int r_in = lane >> 3, slot = lane & 7;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int row = wave * 16 + i * 8 + r_in;
+      const uint16_t* src = base_bt + static_cast<int64_t>(row) * a.ld + hoff;
+      dsrc[2 * i] = src + kAttnD * a.H + (slot ^ kswz(row)) * 8;
+      dsrc[2 * i + 1] = src + 2 * kAttnD * a.H + (slot ^ vswz(row)) * 8;
+    }
+  }
+  auto stage = [&](int k0, char* tk, char* tv) {
+    if constexpr ((V & 4) != 0) {
+      if (k0 + kKB <= a.T) {                        // wave-uniform: no row past T
+        const int64_t off = static_cast<int64_t>(k0) * a.ld;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          attn_glds16(dsrc[2 * i] + off, tk + (wave * 16 + i * 8) * 128);
+          attn_glds16(dsrc[2 * i + 1] + off, tv + (wave * 16 + i * 8) * 128);
+        }
+        return;
+      }
+    }
+    attn_stage(a, base_bt, k0, hoff, tk, tv, wave, lane);
+  };
+  stage(0, tileK(0), tileV(0));
   for (int kt = 0; kt < nt; ++kt) {
     const int cur = kt & 1;
     // one barrier per tile: it both publishes tile kt (every wave's DMA retired) and frees
     // buffer cur^1 (every wave finished tile kt-1), so the restage goes right after it
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-    if (kt + 1 < nt)
-      attn_stage(a, base_bt, (kt + 1) * kKB, hoff, tileK(cur ^ 1), tileV(cur ^ 1), wave, lane);
+    if (kt + 1 < nt) stage((kt + 1) * kKB, tileK(cur ^ 1), tileV(cur ^ 1));
     const int k0 = kt * kKB;
     if (k0 <= q_hi) {                               // wave-uniform: tile has keys <= a query
       const char* tk = tileK(cur);
@@ -147,16 +189,44 @@ __global__ void __launch_bounds__(kAttnThreads, 2) attn_fwd_d64_kernel(AttnArgs 
       // ---- S^T for the two 32-key halves
       f32x16 s[2];
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
+      for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
         for (int e = 0; e < 16; ++e) s[kk][e] = 0.f;
-        const int row = kk * 32 + r;
+      if constexpr ((V & 1) != 0) {
+        // rows r and 32 + r share kswz (it depends on row bits 1..3): the second half is the
+        // first's addresses + 4 KiB (read immediate)
+        f32x4 kr[2][4];
+        const char* krow = tk + r * 128;
+        const int sw = kswz(r);
+        const char* kp[4];
 #pragma unroll
-        for (int ks = 0; ks < 4; ++ks) {
-          const int c = 2 * ks + hi;
-          const bf16x8 kf =
-              *reinterpret_cast<const bf16x8*>(tk + row * 128 + ((c ^ kswz(row)) << 4));
-          s[kk] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[ks], s[kk], 0, 0, 0);
+        for (int ks = 0; ks < 4; ++ks) kp[ks] = krow + (((2 * ks + hi) ^ sw) << 4);
+        // issue order = wait order: half 0's four reads, then half 1's (asm volatile keeps it)
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) kr[0][ks] = ds_read_b128_asm<0>(kp[ks]);
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) kr[1][ks] = ds_read_b128_asm<4096>(kp[ks]);
+        lgk_wait<4>(kr[0][0], kr[0][1], kr[0][2], kr[0][3]);
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks)
+          s[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, kr[0][ks]),
+                                                         qf[ks], s[0], 0, 0, 0);
+        lgk_wait<0>(kr[1][0], kr[1][1], kr[1][2], kr[1][3]);
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks)
+          s[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, kr[1][ks]),
+                                                         qf[ks], s[1], 0, 0, 0);
+      } else {
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+          const int row = kk * 32 + r;
+#pragma unroll
+          for (int ks = 0; ks < 4; ++ks) {
+            const int c = 2 * ks + hi;
+            const bf16x8 kf =
+                *reinterpret_cast<const bf16x8*>(tk + row * 128 + ((c ^ kswz(row)) << 4));
+            s[kk] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[ks], s[kk], 0, 0, 0);
+          }
         }
       }
       // ---- scale, causal mask, online softmax (lane = one query; keys in registers)
@@ -175,7 +245,10 @@ __global__ void __launch_bounds__(kAttnThreads, 2) attn_fwd_d64_kernel(AttnArgs 
       for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
         for (int e = 0; e < 16; ++e) mx = fmaxf(mx, s[kk][e]);
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      if constexpr ((V & 2) != 0)
+        mx = xhalf_max(mx);
+      else
+        mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
       const float mn = fmaxf(m, mx * a.scale_log2);
       const float alpha = __builtin_amdgcn_exp2f(m - mn);   // m = -inf on the first tile -> 0
       const bool rescale = m != mn;
@@ -681,10 +754,14 @@ static int g_attn_concurrent = [] {
 // delta / nls computed inside the dQ kernel (1, default) or by the separate row kernel first (0);
 // the concurrent form always uses the separate kernel (A/B: dlbb_attn_set_fuse_delta)
 static int g_attn_fuse_delta = 1;
+// forward kernel variant (attn_fwd_d64_kernel<V> bit mask; A/B: dlbb_attn_set_fwd_variant)
+static int g_attn_fwd_variant = 0;
 
 DLBB_API void dlbb_attn_set_xcd(int on) { g_attn_xcd = on ? 1 : 0; }
 DLBB_API void dlbb_attn_set_fuse_delta(int on) { g_attn_fuse_delta = on ? 1 : 0; }
 DLBB_API void dlbb_attn_set_concurrent(int on) { g_attn_concurrent = on ? 1 : 0; }
+DLBB_API void dlbb_attn_set_fwd_variant(int v) { g_attn_fwd_variant = v >= 0 && v <= 7 ? v : 0; }
+DLBB_API int dlbb_attn_get_fwd_variant() { return g_attn_fwd_variant; }
 
 // Per-device side stream + fork/join events for the concurrent backward (created once; a fork
 // through an event recorded on the caller's stream is also how a HIP-graph capture of that
@@ -723,7 +800,16 @@ DLBB_API int dlbb_attn_fwd(const void* qkv, int64_t ld, void* out, int64_t ldo, 
   AttnArgs a{static_cast<const uint16_t*>(qkv), static_cast<uint16_t*>(out), lse, ld, ldo,
              B, T, H, scale * 1.4426950408889634f, g_attn_xcd};
   const dim3 grid((T + kQB - 1) / kQB, H, B);
-  hipLaunchKernelGGL(attn_fwd_d64_kernel, grid, dim3(kAttnThreads), 4 * kTileKV, stream, a);
+  switch (g_attn_fwd_variant) {
+#define FWD_V(N)                                                                           \
+  case N:                                                                                  \
+    hipLaunchKernelGGL(attn_fwd_d64_kernel<N>, grid, dim3(kAttnThreads), 4 * kTileKV, stream, a); \
+    break;
+    FWD_V(1) FWD_V(2) FWD_V(3) FWD_V(4) FWD_V(5) FWD_V(6) FWD_V(7)
+#undef FWD_V
+    default:
+      hipLaunchKernelGGL(attn_fwd_d64_kernel<0>, grid, dim3(kAttnThreads), 4 * kTileKV, stream, a);
+  }
   return hipGetLastError();
 }
 

@@ -71,6 +71,14 @@ __device__ __forceinline__ void tr_wait(F& f, R&... r) {
   asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(f));
   (tr_tie(r), ...);
 }
+// Counted form: the reads issued BEFORE the last N LDS operations have landed (LDS returns in
+// order; any other LDS op issued in between only makes the wait stricter). The arguments are
+// those reads' destinations.
+template <int N, typename F, typename... R>
+__device__ __forceinline__ void lgk_wait(F& f, R&... r) {
+  asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(f) : "n"(N));
+  (tr_tie(r), ...);
+}
 
 __device__ __forceinline__ float bf16_to_f32(uint16_t v) {
   return __uint_as_float(static_cast<uint32_t>(v) << 16);

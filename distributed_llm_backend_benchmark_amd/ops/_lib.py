@@ -120,6 +120,8 @@ _SIGS = {
     "dlbb_reduce_set_variant": (None, [c_int]),
     "dlbb_sort_ids": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int, c_void_p]),
     "dlbb_attn_set_fuse_delta": (None, [c_int]),
+    "dlbb_attn_set_fwd_variant": (None, [c_int]),
+    "dlbb_attn_get_fwd_variant": (c_int, []),
     "dlbb_split_reduce": (c_int, [c_void_p, c_void_p, c_int, c_int64, c_void_p, c_int64, c_int,
                                   c_int, c_void_p]),
     "dlbb_embedding_fwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int, c_int,
@@ -203,7 +205,8 @@ def _load() -> ctypes.CDLL:
                                 ("DLBB_WGRAD_ORDER", "dlbb_gemm_wgrad_set_order"),
                                 ("DLBB_CHUNK_NT", "dlbb_chunk_copy_set_nt"),
                                 ("DLBB_SPLIT_REDUCE_VARIANT", "dlbb_split_reduce_set_variant"),
-                                ("DLBB_ATTN_FUSE_DELTA", "dlbb_attn_set_fuse_delta")):
+                                ("DLBB_ATTN_FUSE_DELTA", "dlbb_attn_set_fuse_delta"),
+                                ("DLBB_ATTN_FWD_VARIANT", "dlbb_attn_set_fwd_variant")):
                 if os.environ.get(env, "") != "":
                     getattr(lib, setter)(int(os.environ[env]))
             _lib = lib

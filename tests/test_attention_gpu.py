@@ -36,6 +36,40 @@ def test_attn_fwd_matches_fp32_reference(B, T, H):
     torch.testing.assert_close(lse, ref_lse, rtol=1e-3, atol=2e-3)
 
 
+@pytest.mark.parametrize("variant", list(range(8)))
+@pytest.mark.parametrize("B,T,H", [(2, 200, 2), (2, 1024, 2), (1, 333, 1)])
+def test_attn_fwd_variants_match_fp32_reference(B, T, H, variant):
+    """Every forward schedule variant (batched K reads / permlane exchange / incremental DMA
+    addresses, csrc/attention.hip) against the fp32 reference, incl. T not a multiple of 64
+    (the clamped last tile) and the asymmetric one-hot V check."""
+    from distributed_llm_backend_benchmark_amd.ops import _lib
+    from distributed_llm_backend_benchmark_amd.ops.attention import attn_fwd
+
+    lib = _lib.lib()
+    old = lib.dlbb_attn_get_fwd_variant()
+    try:
+        lib.dlbb_attn_set_fwd_variant(variant)
+        g = torch.Generator(device="cuda").manual_seed(T + H + variant)
+        qkv = (torch.randn(B, T, 3 * H * 64, device="cuda", generator=g) * 1.5).to(torch.bfloat16)
+        out, lse = attn_fwd(qkv, H)
+        ref, ref_lse = _ref(qkv, H)
+        torch.testing.assert_close(out.float(), ref, rtol=2e-2, atol=2e-2)
+        torch.testing.assert_close(lse, ref_lse, rtol=1e-3, atol=2e-3)
+        D = 64
+        q = torch.zeros(1, 128, 3 * D, device="cuda")
+        q[0, :, D:2 * D] = torch.randn(128, D, device="cuda", generator=g)
+        q[0, :, :D] = torch.randn(128, D, device="cuda", generator=g)
+        vv = torch.zeros(128, D, device="cuda")
+        vv[torch.arange(128), torch.arange(128) % D] = torch.arange(128, device="cuda").float() / 128
+        q[0, :, 2 * D:] = vv
+        q = q.to(torch.bfloat16)
+        o1, _ = attn_fwd(q, 1)
+        r1, _ = _ref(q, 1)
+        torch.testing.assert_close(o1.float(), r1, rtol=2e-2, atol=1e-2)
+    finally:
+        lib.dlbb_attn_set_fwd_variant(old)
+
+
 def test_attn_asymmetric_values():
     """V = one-hot rows: the output picks softmax weights of the right keys (catches a
     transposed V read or a permuted key order in P)."""
