@@ -448,6 +448,10 @@ constexpr int kBwdKeys = 128;
 constexpr int kSlice = 64;                   // queries staged per barrier pair (2 x 32)
 constexpr int kSliceImg = kSlice * 128;      // 8 KiB
 
+// INC: DMA sources of the Q / dO slice images from per-lane base pointers + one uniform offset
+// per slice (the clamped per-row 64-bit address arithmetic only on a slice that crosses T); the
+// forward's variant bit 4, measured 3 % there (A/B: dlbb_attn_set_bwd_incr)
+template <bool INC>
 __global__ void __launch_bounds__(kAttnThreads, 2) attn_bwd_dkdv_d64_kernel(AttnBwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = threadIdx.x & 63;
@@ -497,8 +501,35 @@ __global__ void __launch_bounds__(kAttnThreads, 2) attn_bwd_dkdv_d64_kernel(Attn
                                        (lds_vptr_t)(rowv(c) + 64 * wave), 4, 0, 0);
     }
   };
-  stage64(base_bt + hoff, a.ld, kb0, a.T, imgQ(0), wave, lane);
-  stage64(dout_bt + hoff, a.ldo, kb0, a.T, imgG(0), wave, lane);
+  // INC: this lane's Q / dO sources for image rows wave * 16 + i * 8 + lane / 8 of slice 0
+  const uint16_t* qsrc[2];
+  const uint16_t* gsrc[2];
+  if constexpr (INC) {
+    const int r_in = lane >> 3, slot = lane & 7;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int row = wave * 16 + i * 8 + r_in;
+      qsrc[i] = base_bt + hoff + static_cast<int64_t>(kb0 + row) * a.ld + (slot ^ bswz(row)) * 8;
+      gsrc[i] = dout_bt + hoff + static_cast<int64_t>(kb0 + row) * a.ldo + (slot ^ bswz(row)) * 8;
+    }
+  }
+  auto stage_slice = [&](int q0, int c) {
+    if constexpr (INC) {
+      if (q0 + kSlice <= a.T) {                     // wave-uniform: no row past T
+        const int d = q0 - kb0;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          attn_glds16(qsrc[i] + static_cast<int64_t>(d) * a.ld, imgQ(c) + (wave * 16 + i * 8) * 128);
+          attn_glds16(gsrc[i] + static_cast<int64_t>(d) * a.ldo,
+                      imgG(c) + (wave * 16 + i * 8) * 128);
+        }
+        return;
+      }
+    }
+    stage64(base_bt + hoff, a.ld, q0, a.T, imgQ(c), wave, lane);
+    stage64(dout_bt + hoff, a.ldo, q0, a.T, imgG(c), wave, lane);
+  };
+  stage_slice(kb0, 0);
   stage_rows(kb0, 0);
   for (int i = 0; i < ns; ++i) {
     const int cur = i & 1;
@@ -506,8 +537,7 @@ __global__ void __launch_bounds__(kAttnThreads, 2) attn_bwd_dkdv_d64_kernel(Attn
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();                   // publishes slice i, frees buffer cur^1
     if (i + 1 < ns) {
-      stage64(base_bt + hoff, a.ld, qs + kSlice, a.T, imgQ(cur ^ 1), wave, lane);
-      stage64(dout_bt + hoff, a.ldo, qs + kSlice, a.T, imgG(cur ^ 1), wave, lane);
+      stage_slice(qs + kSlice, cur ^ 1);
       stage_rows(qs + kSlice, cur ^ 1);
     }
     const char* iq = imgQ(cur);
@@ -610,6 +640,7 @@ __device__ __forceinline__ void stage_kv64(const AttnBwdArgs& a, const uint16_t*
   }
 }
 
+template <bool INC>   // as the dK/dV kernel: incremental K / V tile DMA sources
 __global__ void __launch_bounds__(kAttnThreads, 2) attn_bwd_dq_d64_kernel(AttnBwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = threadIdx.x & 63;
@@ -673,13 +704,36 @@ __global__ void __launch_bounds__(kAttnThreads, 2) attn_bwd_dq_d64_kernel(AttnBw
   const int nt = last_key / kKB + 1;
   auto tileK = [&](int c) { return smem + c * 2 * kTileKV; };
   auto tileV = [&](int c) { return smem + c * 2 * kTileKV + kTileKV; };
-  stage_kv64(a, base_bt, 0, hoff, tileK(0), tileV(0), wave, lane);
+  const uint16_t* ksrc[2];
+  if constexpr (INC) {
+    const int r_in = lane >> 3, slot = lane & 7;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int row = wave * 16 + i * 8 + r_in;
+      ksrc[i] = base_bt + static_cast<int64_t>(row) * a.ld + hoff + (slot ^ bswz(row)) * 8 +
+                kAttnD * a.H;
+    }
+  }
+  auto stage = [&](int k0, char* tk, char* tv) {
+    if constexpr (INC) {
+      if (k0 + kKB <= a.T) {                        // wave-uniform: no row past T
+        const int64_t off = static_cast<int64_t>(k0) * a.ld;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          attn_glds16(ksrc[i] + off, tk + (wave * 16 + i * 8) * 128);
+          attn_glds16(ksrc[i] + off + kAttnD * a.H, tv + (wave * 16 + i * 8) * 128);
+        }
+        return;
+      }
+    }
+    stage_kv64(a, base_bt, k0, hoff, tk, tv, wave, lane);
+  };
+  stage(0, tileK(0), tileV(0));
   for (int kt = 0; kt < nt; ++kt) {
     const int cur = kt & 1;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();                   // publishes tile kt, frees buffer cur^1
-    if (kt + 1 < nt)
-      stage_kv64(a, base_bt, (kt + 1) * kKB, hoff, tileK(cur ^ 1), tileV(cur ^ 1), wave, lane);
+    if (kt + 1 < nt) stage((kt + 1) * kKB, tileK(cur ^ 1), tileV(cur ^ 1));
     const int k0 = kt * kKB;
     if (k0 <= q_hi) {
       const char* tk = tileK(cur);
@@ -754,14 +808,22 @@ static int g_attn_concurrent = [] {
 // delta / nls computed inside the dQ kernel (1, default) or by the separate row kernel first (0);
 // the concurrent form always uses the separate kernel (A/B: dlbb_attn_set_fuse_delta)
 static int g_attn_fuse_delta = 1;
-// forward kernel variant (attn_fwd_d64_kernel<V> bit mask; A/B: dlbb_attn_set_fwd_variant)
-static int g_attn_fwd_variant = 0;
+// forward kernel variant (attn_fwd_d64_kernel<V> bit mask; A/B: dlbb_attn_set_fwd_variant).
+// 6 = permlane32 exchange + incremental DMA addresses: 49.8 vs 52.2 us at the GPT-2 shape,
+// 85.6 vs 90.3 (T 2048), 197.2 vs 201.9 (T 4096); the batched K reads (bit 1) measured no gain
+// (profiles/r05_attention/fwd_variants.jsonl)
+static int g_attn_fwd_variant = 6;
+// backward kernels with incremental DMA sources, bit mask: 1 dQ, 2 dK/dV (0: per-row clamped
+// addresses). dK/dV<true> holds 174 VGPRs (occupancy 2 waves / SIMD, vs 3 at 166)
+static int g_attn_bwd_incr = 1;
 
 DLBB_API void dlbb_attn_set_xcd(int on) { g_attn_xcd = on ? 1 : 0; }
 DLBB_API void dlbb_attn_set_fuse_delta(int on) { g_attn_fuse_delta = on ? 1 : 0; }
 DLBB_API void dlbb_attn_set_concurrent(int on) { g_attn_concurrent = on ? 1 : 0; }
-DLBB_API void dlbb_attn_set_fwd_variant(int v) { g_attn_fwd_variant = v >= 0 && v <= 7 ? v : 0; }
+DLBB_API void dlbb_attn_set_fwd_variant(int v) { g_attn_fwd_variant = v >= 0 && v <= 7 ? v : 6; }
 DLBB_API int dlbb_attn_get_fwd_variant() { return g_attn_fwd_variant; }
+DLBB_API void dlbb_attn_set_bwd_incr(int m) { g_attn_bwd_incr = m & 3; }
+DLBB_API int dlbb_attn_get_bwd_incr() { return g_attn_bwd_incr; }
 
 // Per-device side stream + fork/join events for the concurrent backward (created once; a fork
 // through an event recorded on the caller's stream is also how a HIP-graph capture of that
@@ -853,10 +915,19 @@ DLBB_API int dlbb_attn_bwd(const void* qkv, int64_t ld, const void* out, const v
     if ((e = hipStreamWaitEvent(sd->s, sd->fork, 0)) != hipSuccess) return e;
     dq_stream = sd->s;
   }
-  hipLaunchKernelGGL(attn_bwd_dq_d64_kernel, dim3((T + kQB - 1) / kQB, H, B),
-                     dim3(kAttnThreads), 4 * kTileKV, dq_stream, a);
-  hipLaunchKernelGGL(attn_bwd_dkdv_d64_kernel, dim3((T + kBwdKeys - 1) / kBwdKeys, H, B),
-                     dim3(kAttnThreads), 4 * kSliceImg + 1024, stream, a);
+  const dim3 gq((T + kQB - 1) / kQB, H, B), gk((T + kBwdKeys - 1) / kBwdKeys, H, B);
+  if (g_attn_bwd_incr & 1)
+    hipLaunchKernelGGL(attn_bwd_dq_d64_kernel<true>, gq, dim3(kAttnThreads), 4 * kTileKV,
+                       dq_stream, a);
+  else
+    hipLaunchKernelGGL(attn_bwd_dq_d64_kernel<false>, gq, dim3(kAttnThreads), 4 * kTileKV,
+                       dq_stream, a);
+  if (g_attn_bwd_incr & 2)
+    hipLaunchKernelGGL(attn_bwd_dkdv_d64_kernel<true>, gk, dim3(kAttnThreads),
+                       4 * kSliceImg + 1024, stream, a);
+  else
+    hipLaunchKernelGGL(attn_bwd_dkdv_d64_kernel<false>, gk, dim3(kAttnThreads),
+                       4 * kSliceImg + 1024, stream, a);
   if (sd) {
     hipError_t e;
     if ((e = hipEventRecord(sd->join, sd->s)) != hipSuccess) return e;

@@ -122,6 +122,8 @@ _SIGS = {
     "dlbb_attn_set_fuse_delta": (None, [c_int]),
     "dlbb_attn_set_fwd_variant": (None, [c_int]),
     "dlbb_attn_get_fwd_variant": (c_int, []),
+    "dlbb_attn_set_bwd_incr": (None, [c_int]),
+    "dlbb_attn_get_bwd_incr": (c_int, []),
     "dlbb_split_reduce": (c_int, [c_void_p, c_void_p, c_int, c_int64, c_void_p, c_int64, c_int,
                                   c_int, c_void_p]),
     "dlbb_embedding_fwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int, c_int,
@@ -206,7 +208,8 @@ def _load() -> ctypes.CDLL:
                                 ("DLBB_CHUNK_NT", "dlbb_chunk_copy_set_nt"),
                                 ("DLBB_SPLIT_REDUCE_VARIANT", "dlbb_split_reduce_set_variant"),
                                 ("DLBB_ATTN_FUSE_DELTA", "dlbb_attn_set_fuse_delta"),
-                                ("DLBB_ATTN_FWD_VARIANT", "dlbb_attn_set_fwd_variant")):
+                                ("DLBB_ATTN_FWD_VARIANT", "dlbb_attn_set_fwd_variant"),
+                                ("DLBB_ATTN_BWD_INCR", "dlbb_attn_set_bwd_incr")):
                 if os.environ.get(env, "") != "":
                     getattr(lib, setter)(int(os.environ[env]))
             _lib = lib

@@ -132,6 +132,30 @@ def test_attn_bwd_matches_fp32_reference(B, T, H):
         assert err <= 0.03 * scale + 0.02, (name, err, scale)
 
 
+@pytest.mark.parametrize("incr", [0, 1, 2, 3])
+@pytest.mark.parametrize("B,T,H", [(2, 200, 2), (1, 333, 2), (2, 1024, 1)])
+def test_attn_bwd_incremental_dma_bit_exact(B, T, H, incr):
+    """The backward kernels with incremental DMA sources (dQ: bit 1, dK/dV: bit 2) stage the
+    same rows as the per-row clamped form: dQKV bit for bit equal, incl. T % 64 != 0."""
+    from distributed_llm_backend_benchmark_amd.ops import _lib
+    from distributed_llm_backend_benchmark_amd.ops.attention import attn_bwd, attn_fwd
+
+    lib = _lib.lib()
+    old = lib.dlbb_attn_get_bwd_incr()
+    g = torch.Generator(device="cuda").manual_seed(11 * T + H)
+    qkv = torch.randn(B, T, 3 * H * 64, device="cuda", generator=g).to(torch.bfloat16)
+    gout = torch.randn(B, T, H * 64, device="cuda", generator=g).to(torch.bfloat16)
+    out, lse = attn_fwd(qkv, H)
+    try:
+        lib.dlbb_attn_set_bwd_incr(0)
+        ref = attn_bwd(qkv, out, lse, gout, H)
+        lib.dlbb_attn_set_bwd_incr(incr)
+        got = attn_bwd(qkv, out, lse, gout, H)
+    finally:
+        lib.dlbb_attn_set_bwd_incr(old)
+    assert torch.equal(got, ref)
+
+
 def test_attn_bwd_concurrent_matches_sequential():
     """The opt-in concurrent backward (dQ on a forked side stream, joined back) gives bitwise the
     same dQKV as the sequential launch, eagerly and inside a captured HIP graph."""
