@@ -49,7 +49,7 @@ def set_tune_agreement(fn) -> None:
 # timings of different kernels
 _AGREED_ENV = ("DLBB_GEMM", "DLBB_TUNE_TIMING", "DLBB_WGRAD256", "DLBB_PP_TAIL",
                "DLBB_WGRAD_FUSED", "DLBB_GEMM_PERSIST", "DLBB_GEMM_PERSIST_EPI",
-               "DLBB_WGRAD_STREAM", "DLBB_WGRAD_SLOTS")
+               "DLBB_WGRAD_STREAM", "DLBB_WGRAD_SLOTS", "DLBB_WGRAD_IMPL")
 
 
 def _agree_names(kind: str, key, names) -> list:
@@ -568,12 +568,12 @@ def _wgrad_hip_wide(dy2, x2, out, accumulate, split=None, bias_out=None):
 
 
 def wgrad_pp_supported(dy2, x2, out, accumulate, bias_out=None) -> bool:
-    """Contract of the 256^2 ping-pong weight-gradient kernel (``dlbb_gemm_bf16_tn``): no fused
-    bias, accumulate only into bf16, output rows N % 128, columns K % 256, reduction M % 64,
-    32-bit buffer offsets over both operands."""
+    """Contract of the 256^2 ping-pong weight-gradient kernel (``dlbb_gemm_bf16_tn``): accumulate
+    only into bf16, output rows N % 128, columns K % 256, reduction M % 64, 32-bit buffer offsets
+    over both operands (a bias gradient is a separate column sum, :func:`_wgrad_pp`)."""
     M, N = dy2.shape
     K = x2.shape[1]
-    return (bias_out is None and (not accumulate or out.dtype == torch.bfloat16)
+    return ((not accumulate or out.dtype == torch.bfloat16)
             and N % 128 == 0 and K % 256 == 0 and M % 64 == 0
             and M * dy2.stride(0) * 2 < 2 ** 31 and M * x2.stride(0) * 2 < 2 ** 31)
 
@@ -627,6 +627,12 @@ def _wgrad_pp(dy2, x2, out, accumulate, split=None, bias_out=None):
     _pp_launch(dy2, x2, out, accumulate, 0, head, 1)
     if head < N:
         _pp_launch(dy2, x2, out, accumulate, head, N, tsplit)
+    if bias_out is not None:            # no fused bias on this kernel: one column-sum pass
+        db = dy2.sum(0, dtype=torch.float32)
+        if accumulate:
+            bias_out.add_(db.to(bias_out.dtype))
+        else:
+            bias_out.copy_(db)
 
 
 def _wgrad_blas(dy2, x2, out, accumulate, split=None, bias_out=None):
@@ -652,6 +658,14 @@ _WGRAD_IMPLS = {"mfma": _wgrad_hip, "mfma256": _wgrad_hip256, "mfma_wide": _wgra
 
 
 def _wgrad_choice(dy2, x2, out, bias_out=None) -> str:
+    forced = os.environ.get("DLBB_WGRAD_IMPL", "").lower()   # A/B: weight gradients only
+    if forced in _WGRAD_IMPLS:
+        if forced == "pp" and not wgrad_pp_supported(dy2, x2, out, False, bias_out):
+            return "mfma"
+        if (forced == "mfma256" and dy2.shape[1] % 256) or (forced == "mfma_wide" and
+                                                             x2.shape[1] % 256):
+            return "mfma"
+        return forced
     mode = os.environ.get("DLBB_GEMM", "auto").lower()
     if mode in _WGRAD_IMPLS:
         if mode == "pp" and not wgrad_pp_supported(dy2, x2, out, False, bias_out):

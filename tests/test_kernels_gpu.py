@@ -774,6 +774,31 @@ def test_wgrad_matches_fp32(M, N, K, split):
     torch.testing.assert_close(b32, refb + 1, rtol=2e-3, atol=2e-3 * (M ** 0.5))
 
 
+@pytest.mark.parametrize("M,N,K", [(16384, 768, 768), (4096, 2304, 768), (1024, 256, 3072)])
+def test_wgrad_forced_pp_with_bias(monkeypatch, M, N, K):
+    """DLBB_WGRAD_IMPL=pp: the unsplit 256^2 TN ping-pong for dW plus a column-sum pass for the
+    bias gradient (the kernel has no fused bias): bf16 store and bf16 accumulate."""
+    from distributed_llm_backend_benchmark_amd.ops import gemm as G
+
+    monkeypatch.setenv("DLBB_WGRAD_IMPL", "pp")
+    dy = _randn(M, N, seed=31, scale=0.5)
+    x = _randn(M, K, seed=32, scale=0.5)
+    assert G._wgrad_choice(dy, x, torch.empty(N, K, dtype=torch.bfloat16, device=DEV),
+                           torch.empty(N, dtype=torch.bfloat16, device=DEV)) == "pp"
+    ref = dy.float().t() @ x.float()
+    refb = dy.float().sum(0)
+    w = torch.empty(N, K, dtype=torch.bfloat16, device=DEV)
+    b = torch.empty(N, dtype=torch.bfloat16, device=DEV)
+    G.wgrad(dy, x, out=w, bias_out=b)
+    torch.testing.assert_close(w.float(), ref, rtol=2e-2, atol=2e-2 * (M ** 0.5))
+    torch.testing.assert_close(b.float(), refb, rtol=2e-2, atol=2e-2 * (M ** 0.5))
+    w.fill_(1.0)
+    b.fill_(1.0)
+    G.wgrad(dy, x, out=w, accumulate=True, bias_out=b)
+    torch.testing.assert_close(w.float(), ref + 1, rtol=2e-2, atol=2e-2 * (M ** 0.5))
+    torch.testing.assert_close(b.float(), refb + 1, rtol=2e-2, atol=2e-2 * (M ** 0.5))
+
+
 @pytest.mark.parametrize("M,N,K", [(16384, 768, 768), (4096, 2304, 768), (1024, 256, 3072),
                                    (512, 3072, 768), (96, 512, 128)])
 @pytest.mark.parametrize("split", [None, 1, 3])
