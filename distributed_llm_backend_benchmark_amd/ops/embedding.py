@@ -67,6 +67,11 @@ class _EmbeddingFn(torch.autograd.Function):
         sorted_ids = order = None
         if ge is not None:
             sorted_ids, order = sort_ids(ids, wte.shape[0])
+        if sink_e is not None and getattr(wte, "_dlbb_grad_event", None) is not None:
+            # the tied LM head's weight gradient may still be accumulating into the same buffer
+            # on a weight-gradient side stream (ops/linear_fn.py): order after that enqueue (not
+            # after the whole side stream, whose later weight gradients may overlap this kernel)
+            torch.cuda.current_stream(d2.device).wait_event(wte._dlbb_grad_event)
         for e, p in groups:
             g_dt = (e if e is not None else p).dtype
             check(_lib.lib().dlbb_embedding_bwd(

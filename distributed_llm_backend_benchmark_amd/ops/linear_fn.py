@@ -107,6 +107,13 @@ def _weight_grads(weight, bias, du, x2, need_w: bool, want_db: bool, db=None):
                       bias_out=bias.grad if want_db else None)
             du.record_stream(side)
             x2.record_stream(side)
+            if getattr(weight, "_dlbb_sink_uses", 1) > 1:
+                # a multi-use sink (tied LM head / embedding): its other uses accumulate into the
+                # same buffer from other streams and wait for THIS enqueue only (ops/embedding.py)
+                ev = getattr(weight, "_dlbb_grad_event", None)
+                if ev is None:
+                    ev = weight._dlbb_grad_event = torch.cuda.Event()
+                ev.record(side)
         else:
             wgrad(du, x2, out=weight.grad, accumulate=acc,
                   bias_out=bias.grad if want_db else None)

@@ -725,6 +725,6 @@ class FlatParamTrainer:
             h.remove()
         for p in self._params:
             for attr in ("_dlbb_grad_sink", "_dlbb_grad_stream", "_dlbb_sink_count",
-                         "_dlbb_grad_fresh"):
+                         "_dlbb_grad_fresh", "_dlbb_grad_event"):
                 if hasattr(p, attr):
                     delattr(p, attr)
