@@ -723,6 +723,38 @@ def test_gpt2_grad_sinks_match_autograd():
     assert not any(hasattr(p, "_dlbb_grad_sink") for p in m.parameters())
 
 
+def test_gpt2_tied_sink_unfused_lm_head_matches_autograd():
+    """LM head through linear_train (targets=None: loss computed outside the model): the tied
+    weight's LM-head gradient runs on the weight-gradient side stream, the embedding backward
+    accumulates into the same buffer on the main stream after waiting for that enqueue — the flat
+    gradient of wte must equal plain autograd (repeated: a missing wait shows as a race)."""
+    import torch.nn.functional as F
+
+    from distributed_llm_backend_benchmark_amd.models.gpt2 import GPT2, GPT2Config
+    from distributed_llm_backend_benchmark_amd.parallel.ddp import FlatParamTrainer
+
+    cfg = GPT2Config(vocab_size=4096, block_size=256, n_layer=2, n_head=4, n_embd=256)
+    dev = torch.device("cuda")
+    idx = torch.randint(0, cfg.vocab_size, (8, 256), device=dev)
+    ref = GPT2(cfg, device=dev, seed=12)
+    F.cross_entropy(ref(idx).float().view(-1, cfg.vocab_size), idx.view(-1)).backward()
+    m = GPT2(cfg, device=dev, seed=12)
+    tr = FlatParamTrainer(m, None, lr=1e-3, bucket_mb=0.25)
+    assert getattr(m.wte, "_dlbb_grad_stream", None) is not None
+    o = tr._offsets[id(m.wte)]
+    want = ref.wte.grad.float()
+    for _ in range(3):
+        tr.zero_grad()
+        tr._reset()
+        F.cross_entropy(m(idx).float().view(-1, cfg.vocab_size), idx.view(-1)).backward()
+        tr.finish()
+        torch.cuda.synchronize()
+        g = tr.flat_grad[o:o + m.wte.numel()].float().view_as(m.wte)
+        err = float((g - want).abs().max())
+        assert err <= 2e-2 * max(1.0, float(want.abs().max())), err
+    tr.close()
+
+
 def test_zero2_and_checkpoint_world1_gpu(tmp_path):
     """ZeRO-2 trainer on the GPU (world 1 over RCCL) tracks DDP, and its checkpoint resumes
     bit-exactly with HIP kernels (AdamW, LN, attention, GEMMs) in the loop."""
