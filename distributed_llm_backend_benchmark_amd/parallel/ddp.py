@@ -41,7 +41,7 @@ from ..ops import FlatAdamW
 from ..ops.elementwise import ChunkTable, ScaleTable, reduce_sum, spin_ns
 from ..utils import tracing
 from .comm import Comm
-from .streams import concurrent_stream
+from .streams import concurrent_stream, cu_share_stream
 
 _GRAD_SINKS = os.environ.get("DLBB_GRAD_SINKS", "1") != "0"   # A/B switch for the sinks
 # sink dW GEMMs on a side stream (default on; DLBB_WGRAD_STREAM=0 for the A/B). Rounds 1-2
@@ -54,6 +54,9 @@ _WGRAD_STREAM = os.environ.get("DLBB_WGRAD_STREAM", "1") == "1"
 # number of side streams the weight gradients are dealt over, round-robin by parameter (A/B;
 # with k > 1 a weight-gradient kernel depends only on its dY and on the one k layers back)
 _WGRAD_STREAMS = max(1, int(os.environ.get("DLBB_WGRAD_STREAMS", "1")))
+# "num/den": the weight-gradient side stream(s) run on that share of every XCD's CUs (hardware CU
+# mask, parallel/streams.py cu_share_stream), leaving the rest to the critical path (A/B)
+_WGRAD_CU_SHARE = os.environ.get("DLBB_WGRAD_CU_SHARE", "")
 # priority of the dedicated bucket-reduction stream: 0 = normal (default, measured), -1 = high
 # (A/B knob; see the module docstring and profiles/r02_overlap/SUMMARY.md)
 _COMM_PRIORITY = int(os.environ.get("DLBB_COMM_STREAM_PRIORITY", "0"))
@@ -168,12 +171,17 @@ class FlatParamTrainer:
         self._params = order
         # weight-gradient GEMMs of sink params run on this side stream (off the backward's
         # critical path); bucket reductions and the optimizer are ordered after it
-        self._wgrad_stream = (concurrent_stream(dev, "ddp_wgrad")
-                              if mode == "view" and dev.type == "cuda" and _GRAD_SINKS
-                              and _WGRAD_STREAM else None)
-        self._wgrad_streams = ([self._wgrad_stream] + [concurrent_stream(dev, f"ddp_wgrad{i}")
-                                                       for i in range(1, _WGRAD_STREAMS)]
-                               if self._wgrad_stream is not None else [])
+        side_ok = mode == "view" and dev.type == "cuda" and _GRAD_SINKS and _WGRAD_STREAM
+        if side_ok and _WGRAD_CU_SHARE:
+            num, den = (int(v) for v in _WGRAD_CU_SHARE.split("/"))
+            self._wgrad_streams = [cu_share_stream(dev, f"ddp_wgrad{i}", num, den)
+                                   for i in range(_WGRAD_STREAMS)]
+            self._wgrad_stream = self._wgrad_streams[0]
+        else:
+            self._wgrad_stream = concurrent_stream(dev, "ddp_wgrad") if side_ok else None
+            self._wgrad_streams = ([self._wgrad_stream] + [
+                concurrent_stream(dev, f"ddp_wgrad{i}") for i in range(1, _WGRAD_STREAMS)]
+                if self._wgrad_stream is not None else [])
         n_sink = 0
         if mode == "view":
             for p, o in zip(order, offs):

@@ -130,3 +130,39 @@ def reset() -> None:
     """Forget the handed-out streams (tests)."""
     _CACHE.clear()
     _GROUPS.clear()
+
+
+_SHARE_CACHE: Dict[Tuple[int, str, int, int], "torch.cuda.Stream"] = {}
+
+
+def cu_share_stream(device, role: str, num: int, den: int) -> "torch.cuda.Stream":
+    """A stream whose kernels run only on ``num / den`` of every XCD's CUs (a hardware CU mask,
+    ``csrc/streams.hip``), as a torch ``ExternalStream``; created once per (device, role, share)
+    and kept for the process lifetime. Raises if the runtime refuses the mask or the stream does
+    not run beside the current stream."""
+    from ..ops import _lib
+
+    dev = torch.device(device)
+    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    key = (idx, role, int(num), int(den))
+    if key in _SHARE_CACHE:
+        return _SHARE_CACHE[key]
+    import ctypes
+
+    ncu = torch.cuda.get_device_properties(idx).multi_processor_count
+    handle, kept = ctypes.c_void_p(), ctypes.c_int(0)
+    with torch.cuda.device(idx):
+        rc = _lib.lib().dlbb_stream_create_cu_share(ncu, int(num), int(den), ctypes.byref(handle),
+                                                    ctypes.byref(kept))
+    if rc != 0 or not handle.value:
+        raise RuntimeError(f"CU-masked stream for {role!r} refused (hip error {rc})")
+    s = torch.cuda.ExternalStream(handle.value, device=torch.device("cuda", idx))
+    got = _lib.lib().dlbb_stream_cu_count(ctypes.c_void_p(handle.value), ncu)
+    if got != kept.value:
+        raise RuntimeError(f"CU mask of {role!r}: {got} CUs active, {kept.value} requested")
+    if not runs_concurrently(torch.cuda.current_stream(dev), s, dev):
+        warnings.warn(f"CU-masked stream for {role!r} does not run beside the compute stream",
+                      RuntimeWarning, stacklevel=2)
+    s.dlbb_cus = got
+    _SHARE_CACHE[key] = s
+    return s

@@ -897,3 +897,34 @@ def test_ddp_overlapped_optimizer_is_bit_exact(mode):
         tr.close()
     assert out[0][0] == out[1][0]
     assert torch.equal(out[0][1], out[1][1])
+
+
+def test_cu_share_stream_and_ddp_step(monkeypatch):
+    """A weight-gradient side stream confined to a share of every XCD's CUs (hardware CU mask):
+    the mask holds the requested CU count, kernels on it compute correctly, and a DDP step with
+    it trains (same buckets / optimizer path)."""
+    from distributed_llm_backend_benchmark_amd.models.gpt2 import GPT2, GPT2Config
+    from distributed_llm_backend_benchmark_amd.ops import linear
+    from distributed_llm_backend_benchmark_amd.parallel import ddp
+    from distributed_llm_backend_benchmark_amd.parallel.streams import cu_share_stream
+
+    dev = torch.device("cuda", 0)
+    ncu = torch.cuda.get_device_properties(0).multi_processor_count
+    s = cu_share_stream(dev, "test_share", 1, 4)
+    assert s.dlbb_cus == sum(1 for i in range(ncu) if (i // 8) % 4 < 1)
+    assert cu_share_stream(dev, "test_share", 1, 4) is s
+    x = torch.randn(512, 256, device=dev).to(torch.bfloat16)
+    w = torch.randn(384, 256, device=dev).to(torch.bfloat16)
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        y = linear(x, w, out_dtype=torch.float32)
+    torch.cuda.current_stream().wait_stream(s)
+    torch.testing.assert_close(y, x.float() @ w.float().t(), rtol=2e-3, atol=2e-2)
+    monkeypatch.setattr(ddp, "_WGRAD_CU_SHARE", "1/2")
+    cfg = GPT2Config(vocab_size=1024, block_size=128, n_layer=2, n_head=4, n_embd=256)
+    tr = ddp.FlatParamTrainer(GPT2(cfg, device=dev, seed=3), None, lr=1e-3, bucket_mb=0.5)
+    assert tr._wgrad_stream is not None and getattr(tr._wgrad_stream, "dlbb_cus", 0) > 0
+    idx = torch.randint(0, cfg.vocab_size, (4, 129), device=dev)
+    losses = [tr.step(idx[:, :-1], idx[:, 1:]) for _ in range(6)]
+    assert all(map(lambda v: v == v, losses)) and losses[-1] < losses[0], losses
+    tr.close()
