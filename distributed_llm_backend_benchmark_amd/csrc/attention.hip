@@ -101,13 +101,22 @@ __device__ __forceinline__ float xhalf_max(float x) {
   return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
 }
 
+// v_max3_f32 as one instruction (fmaxf on MFMA outputs gets canonicalising v_max first)
+__device__ __forceinline__ float max3_asm(float a, float b, float c) {
+  float r;
+  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+
 // Forward variants (bit mask, A/B via dlbb_attn_set_fwd_variant):
 //   1: the tile's 8 K fragments read up front (asm ds_read_b128, one counted lgkmcnt wait per
 //      32-key half) — the compiler's schedule re-used one register quad and waited for each read
 //      in front of its MFMA (8 LDS round trips per tile);
 //   2: the row-max exchange with the other lane half by v_permlane32_swap (no LDS round trip);
 //   4: K/V DMA sources from per-lane base pointers + one uniform offset per tile (the clamped
-//      per-row 64-bit address arithmetic only on a tile that crosses T).
+//      per-row 64-bit address arithmetic only on a tile that crosses T);
+//   8: row max and row sum as pairwise trees (depth 5) instead of 32-long dependent chains
+//      (instantiated as 14 = 2 | 4 | 8 only).
 template <int V>
 __global__ void __launch_bounds__(kAttnThreads, 2) attn_fwd_d64_kernel(AttnArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -233,18 +242,32 @@ __global__ void __launch_bounds__(kAttnThreads, 2) attn_fwd_d64_kernel(AttnArgs 
       const bool diag = k0 + kKB - 1 > qw;          // some key of this tile beyond some query
       float mx = -INFINITY;                          // max of the RAW scores (scale > 0)
       if (diag) {
+        // key(kk, e) = k0 + 4 hi + const(kk, e): one per-lane threshold, compile-time offsets
+        const int th = qme - k0 - 4 * hi;
 #pragma unroll
         for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
-          for (int e = 0; e < 16; ++e) {
-            const int key = k0 + kk * 32 + (e & 3) + 8 * (e >> 2) + 4 * hi;
-            if (key > qme) s[kk][e] = -INFINITY;
-          }
+          for (int e = 0; e < 16; ++e)
+            if (kk * 32 + (e & 3) + 8 * (e >> 2) > th) s[kk][e] = -INFINITY;
       }
+      if constexpr ((V & 8) != 0) {
+        // 3-ary tree of v_max3 (depth 4: 32 -> 11 -> 4 -> 2 -> 1) instead of a 16-long
+        // dependent v_max3 chain
+        float v[32], t[11];
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk)
+        for (int e = 0; e < 16; ++e) { v[e] = s[0][e]; v[16 + e] = s[1][e]; }
 #pragma unroll
-        for (int e = 0; e < 16; ++e) mx = fmaxf(mx, s[kk][e]);
+        for (int j = 0; j < 10; ++j) t[j] = max3_asm(v[3 * j], v[3 * j + 1], v[3 * j + 2]);
+        t[10] = max3_asm(v[30], v[31], v[31]);
+        const float u0 = max3_asm(t[0], t[1], t[2]), u1 = max3_asm(t[3], t[4], t[5]);
+        const float u2 = max3_asm(t[6], t[7], t[8]), u3 = max3_asm(t[9], t[10], t[10]);
+        mx = max3_asm(max3_asm(u0, u1, u2), u3, u3);
+      } else {
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+          for (int e = 0; e < 16; ++e) mx = fmaxf(mx, s[kk][e]);
+      }
       if constexpr ((V & 2) != 0)
         mx = xhalf_max(mx);
       else
@@ -257,11 +280,23 @@ __global__ void __launch_bounds__(kAttnThreads, 2) attn_fwd_d64_kernel(AttnArgs 
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
-        for (int e = 0; e < 16; ++e) {
-          const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(s[kk][e], a.scale_log2, -mn));
-          s[kk][e] = p;
-          ls += p;
-        }
+        for (int e = 0; e < 16; ++e)
+          s[kk][e] = __builtin_amdgcn_exp2f(__builtin_fmaf(s[kk][e], a.scale_log2, -mn));
+      if constexpr ((V & 8) != 0) {
+        float t[16];
+#pragma unroll
+        for (int e = 0; e < 16; ++e) t[e] = s[0][e] + s[1][e];
+#pragma unroll
+        for (int w = 8; w >= 1; w >>= 1)
+#pragma unroll
+          for (int e = 0; e < w; ++e) t[e] += t[e + w];
+        ls = t[0];
+      } else {
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+          for (int e = 0; e < 16; ++e) ls += s[kk][e];
+      }
       l = l * alpha + ls;
       if (__any(rescale)) {                          // wave-uniform skip when no max moved
 #pragma unroll
@@ -820,7 +855,9 @@ static int g_attn_bwd_incr = 1;
 DLBB_API void dlbb_attn_set_xcd(int on) { g_attn_xcd = on ? 1 : 0; }
 DLBB_API void dlbb_attn_set_fuse_delta(int on) { g_attn_fuse_delta = on ? 1 : 0; }
 DLBB_API void dlbb_attn_set_concurrent(int on) { g_attn_concurrent = on ? 1 : 0; }
-DLBB_API void dlbb_attn_set_fwd_variant(int v) { g_attn_fwd_variant = v >= 0 && v <= 7 ? v : 6; }
+DLBB_API void dlbb_attn_set_fwd_variant(int v) {
+  g_attn_fwd_variant = (v >= 0 && v <= 7) || v == 14 ? v : 6;
+}
 DLBB_API int dlbb_attn_get_fwd_variant() { return g_attn_fwd_variant; }
 DLBB_API void dlbb_attn_set_bwd_incr(int m) { g_attn_bwd_incr = m & 3; }
 DLBB_API int dlbb_attn_get_bwd_incr() { return g_attn_bwd_incr; }
@@ -867,7 +904,7 @@ DLBB_API int dlbb_attn_fwd(const void* qkv, int64_t ld, void* out, int64_t ldo, 
   case N:                                                                                  \
     hipLaunchKernelGGL(attn_fwd_d64_kernel<N>, grid, dim3(kAttnThreads), 4 * kTileKV, stream, a); \
     break;
-    FWD_V(1) FWD_V(2) FWD_V(3) FWD_V(4) FWD_V(5) FWD_V(6) FWD_V(7)
+    FWD_V(1) FWD_V(2) FWD_V(3) FWD_V(4) FWD_V(5) FWD_V(6) FWD_V(7) FWD_V(14)
 #undef FWD_V
     default:
       hipLaunchKernelGGL(attn_fwd_d64_kernel<0>, grid, dim3(kAttnThreads), 4 * kTileKV, stream, a);

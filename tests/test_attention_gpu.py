@@ -36,7 +36,7 @@ def test_attn_fwd_matches_fp32_reference(B, T, H):
     torch.testing.assert_close(lse, ref_lse, rtol=1e-3, atol=2e-3)
 
 
-@pytest.mark.parametrize("variant", list(range(8)))
+@pytest.mark.parametrize("variant", list(range(8)) + [14])
 @pytest.mark.parametrize("B,T,H", [(2, 200, 2), (2, 1024, 2), (1, 333, 1)])
 def test_attn_fwd_variants_match_fp32_reference(B, T, H, variant):
     """Every forward schedule variant (batched K reads / permlane exchange / incremental DMA

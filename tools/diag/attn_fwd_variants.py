@@ -12,7 +12,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspa
 from distributed_llm_backend_benchmark_amd.ops import _lib  # noqa: E402
 from distributed_llm_backend_benchmark_amd.ops.attention import attn_fwd  # noqa: E402
 
-VARIANTS = [int(v) for v in os.environ.get("ATTN_VARIANTS", "0,1,2,3,4,5,6,7").split(",")]
+VARIANTS = [int(v) for v in os.environ.get("ATTN_VARIANTS", "0,2,4,6,7,14").split(",")]
 lib = _lib.lib()
 for B, T, H in ((16, 1024, 12), (8, 2048, 12), (4, 4096, 16)):
     qkv = torch.randn(B, T, 3 * H * 64, device="cuda").to(torch.bfloat16)
