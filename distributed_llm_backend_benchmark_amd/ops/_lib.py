@@ -122,6 +122,7 @@ _SIGS = {
     "dlbb_attn_set_fuse_delta": (None, [c_int]),
     "dlbb_stream_create_cu_share": (c_int, [c_int, c_int, c_int, c_void_p, c_void_p]),
     "dlbb_stream_cu_count": (c_int, [c_void_p, c_int]),
+    "dlbb_stream_fork": (c_int, [c_void_p, c_void_p, c_int]),
     "dlbb_attn_set_fwd_variant": (None, [c_int]),
     "dlbb_attn_get_fwd_variant": (c_int, []),
     "dlbb_attn_set_bwd_incr": (None, [c_int]),

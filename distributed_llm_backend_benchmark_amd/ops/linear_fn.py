@@ -101,7 +101,9 @@ def _weight_grads(weight, bias, du, x2, need_w: bool, want_db: bool, db=None):
             # dW is off the backward's critical path: run it on the trainer's side stream
             # so it overlaps the next layer's dgrad / memory-bound kernels; the trainer
             # orders its bucket reductions and the optimizer after that stream
-            side.wait_stream(torch.cuda.current_stream(du.device))
+            from ..parallel.streams import fork
+
+            fork(side)                      # no system-scope fence (parallel/streams.py)
             with torch.cuda.stream(side):
                 wgrad(du, x2, out=weight.grad, accumulate=acc,
                       bias_out=bias.grad if want_db else None)

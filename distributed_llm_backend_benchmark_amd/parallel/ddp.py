@@ -41,7 +41,7 @@ from ..ops import FlatAdamW
 from ..ops.elementwise import ChunkTable, ScaleTable, reduce_sum, spin_ns
 from ..utils import tracing
 from .comm import Comm
-from .streams import concurrent_stream, cu_share_stream
+from .streams import concurrent_stream, cu_share_stream, fork
 
 _GRAD_SINKS = os.environ.get("DLBB_GRAD_SINKS", "1") != "0"   # A/B switch for the sinks
 # sink dW GEMMs on a side stream (default on; DLBB_WGRAD_STREAM=0 for the A/B). Rounds 1-2
@@ -381,7 +381,7 @@ class FlatParamTrainer:
                                 and self._wgrad_stream is not None
                                 else concurrent_stream(dev, "ddp_opt"))
         os_ = self._opt_stream
-        os_.wait_stream(torch.cuda.current_stream(dev))
+        fork(os_)
         self._wait_wgrad(os_)
         with torch.cuda.stream(os_):
             self._wait_bucket(b)
@@ -407,7 +407,7 @@ class FlatParamTrainer:
         if self._emu_zero is not None:
             buf = self.flat_grad[b.start:b.end]
             cs = self._comm_stream
-            cs.wait_stream(torch.cuda.current_stream(buf.device))
+            fork(cs)
             with torch.cuda.stream(cs):
                 self._tl_mark(b, "start", cs)
                 reduce_sum([buf, self._emu_zero[:buf.numel()]], out=buf,
@@ -427,7 +427,7 @@ class FlatParamTrainer:
         ws = self._wgrad_stream
         if b.idx in self._bucket_reg:
             cs = self._comm_stream
-            cs.wait_stream(torch.cuda.current_stream(buf.device))
+            fork(cs)
             if ws is not None:
                 self._wait_wgrad(cs)
             with torch.cuda.stream(cs):
@@ -440,7 +440,7 @@ class FlatParamTrainer:
         elif (self.allreduce == "custom" and self._car is not None and self._car.healthy
               and self._car.supports(buf)):
             cs = self._comm_stream
-            cs.wait_stream(torch.cuda.current_stream(buf.device))
+            fork(cs)
             if ws is not None:
                 self._wait_wgrad(cs)
             with torch.cuda.stream(cs):
@@ -453,7 +453,7 @@ class FlatParamTrainer:
             # our RCCL communicator on the dedicated comm stream, ordered after the
             # producing backward kernels; finish() joins the stream
             cs = self._comm_stream
-            cs.wait_stream(torch.cuda.current_stream(buf.device))
+            fork(cs)
             if ws is not None:
                 self._wait_wgrad(cs)
             self._tl_mark(b, "start", cs)
@@ -477,7 +477,7 @@ class FlatParamTrainer:
         stream waiting on its own event inside a HIP-graph capture crashes capture_end)."""
         for ws in self._wgrad_streams:
             if ws != stream:
-                stream.wait_stream(ws)
+                fork(stream, ws)
 
     def _mark_done(self, b: _Bucket, cs) -> None:
         """Per-bucket completion event on the comm stream (waited per bucket by the split
@@ -559,7 +559,7 @@ class FlatParamTrainer:
                 head, tail = self.buckets[:-1], self.buckets[-1]
                 if self._opt_issued:
                     # head AdamW already issued bucket by bucket during backward
-                    torch.cuda.current_stream(self.flat_grad.device).wait_stream(self._opt_stream)
+                    fork(torch.cuda.current_stream(self.flat_grad.device), self._opt_stream)
                 else:
                     for b in head:
                         self._wait_bucket(b)

@@ -166,3 +166,26 @@ def cu_share_stream(device, role: str, num: int, den: int) -> "torch.cuda.Stream
     s.dlbb_cus = got
     _SHARE_CACHE[key] = s
     return s
+
+
+# how a side stream is ordered after the compute stream: "nofence" (default) / "device" = one
+# event record + wait through csrc/streams.hip dlbb_stream_fork (no system-scope fence / a
+# device-scope release), "torch" = Stream.wait_stream (default HIP event: system-scope fence)
+_FORK_MODE = {"nofence": 1, "device": 2, "torch": 0}[
+    __import__("os").environ.get("DLBB_FORK_EVENT", "nofence")]
+
+
+def fork(to: "torch.cuda.Stream", frm: Optional["torch.cuda.Stream"] = None) -> None:
+    """``to.wait_stream(frm)`` (default: the current stream) without the system-scope fence a
+    default HIP event record performs: on MI355X that fence wrote back and invalidated L2 after
+    every forked-from kernel, a 6-7 us idle gap each on the compute stream (52 per GPT-2 step,
+    ``profiles/r05_step/SUMMARY.md`` §7)."""
+    frm = frm if frm is not None else torch.cuda.current_stream(to.device)
+    if _FORK_MODE == 0 or to.device.type != "cuda":
+        to.wait_stream(frm)
+        return
+    from ..ops import _lib
+
+    rc = _lib.lib().dlbb_stream_fork(frm.cuda_stream, to.cuda_stream, _FORK_MODE)
+    if rc != 0:
+        raise RuntimeError(f"dlbb_stream_fork failed (hip error {rc})")
