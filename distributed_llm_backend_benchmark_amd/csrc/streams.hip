@@ -38,11 +38,9 @@ DLBB_API int dlbb_stream_cu_count(hipStream_t s, int ncu) {
 }
 
 // Fork `to` after the work queued on `from` so far, with an event that skips the system-scope
-// fence. A default HIP event's record performs a system-scope fence — L2 writeback and
-// invalidate — which showed in the GPT-2 step as a 6-7 us idle gap on the compute stream after
-// every kernel that a side stream forked from (52 per step, ~0.36 ms: the weight-gradient
-// forks after each dgrad GEMM). Ordering between two streams of one device needs no system
-// fence: every kernel dispatch already releases its writes at the end of the kernel.
+// fence a default HIP event's record performs (L2 writeback and invalidate, for host
+// visibility). Ordering between two streams of one device needs no system fence: every kernel
+// dispatch already releases its writes at device scope at the end of the kernel.
 // mode 1: hipEventDisableSystemFence, 2: hipEventReleaseToDevice. Events come from a per-device
 // ring (a wait binds to the record that precedes it, so a slot is reusable once re-recorded).
 namespace {

@@ -168,18 +168,22 @@ def cu_share_stream(device, role: str, num: int, den: int) -> "torch.cuda.Stream
     return s
 
 
-# how a side stream is ordered after the compute stream: "nofence" (default) / "device" = one
-# event record + wait through csrc/streams.hip dlbb_stream_fork (no system-scope fence / a
-# device-scope release), "torch" = Stream.wait_stream (default HIP event: system-scope fence)
+# how a side stream is ordered after the compute stream: "device" (default) / "nofence" = one
+# event record + wait through csrc/streams.hip dlbb_stream_fork (a device-scope release / no
+# fence), "torch" = Stream.wait_stream (default HIP event: system-scope fence). GPT-2 step, three
+# interleaved reps (profiles/r05_step/SUMMARY.md §7): torch 17.89-17.98 ms and one 19.53 ms run
+# (compute-stream dispatch stalled ~58 us after every forked-from kernel — the same pattern
+# rocprofv3 shows for torch and nofence events, never for device-scope ones), device
+# 17.86-17.88, nofence 17.81-17.87.
 _FORK_MODE = {"nofence": 1, "device": 2, "torch": 0}[
-    __import__("os").environ.get("DLBB_FORK_EVENT", "nofence")]
+    __import__("os").environ.get("DLBB_FORK_EVENT", "device")]
 
 
 def fork(to: "torch.cuda.Stream", frm: Optional["torch.cuda.Stream"] = None) -> None:
-    """``to.wait_stream(frm)`` (default: the current stream) without the system-scope fence a
-    default HIP event record performs: on MI355X that fence wrote back and invalidated L2 after
-    every forked-from kernel, a 6-7 us idle gap each on the compute stream (52 per GPT-2 step,
-    ``profiles/r05_step/SUMMARY.md`` §7)."""
+    """``to.wait_stream(frm)`` (default: the current stream) through an event without the
+    system-scope fence (cache writeback + invalidate) a default HIP event record performs; two
+    streams of one device need only the device-scope ordering every kernel dispatch already
+    releases (``profiles/r05_step/SUMMARY.md`` §7)."""
     frm = frm if frm is not None else torch.cuda.current_stream(to.device)
     if _FORK_MODE == 0 or to.device.type != "cuda":
         to.wait_stream(frm)
