@@ -19,6 +19,7 @@
 // BM = 32 rows of m per stage, two LDS buffers (32 KiB: three workgroups per CU).
 #include "common.h"
 
+#include <algorithm>
 #include <type_traits>
 
 namespace dlbb {
@@ -488,6 +489,15 @@ static int g_wgrad_stages = 2;
 
 DLBB_API void dlbb_gemm_wgrad_set_stages(int nb) { g_wgrad_stages = nb >= 2 && nb <= 4 ? nb : 2; }
 
+// Minimum dynamic LDS per weight-gradient workgroup (bytes; 0 = what the tile needs). Raising it
+// caps how many of these workgroups one CU holds (48 KiB tiles: 3 per CU), so a CU keeps LDS free
+// for the compute stream's kernels that run beside this side-stream GEMM (A/B:
+// dlbb_gemm_wgrad_set_min_lds, DLBB_WGRAD_MIN_LDS_KB).
+static int g_wgrad_min_lds = 0;
+DLBB_API void dlbb_gemm_wgrad_set_min_lds(int bytes) {
+  g_wgrad_min_lds = bytes > 0 && bytes <= 160 * 1024 ? bytes : 0;
+}
+
 // dW[N][K] = A^T B with A = [M][lda] (N columns used), B = [M][ldb] (K columns used), bf16.
 // Requires M % 32 == 0, N % bn == 0, K % 128 == 0, lda/ldb % 8 == 0, 16-B aligned bases;
 // bn = 128 (128 x 128 tiles) or 256 (256 x 128 tiles). ws: fp32 workspace of
@@ -536,7 +546,7 @@ static int wgrad_launch(const void* A, int64_t lda, const void* B, int64_t ldb, 
   const int stages = g_wgrad_stages;
 #define WG_LAUNCH(BIASV, NBV, WMV, WJV)                                                     \
   hipLaunchKernelGGL((wgrad_kernel<BIASV, NBV, WMV, WJV>), grid, dim3(128 * (WMV)),        \
-                     NBV * ((WMV) / 2 + (WJV) / 4) * kTile, stream, a)
+                     std::max(NBV * ((WMV) / 2 + (WJV) / 4) * kTile, g_wgrad_min_lds), stream, a)
 #define WG_STAGES(BIASV, WMV, WJV)                \
   if (stages == 4) WG_LAUNCH(BIASV, 4, WMV, WJV); \
   else if (stages == 3) WG_LAUNCH(BIASV, 3, WMV, WJV); \

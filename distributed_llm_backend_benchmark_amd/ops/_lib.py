@@ -123,6 +123,7 @@ _SIGS = {
     "dlbb_stream_create_cu_share": (c_int, [c_int, c_int, c_int, c_void_p, c_void_p]),
     "dlbb_stream_cu_count": (c_int, [c_void_p, c_int]),
     "dlbb_stream_fork": (c_int, [c_void_p, c_void_p, c_int]),
+    "dlbb_gemm_wgrad_set_min_lds": (None, [c_int]),
     "dlbb_attn_set_fwd_variant": (None, [c_int]),
     "dlbb_attn_get_fwd_variant": (c_int, []),
     "dlbb_attn_set_bwd_incr": (None, [c_int]),
@@ -215,6 +216,8 @@ def _load() -> ctypes.CDLL:
                                 ("DLBB_ATTN_BWD_INCR", "dlbb_attn_set_bwd_incr")):
                 if os.environ.get(env, "") != "":
                     getattr(lib, setter)(int(os.environ[env]))
+            if os.environ.get("DLBB_WGRAD_MIN_LDS_KB", "") != "":
+                lib.dlbb_gemm_wgrad_set_min_lds(int(float(os.environ["DLBB_WGRAD_MIN_LDS_KB"]) * 1024))
             _lib = lib
             return lib
         except BaseException as e:  # remember and re-raise loudly on every use

@@ -49,7 +49,8 @@ def set_tune_agreement(fn) -> None:
 # timings of different kernels
 _AGREED_ENV = ("DLBB_GEMM", "DLBB_TUNE_TIMING", "DLBB_WGRAD256", "DLBB_PP_TAIL",
                "DLBB_WGRAD_FUSED", "DLBB_GEMM_PERSIST", "DLBB_GEMM_PERSIST_EPI",
-               "DLBB_WGRAD_STREAM", "DLBB_WGRAD_SLOTS", "DLBB_WGRAD_IMPL")
+               "DLBB_WGRAD_STREAM", "DLBB_WGRAD_SLOTS", "DLBB_WGRAD_IMPL",
+               "DLBB_WGRAD_MIN_LDS_KB")
 
 
 def _agree_names(kind: str, key, names) -> list:
