@@ -238,6 +238,44 @@ __global__ void __launch_bounds__(kXentFusedThreads) xent_fused2_kernel(
 
 static int g_xent_variant = 2;   // 1 = the v1 pass (kept for A/B), 2 = v2
 
+// The loss normaliser and the mean in ONE workgroup each (the torch form — compare, sum, clamp,
+// cast, reciprocal, sum, multiply — was seven ~5 us launches on the step's critical path).
+// inv = 1 / max(#(target >= 0), 1)
+__global__ void __launch_bounds__(1024) xent_count_inv_kernel(const int64_t* __restrict__ t,
+                                                              int64_t rows, float* inv) {
+  __shared__ int part[16];
+  int c = 0;
+  for (int64_t i = threadIdx.x; i < rows; i += 1024) c += t[i] >= 0 ? 1 : 0;
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) c += __shfl_xor(c, o, 64);
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int n = 0;
+    for (int w = 0; w < 16; ++w) n += part[w];
+    inv[0] = 1.0f / static_cast<float>(n > 0 ? n : 1);
+  }
+}
+
+// out = inv * sum(loss[0 .. rows)) (fp32, fixed summation order: deterministic)
+__global__ void __launch_bounds__(1024) xent_loss_mean_kernel(const float* __restrict__ loss,
+                                                              int64_t rows,
+                                                              const float* __restrict__ inv,
+                                                              float* out) {
+  __shared__ float part[16];
+  float c = 0.f;
+  for (int64_t i = threadIdx.x; i < rows; i += 1024) c += loss[i];
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) c += __shfl_xor(c, o, 64);
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float n = 0.f;
+    for (int w = 0; w < 16; ++w) n += part[w];
+    out[0] = n * inv[0];
+  }
+}
+
 }  // namespace dlbb
 
 using namespace dlbb;
@@ -261,6 +299,20 @@ DLBB_API int dlbb_xent_fused(void* logits, const int64_t* target, float* loss, i
       : nv == 13 ? xent_fused2_kernel<13> : xent_fused2_kernel<16>;
   hipLaunchKernelGGL(k, dim3(static_cast<unsigned>(rows)), dim3(kXentFusedThreads), 0, stream,
                      static_cast<uint16_t*>(logits), target, loss, V, ld, scale);
+  return hipGetLastError();
+}
+
+DLBB_API int dlbb_xent_count_inv(const int64_t* target, int64_t rows, float* inv,
+                                 hipStream_t stream) {
+  if (rows < 0 || !target || !inv) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(xent_count_inv_kernel, dim3(1), dim3(1024), 0, stream, target, rows, inv);
+  return hipGetLastError();
+}
+
+DLBB_API int dlbb_xent_loss_mean(const float* loss, int64_t rows, const float* inv, float* out,
+                                 hipStream_t stream) {
+  if (rows < 0 || !loss || !inv || !out) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(xent_loss_mean_kernel, dim3(1), dim3(1024), 0, stream, loss, rows, inv, out);
   return hipGetLastError();
 }
 

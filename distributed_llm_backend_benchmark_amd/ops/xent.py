@@ -58,15 +58,19 @@ class _LinearXentFn(torch.autograd.Function):
         logits = linear(x2, w)                          # [rows, V] bf16 (autotuned GEMM)
         t = target.reshape(-1).contiguous().to(torch.int64)
         rows = x2.shape[0]
-        loss = torch.empty(rows, dtype=torch.float32, device=x2.device)
-        inv = (1.0 / (t >= 0).sum().clamp_min(1).float()).reshape(1).contiguous()
+        loss = torch.empty(rows + 2, dtype=torch.float32, device=x2.device)
+        inv, out = loss[rows:rows + 1], loss[rows + 1:]  # 1 / count and the mean, same buffer
+        st = _lib.stream(x2.device)
+        check(_lib.lib().dlbb_xent_count_inv(t.data_ptr(), rows, inv.data_ptr(), st),
+              "xent_count_inv")
         check(_lib.lib().dlbb_xent_fused(logits.data_ptr(), t.data_ptr(), loss.data_ptr(), rows,
-                                         V, V, inv.data_ptr(), _lib.stream(x2.device)),
-              "xent_fused")
+                                         V, V, inv.data_ptr(), st), "xent_fused")
+        check(_lib.lib().dlbb_xent_loss_mean(loss.data_ptr(), rows, inv.data_ptr(),
+                                             out.data_ptr(), st), "xent_loss_mean")
         ctx.save_for_backward(x2, w, logits)            # logits now hold dlogits / count
         ctx.shape = x.shape
         ctx.weight = w                                  # leaf parameter: read for its grad sink
-        return loss.sum() * inv.reshape(())
+        return out.reshape(())
 
     @staticmethod
     def backward(ctx, g):
@@ -75,20 +79,40 @@ class _LinearXentFn(torch.autograd.Function):
         from .linear_fn import _sink, sink_fresh, sink_used
 
         x2, w, dl = ctx.saved_tensors
-        gb = g.to(dl.dtype)                             # 1.0 in the usual loss.backward()
+        # the caller may mark the upstream gradient as exactly 1 (mark_unit_upstream: this output
+        # IS the loss passed to .backward()): then no scaling passes over dX and X (2 x 25 MB on
+        # the GPT-2 step's critical path)
+        unit = getattr(ctx, "dlbb_unit_upstream", False)
+        gb = None if unit else g.to(dl.dtype)
+        xs = x2 if unit else x2 * gb
         dx = dw = None
         if ctx.needs_input_grad[0]:
-            dx = _gemm.dgrad(dl, w).mul_(gb).view(ctx.shape)
+            dx = _gemm.dgrad(dl, w)
+            if not unit:
+                dx.mul_(gb)
+            dx = dx.view(ctx.shape)
         if ctx.needs_input_grad[1]:
             if _sink(ctx.weight) is not None:
                 # gradient sink (e.g. the tied embedding): accumulate into .grad in the GEMM —
                 # or store, when this is the first write since zero_grad (the LM head is the
                 # first op of the backward: a beta = 0 GEMM, no read of the 77 MB buffer)
-                wgrad(dl, x2 * gb, out=ctx.weight.grad, accumulate=not sink_fresh(ctx.weight))
+                wgrad(dl, xs, out=ctx.weight.grad, accumulate=not sink_fresh(ctx.weight))
                 sink_used(ctx.weight)
             else:
-                dw = wgrad(dl, x2 * gb)
+                dw = wgrad(dl, xs)
         return dx, dw, None
+
+
+def mark_unit_upstream(loss: torch.Tensor) -> bool:
+    """Declare that ``loss`` itself is what ``.backward()`` is called on (upstream gradient
+    exactly 1): if it is the output of the fused LM head + loss, its backward then skips the
+    upstream-gradient scaling passes. Returns whether it applied (trainers call it on the loss
+    their model returned)."""
+    fn = getattr(loss, "grad_fn", None)
+    if fn is None or type(fn).__name__ != "_LinearXentFnBackward" or loss.dim() != 0:
+        return False
+    fn.dlbb_unit_upstream = True
+    return True
 
 
 def linear_cross_entropy(x: torch.Tensor, w: torch.Tensor, target: torch.Tensor) -> torch.Tensor:

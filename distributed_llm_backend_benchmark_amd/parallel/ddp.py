@@ -39,6 +39,7 @@ import torch.distributed as dist
 
 from ..ops import FlatAdamW
 from ..ops.elementwise import ChunkTable, ScaleTable, reduce_sum, spin_ns
+from ..ops.xent import mark_unit_upstream
 from ..utils import tracing
 from .comm import Comm
 from .streams import concurrent_stream, cu_share_stream, fork
@@ -60,6 +61,8 @@ _WGRAD_CU_SHARE = os.environ.get("DLBB_WGRAD_CU_SHARE", "")
 # priority of the dedicated bucket-reduction stream: 0 = normal (default, measured), -1 = high
 # (A/B knob; see the module docstring and profiles/r02_overlap/SUMMARY.md)
 _COMM_PRIORITY = int(os.environ.get("DLBB_COMM_STREAM_PRIORITY", "0"))
+# mark the model's loss as the backward root (ops.xent.mark_unit_upstream; A/B: 0 = off)
+_UNIT_UPSTREAM = os.environ.get("DLBB_UNIT_UPSTREAM", "1") != "0"
 # split optimizer only: AdamW of a head bucket is issued as soon as that bucket is reduced,
 # during backward, on a stream of its own (1) or on the weight-gradient side stream (2, default),
 # instead of for all head buckets after backward (0). GPT-2 step, three interleaved reps in one
@@ -548,6 +551,8 @@ class FlatParamTrainer:
         with tracing.range("fwd"):
             loss = self.model(idx, targets)
         with tracing.range("bwd+overlapped_grad_sync"):
+            if _UNIT_UPSTREAM:              # loss.backward(): the fused loss skips its scaling
+                mark_unit_upstream(loss)
             loss.backward()
         if self._tl is not None:
             self._tl["bwd_end"] = torch.cuda.Event(enable_timing=True)

@@ -928,3 +928,27 @@ def test_cu_share_stream_and_ddp_step(monkeypatch):
     losses = [tr.step(idx[:, :-1], idx[:, 1:]) for _ in range(6)]
     assert all(map(lambda v: v == v, losses)) and losses[-1] < losses[0], losses
     tr.close()
+
+
+def test_unit_upstream_mark_is_bit_exact():
+    """Marking the fused LM-head loss as the backward root skips the upstream-gradient scaling
+    passes; gradients and loss must be bit-identical to the unmarked backward."""
+    from distributed_llm_backend_benchmark_amd.models.gpt2 import GPT2, GPT2Config
+    from distributed_llm_backend_benchmark_amd.ops.xent import mark_unit_upstream
+
+    cfg = GPT2Config(vocab_size=1024, block_size=128, n_layer=2, n_head=4, n_embd=256)
+    dev = torch.device("cuda")
+    idx = torch.randint(0, cfg.vocab_size, (4, 129), device=dev)
+    out = []
+    for mark in (False, True):
+        m = GPT2(cfg, device=dev, seed=21)
+        loss = m(idx[:, :-1], idx[:, 1:])
+        assert mark_unit_upstream(loss) if mark else True
+        loss.backward()
+        torch.cuda.synchronize()
+        out.append((loss.detach().clone(), [p.grad.clone() for p in m.parameters()]))
+    assert torch.equal(out[0][0], out[1][0])
+    for a, b in zip(out[0][1], out[1][1]):
+        assert torch.equal(a, b)
+    ref = GPT2(cfg, device=dev, seed=21)
+    assert not mark_unit_upstream(ref(idx[:, :-1], idx[:, 1:]) * 2.0)   # not the fused output
