@@ -58,6 +58,9 @@ _WGRAD_STREAMS = max(1, int(os.environ.get("DLBB_WGRAD_STREAMS", "1")))
 # "num/den": the weight-gradient side stream(s) run on that share of every XCD's CUs (hardware CU
 # mask, parallel/streams.py cu_share_stream), leaving the rest to the critical path (A/B)
 _WGRAD_CU_SHARE = os.environ.get("DLBB_WGRAD_CU_SHARE", "")
+# HIP priority of the weight-gradient side stream(s): 0 = normal (default), 1 = low (where the
+# runtime offers it), -1 = high (A/B)
+_WGRAD_PRIORITY = int(os.environ.get("DLBB_WGRAD_STREAM_PRIORITY", "0"))
 # priority of the dedicated bucket-reduction stream: 0 = normal (default, measured), -1 = high
 # (A/B knob; see the module docstring and profiles/r02_overlap/SUMMARY.md)
 _COMM_PRIORITY = int(os.environ.get("DLBB_COMM_STREAM_PRIORITY", "0"))
@@ -181,9 +184,11 @@ class FlatParamTrainer:
                                    for i in range(_WGRAD_STREAMS)]
             self._wgrad_stream = self._wgrad_streams[0]
         else:
-            self._wgrad_stream = concurrent_stream(dev, "ddp_wgrad") if side_ok else None
+            self._wgrad_stream = (concurrent_stream(dev, "ddp_wgrad", _WGRAD_PRIORITY)
+                                  if side_ok else None)
             self._wgrad_streams = ([self._wgrad_stream] + [
-                concurrent_stream(dev, f"ddp_wgrad{i}") for i in range(1, _WGRAD_STREAMS)]
+                concurrent_stream(dev, f"ddp_wgrad{i}", _WGRAD_PRIORITY)
+                for i in range(1, _WGRAD_STREAMS)]
                 if self._wgrad_stream is not None else [])
         n_sink = 0
         if mode == "view":
