@@ -274,7 +274,17 @@ def init_distributed(backend: str = "auto", timeout_s: float = 600.0,
         eager = be == "nccl" and os.environ.get("DLBB_RCCL_EAGER_INIT", "0") == "1"
         if eager:
             kwargs["device_id"] = dev  # eager RCCL communicator init, fixed device binding
-        dist.init_process_group(**kwargs)
+        standalone = "WORLD_SIZE" not in os.environ
+        for attempt in range(5):
+            try:
+                dist.init_process_group(**kwargs)
+                break
+            except Exception as e:  # noqa: BLE001 - only the standalone port race is retried
+                # a private loopback port can be taken between _free_port() and the store's
+                # bind (another process on the box): pick a new one
+                if not standalone or attempt == 4 or "EADDRINUSE" not in str(e):
+                    raise
+                kwargs["init_method"] = f"tcp://127.0.0.1:{_free_port()}"
         owns = True
         if be == "nccl" and not eager:
             # Lazy communicator creation, forced now by one tiny all-reduce on the bound device.
