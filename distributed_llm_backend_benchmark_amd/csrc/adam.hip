@@ -22,6 +22,11 @@ struct AdamArgs {
   float bc1, bc2;     // 1 - beta^t
   float grad_scale;
   const int* step_dev;   // optional: step count read on the device (HIP-graph replayable)
+  // optional row filter: update only the elements of rows r (row_len elements each, row_len %
+  // 8 == 0) with row_mask[r] == row_sel — one table's rows split between two AdamW calls
+  const uint8_t* row_mask;
+  int64_t row_len;
+  int row_sel;
 };
 
 template <int GDT>
@@ -45,6 +50,7 @@ __global__ void __launch_bounds__(256) adamw_kernel(AdamArgs a) {
   };
   for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < nvec;
        i += stride) {
+    if (a.row_mask && a.row_mask[i * 8 / a.row_len] != a.row_sel) continue;
     float p[8], m[8], v[8], g[8];
     load8<DT_F32>(a.p, i, p);
     load8<DT_F32>(a.m, i, m);
@@ -59,7 +65,7 @@ __global__ void __launch_bounds__(256) adamw_kernel(AdamArgs a) {
   }
   if (blockIdx.x == 0) {
     const int64_t t = nvec * 8 + threadIdx.x;
-    if (t < a.n) {
+    if (t < a.n && !(a.row_mask && a.row_mask[t / a.row_len] != a.row_sel)) {
       float p = a.p[t], m = a.m[t], v = a.v[t];
       const float g = Elem<GDT>::ld(static_cast<const typename Elem<GDT>::T*>(a.g), t);
       body(p, m, v, g);
@@ -91,7 +97,7 @@ DLBB_API int dlbb_adamw(float* p, float* m, float* v, const void* g, int grad_dt
   if (step < 1) return hipErrorInvalidValue;
   AdamArgs a{p, m, v, g, static_cast<uint16_t*>(p_bf16), n, lr, beta1, beta2, eps,
              weight_decay, 1.f - powf(beta1, static_cast<float>(step)),
-             1.f - powf(beta2, static_cast<float>(step)), grad_scale, nullptr};
+             1.f - powf(beta2, static_cast<float>(step)), grad_scale, nullptr, nullptr, 1, 0};
   return launch_adamw(a, grad_dtype, stream);
 }
 
@@ -104,6 +110,23 @@ DLBB_API int dlbb_adamw_devstep(float* p, float* m, float* v, const void* g, int
   if (n <= 0) return hipSuccess;
   if (!step_dev) return hipErrorInvalidValue;
   AdamArgs a{p, m, v, g, static_cast<uint16_t*>(p_bf16), n, lr, beta1, beta2, eps,
-             weight_decay, 1.f, 1.f, grad_scale, step_dev};
+             weight_decay, 1.f, 1.f, grad_scale, step_dev, nullptr, 1, 0};
+  return launch_adamw(a, grad_dtype, stream);
+}
+
+// Row-filtered update (either step form: step_dev non-null = device step count, else `step`):
+// only rows r of the [n / row_len, row_len] range with row_mask[r] == row_sel.
+DLBB_API int dlbb_adamw_rows(float* p, float* m, float* v, const void* g, int grad_dtype,
+                             void* p_bf16, int64_t n, float lr, float beta1, float beta2,
+                             float eps, float weight_decay, int step, const int* step_dev,
+                             float grad_scale, const uint8_t* row_mask, int64_t row_len,
+                             int row_sel, hipStream_t stream) {
+  if (n <= 0) return hipSuccess;
+  if (!row_mask || row_len <= 0 || row_len % 8 || n % row_len) return hipErrorInvalidValue;
+  if (!step_dev && step < 1) return hipErrorInvalidValue;
+  const float b1 = step_dev ? 1.f : 1.f - powf(beta1, static_cast<float>(step));
+  const float b2 = step_dev ? 1.f : 1.f - powf(beta2, static_cast<float>(step));
+  AdamArgs a{p, m, v, g, static_cast<uint16_t*>(p_bf16), n, lr, beta1, beta2, eps,
+             weight_decay, b1, b2, grad_scale, step_dev, row_mask, row_len, row_sel};
   return launch_adamw(a, grad_dtype, stream);
 }

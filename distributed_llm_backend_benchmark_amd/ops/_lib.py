@@ -91,6 +91,9 @@ _SIGS = {
     "dlbb_attn_set_xcd": (None, [c_int]),
     "dlbb_attn_set_concurrent": (None, [c_int]),
     "dlbb_xent_set_variant": (None, [c_int]),
+    "dlbb_adamw_rows": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p,
+                                c_int64, c_float, c_float, c_float, c_float, c_float, c_int,
+                                c_void_p, c_float, c_void_p, c_int64, c_int, c_void_p]),
     "dlbb_xent_count_inv": (c_int, [c_void_p, c_int64, c_void_p, c_void_p]),
     "dlbb_xent_loss_mean": (c_int, [c_void_p, c_int64, c_void_p, c_void_p, c_void_p]),
     "dlbb_xent_fused": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int64,

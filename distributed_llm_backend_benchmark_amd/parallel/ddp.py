@@ -66,6 +66,11 @@ _WGRAD_PRIORITY = int(os.environ.get("DLBB_WGRAD_STREAM_PRIORITY", "0"))
 _COMM_PRIORITY = int(os.environ.get("DLBB_COMM_STREAM_PRIORITY", "0"))
 # mark the model's loss as the backward root (ops.xent.mark_unit_upstream; A/B: 0 = off)
 _UNIT_UPSTREAM = os.environ.get("DLBB_UNIT_UPSTREAM", "1") != "0"
+# world 1, overlapped optimizer: the rows of a tied embedding / LM-head table that this step's
+# input ids do not touch have their final gradient after the LM-head backward (the embedding
+# backward adds only to the input ids' rows): their AdamW runs then, during backward, and only
+# the touched rows stay behind the embedding backward (A/B: 0 = off)
+_EARLY_ROWS = os.environ.get("DLBB_EARLY_ROWS", "1") != "0"
 # split optimizer only: AdamW of a head bucket is issued as soon as that bucket is reduced,
 # during backward, on a stream of its own (1) or on the weight-gradient side stream (2, default),
 # instead of for all head buckets after backward (0). GPT-2 step, three interleaved reps in one
@@ -108,6 +113,7 @@ class _Bucket:
         self.done_event = None
         self.table: Optional[ChunkTable] = None
         self.table_key = None
+        self.opt_done = False       # its AdamW range already queued this step
 
 
 class FlatParamTrainer:
@@ -266,6 +272,18 @@ class FlatParamTrainer:
         self._opt_stream = None
         self._opt_issued = 0          # head-bucket AdamW ranges issued in this step's backward
         self._in_step = False         # only step() (which joins the optimizer stream) overlaps
+        self._rows_param = None       # table whose untouched rows update early (_EARLY_ROWS)
+        self._rows_early = False
+        self._row_mask = None
+        if (_EARLY_ROWS and mode == "view" and dev.type == "cuda" and self.world == 1
+                and len(self.buckets) > 1):
+            cands = [q for q in order if getattr(q, "_dlbb_rows_from_input", False)
+                     and getattr(q, "_dlbb_sink_uses", 1) == 2 and hasattr(q, "_dlbb_grad_sink")
+                     and q.dim() == 2 and q.shape[1] % 8 == 0]
+            if len(cands) == 1 and self._bucket_of[id(cands[0])] is self.buckets[-1]:
+                self._rows_param = cands[0]
+                self._row_mask = torch.zeros(cands[0].shape[0], dtype=torch.uint8, device=dev)
+                cands[0]._dlbb_partial_sink = self._on_partial
         self.timeline = False       # record comm events per bucket (comm_tail_report)
         self._tl = None
         self.step_count = 0
@@ -333,9 +351,9 @@ class FlatParamTrainer:
         self.master = self.flat_param.float()
         self.opt = FlatAdamW(self.master, lr=lr, betas=betas, weight_decay=weight_decay)
 
-    def _optimizer_step(self, ranges=None, advance: bool = True) -> None:
+    def _optimizer_step(self, ranges=None, advance: bool = True, rows=None) -> None:
         self.opt.step(self.flat_grad, working_bf16=self.flat_param, grad_scale=1.0 / self.world,
-                      ranges=ranges, advance=advance)
+                      ranges=ranges, advance=advance, rows=rows)
 
     # ------------------------------------------------------------------ buckets
     def _add_bucket(self, start: int, end: int, params) -> None:
@@ -349,6 +367,9 @@ class FlatParamTrainer:
             b.ready, b.launched, b.work = 0, False, None
         self._next = 0
         self._opt_issued = 0
+        self._rows_early = False
+        for b in self.buckets:
+            b.opt_done = False
         self._seen.clear()
         for p in self._params:          # per-step use counters of multi-use gradient sinks
             if getattr(p, "_dlbb_sink_count", 0):
@@ -383,18 +404,39 @@ class FlatParamTrainer:
         if (not self.opt_overlap or not self._in_step or b.idx == len(self.buckets) - 1
                 or not self._split_optimizer_ok()):
             return
-        dev = self.flat_grad.device
-        if self._opt_stream is None:
-            self._opt_stream = (self._wgrad_stream if self.opt_overlap == 2
-                                and self._wgrad_stream is not None
-                                else concurrent_stream(dev, "ddp_opt"))
-        os_ = self._opt_stream
+        os_ = self._get_opt_stream()
         fork(os_)
         self._wait_wgrad(os_)
         with torch.cuda.stream(os_):
             self._wait_bucket(b)
             self._optimizer_step(ranges=[(b.start, b.end)], advance=self._opt_issued == 0)
         self._opt_issued += 1
+        b.opt_done = True
+
+    def _get_opt_stream(self):
+        if self._opt_stream is None:
+            self._opt_stream = (self._wgrad_stream if self.opt_overlap == 2
+                                and self._wgrad_stream is not None
+                                else concurrent_stream(self.flat_grad.device, "ddp_opt"))
+        return self._opt_stream
+
+    def _on_partial(self, p, n: int) -> None:
+        """First (LM-head) use of the tied table done: AdamW of the rows this step's input ids do
+        not touch (their gradient is final) on the optimizer stream, during backward. Ordered
+        after the main stream (the LM-head dgrad read the table before its gradient was
+        reported) and the weight-gradient streams (an unfused LM head computes it there)."""
+        if (p is not self._rows_param or n != 1 or not self.opt_overlap or not self._in_step
+                or not self._split_optimizer_ok()):
+            return
+        os_ = self._get_opt_stream()
+        fork(os_)
+        self._wait_wgrad(os_)
+        o = self._offsets[id(p)]
+        with torch.cuda.stream(os_):
+            self._optimizer_step(ranges=[(o, o + p.numel())], advance=self._opt_issued == 0,
+                                 rows=(self._row_mask, p.shape[1], 0))
+        self._opt_issued += 1
+        self._rows_early = True
 
     def _launch(self, b: _Bucket) -> None:
         b.launched = True
@@ -551,6 +593,10 @@ class FlatParamTrainer:
         self.zero_grad()
         self._reset()
         self._in_step = True
+        if self._rows_param is not None and self.opt_overlap and self._split_optimizer_ok():
+            # rows of the tied table the embedding backward will add to (= this step's ids)
+            self._row_mask.zero_()
+            self._row_mask.index_fill_(0, idx.reshape(-1), 1)
         if self.timeline and not torch.cuda.is_current_stream_capturing():
             self._tl = {"buckets": {}}
         with tracing.range("fwd"):
@@ -567,18 +613,32 @@ class FlatParamTrainer:
             with tracing.range("grad_sync_tail+optimizer"):
                 self._launch_rest()
                 head, tail = self.buckets[:-1], self.buckets[-1]
+                cur = (torch.cuda.current_stream(self.flat_grad.device)
+                       if self.flat_grad.is_cuda else None)
                 if self._opt_issued:
-                    # head AdamW already issued bucket by bucket during backward
-                    fork(torch.cuda.current_stream(self.flat_grad.device), self._opt_stream)
-                else:
-                    for b in head:
-                        self._wait_bucket(b)
+                    # AdamW ranges already queued on the optimizer stream during backward
+                    fork(cur, self._opt_stream)
+                todo = [b for b in head if not b.opt_done]
+                for b in todo:
+                    self._wait_bucket(b)
                 if self._wgrad_stream is not None:
-                    self._wait_wgrad(torch.cuda.current_stream(self.flat_grad.device))
-                if not self._opt_issued:
-                    self._optimizer_step(ranges=[(0, tail.start)], advance=True)
+                    self._wait_wgrad(cur)
+                adv = self._opt_issued == 0
+                if todo:
+                    self._optimizer_step(
+                        ranges=[(0, tail.start)] if len(todo) == len(head)
+                        else [(b.start, b.end) for b in todo], advance=adv)
+                    adv = False
                 self._wait_bucket(tail)
-                self._optimizer_step(ranges=[(tail.start, self.numel)], advance=False)
+                if self._rows_early:
+                    p = self._rows_param
+                    o = self._offsets[id(p)]
+                    e = o + p.numel()
+                    self._optimizer_step(ranges=[(tail.start, o), (e, self.numel)], advance=adv)
+                    self._optimizer_step(ranges=[(o, e)], advance=False,
+                                         rows=(self._row_mask, p.shape[1], 1))
+                else:
+                    self._optimizer_step(ranges=[(tail.start, self.numel)], advance=adv)
         else:
             with tracing.range("grad_sync_tail"):
                 self.finish()
@@ -743,6 +803,6 @@ class FlatParamTrainer:
             h.remove()
         for p in self._params:
             for attr in ("_dlbb_grad_sink", "_dlbb_grad_stream", "_dlbb_sink_count",
-                         "_dlbb_grad_fresh", "_dlbb_grad_event"):
+                         "_dlbb_grad_fresh", "_dlbb_grad_event", "_dlbb_partial_sink"):
                 if hasattr(p, attr):
                     delattr(p, attr)

@@ -952,3 +952,31 @@ def test_unit_upstream_mark_is_bit_exact():
         assert torch.equal(a, b)
     ref = GPT2(cfg, device=dev, seed=21)
     assert not mark_unit_upstream(ref(idx[:, :-1], idx[:, 1:]) * 2.0)   # not the fused output
+
+
+def test_early_rows_adamw_bit_exact(monkeypatch):
+    """The tied table's rows untouched by the step's ids are updated right after the LM-head
+    backward (row-filtered AdamW), the touched rows after the embedding backward: losses and
+    masters bit-identical to the whole-table update, eager and graph-replayed."""
+    from distributed_llm_backend_benchmark_amd.models.gpt2 import GPT2, GPT2Config
+    from distributed_llm_backend_benchmark_amd.parallel import ddp
+
+    dev = torch.device("cuda", 0)
+    cfg = GPT2Config(vocab_size=4096, block_size=64, n_layer=2, n_head=4, n_embd=256)
+    g = torch.Generator(device="cuda").manual_seed(9)
+    data = torch.randint(0, 1024, (6, 4, 65), device=dev, generator=g)   # rows >= 1024 untouched
+    out = []
+    for early in (False, True):
+        monkeypatch.setattr(ddp, "_EARLY_ROWS", early)
+        tr = ddp.FlatParamTrainer(GPT2(cfg, device=dev, seed=8), None, lr=1e-3, bucket_mb=0.3)
+        assert (tr._rows_param is not None) == early
+        losses = [tr.step(data[s, :, :-1], data[s, :, 1:]) for s in range(3)]
+        if early:
+            assert tr._rows_early
+        replay = tr.capture_step(data[3, :, :-1], data[3, :, 1:])
+        losses += [float(replay(data[s, :, :-1], data[s, :, 1:]).item()) for s in (4, 5)]
+        torch.cuda.synchronize()
+        out.append((losses, tr.master.clone(), tr.opt.m.clone()))
+        tr.close()
+    assert out[0][0] == out[1][0]
+    assert torch.equal(out[0][1], out[1][1]) and torch.equal(out[0][2], out[1][2])
