@@ -69,8 +69,10 @@ _UNIT_UPSTREAM = os.environ.get("DLBB_UNIT_UPSTREAM", "1") != "0"
 # world 1, overlapped optimizer: the rows of a tied embedding / LM-head table that this step's
 # input ids do not touch have their final gradient after the LM-head backward (the embedding
 # backward adds only to the input ids' rows): their AdamW runs then, during backward, and only
-# the touched rows stay behind the embedding backward (A/B: 0 = off)
-_EARLY_ROWS = os.environ.get("DLBB_EARLY_ROWS", "1") != "0"
+# the touched rows stay behind the embedding backward. Bit-exact, but measured no faster on the
+# GPT-2 step (17.30-17.42 vs 17.29-17.32 ms, profiles/r05_step/SUMMARY.md §11): off by default
+# (DLBB_EARLY_ROWS=1 enables it)
+_EARLY_ROWS = os.environ.get("DLBB_EARLY_ROWS", "0") == "1"
 # split optimizer only: AdamW of a head bucket is issued as soon as that bucket is reduced,
 # during backward, on a stream of its own (1) or on the weight-gradient side stream (2, default),
 # instead of for all head buckets after backward (0). GPT-2 step, three interleaved reps in one
