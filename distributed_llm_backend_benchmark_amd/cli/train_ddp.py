@@ -184,6 +184,7 @@ def _train(args, comm, tr, model, cfg):
         "gemm_tune_timing": _gemm.tune_timing(),
         # per-bucket AdamW during backward (parallel/ddp.py _OPT_OVERLAP; 0 = after backward)
         "opt_overlap": getattr(tr, "opt_overlap", 0),
+        "side_stream_checks": getattr(tr, "side_stream_checks", []),
     }
     if args.comm_timeline and not args.zero:
         tr.timeline = True

@@ -42,7 +42,7 @@ from ..ops.elementwise import ChunkTable, ScaleTable, reduce_sum, spin_ns
 from ..ops.xent import mark_unit_upstream
 from ..utils import tracing
 from .comm import Comm
-from .streams import concurrent_stream, cu_share_stream, fork
+from .streams import concurrent_stream, cu_share_stream, fork, runs_concurrently
 
 _GRAD_SINKS = os.environ.get("DLBB_GRAD_SINKS", "1") != "0"   # A/B switch for the sinks
 # sink dW GEMMs on a side stream (default on; DLBB_WGRAD_STREAM=0 for the A/B). Rounds 1-2
@@ -274,6 +274,7 @@ class FlatParamTrainer:
         self._opt_stream = None
         self._opt_issued = 0          # head-bucket AdamW ranges issued in this step's backward
         self._in_step = False         # only step() (which joins the optimizer stream) overlaps
+        self.side_stream_checks = []  # warm-up concurrency re-checks (_recheck_side_streams)
         self._rows_param = None       # table whose untouched rows update early (_EARLY_ROWS)
         self._rows_early = False
         self._row_mask = None
@@ -414,6 +415,39 @@ class FlatParamTrainer:
             self._optimizer_step(ranges=[(b.start, b.end)], advance=self._opt_issued == 0)
         self._opt_issued += 1
         b.opt_done = True
+
+    def _recheck_side_streams(self) -> None:
+        """Warm-up check (steps 2 and 4) that every weight-gradient stream still runs beside the
+        stream the step runs on. A run whose compute stream waited, after every forked-from
+        kernel, for exactly the side stream's weight-gradient + reduce kernels — the in-order
+        execution of two streams sharing one hardware queue — took 19-19.6 ms instead of
+        17.3-18 (profiles/r05_step/SUMMARY.md §12); a serialised side stream is replaced by a
+        fresh one verified against the current compute stream."""
+        dev = self.flat_grad.device
+        cur = torch.cuda.current_stream(dev)
+        bad = [i for i, ws in enumerate(self._wgrad_streams) if not runs_concurrently(cur, ws, dev)]
+        rec = {"step": self.step_count, "serialised": len(bad)}
+        if bad:
+            new = list(self._wgrad_streams)
+            for i in bad:
+                new[i] = concurrent_stream(dev, f"ddp_wgrad_s{self.step_count}_{i}",
+                                           _WGRAD_PRIORITY, ref=cur)
+            remap = {i: new[i] for i in bad}
+            for q in self._params:
+                old = getattr(q, "_dlbb_grad_stream", None)
+                if old is None:
+                    continue
+                for i in bad:
+                    if old is self._wgrad_streams[i]:
+                        q._dlbb_grad_stream = remap[i]
+            if self._opt_stream is not None and any(self._opt_stream is self._wgrad_streams[i]
+                                                    for i in bad):
+                self._opt_stream = None
+            self._wgrad_streams = new
+            self._wgrad_stream = new[0]
+            rec["replaced"] = bad
+            rec["now_concurrent"] = all(runs_concurrently(cur, ws, dev) for ws in new)
+        self.side_stream_checks.append(rec)
 
     def _get_opt_stream(self):
         if self._opt_stream is None:
@@ -592,6 +626,9 @@ class FlatParamTrainer:
 
     def step(self, idx: torch.Tensor, targets: torch.Tensor, sync_loss: bool = True):
         """One full training step: forward, backward (+ overlapped all-reduce), AdamW."""
+        if (self._wgrad_stream is not None and self.step_count in (1, 3)
+                and not _WGRAD_CU_SHARE and not torch.cuda.is_current_stream_capturing()):
+            self._recheck_side_streams()
         self.zero_grad()
         self._reset()
         self._in_step = True
