@@ -427,6 +427,11 @@ class FlatParamTrainer:
         cur = torch.cuda.current_stream(dev)
         bad = [i for i, ws in enumerate(self._wgrad_streams) if not runs_concurrently(cur, ws, dev)]
         rec = {"step": self.step_count, "serialised": len(bad)}
+        if self._comm_stream is not None and not runs_concurrently(cur, self._comm_stream, dev):
+            # the bucket reductions' stream (IPC / native RCCL / emulated): same check
+            self._comm_stream = concurrent_stream(dev, f"ddp_comm_s{self.step_count}",
+                                                  comm_stream_priority(), ref=cur)
+            rec["comm_replaced"] = True
         if bad:
             new = list(self._wgrad_streams)
             for i in bad:
@@ -626,8 +631,9 @@ class FlatParamTrainer:
 
     def step(self, idx: torch.Tensor, targets: torch.Tensor, sync_loss: bool = True):
         """One full training step: forward, backward (+ overlapped all-reduce), AdamW."""
-        if (self._wgrad_stream is not None and self.step_count in (1, 3)
-                and not _WGRAD_CU_SHARE and not torch.cuda.is_current_stream_capturing()):
+        if ((self._wgrad_stream is not None or self._comm_stream is not None)
+                and self.step_count in (1, 3, 6) and not _WGRAD_CU_SHARE
+                and not torch.cuda.is_current_stream_capturing()):
             self._recheck_side_streams()
         self.zero_grad()
         self._reset()

@@ -981,3 +981,33 @@ def test_early_rows_adamw_bit_exact(monkeypatch):
         tr.close()
     assert out[0][0] == out[1][0]
     assert torch.equal(out[0][1], out[1][1]) and torch.equal(out[0][2], out[1][2])
+
+
+def test_side_stream_recheck_replaces_a_serialised_stream():
+    """The warm-up re-check finds a weight-gradient stream that no longer runs beside the
+    compute stream (here: forced onto the compute stream itself), replaces it with a verified
+    one everywhere it is referenced, and training continues."""
+    from distributed_llm_backend_benchmark_amd.models.gpt2 import GPT2, GPT2Config
+    from distributed_llm_backend_benchmark_amd.parallel.ddp import FlatParamTrainer
+    from distributed_llm_backend_benchmark_amd.parallel.streams import runs_concurrently
+
+    dev = torch.device("cuda", 0)
+    cfg = GPT2Config(vocab_size=512, block_size=64, n_layer=2, n_head=4, n_embd=256)
+    tr = FlatParamTrainer(GPT2(cfg, device=dev, seed=2), None, lr=1e-3, bucket_mb=0.3)
+    idx = torch.randint(0, cfg.vocab_size, (4, 65), device=dev)
+    tr.step(idx[:, :-1], idx[:, 1:])
+    cur = torch.cuda.current_stream(dev)
+    old = tr._wgrad_stream
+    for p in tr._params:
+        if getattr(p, "_dlbb_grad_stream", None) is old:
+            p._dlbb_grad_stream = cur
+    tr._wgrad_streams[0] = cur
+    tr._wgrad_stream = cur
+    tr._recheck_side_streams()
+    rec = tr.side_stream_checks[-1]
+    assert rec["serialised"] == 1 and rec["replaced"] == [0] and rec["now_concurrent"], rec
+    assert tr._wgrad_stream is not cur and runs_concurrently(cur, tr._wgrad_stream, dev)
+    assert all(getattr(p, "_dlbb_grad_stream", None) is not cur for p in tr._params)
+    losses = [tr.step(idx[:, :-1], idx[:, 1:]) for _ in range(3)]
+    assert losses[-1] < losses[0] + 0.5
+    tr.close()
