@@ -989,7 +989,6 @@ def test_side_stream_recheck_replaces_a_serialised_stream():
     one everywhere it is referenced, and training continues."""
     from distributed_llm_backend_benchmark_amd.models.gpt2 import GPT2, GPT2Config
     from distributed_llm_backend_benchmark_amd.parallel.ddp import FlatParamTrainer
-    from distributed_llm_backend_benchmark_amd.parallel.streams import runs_concurrently
 
     dev = torch.device("cuda", 0)
     cfg = GPT2Config(vocab_size=512, block_size=64, n_layer=2, n_head=4, n_embd=256)
