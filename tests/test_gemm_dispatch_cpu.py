@@ -77,7 +77,7 @@ def test_wgrad_pingpong_contract():
     assert ok(16384, 50304, 768, acc=True)
     assert not ok(16384, 50304, 768, acc=True, out_dtype=torch.float32)
     assert ok(16384, 50304, 768, out_dtype=torch.float32)
-    assert not ok(16384, 768, 768, bias=True)
+    assert ok(16384, 768, 768, bias=True)    # bias gradient: a separate column-sum pass
     assert not ok(16384, 200, 768) and not ok(16384, 768, 640) and not ok(100, 768, 768)
     assert "pp" in gemm._WGRAD_IMPLS
 
