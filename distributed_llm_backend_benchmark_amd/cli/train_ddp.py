@@ -151,6 +151,8 @@ def _train(args, comm, tr, model, cfg):
     def step_fn(x, y):
         set_lr()
         return tr.step(x, y, sync_loss=False)
+    if hasattr(tr, "recheck_side_streams"):
+        tr.recheck_side_streams()       # after warm-up, outside the timed steps
     if args.graph:
         x, y = data.get_batch()
         step_fn = tr.capture_step(x, y)

@@ -416,8 +416,16 @@ class FlatParamTrainer:
         self._opt_issued += 1
         b.opt_done = True
 
+    def recheck_side_streams(self) -> None:
+        """Public form of the re-check (no-op without side streams, under CU-masked streams or
+        during a capture); runners call it once after their warm-up steps."""
+        if ((self._wgrad_stream is not None or self._comm_stream is not None)
+                and not _WGRAD_CU_SHARE and not torch.cuda.is_current_stream_capturing()):
+            self._recheck_side_streams()
+
     def _recheck_side_streams(self) -> None:
-        """Warm-up check (steps 2 and 4) that every weight-gradient stream still runs beside the
+        """Warm-up check (starts of steps 2 and 3, and once after a runner's warm-up) that every
+        weight-gradient stream still runs beside the
         stream the step runs on. A run whose compute stream waited, after every forked-from
         kernel, for exactly the side stream's weight-gradient + reduce kernels — the in-order
         execution of two streams sharing one hardware queue — took 19-19.6 ms instead of
@@ -631,10 +639,8 @@ class FlatParamTrainer:
 
     def step(self, idx: torch.Tensor, targets: torch.Tensor, sync_loss: bool = True):
         """One full training step: forward, backward (+ overlapped all-reduce), AdamW."""
-        if ((self._wgrad_stream is not None or self._comm_stream is not None)
-                and self.step_count in (1, 3, 6) and not _WGRAD_CU_SHARE
-                and not torch.cuda.is_current_stream_capturing()):
-            self._recheck_side_streams()
+        if self.step_count in (1, 2):       # early warm-up steps (a runner adds one after)
+            self.recheck_side_streams()
         self.zero_grad()
         self._reset()
         self._in_step = True
