@@ -29,7 +29,26 @@ struct AdamArgs {
   int row_sel;
 };
 
-template <int GDT>
+// fp32 state streamed once per step (p, m, v: 12 B/param in, 12 B out — past the 256 MiB MALL
+// for any real model): NT = non-temporal loads/stores for them (A/B, DLBB_ADAMW_NT)
+template <bool NT>
+__device__ __forceinline__ void ld8f(const float* base, int64_t i8, float (&v)[8]) {
+  const f32x4* q = reinterpret_cast<const f32x4*>(base) + 2 * i8;
+  f32x4 x, y;
+  if constexpr (NT) { x = __builtin_nontemporal_load(q); y = __builtin_nontemporal_load(q + 1); }
+  else { x = q[0]; y = q[1]; }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) { v[j] = x[j]; v[4 + j] = y[j]; }
+}
+template <bool NT>
+__device__ __forceinline__ void st8f(float* base, int64_t i8, const float (&v)[8]) {
+  f32x4* q = reinterpret_cast<f32x4*>(base) + 2 * i8;
+  const f32x4 x = {v[0], v[1], v[2], v[3]}, y = {v[4], v[5], v[6], v[7]};
+  if constexpr (NT) { __builtin_nontemporal_store(x, q); __builtin_nontemporal_store(y, q + 1); }
+  else { q[0] = x; q[1] = y; }
+}
+
+template <int GDT, bool NT = false>
 __global__ void __launch_bounds__(256) adamw_kernel(AdamArgs a) {
   const int64_t nvec = a.n / 8;
   const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
@@ -52,15 +71,15 @@ __global__ void __launch_bounds__(256) adamw_kernel(AdamArgs a) {
        i += stride) {
     if (a.row_mask && a.row_mask[i * 8 / a.row_len] != a.row_sel) continue;
     float p[8], m[8], v[8], g[8];
-    load8<DT_F32>(a.p, i, p);
-    load8<DT_F32>(a.m, i, m);
-    load8<DT_F32>(a.v, i, v);
+    ld8f<NT>(a.p, i, p);
+    ld8f<NT>(a.m, i, m);
+    ld8f<NT>(a.v, i, v);
     load8<GDT>(a.g, i, g);
 #pragma unroll
     for (int j = 0; j < 8; ++j) body(p[j], m[j], v[j], g[j]);
-    store8<DT_F32>(a.p, i, p);
-    store8<DT_F32>(a.m, i, m);
-    store8<DT_F32>(a.v, i, v);
+    st8f<NT>(a.p, i, p);
+    st8f<NT>(a.m, i, m);
+    st8f<NT>(a.v, i, v);
     if (a.p_bf16) store8<DT_BF16>(a.p_bf16, i, p);
   }
   if (blockIdx.x == 0) {
@@ -79,14 +98,23 @@ __global__ void __launch_bounds__(256) adamw_kernel(AdamArgs a) {
 
 using namespace dlbb;
 
+static int g_adamw_nt = 0;   // non-temporal fp32 state traffic (A/B: dlbb_adamw_set_nt)
+DLBB_API void dlbb_adamw_set_nt(int on) { g_adamw_nt = on ? 1 : 0; }
+
 static int launch_adamw(const AdamArgs& a, int grad_dtype, hipStream_t stream) {
   const int grid = stream_grid((a.n + 7) / 8, 256);
-  if (grad_dtype == DT_BF16)
-    hipLaunchKernelGGL(adamw_kernel<DT_BF16>, dim3(grid), dim3(256), 0, stream, a);
-  else if (grad_dtype == DT_F32)
-    hipLaunchKernelGGL(adamw_kernel<DT_F32>, dim3(grid), dim3(256), 0, stream, a);
-  else
+  // 32-byte alignment of the fp32 arrays for the two float4 halves of an 8-vector
+  const bool nt = g_adamw_nt && !((reinterpret_cast<uintptr_t>(a.p) | reinterpret_cast<uintptr_t>(a.m) |
+                                   reinterpret_cast<uintptr_t>(a.v)) & 15);
+  if (grad_dtype == DT_BF16) {
+    if (nt) hipLaunchKernelGGL((adamw_kernel<DT_BF16, true>), dim3(grid), dim3(256), 0, stream, a);
+    else hipLaunchKernelGGL((adamw_kernel<DT_BF16, false>), dim3(grid), dim3(256), 0, stream, a);
+  } else if (grad_dtype == DT_F32) {
+    if (nt) hipLaunchKernelGGL((adamw_kernel<DT_F32, true>), dim3(grid), dim3(256), 0, stream, a);
+    else hipLaunchKernelGGL((adamw_kernel<DT_F32, false>), dim3(grid), dim3(256), 0, stream, a);
+  } else {
     return hipErrorInvalidValue;
+  }
   return hipGetLastError();
 }
 

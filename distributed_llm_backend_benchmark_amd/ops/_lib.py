@@ -91,6 +91,7 @@ _SIGS = {
     "dlbb_attn_set_xcd": (None, [c_int]),
     "dlbb_attn_set_concurrent": (None, [c_int]),
     "dlbb_xent_set_variant": (None, [c_int]),
+    "dlbb_adamw_set_nt": (None, [c_int]),
     "dlbb_adamw_rows": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p,
                                 c_int64, c_float, c_float, c_float, c_float, c_float, c_int,
                                 c_void_p, c_float, c_void_p, c_int64, c_int, c_void_p]),
@@ -218,7 +219,8 @@ def _load() -> ctypes.CDLL:
                                 ("DLBB_SPLIT_REDUCE_VARIANT", "dlbb_split_reduce_set_variant"),
                                 ("DLBB_ATTN_FUSE_DELTA", "dlbb_attn_set_fuse_delta"),
                                 ("DLBB_ATTN_FWD_VARIANT", "dlbb_attn_set_fwd_variant"),
-                                ("DLBB_ATTN_BWD_INCR", "dlbb_attn_set_bwd_incr")):
+                                ("DLBB_ATTN_BWD_INCR", "dlbb_attn_set_bwd_incr"),
+                                ("DLBB_ADAMW_NT", "dlbb_adamw_set_nt")):
                 if os.environ.get(env, "") != "":
                     getattr(lib, setter)(int(os.environ[env]))
             if os.environ.get("DLBB_WGRAD_MIN_LDS_KB", "") != "":

@@ -1144,3 +1144,29 @@ def test_sort_ids_matches_stable_torch_sort(n, vocab):
     s, o = sort_ids(ids, vocab)
     rs, ro = torch.sort(ids, stable=True)
     assert torch.equal(s, rs) and torch.equal(o, ro)
+
+
+def test_adamw_nontemporal_bit_exact():
+    """The non-temporal AdamW form (DLBB_ADAMW_NT) changes only the cache policy of the fp32
+    state traffic: identical parameters, moments and bf16 working copy, incl. a row-filtered
+    call."""
+    from distributed_llm_backend_benchmark_amd.ops import _lib
+    from distributed_llm_backend_benchmark_amd.ops.optim import FlatAdamW
+
+    n = (1 << 20) + 8 * 96
+    g = _randn(n, seed=41).float().to(torch.bfloat16)
+    outs = []
+    for nt in (0, 1):
+        _lib.lib().dlbb_adamw_set_nt(nt)
+        master = _randn(n, seed=40).float()
+        opt = FlatAdamW(master, lr=1e-3, weight_decay=0.1)
+        w = torch.empty(n, dtype=torch.bfloat16, device=DEV)
+        for _ in range(3):
+            opt.step(g, working_bf16=w)
+        mask = (torch.arange(n // 96, device=DEV) % 3 == 0).to(torch.uint8)
+        opt.step(g, working_bf16=w, rows=(mask, 96, 1))
+        torch.cuda.synchronize()
+        outs.append((master.clone(), opt.m.clone(), opt.v.clone(), w.clone()))
+    _lib.lib().dlbb_adamw_set_nt(0)
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
