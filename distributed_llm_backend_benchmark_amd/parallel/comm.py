@@ -28,12 +28,6 @@ import torch.distributed as dist
 BACKEND_ALIASES = {"rccl": "nccl", "nccl": "nccl", "gloo": "gloo", "cpu": "gloo"}
 
 
-def _free_port() -> int:
-    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
-
-
 def resolve_backend(name: str = "auto") -> str:
     name = (name or "auto").lower()
     if name == "auto":
@@ -265,8 +259,9 @@ def init_distributed(backend: str = "auto", timeout_s: float = 600.0,
         kwargs = dict(backend=be, rank=rank, world_size=world,
                       timeout=datetime.timedelta(seconds=timeout_s))
         if "WORLD_SIZE" not in os.environ:
-            # standalone single process: private rendezvous on a fresh loopback port
-            kwargs["init_method"] = f"tcp://127.0.0.1:{_free_port()}"
+            # standalone single process: an in-process store, so no port is bound at all (a
+            # loopback port picked in advance can be taken by another process before the bind)
+            kwargs["store"] = dist.HashStore()
         else:
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
             if "MASTER_PORT" not in os.environ:
@@ -274,17 +269,7 @@ def init_distributed(backend: str = "auto", timeout_s: float = 600.0,
         eager = be == "nccl" and os.environ.get("DLBB_RCCL_EAGER_INIT", "0") == "1"
         if eager:
             kwargs["device_id"] = dev  # eager RCCL communicator init, fixed device binding
-        standalone = "WORLD_SIZE" not in os.environ
-        for attempt in range(5):
-            try:
-                dist.init_process_group(**kwargs)
-                break
-            except Exception as e:  # noqa: BLE001 - only the standalone port race is retried
-                # a private loopback port can be taken between _free_port() and the store's
-                # bind (another process on the box): pick a new one
-                if not standalone or attempt == 4 or "EADDRINUSE" not in str(e):
-                    raise
-                kwargs["init_method"] = f"tcp://127.0.0.1:{_free_port()}"
+        dist.init_process_group(**kwargs)
         owns = True
         if be == "nccl" and not eager:
             # Lazy communicator creation, forced now by one tiny all-reduce on the bound device.

@@ -28,12 +28,12 @@ def _run(cmd, timeout, env=None):
 
 
 def _torchrun(nproc, args, timeout):
-    from conftest import free_port
+    from launch_utils import run_torchrun
 
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node",
-           str(nproc), "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
-           "-m", "distributed_llm_backend_benchmark_amd.cli.collectives"] + args
-    return _run(cmd, timeout)
+    out = run_torchrun(nproc, ["-m", "distributed_llm_backend_benchmark_amd.cli.collectives"]
+                       + args, timeout)
+    assert out.returncode == 0, (out.args, out.stdout[-2000:], out.stderr[-4000:])
+    return out
 
 
 def run_pipeline(tmp, nproc, backend="rccl", device="auto", direct_ipc=False,

@@ -16,14 +16,12 @@ HEADLINE_KEYS = ("metric", "unit", "n_gpus", "steps", "warmup", "higher_is_bette
 
 
 def _bench(extra_env=None):
-    from conftest import free_port
+    from launch_utils import run_torchrun
 
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-           "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
-           os.path.join(REPO, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "1"] + SMALL
     env = {k: v for k, v in os.environ.items() if k != "CUDA_VISIBLE_DEVICES"}
     env.update(extra_env or {})
-    out = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=REPO, env=env)
+    out = run_torchrun(2, [os.path.join(REPO, "bench.py"), "--gpus", "2", "--steps", "3",
+                           "--warmup", "1"] + SMALL, 300, env=env)
     assert out.returncode == 0, out.stderr[-3000:]
     lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1, out.stdout

@@ -614,15 +614,13 @@ def test_bench_py_world1():
 def test_bench_py_two_ranks_rehearsal():
     """bench.py's multi-rank path (candidate agreement, IPC kernel, native-engine refusal of a
     shared GPU) with 2 ranks on one GPU over a gloo process group (DLBB_BENCH_BACKEND=gloo)."""
-    from conftest import free_port
+    from launch_utils import run_torchrun
 
     env = dict(os.environ, DLBB_BENCH_BACKEND="gloo", HSA_ENABLE_IPC_MODE_LEGACY="0")
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-           "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
-           os.path.join(REPO, "bench.py"), "--gpus", "2", "--steps", "5", "--warmup", "2",
-           "--sweep-max-mib", "32", "--grid", "2,1024,1024;1,2048,2048", "--moe", "2048,1024",
-           "--ddp-model", "2,4,256,4096,4,256", "--ddp-steps", "4"]
-    out = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=REPO, env=env)
+    out = run_torchrun(2, [os.path.join(REPO, "bench.py"), "--gpus", "2", "--steps", "5",
+                           "--warmup", "2", "--sweep-max-mib", "32", "--grid",
+                           "2,1024,1024;1,2048,2048", "--moe", "2048,1024", "--ddp-model",
+                           "2,4,256,4096,4,256", "--ddp-steps", "4"], 600, env=env)
     assert out.returncode == 0, out.stderr[-3000:]
     rec = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][-1])
     assert rec["n_gpus"] == 2 and rec["value"] > 0 and rec["vs_baseline"] is not None

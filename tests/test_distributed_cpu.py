@@ -398,15 +398,13 @@ def test_bench_py_gloo_world2_contract():
     import subprocess
     import sys
 
-    from conftest import free_port
+    from launch_utils import run_torchrun
 
     repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-           "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
-           os.path.join(repo, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "1",
+    cmd = [os.path.join(repo, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "1",
            "--shape", "1,64,256", "--sweep-max-mib", "1"]
     env = {k: v for k, v in os.environ.items() if k not in ("CUDA_VISIBLE_DEVICES",)}
-    out = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=repo, env=env)
+    out = run_torchrun(2, cmd, 300, env=env, cwd=repo)
     assert out.returncode == 0, out.stderr[-3000:]
     lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1, out.stdout
@@ -426,15 +424,13 @@ def test_bench_py_deadline_keeps_the_headline():
     import subprocess
     import sys
 
-    from conftest import free_port
+    from launch_utils import run_torchrun
 
     repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-           "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
-           os.path.join(repo, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "1",
+    cmd = [os.path.join(repo, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "1",
            "--shape", "1,64,256", "--sweep-max-mib", "1", "--deadline-s", "0"]
     env = {k: v for k, v in os.environ.items() if k not in ("CUDA_VISIBLE_DEVICES",)}
-    out = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=repo, env=env)
+    out = run_torchrun(2, cmd, 300, env=env, cwd=repo)
     assert out.returncode == 0, out.stderr[-3000:]
     lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1, out.stdout

@@ -28,13 +28,9 @@ def _ngpus() -> int:
 
 
 def _torchrun(nproc, script_args, timeout=900, env=None):
-    from conftest import free_port
+    from launch_utils import run_torchrun
 
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node",
-           str(nproc), "--master-addr", "127.0.0.1", "--master-port", str(free_port())]
-    out = subprocess.run(cmd + script_args, capture_output=True, text=True, timeout=timeout,
-                         cwd=REPO, env=dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0",
-                                            **(env or {})))
+    out = run_torchrun(nproc, script_args, timeout, env=dict(os.environ, **(env or {})))
     assert out.returncode == 0, out.stderr[-4000:]
     return out
 
