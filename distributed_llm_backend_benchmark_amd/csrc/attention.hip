@@ -827,6 +827,322 @@ __global__ void __launch_bounds__(kAttnThreads, 2) attn_bwd_dq_d64_kernel(AttnBw
       }
   }
 }
+
+// ============================================================================ pipelined forward
+// Round-6 forward body (the round-5 kernel ran QK^T -> softmax -> PV of a tile back to back in
+// one wave: MFMA busy 19 %, the VALU softmax never beside the matrix work). Each wave now runs
+// a software pipeline over its key tiles: iteration `it` issues the QK^T MFMAs of tile it + 1,
+// the softmax (VALU) of tile it and the PV MFMAs of tile it - 1 as ONE straight-line block, so
+// the softmax's exps / max / sums fill the issue gaps of 16 independent MFMAs instead of
+// waiting for their own (CDNA guide §B "Fused attention prefill": P of tile j beside PV of
+// tile j - 1).
+//   * K and V are staged in rings of 4 x 8 KiB (64 KiB per workgroup, 2 workgroups per CU):
+//     at the top of iteration it (after the one barrier) K_{it+3} and V_{it+2} are issued, so a
+//     K tile has two iterations to land and a V tile three; the counted wait vmcnt(6) retires
+//     exactly K_{it+1} (and everything older: V_{it-1}). Past the last tile the loads repeat
+//     the last tile (uniform instruction counts keep the count constant).
+//   * lazy rescaling: a row's reference max m moves only when a tile's max exceeds it by more
+//     than 2^8 (p = exp2(s c - m) <= 256 otherwise, exact in bf16 / fp32 sums); the O
+//     rescale (32 multiplies, wave-uniformly skipped when no lane moved) is applied one
+//     iteration late, right before the PV of the tile whose softmax moved m.
+//   * only a wave's LAST key tile meets the diagonal (queries qw .. qw + 31, qw % 32 == 0, tiles
+//     of 64): it is the one masked softmax.
+//   * layouts as the round-5 kernel: swapped scores S^T = K Q^T (lane = query), K image kswz
+//     (ds_read_b128 rows), V image vswz (ds_read_b64_tr_b16), O^T = V^T P^T in registers.
+constexpr int kRing = 4;
+constexpr float kLazyLog2 = 8.f;
+
+struct FwdRegs {
+  bf16x8 qf[4];
+  f32x16 o[2];
+  float m, l, alpha;      // reference max (log2 units), row sum, pending O rescale
+};
+
+// K fragments of the key tile in image `tk` (8 row reads, issued in wait order: half 0 first)
+__device__ __forceinline__ void fwd_kreads(const char* tk, f32x4 (&kr)[2][4], int lane) {
+  const int r = lane & 31, hi = lane >> 5;
+  const char* krow = tk + r * 128;
+  const int sw = kswz(r);
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) kr[0][ks] = ds_read_b128_asm<0>(krow + (((2 * ks + hi) ^ sw) << 4));
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) kr[1][ks] = ds_read_b128_asm<4096>(krow + (((2 * ks + hi) ^ sw) << 4));
+}
+
+// S^T half KK (32 keys) = K Q^T; the caller has waited for kr[KK]
+template <int KK>
+__device__ __forceinline__ void fwd_scores_half(const f32x4 (&kr)[2][4], const bf16x8 (&qf)[4],
+                                                f32x16 (&s)[2]) {
+#pragma unroll
+  for (int e = 0; e < 16; ++e) s[KK][e] = 0.f;
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks)
+    s[KK] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, kr[KK][ks]), qf[ks],
+                                                    s[KK], 0, 0, 0);
+}
+
+// V^T fragments of keys [32 KK, 32 KK + 32) of the tile in image `tv` (8 transposed reads;
+// the caller waits). row = KK*32 + 16 st + 8 half + 4 (g >> 1) + tq: vswz(row) depends on bit 1
+// of tq only, so the address is a per-lane base per dt plus an immediate.
+template <int KK>
+__device__ __forceinline__ void fwd_vreads(const char* tv, i16x4 (&vt)[2][2][2], int lane) {
+  const int g = lane >> 4, i16 = lane & 15;
+  const int tq = i16 >> 2, tp = i16 & 3;
+  const int row0 = 4 * (g >> 1) + tq;
+  const int sw = vswz(row0);
+#pragma unroll
+  for (int dt = 0; dt < 2; ++dt) {
+    const int col = dt * 32 + 16 * (g & 1) + 4 * tp;
+    const char* b = tv + row0 * 128 + (((col >> 3) ^ sw) << 4) + (col & 7) * 2;
+    vt[0][dt][0] = ds_read_tr16<(KK * 32 + 0) * 128>(b);
+    vt[0][dt][1] = ds_read_tr16<(KK * 32 + 8) * 128>(b);
+    vt[1][dt][0] = ds_read_tr16<(KK * 32 + 16) * 128>(b);
+    vt[1][dt][1] = ds_read_tr16<(KK * 32 + 24) * 128>(b);
+  }
+}
+
+template <int N>
+__device__ __forceinline__ void vt_wait(i16x4 (&vt)[2][2][2]) {
+  lgk_wait<N>(vt[0][0][0], vt[0][0][1], vt[0][1][0], vt[0][1][1], vt[1][0][0], vt[1][0][1],
+              vt[1][1][0], vt[1][1][1]);
+}
+
+// O^T += V^T P^T for keys half KK of a tile (4 MFMA)
+template <int KK>
+__device__ __forceinline__ void fwd_pv_half(f32x16 (&o)[2], const i16x4 (&vt)[2][2][2],
+                                            const bf16x8 (&p)[2][2]) {
+#pragma unroll
+  for (int st = 0; st < 2; ++st)
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt) {
+      bf16x8 vf;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        vf[u] = vt[st][dt][0][u];
+        vf[4 + u] = vt[st][dt][1][u];
+      }
+      o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, p[KK][st], o[dt], 0, 0, 0);
+    }
+}
+
+__device__ __forceinline__ void fwd_rescale(FwdRegs& R) {
+  if (__builtin_amdgcn_ballot_w64(R.alpha != 1.f) != 0) {   // wave-uniform skip
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) R.o[dt][e] *= R.alpha;
+  }
+}
+
+// softmax part 1 of the scores `s` of key tile k0 (in place: s becomes p in fp32), updating
+// m / l; returns the tile's O rescale factor (applied before the PV of this tile)
+template <bool DIAG>
+__device__ __forceinline__ float fwd_softmax(FwdRegs& R, f32x16 (&s)[2], int k0, int qme,
+                                             float c, int lane) {
+  const int hi = lane >> 5;
+  if constexpr (DIAG) {
+    // key(kk, e) = k0 + 4 hi + kk*32 + (e & 3) + 8 (e >> 2): one per-lane threshold
+    const int th = qme - k0 - 4 * hi;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int e = 0; e < 16; ++e)
+        if (kk * 32 + (e & 3) + 8 * (e >> 2) > th) s[kk][e] = -INFINITY;
+  }
+  float mx = max3_asm(s[0][0], s[0][1], s[0][2]);
+#pragma unroll
+  for (int e = 3; e < 15; e += 2) mx = max3_asm(mx, s[0][e], s[0][e + 1]);
+  mx = max3_asm(mx, s[0][15], s[1][0]);
+#pragma unroll
+  for (int e = 1; e < 15; e += 2) mx = max3_asm(mx, s[1][e], s[1][e + 1]);
+  mx = fmaxf(mx, s[1][15]);
+  mx = xhalf_max(mx) * c;
+  const float mn = mx > R.m + kLazyLog2 ? mx : R.m;     // m = -inf on the first tile
+  const float alpha = __builtin_amdgcn_exp2f(R.m - mn);
+  R.m = mn;
+  float ls0 = 0.f, ls1 = 0.f;
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const float v = __builtin_amdgcn_exp2f(__builtin_fmaf(s[kk][e], c, -mn));
+      s[kk][e] = v;
+      if (kk == 0) ls0 += v; else ls1 += v;
+    }
+  R.l = R.l * alpha + (ls0 + ls1);
+  return alpha;
+}
+
+// softmax part 2: the probabilities to bf16 MFMA operands
+__device__ __forceinline__ void fwd_pack(const f32x16 (&s)[2], bf16x8 (&p)[2][2]) {
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+    for (int st = 0; st < 2; ++st)
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        p[kk][st][j] = __builtin_bit_cast(short, static_cast<__bf16>(s[kk][8 * st + j]));
+}
+
+__global__ void __launch_bounds__(kAttnThreads, 2) attn_fwd_pipe_kernel(AttnArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int nqb = (a.T + kQB - 1) / kQB;
+  int blk, h, b;
+  head_block(a.xcd, blk, h, b);
+  const int qb = nqb - 1 - blk;                   // heaviest first
+  const int q0 = qb * kQB;
+  const int qw = q0 + wave * 32;
+  const int r = lane & 31, hi = lane >> 5;
+  const uint16_t* base_bt = a.qkv + static_cast<int64_t>(b) * a.T * a.ld;
+  const int hoff = h * kAttnD;
+  const int qme = qw + r;
+  const float c = a.scale_log2;
+  // key tiles of the workgroup (barriers) and of this wave (work); nt_w = 0: no query < T
+  const int last_key = (q0 + kQB - 1) < (a.T - 1) ? (q0 + kQB - 1) : (a.T - 1);
+  const int nt = last_key / kKB + 1;
+  const int q_hi = (qw + 31) < (a.T - 1) ? (qw + 31) : (a.T - 1);
+  const int nt_w = qw < a.T ? q_hi / kKB + 1 : 0;
+
+  FwdRegs R;
+  {
+    const int q = qme < a.T ? qme : a.T - 1;
+    const uint16_t* qp = base_bt + static_cast<int64_t>(q) * a.ld + hoff + 8 * hi;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) R.qf[ks] = *reinterpret_cast<const bf16x8*>(qp + 16 * ks);
+  }
+#pragma unroll
+  for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) R.o[dt][e] = 0.f;
+  R.m = -INFINITY;
+  R.l = 0.f;
+  R.alpha = 1.f;
+
+  auto ringK = [&](int t) { return smem + (t & (kRing - 1)) * kTileKV; };
+  auto ringV = [&](int t) { return smem + (kRing + (t & (kRing - 1))) * kTileKV; };
+  // K / V staging by buffer_load ... lds: the (b, h) section bases in buffer resources
+  // (SGPRs), this lane's row-in-tile + swizzled chunk as a 32-bit offset (rows wave * 16 +
+  // i * 8 + lane / 8), a tile's rows as a uniform offset; a tile crossing T clamps its rows
+  const int r_in = lane >> 3, slot = lane & 7;
+  const uint32_t ld2 = static_cast<uint32_t>(a.ld) * 2;
+  const __amdgpu_buffer_rsrc_t rk = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint16_t*>(base_bt + hoff + kAttnD * a.H), 0, 0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint16_t*>(base_bt + hoff + 2 * kAttnD * a.H), 0, 0x7fffffff, 0x00020000);
+  uint32_t koff[2], voff[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int row = wave * 16 + i * 8 + r_in;
+    koff[i] = static_cast<uint32_t>(row) * ld2 + ((slot ^ kswz(row)) << 4);
+    voff[i] = static_cast<uint32_t>(row) * ld2 + ((slot ^ vswz(row)) << 4);
+  }
+  // stage K (sec 1) or V (sec 2) of key index ts into its ring slot (tile min(ts, nt - 1))
+  auto stage = [&](int ts, int sec) __attribute__((always_inline)) {
+    char* dst = sec == 1 ? ringK(ts) : ringV(ts);
+    const int t = ts < nt - 1 ? ts : nt - 1;
+    const int k0 = t * kKB;
+    const __amdgpu_buffer_rsrc_t rs = sec == 1 ? rk : rv;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      uint32_t off;
+      if (k0 + kKB <= a.T) {                       // wave-uniform: no row past T
+        off = (sec == 1 ? koff[i] : voff[i]) + static_cast<uint32_t>(k0) * ld2;
+      } else {
+        const int row = wave * 16 + i * 8 + r_in;
+        const int key = k0 + row < a.T ? k0 + row : a.T - 1;
+        off = static_cast<uint32_t>(key) * ld2 +
+              ((slot ^ (sec == 1 ? kswz(row) : vswz(row))) << 4);
+      }
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_vptr_t)(dst + (wave * 16 + i * 8) * 128), 16,
+                                               off, 0, 0, 0);
+    }
+  };
+
+  f32x16 s[2];
+  bf16x8 p[2][2];
+  // prologue: K_0 | K_1, V_0 -> K_0 landed; iteration -1: K_2, V_1 issued, S_0
+  stage(0, 1);
+  stage(1, 1);
+  stage(0, 2);
+  asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  stage(2, 1);
+  stage(1, 2);
+  auto scores = [&](int t) __attribute__((always_inline)) {
+    f32x4 kr[2][4];
+    fwd_kreads(ringK(t), kr, lane);
+    lgk_wait<4>(kr[0][0], kr[0][1], kr[0][2], kr[0][3]);
+    fwd_scores_half<0>(kr, R.qf, s);
+    lgk_wait<0>(kr[1][0], kr[1][1], kr[1][2], kr[1][3]);
+    fwd_scores_half<1>(kr, R.qf, s);
+  };
+  auto pv = [&](int t) __attribute__((always_inline)) {
+    i16x4 vt[2][2][2];
+    fwd_vreads<0>(ringV(t), vt, lane);
+    vt_wait<0>(vt);
+    fwd_rescale(R);
+    fwd_pv_half<0>(R.o, vt, p);
+    fwd_vreads<1>(ringV(t), vt, lane);
+    vt_wait<0>(vt);
+    fwd_pv_half<1>(R.o, vt, p);
+  };
+  if (nt_w > 0) scores(0);
+  // iteration it: [PV_{it-1} | softmax_it] then S_{it+1}. The PV MFMAs (independent of the
+  // softmax) are issued between its VALU; p holds tile it - 1's probabilities until the PV
+  // has read them, then tile it's.
+  for (int it = 0; it <= nt; ++it) {
+    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");   // K_{it+1} (and V_{it-1}) landed
+    __builtin_amdgcn_s_barrier();                      // ... for every wave; slots it-1 free
+    stage(it + 3, 1);
+    stage(it + 2, 2);
+    const int k0 = it * kKB;
+    if (it >= 1 && it + 1 < nt_w) {                    // steady state: one straight block
+      i16x4 vt[2][2][2];
+      fwd_vreads<0>(ringV(it - 1), vt, lane);
+      const float al = fwd_softmax<false>(R, s, k0, qme, c, lane);
+      vt_wait<0>(vt);
+      fwd_rescale(R);
+      fwd_pv_half<0>(R.o, vt, p);
+      fwd_vreads<1>(ringV(it - 1), vt, lane);
+      vt_wait<0>(vt);
+      fwd_pv_half<1>(R.o, vt, p);
+      fwd_pack(s, p);
+      R.alpha = al;
+      scores(it + 1);
+    } else {                                           // first / diagonal / drain iterations
+      if (it >= 1 && it <= nt_w) pv(it - 1);
+      if (it < nt_w) {
+        const float al = it == nt_w - 1 ? fwd_softmax<true>(R, s, k0, qme, c, lane)
+                                        : fwd_softmax<false>(R, s, k0, qme, c, lane);
+        fwd_pack(s, p);
+        R.alpha = al;
+      }
+      if (it + 1 < nt_w) scores(it + 1);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no LDS-DMA in flight at exit
+
+  // ---- finalize: l over both lane halves, O / l, store O [B,T,H,D] and LSE
+  const float lt = R.l + __shfl_xor(R.l, 32, 64);
+  const float inv = lt > 0.f ? 1.f / lt : 0.f;
+  if (qme < a.T) {
+    uint16_t* op = a.out + (static_cast<int64_t>(b) * a.T + qme) * a.ldo + hoff;
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+      for (int gg = 0; gg < 4; ++gg) {
+        u16x4 w;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) w[u] = f32_to_bf16(R.o[dt][4 * gg + u] * inv);
+        *reinterpret_cast<u16x4*>(op + dt * 32 + 8 * gg + 4 * hi) = w;
+      }
+    if (hi == 0 && a.lse)
+      a.lse[(static_cast<int64_t>(b) * a.H + h) * a.T + qme] =
+          (R.m + __builtin_amdgcn_logf(lt)) * 0.69314718055994531f;
+  }
+}
 }  // namespace dlbb
 
 using namespace dlbb;
@@ -856,7 +1172,7 @@ DLBB_API void dlbb_attn_set_xcd(int on) { g_attn_xcd = on ? 1 : 0; }
 DLBB_API void dlbb_attn_set_fuse_delta(int on) { g_attn_fuse_delta = on ? 1 : 0; }
 DLBB_API void dlbb_attn_set_concurrent(int on) { g_attn_concurrent = on ? 1 : 0; }
 DLBB_API void dlbb_attn_set_fwd_variant(int v) {
-  g_attn_fwd_variant = (v >= 0 && v <= 7) || v == 14 ? v : 6;
+  g_attn_fwd_variant = (v >= 0 && v <= 7) || v == 14 || v == 100 ? v : 6;
 }
 DLBB_API int dlbb_attn_get_fwd_variant() { return g_attn_fwd_variant; }
 DLBB_API void dlbb_attn_set_bwd_incr(int m) { g_attn_bwd_incr = m & 3; }
@@ -899,6 +1215,11 @@ DLBB_API int dlbb_attn_fwd(const void* qkv, int64_t ld, void* out, int64_t ldo, 
   AttnArgs a{static_cast<const uint16_t*>(qkv), static_cast<uint16_t*>(out), lse, ld, ldo,
              B, T, H, scale * 1.4426950408889634f, g_attn_xcd};
   const dim3 grid((T + kQB - 1) / kQB, H, B);
+  if (g_attn_fwd_variant == 100) {
+    hipLaunchKernelGGL(attn_fwd_pipe_kernel, grid, dim3(kAttnThreads), 2 * kRing * kTileKV, stream,
+                       a);
+    return hipGetLastError();
+  }
   switch (g_attn_fwd_variant) {
 #define FWD_V(N)                                                                           \
   case N:                                                                                  \

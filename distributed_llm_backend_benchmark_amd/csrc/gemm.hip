@@ -1770,6 +1770,286 @@ __global__ void __launch_bounds__(kThreads2, 1) gemm_bf16_nn_256_pp_persist_bal(
 }
 
 // ---------------------------------------------------------------------------------------
+// Stream-K NT GEMM (256² tiles, the balanced / plain ping-pong schedule of pp_persist_body) for
+// grids below one round of the CUs — the 7B TP shard projections (models.py:47,81 at
+// baseline_config.yaml:17 P = 4 / 8: 96-128 tiles on 256 CUs). The output
+// tiles' K-loops are laid end to end as ONE stream of tiles * nk K-tile iterations; workgroup v
+// (one per CU) runs the contiguous range [v L, v L + L) of it, so every CU gets the same work
+// whatever the tile count. With tiles < workgroups a range is at most nk long, so it touches at
+// most two tiles: the tail of tile P and the head of tile P + 1. A tile covered by ONE range is
+// stored directly (full epilogue); a tile split between ranges is combined in the launch, per
+// WAVE (each wave owns a 128 x 64 block of every tile, so no workgroup barrier is needed, and
+// the staggered wave rows of the ping-pong keep their barrier pairing):
+//   poll the (tile, wave) arrival counter; unless every other contributor has already arrived,
+//   store the 32 fp32 accumulators write-through (sc1, 1 KiB per wave-instruction), drain them
+//   (s_waitcnt vmcnt(0)) and add 1 to the counter. The wave that sees the last arrival (its poll
+//   or the value its add returned) reads the other contributors' blocks with sc1 loads, adds
+//   them in registers, resets the counter to 0 and runs the whole epilogue (bias, GELU,
+//   pre-activation, residual, bf16 | fp32 store). MI355X_MICROARCH.md 'Valid forms' row 1: sc1
+//   stores, vmcnt(0) before the add, one workgroup per CU, loads after the add returned, sc1
+//   loads — no release / acquire fences (a release writes back the whole XCD L2). Nobody waits
+//   for anybody, so the launch cannot deadlock beside other kernels holding CUs.
+// Partial block of (slot, wave): ws + (slot * 8 + wave) * 32 KiB, register r of lane l at
+// r * 1 KiB + 16 l. Slots: workgroup v's first segment (its range starts inside the tile) uses
+// slot 2 v, its second segment slot 2 v + 1; a contributor u of tile t used slot 2 u iff
+// u L >= t nk. Counters: tiles * 8 ints, zero on entry and left zero.
+typedef unsigned sk_u32v4 __attribute__((vector_size(16)));   // the buffer builtins' b128 type
+
+struct SkArgs {
+  float* ws;
+  int* cnt;
+  int L;       // K-tile iterations per workgroup
+  int nk;      // K-tiles per output tile
+};
+
+// tile index -> 256² output tile, GROUP_M order without the XCD remap (consecutive stream
+// ranges are placed on one XCD instead, see pp_streamk_body)
+__device__ __forceinline__ Tile256 tile_linear(const GemmArgs& a, int wid) {
+  const int tiles_m = static_cast<int>((a.M + BM2 - 1) / BM2);
+  const int tiles_n = static_cast<int>((a.N + BN2 - 1) / BN2);
+  const int group_size = kGroupM * tiles_n;
+  const int group = wid / group_size;
+  const int first_m = group * kGroupM;
+  const int gm = (tiles_m - first_m) < kGroupM ? (tiles_m - first_m) : kGroupM;
+  const int in_group = wid - group * group_size;
+  return Tile256{static_cast<int64_t>(first_m + in_group % gm) * BM2,
+                 static_cast<int64_t>(in_group / gm) * BN2};
+}
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const void* p) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, 0x7fffffff, 0x00020000);
+}
+
+// One wave's end of a segment of tile t (see above). `full`: the segment is the whole K range.
+__device__ __forceinline__ void sk_finish(const GemmArgs& a, const SkArgs& s, f32x4 (&acc)[8][4],
+                                          int t, bool full, int v, int slot, int wave, int lane) {
+  const Tile256 T = tile_linear(a, t);
+  if (!full) {
+    int* cnt = s.cnt + t * 8 + wave;
+    const int first = (t * s.nk) / s.L, last = ((t + 1) * s.nk - 1) / s.L;
+    const int others = last - first;                  // contributors besides this one
+    const __amdgpu_buffer_rsrc_t rw = rsrc_of(s.ws);
+    const uint32_t lo = static_cast<uint32_t>(lane) * 16;
+    int seen = 0;
+    if (lane == 0) seen = __hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    seen = __builtin_amdgcn_readfirstlane(seen);
+    bool is_last = seen == others;
+    if (!is_last) {
+      const uint32_t base = static_cast<uint32_t>(slot * 8 + wave) * 32768u;
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(sk_u32v4, acc[i][j]), rw, lo,
+                                                 base + (i * 4 + j) * 1024, 16);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      int prev = 0;
+      if (lane == 0)
+        prev = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      prev = __builtin_amdgcn_readfirstlane(prev);
+      is_last = prev == others;
+    }
+    if (!is_last) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      return;
+    }
+    for (int u = first; u <= last; ++u) {
+      if (u == v) continue;
+      const int su = u * s.L >= t * s.nk ? 2 * u : 2 * u + 1;
+      const uint32_t base = static_cast<uint32_t>(su * 8 + wave) * 32768u;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {                   // 16 loads in flight, then 16 adds
+        f32x4 p[4][4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            p[i][j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                rw, lo, base + ((4 * h + i) * 4 + j) * 1024, 16));
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[4 * h + i][j] += p[i][j];
+      }
+    }
+    if (lane == 0) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  store_tile_256(a, acc, T.m0, T.n0, wave, lane);
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+}
+
+template <bool BAL>
+__device__ __forceinline__ void pp_streamk_body(GemmArgs a, SkArgs s, char* smem) {
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = wave >> 2, wc = wave & 3;
+  const int fr = lane & 15, fq = lane >> 4;
+  const int nk = s.nk;
+  // stream position v of this workgroup: consecutive ranges (which share tiles, so their
+  // partial blocks and A / B panels) on one XCD (blockIdx % 8 under round-robin dispatch —
+  // speed only, never correctness); the same bijective remap as tile_of
+  const int nwg = static_cast<int>(gridDim.x), bx = static_cast<int>(blockIdx.x);
+  const int q8 = nwg >> 3, r8 = nwg & 7, x8 = bx & 7;
+  const int v = (x8 < r8 ? x8 * (q8 + 1) : r8 * (q8 + 1) + (x8 - r8) * q8) + (bx >> 3);
+  const int tiles = static_cast<int>(((a.M + BM2 - 1) / BM2) * ((a.N + BN2 - 1) / BN2));
+  const int it0 = v * s.L;
+  const int itend = it0 + s.L < tiles * nk ? it0 + s.L : tiles * nk;
+  if (it0 >= itend) return;                          // (host: never; whole workgroup)
+  const int G = itend - it0;                          // this range's K-tiles (host: >= 2)
+  const int tP = it0 / nk, kP = it0 - tP * nk;        // first tile and its first K-tile
+  const int gb = nk - kP;                             // first iteration of tile P + 1
+  const Tile256 TP = tile_linear(a, tP);
+  const Tile256 TQ = gb < G ? tile_linear(a, tP + 1) : TP;
+  char* const abuf0 = smem;
+  char* const bbuf0 = smem + 2 * kTile2Bytes;
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 af[2][8], bf[2][4];
+  const int r_in = lane >> 3, chunk = (lane & 7) ^ (lane >> 3);
+  const uint32_t lda2 = static_cast<uint32_t>(a.lda) * 2, ldb2 = static_cast<uint32_t>(a.ldb) * 2;
+  const uint32_t aoff = static_cast<uint32_t>(r_in) * lda2 + chunk * 16;
+  const uint32_t boff = static_cast<uint32_t>(perm_brow(r_in)) * ldb2 + chunk * 16;
+  constexpr uint32_t kStep = BK * 2;
+  const __amdgpu_buffer_rsrc_t raP = rsrc_of(a.A + TP.m0 * a.lda);
+  const __amdgpu_buffer_rsrc_t rbP = rsrc_of(a.B + TP.n0 * a.ldb);
+  const __amdgpu_buffer_rsrc_t raQ = rsrc_of(a.A + TQ.m0 * a.lda);
+  const __amdgpu_buffer_rsrc_t rbQ = rsrc_of(a.B + TQ.n0 * a.ldb);
+  const int rows_aP = static_cast<int>(a.M - TP.m0), rows_bP = static_cast<int>(a.N - TP.n0);
+  const int rows_aQ = static_cast<int>(a.M - TQ.m0), rows_bQ = static_cast<int>(a.N - TQ.n0);
+  // iteration g -> (tile P or Q, K-tile index inside it)
+  auto in_q = [&](int g) __attribute__((always_inline)) { return g >= gb; };
+  auto kt = [&](int g) __attribute__((always_inline)) { return g >= gb ? g - gb : kP + g; };
+  auto stage_a = [&](int g, char* buf, int half) __attribute__((always_inline)) {
+    const bool q = in_q(g);
+    stage_a_half(q ? raQ : raP, lda2, q ? rows_aQ : rows_aP, static_cast<uint32_t>(kt(g)) * kStep,
+                 buf, half, wc, aoff);
+  };
+  auto stage_bh = [&](auto i0, auto i1, int g, char* buf) __attribute__((always_inline)) {
+    constexpr int I0 = decltype(i0)::value, I1 = decltype(i1)::value;
+    const bool q = in_q(g);
+    stage_b<I0, I1>(q ? rbQ : rbP, ldb2, q ? rows_bQ : rows_bP,
+                    static_cast<uint32_t>(kt(g)) * kStep, buf, wc, boff);
+  };
+  using Z = std::integral_constant<int, 0>;
+  using H = std::integral_constant<int, 4>;
+  using F = std::integral_constant<int, 8>;
+  // end of a segment: tile P after iteration gb - 1 (when Q follows), the last tile after G - 1
+  auto finish = [&](int g) __attribute__((always_inline)) {
+    const bool q = in_q(g);
+    const int kb = q ? 0 : kP, ke = kt(g) + 1;
+    int ln = lane;
+    asm volatile("" : "+v"(ln));                    // epilogue addresses not hoisted
+    sk_finish(a, s, acc, q ? tP + 1 : tP, kb == 0 && ke == nk, v, q ? 2 * v + 1 : 2 * v, wave, ln);
+  };
+
+  if (wr == 0) {                                    // prologue: A-lo(0), B(0), B(1)
+    stage_a(0, abuf0, 0);
+    stage_bh(Z{}, F{}, 0, bbuf0);
+    stage_bh(Z{}, F{}, 1, bbuf0 + kTile2Bytes);
+    DLBB_WAIT_VM(8);
+    __builtin_amdgcn_s_barrier();
+  } else {                                          // A-hi(0), A-lo(1)
+    stage_a(0, abuf0, 1);
+    stage_a(1, abuf0 + kTile2Bytes, 0);
+    __builtin_amdgcn_s_barrier();
+    DLBB_WAIT_VM(4);
+    __builtin_amdgcn_s_barrier();                   // end of interval 0
+  }
+  int cb = 0;                                       // B buffer of iteration g (g % 3)
+  if (wr == 0) {
+    for (int g = 0; g < G; ++g) {
+      const bool bnd = g == gb && g > 0;            // first K-tile of tile Q
+      read_split_any<false>(abuf0 + (g & 1) * kTile2Bytes, bbuf0 + cb * kTile2Bytes, 0, wc, fr,
+                            fq, af, bf);
+      const bool h1 = g + 1 < G, b2 = g + 2 < G;
+      if (h1) stage_a(g + 1, abuf0 + ((g + 1) & 1) * kTile2Bytes, 1);   // A-hi(g+1)
+      if (b2) {                                     // B(g+2) (BAL: its first half)
+        char* const bn = bbuf0 + (cb == 0 ? 2 : cb - 1) * kTile2Bytes;
+        if (BAL) stage_bh(Z{}, H{}, g + 2, bn);
+        else stage_bh(Z{}, F{}, g + 2, bn);
+      }
+      if (bnd) {
+        // A-hi(g) retired by the segment end's drain
+      } else if (BAL) {
+        if (b2) DLBB_WAIT_VM(12);
+        else if (h1) DLBB_WAIT_VM(8);
+        else DLBB_WAIT_VM(0);
+      } else {
+        if (b2) DLBB_WAIT_VM(20);
+        else if (h1) DLBB_WAIT_VM(12);
+        else DLBB_WAIT_VM(0);
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();                 // end of interval 2g
+      __builtin_amdgcn_sched_barrier(0);
+      mfma_full(acc, af, bf);
+      __builtin_amdgcn_sched_barrier(0);
+      if (h1 && !bnd) {
+        if (b2) { if (BAL) DLBB_WAIT_VM(8); else DLBB_WAIT_VM(12); }
+        else DLBB_WAIT_VM(4);
+      }
+      __builtin_amdgcn_s_barrier();                 // end of interval 2g+1
+      cb = cb == 2 ? 0 : cb + 1;
+      if (g == gb - 1 || g == G - 1) {
+        DLBB_WAIT_VM(0);
+        __builtin_amdgcn_sched_barrier(0);
+        finish(g);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+  } else {
+    for (int g = 0; g < G; ++g) {
+      const bool bnd = g == gb && g > 0;
+      read_split_any<false>(abuf0 + (g & 1) * kTile2Bytes, bbuf0 + cb * kTile2Bytes, 1, wc, fr,
+                            fq, af, bf);
+      const bool l2 = g + 2 < G;
+      if (l2) {                                     // A-lo(g+2) (BAL: and B1(g+2))
+        stage_a(g + 2, abuf0 + (g & 1) * kTile2Bytes, 0);
+        if (BAL) stage_bh(H{}, F{}, g + 2, bbuf0 + (cb == 0 ? 2 : cb - 1) * kTile2Bytes);
+      }
+      if (g + 1 < G && !bnd) {
+        if (l2) { if (BAL) DLBB_WAIT_VM(8); else DLBB_WAIT_VM(4); }
+        else DLBB_WAIT_VM(0);
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();                 // end of interval 2g+1
+      __builtin_amdgcn_sched_barrier(0);
+      mfma_full(acc, af, bf);
+      __builtin_amdgcn_sched_barrier(0);
+      if (g + 1 < G) __builtin_amdgcn_s_barrier();  // end of interval 2g+2
+      cb = cb == 2 ? 0 : cb + 1;
+      if (g == gb - 1 || g == G - 1) {
+        DLBB_WAIT_VM(0);
+        __builtin_amdgcn_sched_barrier(0);
+        finish(g);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+  }
+}
+
+__global__ void __launch_bounds__(kThreads2, 1) gemm_bf16_nt_256_streamk(GemmArgs a, SkArgs s) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  pp_streamk_body<false>(a, s, smem);
+}
+__global__ void __launch_bounds__(kThreads2, 1) gemm_bf16_nt_256_streamk_bal(GemmArgs a, SkArgs s) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  pp_streamk_body<true>(a, s, smem);
+}
+
+// ---------------------------------------------------------------------------------------
 // Persistent 256 x 192 ping-pong with the C stores SPREAD under the next tile's K-loop (plain
 // bf16 output; autotune candidate `mfma192p`). Built to test whether a tile's C stores, flushed in
 // one burst by pp_persist_body at the next tile's first memory interval, cost the GPT-2 LM head
@@ -2379,97 +2659,68 @@ DLBB_API void dlbb_gemm_set_group_m(int g) { dlbb_group_m = g > 0 ? g : 0; }
 DLBB_API void dlbb_gemm_set_bal(int mode) { dlbb_gemm_bal = mode >= 0 && mode <= 2 ? mode : 2; }
 
 // ---------------------------------------------------------------------------------------
-// NT split-K (grids well below one round of the CUs — the 7B TP projections at P = 8: 96-128
-// tiles on 256 CUs — VERDICT r03 item 2): slice s of the reduction writes fp32 partials
-// [M][N] into ws + s M N (ping-pong body, plain fp32 epilogue), then ONE pass sums the slices
-// and applies the whole epilogue: + bias -> pre-activation store -> GELU -> + residual ->
-// bf16 | fp32 store. 4 consecutive columns per thread (N % 4 == 0, 8-B aligned rows).
-__global__ void __launch_bounds__(256) nt_split_epilogue_kernel(
-    const float* __restrict__ ws, int split, int64_t M, int64_t N, const uint16_t* bias,
-    const uint16_t* residual, int64_t ldr, uint16_t* preact, void* C, int64_t ldc, int out_f32,
-    int epi) {
-  const int64_t nq = N >> 2, total = M * nq, slab = M * N;
-  for (int64_t q = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; q < total;
-       q += static_cast<int64_t>(gridDim.x) * blockDim.x) {
-    const int64_t m = q / nq, n = (q - m * nq) << 2;
-    const float* p = ws + m * N + n;
-    float4 v = *reinterpret_cast<const float4*>(p);
-    for (int s = 1; s < split; ++s) {
-      const float4 w = *reinterpret_cast<const float4*>(p + s * slab);
-      v.x += w.x; v.y += w.y; v.z += w.z; v.w += w.w;
-    }
-    float x[4] = {v.x, v.y, v.z, v.w};
-    if (epi & EPI_BIAS) {
-      const u16x4 b = *reinterpret_cast<const u16x4*>(bias + n);
-#pragma unroll
-      for (int c = 0; c < 4; ++c) x[c] += bf16_to_f32(b[c]);
-    }
-    if (preact)
-      *reinterpret_cast<u16x4*>(preact + m * ldc + n) =
-          u16x4{f32_to_bf16(x[0]), f32_to_bf16(x[1]), f32_to_bf16(x[2]), f32_to_bf16(x[3])};
-#pragma unroll
-    for (int c = 0; c < 4; ++c) x[c] = apply_act(x[c], epi);
-    if (epi & EPI_RESIDUAL) {
-      const u16x4 r = *reinterpret_cast<const u16x4*>(residual + m * ldr + n);
-#pragma unroll
-      for (int c = 0; c < 4; ++c) x[c] += bf16_to_f32(r[c]);
-    }
-    if (out_f32)
-      *reinterpret_cast<float4*>(static_cast<float*>(C) + m * ldc + n) =
-          make_float4(x[0], x[1], x[2], x[3]);
-    else
-      *reinterpret_cast<u16x4*>(static_cast<uint16_t*>(C) + m * ldc + n) =
-          u16x4{f32_to_bf16(x[0]), f32_to_bf16(x[1]), f32_to_bf16(x[2]), f32_to_bf16(x[3])};
-  }
+// Stream-K plan (pp_streamk_body) for an NT shape on `ncu` CUs: out = {grid, L, ws bytes,
+// counters}; returns 0 when the shape is outside the Stream-K contract (256² tiles below one
+// round of the CUs, >= 8 K-tiles per tile). Every range is >= kSkMinL K-tiles long (the
+// combine of a split tile costs about a tile's partial block per extra contributor, so very
+// short ranges do not pay) and no range is a single K-tile (the prologue stages two).
+constexpr int kSkMinL = 8;
+DLBB_API int dlbb_gemm_streamk_plan(int64_t M, int64_t N, int64_t K, int ncu, int64_t* out) {
+  if (M <= 0 || N <= 0 || K <= 0 || K % BK != 0 || ncu <= 0) return 0;
+  const int64_t tiles = ((M + BM2 - 1) / BM2) * ((N + BN2 - 1) / BN2);
+  const int64_t nk = K / BK;
+  if (nk < kSkMinL || tiles >= ncu) return 0;
+  const int64_t iters = tiles * nk;
+  int64_t grid = iters / kSkMinL < ncu ? iters / kSkMinL : ncu;
+  if (grid < 2) return 0;
+  int64_t L = (iters + grid - 1) / grid;
+  while (iters % L == 1) ++L;          // no one-K-tile range
+  if (L > nk) return 0;                // (cannot happen for tiles < ncu) a range spans <= 2 tiles
+  grid = (iters + L - 1) / L;
+  out[0] = grid;
+  out[1] = L;
+  out[2] = 2 * grid * 8 * 32768;       // two partial slots per workgroup, 8 waves x 32 KiB
+  out[3] = tiles * 8;                  // (tile, wave) arrival counters
+  return 1;
 }
 
-// Split-K NT GEMM: nj = 4 (256² tiles, N % 64 == 0) or 3 (256 x 192, N % 192 == 0); ws holds
-// split x M x N floats (16-B aligned). Same result contract as dlbb_gemm_bf16_nt except the
-// dGELU epilogues (forward only).
-DLBB_API int dlbb_gemm_bf16_nt_sk(const void* A, int64_t lda, const void* B, int64_t ldb, void* C,
-                                  int64_t ldc, int64_t M, int64_t N, int64_t K, const void* bias,
-                                  const void* residual, int64_t ldr, void* preact, int epi,
-                                  int out_f32, int nj, int split, float* ws,
-                                  hipStream_t stream) {
+// Stream-K NT GEMM, the same result contract as dlbb_gemm_bf16_nt (every epilogue); `ws` /
+// `cnt` as planned by dlbb_gemm_streamk_plan(..., ncu = grid owner's CU count), cnt ZERO on
+// entry (left zero). Host contract as the ping-pong: M % 8 == 0, N % 64 == 0, 16-B aligned
+// A / B / ws rows, 32-bit offsets within a 256-row panel.
+DLBB_API int dlbb_gemm_bf16_nt_streamk(const void* A, int64_t lda, const void* B, int64_t ldb,
+                                       void* C, int64_t ldc, int64_t M, int64_t N, int64_t K,
+                                       const void* bias, const void* residual, int64_t ldr,
+                                       void* preact, int epi, int out_f32, int ncu, void* ws,
+                                       int64_t ws_bytes, int* cnt, int64_t ncnt,
+                                       hipStream_t stream) {
   if (M <= 0 || N <= 0) return hipSuccess;
-  const int64_t nkt = K / BK;
-  if (K <= 0 || K % BK != 0 || split < 2 || split > nkt || !ws) return hipErrorInvalidValue;
-  if (lda % 8 || ldb % 8 || ldc % 4 || M % 8 || M < 8) return hipErrorInvalidValue;
+  int64_t plan[4];
+  if (!dlbb_gemm_streamk_plan(M, N, K, ncu, plan)) return hipErrorInvalidValue;
+  if (!ws || !cnt || ws_bytes < plan[2] || ncnt < plan[3]) return hipErrorInvalidValue;
+  if (lda % 8 || ldb % 8 || M % 8 || N % 64 || M < 8) return hipErrorInvalidValue;
   if ((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(B) |
        reinterpret_cast<uintptr_t>(ws)) & 15)
     return hipErrorInvalidValue;
-  if (nj == 3 ? N % 192 != 0 : (nj != 4 || N % 64 != 0)) return hipErrorInvalidValue;
-  if (lda * 2 * 256 + K * 2 >= (1LL << 31) || ldb * 2 * 256 + K * 2 >= (1LL << 31))
+  if (lda * 2 * 256 + K * 2 >= (1LL << 31) || ldb * 2 * 256 + K * 2 >= (1LL << 31) ||
+      plan[2] >= (1LL << 32))
     return hipErrorInvalidValue;
-  if (epi & ~(EPI_BIAS | EPI_GELU_ERF | EPI_GELU_TANH | EPI_RESIDUAL)) return hipErrorInvalidValue;
-  if ((epi & EPI_BIAS) && (!bias || (reinterpret_cast<uintptr_t>(bias) & 7)))
-    return hipErrorInvalidValue;
-  if ((epi & EPI_RESIDUAL) && (!residual || ldr % 4 || (reinterpret_cast<uintptr_t>(residual) & 7)))
-    return hipErrorInvalidValue;
-  if ((reinterpret_cast<uintptr_t>(C) & 15) || (preact && (reinterpret_cast<uintptr_t>(preact) & 7)))
-    return hipErrorInvalidValue;
-  GemmArgs a{static_cast<const uint16_t*>(A), static_cast<const uint16_t*>(B), ws, nullptr,
-             nullptr, nullptr, M, N, K, lda, ldb, N, 0, 0, 1, 1, 0};
-  a.kt_split = static_cast<int>((nkt + split - 1) / split);
-  split = static_cast<int>((nkt + a.kt_split - 1) / a.kt_split);   // no empty trailing slice
-  const int64_t tiles = ((M + BM2 - 1) / BM2) * ((N + 64 * nj - 1) / (64 * nj));
-  const dim3 g(static_cast<unsigned>(tiles), static_cast<unsigned>(split)), b(kThreads2);
-  const bool bal = use_bal(a.kt_split, false);
-  if (nj == 3) {
-    if (bal) hipLaunchKernelGGL(gemm_bf16_nt_192_pingpong3_bal, g, b, kPP192Lds, stream, a);
-    else hipLaunchKernelGGL(gemm_bf16_nt_192_pingpong3, g, b, kPP192Lds, stream, a);
-  } else {
-    if (bal) hipLaunchKernelGGL(gemm_bf16_nt_256_pingpong3_bal, g, b, kPP6Lds, stream, a);
-    else hipLaunchKernelGGL(gemm_bf16_nt_256_pingpong3, g, b, kPP6Lds, stream, a);
-  }
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return e;
-  const int64_t work = M * (N / 4);
-  const int64_t blocks = (work + 255) / 256 < 4096 ? (work + 255) / 256 : 4096;
-  hipLaunchKernelGGL(nt_split_epilogue_kernel, dim3(static_cast<unsigned>(blocks)), dim3(256), 0,
-                     stream, ws, split, M, N, static_cast<const uint16_t*>(bias),
-                     static_cast<const uint16_t*>(residual), ldr, static_cast<uint16_t*>(preact),
-                     C, ldc, out_f32, epi);
+  if ((epi & EPI_BIAS) && !bias) return hipErrorInvalidValue;
+  if ((epi & EPI_READS_R) && !residual) return hipErrorInvalidValue;
+  auto al16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+  const int vec_ok = (ldc % 8 == 0) && al16(C) && (!preact || al16(preact)) &&
+                     (!(epi & EPI_READS_R) || (ldr % 8 == 0 && al16(residual))) &&
+                     (!(epi & EPI_BIAS) || al16(bias));
+  GemmArgs a{static_cast<const uint16_t*>(A), static_cast<const uint16_t*>(B), C,
+             static_cast<const uint16_t*>(bias), static_cast<const uint16_t*>(residual),
+             static_cast<uint16_t*>(preact), M, N, K, lda, ldb, ldc, ldr, epi, out_f32,
+             vec_ok, 0};
+  SkArgs s{static_cast<float*>(ws), cnt, static_cast<int>(plan[1]), static_cast<int>(K / BK)};
+  const dim3 g(static_cast<unsigned>(plan[0])), b(kThreads2);
+  if (use_bal(plan[1], false))
+    hipLaunchKernelGGL(gemm_bf16_nt_256_streamk_bal, g, b, kPP6Lds, stream, a, s);
+  else
+    hipLaunchKernelGGL(gemm_bf16_nt_256_streamk, g, b, kPP6Lds, stream, a, s);
   return hipGetLastError();
 }
 

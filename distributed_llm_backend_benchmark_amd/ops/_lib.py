@@ -66,9 +66,11 @@ _SIGS = {
     "dlbb_gemm_bf16_nt_v": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64,
                                     c_int64, c_int64, c_int64, c_void_p, c_void_p, c_int64,
                                     c_void_p, c_int, c_int, c_int, c_void_p]),
-    "dlbb_gemm_bf16_nt_sk": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64,
-                                     c_int64, c_int64, c_int64, c_void_p, c_void_p, c_int64,
-                                     c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p]),
+    "dlbb_gemm_streamk_plan": (c_int, [c_int64, c_int64, c_int64, c_int, c_void_p]),
+    "dlbb_gemm_bf16_nt_streamk": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_void_p,
+                                          c_int64, c_int64, c_int64, c_int64, c_void_p,
+                                          c_void_p, c_int64, c_void_p, c_int, c_int, c_int,
+                                          c_void_p, c_int64, c_void_p, c_int64, c_void_p]),
     "dlbb_gemm_nt_phase_probe": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_void_p,
                                          c_int64, c_int64, c_int64, c_int, c_void_p, c_void_p]),
     "dlbb_gemm_bf16_nn": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64,

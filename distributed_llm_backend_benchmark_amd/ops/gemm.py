@@ -12,6 +12,7 @@ and counted in :data:`FALLBACKS` so benchmarks can report it.
 
 from __future__ import annotations
 
+import ctypes
 import os
 from typing import Optional
 
@@ -272,69 +273,69 @@ def _num_cus(device) -> int:
     return _NCU[idx]
 
 
-def nt_split_plan(M: int, N: int, K: int, nj: int, ncu: int) -> int:
-    """Split-K factor for the NT ping-pong on a grid well below one round of the CUs (1 = no
-    split): the smallest split whose grid fills >= 90 % of its last round (else the best fill),
-    keeping >= 8 K-tiles per slice. 7B TP at P = 8, 4096 x 1536 x 4096 on 256² tiles: 96 tiles
-    -> split 5 (480 of 512 slots); on 256 x 192 tiles 128 -> split 2 (one full round)."""
-    tiles = -(-M // 256) * -(-N // (64 * nj))
-    nkt = K // 64
-    if tiles <= 0 or tiles >= 0.75 * ncu:
-        return 1
-    best, best_fill = 1, tiles / (-(-tiles // ncu) * ncu)
-    for sp in range(2, 9):
-        if nkt // sp < 8:
-            break
-        n = tiles * sp
-        fill = n / (-(-n // ncu) * ncu)
-        if fill >= 0.9:
-            return sp
-        if fill > best_fill + 1e-9:
-            best, best_fill = sp, fill
-    return best
+def streamk_plan(M: int, N: int, K: int, ncu: int):
+    """(grid, L, ws bytes, counters) of the Stream-K NT GEMM (``csrc/gemm.hip``
+    ``dlbb_gemm_streamk_plan``) or None outside its contract: 256² tiles below one round of the
+    CUs (the 7B TP shard projections: 4096 x 1536 x 4096 = 96 tiles -> 256 workgroups of 24
+    K-tiles each), >= 8 K-tiles per tile."""
+    out = (ctypes.c_int64 * 4)()
+    if not _lib.lib().dlbb_gemm_streamk_plan(M, N, K, ncu, out):
+        return None
+    return tuple(int(v) for v in out)
 
 
-def _mfma_sk_linear(x2, w, bias, act, r2, out, preact, nj: int = 4):
-    """Split-K NT ping-pong (fp32 partials, one fused reduce + epilogue pass): grids well below
-    one round of the CUs (``csrc/gemm.hip`` ``dlbb_gemm_bf16_nt_sk``)."""
+_SK_WS = {}      # (device index, stream handle) -> (fp32 partial workspace, int32 counters)
+
+
+def _streamk_buffers(device: torch.device, ws_bytes: int, ncnt: int):
+    """Partial-block workspace and (tile, wave) arrival counters, private to the current stream
+    (launches on one stream are ordered; every launch leaves its counters zero), grown on
+    demand — one zero-fill per stream, no per-call allocation or memset."""
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    key = (idx, _lib.stream(device))
+    ws, cnt = _SK_WS.get(key, (None, None))
+    if ws is None or ws.numel() * 4 < ws_bytes:
+        ws = torch.empty(max(ws_bytes // 4, 1 << 20), dtype=torch.float32, device=device)
+    if cnt is None or cnt.numel() < ncnt:
+        cnt = torch.zeros(max(ncnt, 4096), dtype=torch.int32, device=device)
+    _SK_WS[key] = (ws, cnt)
+    return ws, cnt
+
+
+def _mfma_streamk_linear(x2, w, bias, act, r2, out, preact):
+    """Stream-K NT ping-pong (``csrc/gemm.hip`` ``pp_streamk_body``): every CU gets an equal
+    contiguous range of the output tiles' K-loops; tiles split between ranges are combined in
+    the launch by the last-arriving wave. Outside its contract: the default ping-pong."""
     M, K = x2.shape
     N = w.shape[0]
-    split = nt_split_plan(M, N, K, nj, _num_cus(x2.device))
-    if split < 2:
-        return _mfma_linear(x2, w, bias, act, r2, out, preact, variant=1 if nj == 3 else 0)
+    ncu = _num_cus(x2.device)
+    plan = streamk_plan(M, N, K, ncu)
+    if plan is None:
+        return _mfma_linear(x2, w, bias, act, r2, out, preact)
     epi = ACTS[act]
     if bias is not None:
         epi |= EPI_BIAS
     if r2 is not None:
         epi |= EPI_RESIDUAL
-    ws = torch.empty(split * M * N, dtype=torch.float32, device=x2.device)
-    check(_lib.lib().dlbb_gemm_bf16_nt_sk(
+    ws, cnt = _streamk_buffers(x2.device, plan[2], plan[3])
+    check(_lib.lib().dlbb_gemm_bf16_nt_streamk(
         x2.data_ptr(), x2.stride(0), w.data_ptr(), w.stride(0), out.data_ptr(), out.stride(0),
         M, N, K, _lib.ptr(bias), _lib.ptr(r2), r2.stride(0) if r2 is not None else 0,
-        _lib.ptr(preact), epi, 1 if out.dtype == torch.float32 else 0, int(nj), int(split),
-        ws.data_ptr(), _lib.stream(x2.device)), "gemm_bf16_nt_sk")
+        _lib.ptr(preact), epi, 1 if out.dtype == torch.float32 else 0, ncu, ws.data_ptr(),
+        ws.numel() * 4, cnt.data_ptr(), cnt.numel(), _lib.stream(x2.device)),
+        "gemm_bf16_nt_streamk")
     return out
 
 
-def _mfma192_sk_linear(x2, w, bias, act, r2, out, preact):
-    return _mfma_sk_linear(x2, w, bias, act, r2, out, preact, nj=3)
-
-
-def mfma_sk_ok(x2, w, r2, out, preact, nj: int) -> bool:
-    """Contract of the split-K candidates (host-checked again in C) and a split >= 2 plan."""
+def streamk_ok(x2: torch.Tensor, w: torch.Tensor) -> bool:
+    """Host contract of the Stream-K candidate (checked again in C) and a valid plan."""
     M, K = x2.shape
     N = w.shape[0]
-    if nj == 3 and not mfma192_ok(M, N):
-        return False
-    if nj == 4 and (N % 64 or M % 8):
-        return False
-    al = lambda t: t is None or t.data_ptr() % 16 == 0  # noqa: E731
-    if not (al(out) and al(preact) and al(r2) and out.stride(0) % 4 == 0
-            and (r2 is None or r2.stride(0) % 4 == 0)):
+    if N % 64 or M % 8 or M < 8:
         return False
     if (x2.stride(0) * 512 + K * 2) >= 2 ** 31 or (w.stride(0) * 512 + K * 2) >= 2 ** 31:
         return False
-    return nt_split_plan(M, N, K, nj, _num_cus(x2.device)) >= 2
+    return streamk_plan(M, N, K, _num_cus(x2.device)) is not None
 
 
 _APPROX = {"gelu": 0, "gelu_erf": 0, "gelu_tanh": 1}
@@ -373,12 +374,8 @@ def _blas_linear(x2, w, bias, act, r2, out, preact):
 
 CHOICES = {}          # (M, N, K, epi-signature) -> "mfma" | "mfma192" | "mfma_sk" | ... | "blas"
 CALLS = {}            # ("linear" | "wgrad", key) -> calls since import (kernel-mix accounting)
-# Split-K (_mfma_sk_linear) is NOT an autotune candidate: measured 1.1-1.7x slower than the
-# ping-pong on every sub-round TP shape (7B P = 8: qkv 0.102 / 0.065 ms split on 256² / 256 x 192
-# vs 0.059 unsplit; profiles/r04_gemm/gemm_table.jsonl) — a workgroup's fixed cost (prologue,
-# C store, launch: ~10 us) is paid per slice, and the partial slabs add a pass. Kept for A/B.
 _IMPLS = {"mfma": _mfma_linear, "mfma192": _mfma192_linear, "mfma192p": _mfma192p_linear,
-          "blas": _blas_linear}
+          "mfma_sk": _mfma_streamk_linear, "blas": _blas_linear}
 
 
 # > 0 while GEMMs share the chip with communication kernels on another stream (the overlapped
@@ -426,6 +423,10 @@ def _autotune(key, args) -> str:
              and not key[8] and key[-1] != "concurrent")
     if not mfma192p_ok(key[0], key[1], key[2], plain):
         del impls["mfma192p"]
+    # Stream-K: grids below one round of the CUs; off beside comm kernels (its ranges assume
+    # every CU is free, like the persistent forms)
+    if key[-1] == "concurrent" or not streamk_ok(args[0], args[1]):
+        del impls["mfma_sk"]
     times = _time_interleaved({n: (lambda f=f: f(*args)) for n, f in impls.items()})
     best, times = _choose(times, "linear", key)
     CHOICES[key] = best

@@ -190,6 +190,9 @@ def fork(to: "torch.cuda.Stream", frm: Optional["torch.cuda.Stream"] = None) -> 
         return
     from ..ops import _lib
 
-    rc = _lib.lib().dlbb_stream_fork(frm.cuda_stream, to.cuda_stream, _FORK_MODE)
+    # the event ring is per device (csrc/streams.hip picks it by the current device): make it
+    # the streams' device, whatever device is current
+    with torch.cuda.device(to.device):
+        rc = _lib.lib().dlbb_stream_fork(frm.cuda_stream, to.cuda_stream, _FORK_MODE)
     if rc != 0:
         raise RuntimeError(f"dlbb_stream_fork failed (hip error {rc})")

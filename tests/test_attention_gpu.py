@@ -36,7 +36,7 @@ def test_attn_fwd_matches_fp32_reference(B, T, H):
     torch.testing.assert_close(lse, ref_lse, rtol=1e-3, atol=2e-3)
 
 
-@pytest.mark.parametrize("variant", list(range(8)) + [14])
+@pytest.mark.parametrize("variant", list(range(8)) + [14, 100])
 @pytest.mark.parametrize("B,T,H", [(2, 200, 2), (2, 1024, 2), (1, 333, 1)])
 def test_attn_fwd_variants_match_fp32_reference(B, T, H, variant):
     """Every forward schedule variant (batched K reads / permlane exchange / incremental DMA
@@ -66,6 +66,34 @@ def test_attn_fwd_variants_match_fp32_reference(B, T, H, variant):
         o1, _ = attn_fwd(q, 1)
         r1, _ = _ref(q, 1)
         torch.testing.assert_close(o1.float(), r1, rtol=2e-2, atol=1e-2)
+    finally:
+        lib.dlbb_attn_set_fwd_variant(old)
+
+
+@pytest.mark.parametrize("variant", [6, 100])
+def test_attn_fwd_growing_scores(variant):
+    """Scores whose row max keeps growing along the keys (key rows scaled up with their index):
+    the pipelined forward's lazy rescale (reference max moved only past a 2^8 growth) must
+    still give the exact softmax."""
+    from distributed_llm_backend_benchmark_amd.ops import _lib
+    from distributed_llm_backend_benchmark_amd.ops.attention import attn_fwd
+
+    lib = _lib.lib()
+    old = lib.dlbb_attn_get_fwd_variant()
+    try:
+        lib.dlbb_attn_set_fwd_variant(variant)
+        B, T, H, D = 2, 777, 2, 64
+        g = torch.Generator(device="cuda").manual_seed(5)
+        x = torch.randn(B, T, 3, H, D, device="cuda", generator=g)
+        q = torch.randn(D, device="cuda", generator=g)
+        x[:, :, 0] = q + 0.1 * x[:, :, 0]                 # every query ~ q
+        ramp = torch.linspace(0.0, 6.0, T, device="cuda").view(1, T, 1, 1)
+        x[:, :, 1] = q * ramp + 0.1 * x[:, :, 1]           # scores grow ~ linearly with the key
+        qkv = x.reshape(B, T, 3 * H * D).to(torch.bfloat16)
+        out, lse = attn_fwd(qkv, H)
+        ref, ref_lse = _ref(qkv, H)
+        torch.testing.assert_close(out.float(), ref, rtol=2e-2, atol=2e-2)
+        torch.testing.assert_close(lse, ref_lse, rtol=1e-3, atol=5e-3)
     finally:
         lib.dlbb_attn_set_fwd_variant(old)
 

@@ -708,7 +708,7 @@ def _list_allgather_worker(rank, world):
             op.run()
             ins = [make_data((n,), torch.bfloat16, r, comm.device) for r in range(world)]
             exact = all(torch.equal(o, i) for o, i in zip(op.outs, ins))
-            res.append((n, exact, op._tensor_ok))
+            res.append((n, exact, op.impl))
         return res
     finally:
         comm.destroy()
@@ -718,5 +718,6 @@ def test_allgather_list_form_unpack_bit_exact():
     """Reference list form (collectives/1d/dsccl.py:72-76): gathered once into a flat staging
     buffer, unpacked into the list by one chunk-copy table; every entry bit-exact."""
     for rank, res in enumerate(run_multiprocess(_list_allgather_worker, 2, timeout=300)):
-        for n, exact, _ in res:
+        for n, exact, impl in res:
             assert exact, (rank, n)
+            assert impl == "allgather_into_tensor+unpack", impl   # recorded as op_impl

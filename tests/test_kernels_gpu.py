@@ -1018,14 +1018,14 @@ def test_gemm_autotune_beside_comm_keeps_to_hand_written_kernels(monkeypatch):
     assert gemm._CONCURRENT[0] == 0
 
 
-@pytest.mark.parametrize("M,N,K,nj", [(4096, 1536, 4096, 4), (4096, 1536, 4096, 3),
-                                      (4096, 2048, 4096, 4), (520, 384, 2048, 3),
-                                      (1000, 640, 1024, 4)])
+@pytest.mark.parametrize("M,N,K", [(4096, 1536, 4096), (4096, 2048, 4096), (4096, 3072, 1024),
+                                   (1000, 640, 1024), (520, 384, 2048), (2048, 1024, 512)])
 @pytest.mark.parametrize("epi", ["plain_f32", "bias_gelu_pre_res", "plain_bf16"])
-def test_gemm_nt_split_k_matches_fp32(M, N, K, nj, epi):
-    """Split-K NT ping-pong (fp32 partial slabs + one fused reduce / epilogue pass) for grids
-    well below one round of the CUs, against fp32: ragged M, 256² and 256 x 192 tiles, the
-    whole epilogue chain."""
+def test_gemm_nt_streamk_matches_fp32(M, N, K, epi):
+    """Stream-K NT ping-pong (equal K-tile ranges per CU, split tiles combined in the launch by
+    the last-arriving wave) for grids below one round of the CUs, against fp32: ragged M, tiles
+    split between 2-4 ranges, the whole epilogue chain; run twice so the arrival counters are
+    shown to be left zero."""
     from distributed_llm_backend_benchmark_amd.ops import gemm
 
     x = _randn(M, K, seed=51, scale=0.3)
@@ -1033,25 +1033,53 @@ def test_gemm_nt_split_k_matches_fp32(M, N, K, nj, epi):
     b = _randn(N, seed=53)
     r = _randn(M, N, seed=54)
     ncu = torch.cuda.get_device_properties(0).multi_processor_count
-    assert gemm.nt_split_plan(M, N, K, nj, ncu) >= 2
+    plan = gemm.streamk_plan(M, N, K, ncu)
+    assert plan is not None and gemm.streamk_ok(x, w), plan
     u = x.float() @ w.float().t()
-    if epi == "plain_f32":
+    for _ in range(2):
+        if epi == "plain_f32":
+            y = torch.empty(M, N, dtype=torch.float32, device=DEV)
+            gemm._mfma_streamk_linear(x, w, None, None, None, y, None)
+            torch.testing.assert_close(y, u, rtol=2e-3, atol=2e-3 * K ** 0.5)
+        elif epi == "plain_bf16":
+            y = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+            gemm._mfma_streamk_linear(x, w, None, None, None, y, None)
+            torch.testing.assert_close(y.float(), u, rtol=2e-2, atol=2e-2 * K ** 0.5)
+        else:
+            y = torch.empty(M, N, dtype=torch.float32, device=DEV)
+            pre = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+            gemm._mfma_streamk_linear(x, w, b, "gelu", r, y, pre)
+            ub = u + b.float()
+            torch.testing.assert_close(y, F.gelu(ub) + r.float(), rtol=2e-3, atol=2e-3 * K ** 0.5)
+            torch.testing.assert_close(pre.float(), ub, rtol=2e-2, atol=2e-2 * K ** 0.5)
+        torch.cuda.synchronize()
+    _, cnt = gemm._SK_WS[(0, _lib_stream())]
+    assert int(cnt.abs().sum()) == 0
+
+
+def _lib_stream():
+    from distributed_llm_backend_benchmark_amd.ops import _lib
+
+    return _lib.stream(torch.device(DEV))
+
+
+def test_gemm_nt_streamk_repeatable():
+    """Repeated launches agree to fp32 rounding: the last-arriving wave of a split tile adds the
+    other contributors' blocks to its own, so the summation order follows the arrival order
+    (like float-atomic split-K), never more than one rounding per contributor apart."""
+    from distributed_llm_backend_benchmark_amd.ops import gemm
+
+    M, N, K = 4096, 1536, 4096
+    x = _randn(M, K, seed=61, scale=0.3)
+    w = _randn(N, K, seed=62, scale=0.3)
+    ys = []
+    for _ in range(3):
         y = torch.empty(M, N, dtype=torch.float32, device=DEV)
-        assert gemm.mfma_sk_ok(x, w, None, y, None, nj)
-        gemm._mfma_sk_linear(x, w, None, None, None, y, None, nj=nj)
-        torch.testing.assert_close(y, u, rtol=2e-3, atol=2e-3 * K ** 0.5)
-    elif epi == "plain_bf16":
-        y = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
-        gemm._mfma_sk_linear(x, w, None, None, None, y, None, nj=nj)
-        torch.testing.assert_close(y.float(), u, rtol=2e-2, atol=2e-2 * K ** 0.5)
-    else:
-        y = torch.empty(M, N, dtype=torch.float32, device=DEV)
-        pre = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
-        gemm._mfma_sk_linear(x, w, b, "gelu", r, y, pre, nj=nj)
-        ub = u + b.float()
-        torch.testing.assert_close(y, F.gelu(ub) + r.float(), rtol=2e-3, atol=2e-3 * K ** 0.5)
-        torch.testing.assert_close(pre.float(), ub, rtol=2e-2, atol=2e-2 * K ** 0.5)
+        gemm._mfma_streamk_linear(x, w, None, None, None, y, None)
+        ys.append(y)
     torch.cuda.synchronize()
+    for y in ys[1:]:
+        torch.testing.assert_close(y, ys[0], rtol=1e-5, atol=1e-4)
 
 
 def test_gemm_autotune_offers_tile_variants(monkeypatch):

@@ -7,8 +7,8 @@ interleaved rounds, uniform random operands (CDNA guide §5.4 rules 24/25). One 
 ``--modes``: comma list of our-kernel variants to time: ``auto`` = the library dispatch
 (``DLBB_GEMM=mfma``), ``t128`` / ``t256`` force the tile, ``s<N>`` = set_stagger(N), ``v192`` =
 the 256 x 192 tile variant (N % 192 == 0 shapes only), ``v192p`` / ``v192p18`` = its persistent
-spread-store form (variant 2; 12 / 18 stores at the tile boundary), ``sk`` / ``sk192`` = split-K on 256² /
-256 x 192 tiles (grids well below one round only). ``--gpt2`` adds the GPT-2 forward GEMMs.
+spread-store form (variant 2; 12 / 18 stores at the tile boundary), ``sk`` = Stream-K on 256²
+tiles (grids below one round of the CUs only). ``--gpt2`` adds the GPT-2 forward GEMMs.
 """
 import argparse
 import json
@@ -91,8 +91,7 @@ def main():
         ok = {"v192": gemm.mfma192_ok(M, N),
               "v192p": gemm.mfma192p_ok(M, N, K, True),
               "v192p18": gemm.mfma192p_ok(M, N, K, True),
-              "sk": gemm.mfma_sk_ok(x, w, None, out, None, 4),
-              "sk192": gemm.mfma_sk_ok(x, w, None, out, None, 3)}
+              "sk": gemm.streamk_ok(x, w)}
         ms = [m for m in modes if ok.get(m, True)]
 
         def run(m):
@@ -101,9 +100,8 @@ def main():
             if m in ("v192p", "v192p18"):   # persistent, spread C stores (variant 2)
                 _lib.lib().dlbb_gemm_set_spread_early(18 if m == "v192p18" else 12)
                 return gemm._mfma192p_linear(x, w, None, None, None, out, None)
-            if m in ("sk", "sk192"):      # split-K ping-pong + fused reduce / epilogue
-                return gemm._mfma_sk_linear(x, w, None, None, None, out, None,
-                                            nj=3 if m == "sk192" else 4)
+            if m == "sk":                 # Stream-K ping-pong, in-launch combine
+                return gemm._mfma_streamk_linear(x, w, None, None, None, out, None)
             return ops.linear(x, w)
         for m in ms:
             set_mode(m)
