@@ -37,7 +37,9 @@ def parse_args(argv=None):
                          "several ranks sharing one GPU over a gloo process group (rehearsal "
                          "of the multi-rank path; RCCL needs one GPU per rank)")
     ap.add_argument("--allreduce-dtype", choices=["bf16", "fp32"], default=None)
-    ap.add_argument("--attention", choices=["slice", "sdpa"], default=None)
+    ap.add_argument("--attention", choices=["slice", "sdpa", "flash"], default=None,
+                    help="slice = the reference's stub (models.py:162-167, default); sdpa = "
+                         "torch causal attention; flash = our causal flash kernel")
     ap.add_argument("--kernels", choices=["hip", "torch"], default=None)
     ap.add_argument("--model-size", default=None, help="override with a MODEL_CONFIGS size")
     ap.add_argument("--num-layers", type=int, default=None)

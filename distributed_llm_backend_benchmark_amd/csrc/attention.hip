@@ -76,23 +76,6 @@ __device__ __forceinline__ void head_block(int xcd_on, int& blk, int& h, int& b)
   b = hh / H;
 }
 
-// Stage keys [k0, k0 + 64) of head h: K (section 1 of the row) and V (section 2) tiles.
-// 64 rows x 128 B per image = 8 KiB = 8 wave-instructions; wave w issues rows [16w, 16w + 16)
-// of each (2 + 2 instructions). Rows past T are clamped (their scores are masked).
-__device__ __forceinline__ void attn_stage(const AttnArgs& a, const uint16_t* base_bt, int k0,
-                                           int hoff, char* tk, char* tv, int wave, int lane) {
-  const int r_in = lane >> 3, slot = lane & 7;
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int row = wave * 16 + i * 8 + r_in;
-    int key = k0 + row;
-    key = key < a.T ? key : a.T - 1;
-    const uint16_t* src = base_bt + static_cast<int64_t>(key) * a.ld + hoff;
-    attn_glds16(src + kAttnD * a.H + (slot ^ kswz(row)) * 8, tk + (wave * 16 + i * 8) * 128);
-    attn_glds16(src + 2 * kAttnD * a.H + (slot ^ vswz(row)) * 8, tv + (wave * 16 + i * 8) * 128);
-  }
-}
-
 // lane ^ 32 half exchange of a per-lane value by v_permlane32_swap (a VALU op) instead of a
 // ds_bpermute LDS round trip; max over both halves ends in every lane
 __device__ __forceinline__ float xhalf_max(float x) {
@@ -101,24 +84,41 @@ __device__ __forceinline__ float xhalf_max(float x) {
   return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
 }
 
-// v_max3_f32 as one instruction (fmaxf on MFMA outputs gets canonicalising v_max first)
-__device__ __forceinline__ float max3_asm(float a, float b, float c) {
-  float r;
-  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
-  return r;
-}
+// Forward tile geometry per head dim: one 8-KiB image per K / V tile — 64 keys x 128 B at
+// D = 64, 32 keys x 256 B at D = 128 (the TP model's heads, models/tp_transformer.py) — so both
+// keep 32 KiB of LDS per workgroup (double-buffered K and V) and 2 DMA wave-instructions per
+// wave per image.
+template <int D>
+struct FwdGeo {
+  static constexpr int KB = 8192 / (2 * D);   // keys per tile
+  static constexpr int NKK = KB / 32;         // 32-key halves per tile
+  static constexpr int NKS = D / 16;          // k-steps of S^T = K Q^T
+  static constexpr int NDT = D / 32;          // 32-dim blocks of O^T
+  static constexpr int ROW = 2 * D;           // image row bytes
+  static constexpr int RPI = 1024 / ROW;      // rows per DMA wave-instruction
+  static constexpr int TILE = KB * ROW;       // 8 KiB
+};
+// K image (ds_read_b128 row reads) and V image (ds_read_b64_tr_b16) swizzles: 16-B chunk c of
+// row r in slot c ^ swz(r). D = 64 (128-B rows): kswz / vswz above. D = 128 (256-B rows: every
+// row covers all 64 banks): r & 15 makes the 16 rows of each ds_read_b128 lane group hit 16
+// distinct bank quads; (r & 3) << 2 puts the 4 rows of a transposed read's 32-lane group in 4
+// distinct 64-B bank segments.
+template <int D>
+__device__ __forceinline__ int kswz_d(int r) { return D == 64 ? kswz(r) : (r & 15); }
+template <int D>
+__device__ __forceinline__ int vswz_d(int r) { return D == 64 ? vswz(r) : ((r & 3) << 2); }
 
-// Forward variants (bit mask, A/B via dlbb_attn_set_fwd_variant):
-//   1: the tile's 8 K fragments read up front (asm ds_read_b128, one counted lgkmcnt wait per
-//      32-key half) — the compiler's schedule re-used one register quad and waited for each read
-//      in front of its MFMA (8 LDS round trips per tile);
-//   2: the row-max exchange with the other lane half by v_permlane32_swap (no LDS round trip);
-//   4: K/V DMA sources from per-lane base pointers + one uniform offset per tile (the clamped
-//      per-row 64-bit address arithmetic only on a tile that crosses T);
-//   8: row max and row sum as pairwise trees (depth 5) instead of 32-long dependent chains
-//      (instantiated as 14 = 2 | 4 | 8 only).
-template <int V>
-__global__ void __launch_bounds__(kAttnThreads, 2) attn_fwd_d64_kernel(AttnArgs a) {
+// Causal forward, head dim D (64 or 128). Round-5 schedule (variant 6 of its A/B: row-max
+// exchange by v_permlane32_swap, incremental DMA sources; 128 VGPRs at D = 64 = 4 waves per
+// SIMD). Round 6 measured a software-pipelined body (QK^T of tile j+1 and PV of tile j-1 beside
+// the softmax of tile j in one straight block): 75.1 vs 56.5 us at the GPT-2 shape — its 212
+// VGPRs left 2 waves per SIMD, and the hardware's interleave of 4 waves beat the compiler's
+// in-wave interleave (profiles/r06_kernels/attn_fwd_pipelined_ab.jsonl); removed.
+template <int D>
+__global__ void __launch_bounds__(kAttnThreads, 2) attn_fwd_kernel(AttnArgs a) {
+  using G = FwdGeo<D>;
+  constexpr int KB = G::KB, ROW = G::ROW, RPI = G::RPI, TILE = G::TILE;
+  constexpr int WROWS = KB / 4;                   // image rows staged per wave
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -130,58 +130,64 @@ __global__ void __launch_bounds__(kAttnThreads, 2) attn_fwd_d64_kernel(AttnArgs 
   const int qw = q0 + wave * 32;                  // this wave's first query
   const int r = lane & 31, hi = lane >> 5;
   const uint16_t* base_bt = a.qkv + static_cast<int64_t>(b) * a.T * a.ld;
-  const int hoff = h * kAttnD;
+  const int hoff = h * D;
 
   // Q fragments (B operand of S^T = K Q^T): lane holds Q[qw + r][16 ks + 8 hi + j]
-  bf16x8 qf[4];
+  bf16x8 qf[G::NKS];
   {
     int q = qw + r;
     q = q < a.T ? q : a.T - 1;
     const uint16_t* qp = base_bt + static_cast<int64_t>(q) * a.ld + hoff + 8 * hi;
 #pragma unroll
-    for (int ks = 0; ks < 4; ++ks) qf[ks] = *reinterpret_cast<const bf16x8*>(qp + 16 * ks);
+    for (int ks = 0; ks < G::NKS; ++ks) qf[ks] = *reinterpret_cast<const bf16x8*>(qp + 16 * ks);
   }
 
-  f32x16 o[2];
+  f32x16 o[G::NDT];
 #pragma unroll
-  for (int dt = 0; dt < 2; ++dt)
+  for (int dt = 0; dt < G::NDT; ++dt)
 #pragma unroll
     for (int e = 0; e < 16; ++e) o[dt][e] = 0.f;
   float m = -INFINITY, l = 0.f;
   const int qme = qw + r;                          // this lane's query
   const int q_hi = qw + 31;                        // wave's last query
   const int last_key = (q0 + kQB - 1) < (a.T - 1) ? (q0 + kQB - 1) : (a.T - 1);
-  const int nt = last_key / kKB + 1;
+  const int nt = last_key / KB + 1;
 
-  auto tileK = [&](int c) { return smem + c * 2 * kTileKV; };
-  auto tileV = [&](int c) { return smem + c * 2 * kTileKV + kTileKV; };
+  auto tileK = [&](int c) { return smem + c * 2 * TILE; };
+  auto tileV = [&](int c) { return smem + c * 2 * TILE + TILE; };
 
-  // V & 4: this lane's 4 DMA sources of key-tile 0 (rows wave * 16 + i * 8 + lane / 8, K and V
-  // sections); tile kt adds kt * 64 rows, uniform
+  // DMA: this lane's sources of image rows wave * WROWS + i * RPI + lane / (ROW / 16) of key
+  // tile 0 (K and V sections, swizzled chunk); tile kt adds kt * KB rows, uniform
+  const int r_in = lane / (ROW / 16), slot = lane % (ROW / 16);
   const uint16_t* dsrc[4];
-  if constexpr ((V & 4) != 0) {
-    const int r_in = lane >> 3, slot = lane & 7;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int row = wave * 16 + i * 8 + r_in;
-      const uint16_t* src = base_bt + static_cast<int64_t>(row) * a.ld + hoff;
-      dsrc[2 * i] = src + kAttnD * a.H + (slot ^ kswz(row)) * 8;
-      dsrc[2 * i + 1] = src + 2 * kAttnD * a.H + (slot ^ vswz(row)) * 8;
-    }
+  for (int i = 0; i < 2; ++i) {
+    const int row = wave * WROWS + i * RPI + r_in;
+    const uint16_t* src = base_bt + static_cast<int64_t>(row) * a.ld + hoff;
+    dsrc[2 * i] = src + D * a.H + (slot ^ kswz_d<D>(row)) * 8;
+    dsrc[2 * i + 1] = src + 2 * D * a.H + (slot ^ vswz_d<D>(row)) * 8;
   }
   auto stage = [&](int k0, char* tk, char* tv) {
-    if constexpr ((V & 4) != 0) {
-      if (k0 + kKB <= a.T) {                        // wave-uniform: no row past T
-        const int64_t off = static_cast<int64_t>(k0) * a.ld;
+    if (k0 + KB <= a.T) {                          // wave-uniform: no row past T
+      const int64_t off = static_cast<int64_t>(k0) * a.ld;
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {
-          attn_glds16(dsrc[2 * i] + off, tk + (wave * 16 + i * 8) * 128);
-          attn_glds16(dsrc[2 * i + 1] + off, tv + (wave * 16 + i * 8) * 128);
-        }
-        return;
+      for (int i = 0; i < 2; ++i) {
+        attn_glds16(dsrc[2 * i] + off, tk + (wave * WROWS + i * RPI) * ROW);
+        attn_glds16(dsrc[2 * i + 1] + off, tv + (wave * WROWS + i * RPI) * ROW);
       }
+      return;
     }
-    attn_stage(a, base_bt, k0, hoff, tk, tv, wave, lane);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {                  // rows past T clamped (scores masked)
+      const int row = wave * WROWS + i * RPI + r_in;
+      int key = k0 + row;
+      key = key < a.T ? key : a.T - 1;
+      const uint16_t* src = base_bt + static_cast<int64_t>(key) * a.ld + hoff;
+      attn_glds16(src + D * a.H + (slot ^ kswz_d<D>(row)) * 8,
+                  tk + (wave * WROWS + i * RPI) * ROW);
+      attn_glds16(src + 2 * D * a.H + (slot ^ vswz_d<D>(row)) * 8,
+                  tv + (wave * WROWS + i * RPI) * ROW);
+    }
   };
   stage(0, tileK(0), tileV(0));
   for (int kt = 0; kt < nt; ++kt) {
@@ -190,117 +196,59 @@ __global__ void __launch_bounds__(kAttnThreads, 2) attn_fwd_d64_kernel(AttnArgs 
     // buffer cur^1 (every wave finished tile kt-1), so the restage goes right after it
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-    if (kt + 1 < nt) stage((kt + 1) * kKB, tileK(cur ^ 1), tileV(cur ^ 1));
-    const int k0 = kt * kKB;
+    if (kt + 1 < nt) stage((kt + 1) * KB, tileK(cur ^ 1), tileV(cur ^ 1));
+    const int k0 = kt * KB;
     if (k0 <= q_hi) {                               // wave-uniform: tile has keys <= a query
       const char* tk = tileK(cur);
       const char* tv = tileV(cur);
-      // ---- S^T for the two 32-key halves
-      f32x16 s[2];
+      // ---- S^T for the 32-key halves
+      f32x16 s[G::NKK];
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk)
+      for (int kk = 0; kk < G::NKK; ++kk) {
 #pragma unroll
         for (int e = 0; e < 16; ++e) s[kk][e] = 0.f;
-      if constexpr ((V & 1) != 0) {
-        // rows r and 32 + r share kswz (it depends on row bits 1..3): the second half is the
-        // first's addresses + 4 KiB (read immediate)
-        f32x4 kr[2][4];
-        const char* krow = tk + r * 128;
-        const int sw = kswz(r);
-        const char* kp[4];
+        const int row = kk * 32 + r;
 #pragma unroll
-        for (int ks = 0; ks < 4; ++ks) kp[ks] = krow + (((2 * ks + hi) ^ sw) << 4);
-        // issue order = wait order: half 0's four reads, then half 1's (asm volatile keeps it)
-#pragma unroll
-        for (int ks = 0; ks < 4; ++ks) kr[0][ks] = ds_read_b128_asm<0>(kp[ks]);
-#pragma unroll
-        for (int ks = 0; ks < 4; ++ks) kr[1][ks] = ds_read_b128_asm<4096>(kp[ks]);
-        lgk_wait<4>(kr[0][0], kr[0][1], kr[0][2], kr[0][3]);
-#pragma unroll
-        for (int ks = 0; ks < 4; ++ks)
-          s[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, kr[0][ks]),
-                                                         qf[ks], s[0], 0, 0, 0);
-        lgk_wait<0>(kr[1][0], kr[1][1], kr[1][2], kr[1][3]);
-#pragma unroll
-        for (int ks = 0; ks < 4; ++ks)
-          s[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, kr[1][ks]),
-                                                         qf[ks], s[1], 0, 0, 0);
-      } else {
-#pragma unroll
-        for (int kk = 0; kk < 2; ++kk) {
-          const int row = kk * 32 + r;
-#pragma unroll
-          for (int ks = 0; ks < 4; ++ks) {
-            const int c = 2 * ks + hi;
-            const bf16x8 kf =
-                *reinterpret_cast<const bf16x8*>(tk + row * 128 + ((c ^ kswz(row)) << 4));
-            s[kk] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[ks], s[kk], 0, 0, 0);
-          }
+        for (int ks = 0; ks < G::NKS; ++ks) {
+          const int c = 2 * ks + hi;
+          const bf16x8 kf =
+              *reinterpret_cast<const bf16x8*>(tk + row * ROW + ((c ^ kswz_d<D>(row)) << 4));
+          s[kk] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[ks], s[kk], 0, 0, 0);
         }
       }
       // ---- scale, causal mask, online softmax (lane = one query; keys in registers)
-      const bool diag = k0 + kKB - 1 > qw;          // some key of this tile beyond some query
-      float mx = -INFINITY;                          // max of the RAW scores (scale > 0)
+      const bool diag = k0 + KB - 1 > qw;           // some key of this tile beyond some query
       if (diag) {
-        // key(kk, e) = k0 + 4 hi + const(kk, e): one per-lane threshold, compile-time offsets
+        // key(kk, e) = k0 + 4 hi + kk*32 + (e & 3) + 8 (e >> 2): one per-lane threshold
         const int th = qme - k0 - 4 * hi;
 #pragma unroll
-        for (int kk = 0; kk < 2; ++kk)
+        for (int kk = 0; kk < G::NKK; ++kk)
 #pragma unroll
           for (int e = 0; e < 16; ++e)
             if (kk * 32 + (e & 3) + 8 * (e >> 2) > th) s[kk][e] = -INFINITY;
       }
-      if constexpr ((V & 8) != 0) {
-        // 3-ary tree of v_max3 (depth 4: 32 -> 11 -> 4 -> 2 -> 1) instead of a 16-long
-        // dependent v_max3 chain
-        float v[32], t[11];
+      float mx = -INFINITY;                          // max of the RAW scores (scale > 0)
 #pragma unroll
-        for (int e = 0; e < 16; ++e) { v[e] = s[0][e]; v[16 + e] = s[1][e]; }
+      for (int kk = 0; kk < G::NKK; ++kk)
 #pragma unroll
-        for (int j = 0; j < 10; ++j) t[j] = max3_asm(v[3 * j], v[3 * j + 1], v[3 * j + 2]);
-        t[10] = max3_asm(v[30], v[31], v[31]);
-        const float u0 = max3_asm(t[0], t[1], t[2]), u1 = max3_asm(t[3], t[4], t[5]);
-        const float u2 = max3_asm(t[6], t[7], t[8]), u3 = max3_asm(t[9], t[10], t[10]);
-        mx = max3_asm(max3_asm(u0, u1, u2), u3, u3);
-      } else {
-#pragma unroll
-        for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-          for (int e = 0; e < 16; ++e) mx = fmaxf(mx, s[kk][e]);
-      }
-      if constexpr ((V & 2) != 0)
-        mx = xhalf_max(mx);
-      else
-        mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+        for (int e = 0; e < 16; ++e) mx = fmaxf(mx, s[kk][e]);
+      mx = xhalf_max(mx);
       const float mn = fmaxf(m, mx * a.scale_log2);
       const float alpha = __builtin_amdgcn_exp2f(m - mn);   // m = -inf on the first tile -> 0
       const bool rescale = m != mn;
       m = mn;
       float ls = 0.f;
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk)
+      for (int kk = 0; kk < G::NKK; ++kk)
 #pragma unroll
-        for (int e = 0; e < 16; ++e)
+        for (int e = 0; e < 16; ++e) {
           s[kk][e] = __builtin_amdgcn_exp2f(__builtin_fmaf(s[kk][e], a.scale_log2, -mn));
-      if constexpr ((V & 8) != 0) {
-        float t[16];
-#pragma unroll
-        for (int e = 0; e < 16; ++e) t[e] = s[0][e] + s[1][e];
-#pragma unroll
-        for (int w = 8; w >= 1; w >>= 1)
-#pragma unroll
-          for (int e = 0; e < w; ++e) t[e] += t[e + w];
-        ls = t[0];
-      } else {
-#pragma unroll
-        for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-          for (int e = 0; e < 16; ++e) ls += s[kk][e];
-      }
+          ls += s[kk][e];
+        }
       l = l * alpha + ls;
       if (__any(rescale)) {                          // wave-uniform skip when no max moved
 #pragma unroll
-        for (int dt = 0; dt < 2; ++dt)
+        for (int dt = 0; dt < G::NDT; ++dt)
 #pragma unroll
           for (int e = 0; e < 16; ++e) o[dt][e] *= alpha;
       }
@@ -308,7 +256,7 @@ __global__ void __launch_bounds__(kAttnThreads, 2) attn_fwd_d64_kernel(AttnArgs 
       const int g = lane >> 4, i16 = lane & 15;
       const int tq = i16 >> 2, tp = i16 & 3;        // tr-read lane role: block row / col group
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk)
+      for (int kk = 0; kk < G::NKK; ++kk)
 #pragma unroll
         for (int st = 0; st < 2; ++st) {
           bf16x8 pf;
@@ -316,20 +264,18 @@ __global__ void __launch_bounds__(kAttnThreads, 2) attn_fwd_d64_kernel(AttnArgs 
           for (int j = 0; j < 8; ++j)
             pf[j] = __builtin_bit_cast(short, static_cast<__bf16>(s[kk][8 * st + j]));
 #pragma unroll
-          for (int dt = 0; dt < 2; ++dt) {
+          for (int dt = 0; dt < G::NDT; ++dt) {
             bf16x8 vf;
 #pragma unroll
             for (int half = 0; half < 2; ++half) {
               const int row = kk * 32 + 16 * st + 8 * half + 4 * (g >> 1) + tq;
               const int col = dt * 32 + 16 * (g & 1) + 4 * tp;
-              const int off = row * 128 + (((col >> 3) ^ vswz(row)) << 4) + (col & 7) * 2;
+              const int off = row * ROW + (((col >> 3) ^ vswz_d<D>(row)) << 4) + (col & 7) * 2;
               // builtin read, kept on purpose: the compiler drains the next tile's K/V DMA
               // (vmcnt(0)) before the first of these, but that DMA has had the S MFMAs and the
               // softmax to land, and the builtin lets it interleave the reads with the MFMAs
-              // under counted lgkmcnt waits. The asm form (common.h ds_read_tr16, grouped
-              // waits; also software-pipelined) measured 3-4 % SLOWER here (61-62 vs 58-60 us
-              // at the GPT-2 shape, profiles/r05_attention/), unlike dQ / dK/dV where the
-              // drain sat right behind the DMA issue. tools/isa_check.py allows this kernel.
+              // under counted lgkmcnt waits (the asm form measured 3-4 % slower here,
+              // profiles/r05_attention/). tools/isa_check.py allows this kernel.
               const i16x4 t = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4_ptr)(tv + off));
 #pragma unroll
               for (int u = 0; u < 4; ++u) vf[4 * half + u] = t[u];
@@ -346,7 +292,7 @@ __global__ void __launch_bounds__(kAttnThreads, 2) attn_fwd_d64_kernel(AttnArgs 
   if (qme < a.T) {
     uint16_t* op = a.out + (static_cast<int64_t>(b) * a.T + qme) * a.ldo + hoff;
 #pragma unroll
-    for (int dt = 0; dt < 2; ++dt)
+    for (int dt = 0; dt < G::NDT; ++dt)
 #pragma unroll
       for (int gg = 0; gg < 4; ++gg) {
         u16x4 w;
@@ -398,41 +344,6 @@ struct AttnBwdArgs {
   float scale;             // 1 / sqrt(D)
   int xcd;                 // see head_block
 };
-
-// ndelta[b, h, t] = -sum_d dO[b, t, h, d] * O[b, t, h, d] and nls[b, h, t] = -LSE * sqrt(D): the
-// row constants of the backward, pre-negated / pre-scaled once per row here so the dK/dV loop
-// starts its S and dP accumulators at them (guide: 'row constants as the initial accumulator'):
-// p = exp2(S' * scale_log2) and dS = P * dP' with no subtraction, and no constant held in
-// registers across the MFMA chains; one thread per (b, t, h) row of 64
-__global__ void __launch_bounds__(256) attn_bwd_delta_kernel(const uint16_t* __restrict__ dout,
-                                                             const uint16_t* __restrict__ out,
-                                                             int64_t ldo, const float* __restrict__ lse,
-                                                             float* __restrict__ delta,
-                                                             float* __restrict__ nls,
-                                                             float scale, int B, int T, int H) {
-  const int64_t row = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  const int64_t nrows = static_cast<int64_t>(B) * T * H;
-  if (row >= nrows) return;
-  const int h = static_cast<int>(row % H);
-  const int64_t bt = row / H;
-  const uint16_t* g = dout + bt * ldo + h * kAttnD;
-  const uint16_t* o = out + bt * ldo + h * kAttnD;
-  // even / odd 8-dim chunks summed separately, then added: the order of the dQ kernel's fused
-  // form (lane halves hi = 0 / 1, joined by lane ^ 32), so both give bitwise the same constants
-  float acc2[2] = {0.f, 0.f};
-#pragma unroll
-  for (int c = 0; c < kAttnD / 8; ++c) {
-    float x[8], y[8];
-    load8<DT_BF16>(g, c, x);
-    load8<DT_BF16>(o, c, y);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc2[c & 1] += x[j] * y[j];
-  }
-  const int64_t b = bt / T, t = bt % T;
-  const int64_t i = (b * H + h) * T + t;
-  delta[i] = -(acc2[0] + acc2[1]);
-  nls[i] = -lse[i] / scale;
-}
 
 // transposed operand read of a [rows][64] bf16 image (bswz): A operand of a 32x32x16 MFMA whose
 // k index is the image row: lane (col = colbase + (lane & 31), hi) gets rows
@@ -828,386 +739,19 @@ __global__ void __launch_bounds__(kAttnThreads, 2) attn_bwd_dq_d64_kernel(AttnBw
   }
 }
 
-// ============================================================================ pipelined forward
-// Round-6 forward body (the round-5 kernel ran QK^T -> softmax -> PV of a tile back to back in
-// one wave: MFMA busy 19 %, the VALU softmax never beside the matrix work). Each wave now runs
-// a software pipeline over its key tiles: iteration `it` issues the QK^T MFMAs of tile it + 1,
-// the softmax (VALU) of tile it and the PV MFMAs of tile it - 1 as ONE straight-line block, so
-// the softmax's exps / max / sums fill the issue gaps of 16 independent MFMAs instead of
-// waiting for their own (CDNA guide §B "Fused attention prefill": P of tile j beside PV of
-// tile j - 1).
-//   * K and V are staged in rings of 4 x 8 KiB (64 KiB per workgroup, 2 workgroups per CU):
-//     at the top of iteration it (after the one barrier) K_{it+3} and V_{it+2} are issued, so a
-//     K tile has two iterations to land and a V tile three; the counted wait vmcnt(6) retires
-//     exactly K_{it+1} (and everything older: V_{it-1}). Past the last tile the loads repeat
-//     the last tile (uniform instruction counts keep the count constant).
-//   * lazy rescaling: a row's reference max m moves only when a tile's max exceeds it by more
-//     than 2^8 (p = exp2(s c - m) <= 256 otherwise, exact in bf16 / fp32 sums); the O
-//     rescale (32 multiplies, wave-uniformly skipped when no lane moved) is applied one
-//     iteration late, right before the PV of the tile whose softmax moved m.
-//   * only a wave's LAST key tile meets the diagonal (queries qw .. qw + 31, qw % 32 == 0, tiles
-//     of 64): it is the one masked softmax.
-//   * layouts as the round-5 kernel: swapped scores S^T = K Q^T (lane = query), K image kswz
-//     (ds_read_b128 rows), V image vswz (ds_read_b64_tr_b16), O^T = V^T P^T in registers.
-constexpr int kRing = 4;
-constexpr float kLazyLog2 = 8.f;
-
-struct FwdRegs {
-  bf16x8 qf[4];
-  f32x16 o[2];
-  float m, l, alpha;      // reference max (log2 units), row sum, pending O rescale
-};
-
-// K fragments of the key tile in image `tk` (8 row reads, issued in wait order: half 0 first)
-__device__ __forceinline__ void fwd_kreads(const char* tk, f32x4 (&kr)[2][4], int lane) {
-  const int r = lane & 31, hi = lane >> 5;
-  const char* krow = tk + r * 128;
-  const int sw = kswz(r);
-#pragma unroll
-  for (int ks = 0; ks < 4; ++ks) kr[0][ks] = ds_read_b128_asm<0>(krow + (((2 * ks + hi) ^ sw) << 4));
-#pragma unroll
-  for (int ks = 0; ks < 4; ++ks) kr[1][ks] = ds_read_b128_asm<4096>(krow + (((2 * ks + hi) ^ sw) << 4));
-}
-
-// S^T half KK (32 keys) = K Q^T; the caller has waited for kr[KK]
-template <int KK>
-__device__ __forceinline__ void fwd_scores_half(const f32x4 (&kr)[2][4], const bf16x8 (&qf)[4],
-                                                f32x16 (&s)[2]) {
-#pragma unroll
-  for (int e = 0; e < 16; ++e) s[KK][e] = 0.f;
-#pragma unroll
-  for (int ks = 0; ks < 4; ++ks)
-    s[KK] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, kr[KK][ks]), qf[ks],
-                                                    s[KK], 0, 0, 0);
-}
-
-// V^T fragments of keys [32 KK, 32 KK + 32) of the tile in image `tv` (8 transposed reads;
-// the caller waits). row = KK*32 + 16 st + 8 half + 4 (g >> 1) + tq: vswz(row) depends on bit 1
-// of tq only, so the address is a per-lane base per dt plus an immediate.
-template <int KK>
-__device__ __forceinline__ void fwd_vreads(const char* tv, i16x4 (&vt)[2][2][2], int lane) {
-  const int g = lane >> 4, i16 = lane & 15;
-  const int tq = i16 >> 2, tp = i16 & 3;
-  const int row0 = 4 * (g >> 1) + tq;
-  const int sw = vswz(row0);
-#pragma unroll
-  for (int dt = 0; dt < 2; ++dt) {
-    const int col = dt * 32 + 16 * (g & 1) + 4 * tp;
-    const char* b = tv + row0 * 128 + (((col >> 3) ^ sw) << 4) + (col & 7) * 2;
-    vt[0][dt][0] = ds_read_tr16<(KK * 32 + 0) * 128>(b);
-    vt[0][dt][1] = ds_read_tr16<(KK * 32 + 8) * 128>(b);
-    vt[1][dt][0] = ds_read_tr16<(KK * 32 + 16) * 128>(b);
-    vt[1][dt][1] = ds_read_tr16<(KK * 32 + 24) * 128>(b);
-  }
-}
-
-template <int N>
-__device__ __forceinline__ void vt_wait(i16x4 (&vt)[2][2][2]) {
-  lgk_wait<N>(vt[0][0][0], vt[0][0][1], vt[0][1][0], vt[0][1][1], vt[1][0][0], vt[1][0][1],
-              vt[1][1][0], vt[1][1][1]);
-}
-
-// O^T += V^T P^T for keys half KK of a tile (4 MFMA)
-template <int KK>
-__device__ __forceinline__ void fwd_pv_half(f32x16 (&o)[2], const i16x4 (&vt)[2][2][2],
-                                            const bf16x8 (&p)[2][2]) {
-#pragma unroll
-  for (int st = 0; st < 2; ++st)
-#pragma unroll
-    for (int dt = 0; dt < 2; ++dt) {
-      bf16x8 vf;
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        vf[u] = vt[st][dt][0][u];
-        vf[4 + u] = vt[st][dt][1][u];
-      }
-      o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, p[KK][st], o[dt], 0, 0, 0);
-    }
-}
-
-__device__ __forceinline__ void fwd_rescale(FwdRegs& R) {
-  if (__builtin_amdgcn_ballot_w64(R.alpha != 1.f) != 0) {   // wave-uniform skip
-#pragma unroll
-    for (int dt = 0; dt < 2; ++dt)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) R.o[dt][e] *= R.alpha;
-  }
-}
-
-// softmax part 1 of the scores `s` of key tile k0 (in place: s becomes p in fp32), updating
-// m / l; returns the tile's O rescale factor (applied before the PV of this tile)
-template <bool DIAG>
-__device__ __forceinline__ float fwd_softmax(FwdRegs& R, f32x16 (&s)[2], int k0, int qme,
-                                             float c, int lane) {
-  const int hi = lane >> 5;
-  if constexpr (DIAG) {
-    // key(kk, e) = k0 + 4 hi + kk*32 + (e & 3) + 8 (e >> 2): one per-lane threshold
-    const int th = qme - k0 - 4 * hi;
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-      for (int e = 0; e < 16; ++e)
-        if (kk * 32 + (e & 3) + 8 * (e >> 2) > th) s[kk][e] = -INFINITY;
-  }
-  float mx = max3_asm(s[0][0], s[0][1], s[0][2]);
-#pragma unroll
-  for (int e = 3; e < 15; e += 2) mx = max3_asm(mx, s[0][e], s[0][e + 1]);
-  mx = max3_asm(mx, s[0][15], s[1][0]);
-#pragma unroll
-  for (int e = 1; e < 15; e += 2) mx = max3_asm(mx, s[1][e], s[1][e + 1]);
-  mx = fmaxf(mx, s[1][15]);
-  mx = xhalf_max(mx) * c;
-  const float mn = mx > R.m + kLazyLog2 ? mx : R.m;     // m = -inf on the first tile
-  const float alpha = __builtin_amdgcn_exp2f(R.m - mn);
-  R.m = mn;
-  float ls0 = 0.f, ls1 = 0.f;
-#pragma unroll
-  for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-    for (int e = 0; e < 16; ++e) {
-      const float v = __builtin_amdgcn_exp2f(__builtin_fmaf(s[kk][e], c, -mn));
-      s[kk][e] = v;
-      if (kk == 0) ls0 += v; else ls1 += v;
-    }
-  R.l = R.l * alpha + (ls0 + ls1);
-  return alpha;
-}
-
-// softmax part 2: the probabilities to bf16 MFMA operands
-__device__ __forceinline__ void fwd_pack(const f32x16 (&s)[2], bf16x8 (&p)[2][2]) {
-#pragma unroll
-  for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-    for (int st = 0; st < 2; ++st)
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-        p[kk][st][j] = __builtin_bit_cast(short, static_cast<__bf16>(s[kk][8 * st + j]));
-}
-
-__global__ void __launch_bounds__(kAttnThreads, 2) attn_fwd_pipe_kernel(AttnArgs a) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int nqb = (a.T + kQB - 1) / kQB;
-  int blk, h, b;
-  head_block(a.xcd, blk, h, b);
-  const int qb = nqb - 1 - blk;                   // heaviest first
-  const int q0 = qb * kQB;
-  const int qw = q0 + wave * 32;
-  const int r = lane & 31, hi = lane >> 5;
-  const uint16_t* base_bt = a.qkv + static_cast<int64_t>(b) * a.T * a.ld;
-  const int hoff = h * kAttnD;
-  const int qme = qw + r;
-  const float c = a.scale_log2;
-  // key tiles of the workgroup (barriers) and of this wave (work); nt_w = 0: no query < T
-  const int last_key = (q0 + kQB - 1) < (a.T - 1) ? (q0 + kQB - 1) : (a.T - 1);
-  const int nt = last_key / kKB + 1;
-  const int q_hi = (qw + 31) < (a.T - 1) ? (qw + 31) : (a.T - 1);
-  const int nt_w = qw < a.T ? q_hi / kKB + 1 : 0;
-
-  FwdRegs R;
-  {
-    const int q = qme < a.T ? qme : a.T - 1;
-    const uint16_t* qp = base_bt + static_cast<int64_t>(q) * a.ld + hoff + 8 * hi;
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) R.qf[ks] = *reinterpret_cast<const bf16x8*>(qp + 16 * ks);
-  }
-#pragma unroll
-  for (int dt = 0; dt < 2; ++dt)
-#pragma unroll
-    for (int e = 0; e < 16; ++e) R.o[dt][e] = 0.f;
-  R.m = -INFINITY;
-  R.l = 0.f;
-  R.alpha = 1.f;
-
-  auto ringK = [&](int t) { return smem + (t & (kRing - 1)) * kTileKV; };
-  auto ringV = [&](int t) { return smem + (kRing + (t & (kRing - 1))) * kTileKV; };
-  // K / V staging by buffer_load ... lds: the (b, h) section bases in buffer resources
-  // (SGPRs), this lane's row-in-tile + swizzled chunk as a 32-bit offset (rows wave * 16 +
-  // i * 8 + lane / 8), a tile's rows as a uniform offset; a tile crossing T clamps its rows
-  const int r_in = lane >> 3, slot = lane & 7;
-  const uint32_t ld2 = static_cast<uint32_t>(a.ld) * 2;
-  const __amdgpu_buffer_rsrc_t rk = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<uint16_t*>(base_bt + hoff + kAttnD * a.H), 0, 0x7fffffff, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<uint16_t*>(base_bt + hoff + 2 * kAttnD * a.H), 0, 0x7fffffff, 0x00020000);
-  uint32_t koff[2], voff[2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int row = wave * 16 + i * 8 + r_in;
-    koff[i] = static_cast<uint32_t>(row) * ld2 + ((slot ^ kswz(row)) << 4);
-    voff[i] = static_cast<uint32_t>(row) * ld2 + ((slot ^ vswz(row)) << 4);
-  }
-  // stage K (sec 1) or V (sec 2) of key index ts into its ring slot (tile min(ts, nt - 1))
-  auto stage = [&](int ts, int sec) __attribute__((always_inline)) {
-    char* dst = sec == 1 ? ringK(ts) : ringV(ts);
-    const int t = ts < nt - 1 ? ts : nt - 1;
-    const int k0 = t * kKB;
-    const __amdgpu_buffer_rsrc_t rs = sec == 1 ? rk : rv;
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      uint32_t off;
-      if (k0 + kKB <= a.T) {                       // wave-uniform: no row past T
-        off = (sec == 1 ? koff[i] : voff[i]) + static_cast<uint32_t>(k0) * ld2;
-      } else {
-        const int row = wave * 16 + i * 8 + r_in;
-        const int key = k0 + row < a.T ? k0 + row : a.T - 1;
-        off = static_cast<uint32_t>(key) * ld2 +
-              ((slot ^ (sec == 1 ? kswz(row) : vswz(row))) << 4);
-      }
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_vptr_t)(dst + (wave * 16 + i * 8) * 128), 16,
-                                               off, 0, 0, 0);
-    }
-  };
-
-  f32x16 s[2];
-  bf16x8 p[2][2];
-  // prologue: K_0 | K_1, V_0 -> K_0 landed; iteration -1: K_2, V_1 issued, S_0
-  stage(0, 1);
-  stage(1, 1);
-  stage(0, 2);
-  asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  stage(2, 1);
-  stage(1, 2);
-  auto scores = [&](int t) __attribute__((always_inline)) {
-    f32x4 kr[2][4];
-    fwd_kreads(ringK(t), kr, lane);
-    lgk_wait<4>(kr[0][0], kr[0][1], kr[0][2], kr[0][3]);
-    fwd_scores_half<0>(kr, R.qf, s);
-    lgk_wait<0>(kr[1][0], kr[1][1], kr[1][2], kr[1][3]);
-    fwd_scores_half<1>(kr, R.qf, s);
-  };
-  auto pv = [&](int t) __attribute__((always_inline)) {
-    i16x4 vt[2][2][2];
-    fwd_vreads<0>(ringV(t), vt, lane);
-    vt_wait<0>(vt);
-    fwd_rescale(R);
-    fwd_pv_half<0>(R.o, vt, p);
-    fwd_vreads<1>(ringV(t), vt, lane);
-    vt_wait<0>(vt);
-    fwd_pv_half<1>(R.o, vt, p);
-  };
-  if (nt_w > 0) scores(0);
-  // iteration it: [PV_{it-1} | softmax_it] then S_{it+1}. The PV MFMAs (independent of the
-  // softmax) are issued between its VALU; p holds tile it - 1's probabilities until the PV
-  // has read them, then tile it's.
-  for (int it = 0; it <= nt; ++it) {
-    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");   // K_{it+1} (and V_{it-1}) landed
-    __builtin_amdgcn_s_barrier();                      // ... for every wave; slots it-1 free
-    stage(it + 3, 1);
-    stage(it + 2, 2);
-    const int k0 = it * kKB;
-    if (it >= 1 && it + 1 < nt_w) {                    // steady state: one straight block
-      i16x4 vt[2][2][2];
-      fwd_vreads<0>(ringV(it - 1), vt, lane);
-      const float al = fwd_softmax<false>(R, s, k0, qme, c, lane);
-      vt_wait<0>(vt);
-      fwd_rescale(R);
-      fwd_pv_half<0>(R.o, vt, p);
-      fwd_vreads<1>(ringV(it - 1), vt, lane);
-      vt_wait<0>(vt);
-      fwd_pv_half<1>(R.o, vt, p);
-      fwd_pack(s, p);
-      R.alpha = al;
-      scores(it + 1);
-    } else {                                           // first / diagonal / drain iterations
-      if (it >= 1 && it <= nt_w) pv(it - 1);
-      if (it < nt_w) {
-        const float al = it == nt_w - 1 ? fwd_softmax<true>(R, s, k0, qme, c, lane)
-                                        : fwd_softmax<false>(R, s, k0, qme, c, lane);
-        fwd_pack(s, p);
-        R.alpha = al;
-      }
-      if (it + 1 < nt_w) scores(it + 1);
-    }
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no LDS-DMA in flight at exit
-
-  // ---- finalize: l over both lane halves, O / l, store O [B,T,H,D] and LSE
-  const float lt = R.l + __shfl_xor(R.l, 32, 64);
-  const float inv = lt > 0.f ? 1.f / lt : 0.f;
-  if (qme < a.T) {
-    uint16_t* op = a.out + (static_cast<int64_t>(b) * a.T + qme) * a.ldo + hoff;
-#pragma unroll
-    for (int dt = 0; dt < 2; ++dt)
-#pragma unroll
-      for (int gg = 0; gg < 4; ++gg) {
-        u16x4 w;
-#pragma unroll
-        for (int u = 0; u < 4; ++u) w[u] = f32_to_bf16(R.o[dt][4 * gg + u] * inv);
-        *reinterpret_cast<u16x4*>(op + dt * 32 + 8 * gg + 4 * hi) = w;
-      }
-    if (hi == 0 && a.lse)
-      a.lse[(static_cast<int64_t>(b) * a.H + h) * a.T + qme] =
-          (R.m + __builtin_amdgcn_logf(lt)) * 0.69314718055994531f;
-  }
-}
 }  // namespace dlbb
 
 using namespace dlbb;
 
 static int g_attn_xcd = 1;   // A/B switch for the XCD-aware block order (dlbb_attn_set_xcd)
-// dK/dV and dQ kernels concurrently (fork/join side stream): opt-in, DLBB_ATTN_CONCURRENT=1.
-// The backward alone is 5 % faster (195 vs 205 us at GPT-2 shape) but the GPT-2 step measured
-// 0.25 ms SLOWER in an in-call A/B (20.2 vs 19.95 ms), so the default is sequential.
-static int g_attn_concurrent = [] {
-  const char* v = getenv("DLBB_ATTN_CONCURRENT");
-  return (v && v[0] == '1') ? 1 : 0;
-}();
-
-// delta / nls computed inside the dQ kernel (1, default) or by the separate row kernel first (0);
-// the concurrent form always uses the separate kernel (A/B: dlbb_attn_set_fuse_delta)
-static int g_attn_fuse_delta = 1;
-// forward kernel variant (attn_fwd_d64_kernel<V> bit mask; A/B: dlbb_attn_set_fwd_variant).
-// 6 = permlane32 exchange + incremental DMA addresses: 49.8 vs 52.2 us at the GPT-2 shape,
-// 85.6 vs 90.3 (T 2048), 197.2 vs 201.9 (T 4096); the batched K reads (bit 1) measured no gain
-// (profiles/r05_attention/fwd_variants.jsonl)
-static int g_attn_fwd_variant = 6;
-// backward kernels with incremental DMA sources, bit mask: 1 dQ, 2 dK/dV (0: per-row clamped
-// addresses). dK/dV<true> holds 174 VGPRs (occupancy 2 waves / SIMD, vs 3 at 166)
-static int g_attn_bwd_incr = 1;
-
 DLBB_API void dlbb_attn_set_xcd(int on) { g_attn_xcd = on ? 1 : 0; }
-DLBB_API void dlbb_attn_set_fuse_delta(int on) { g_attn_fuse_delta = on ? 1 : 0; }
-DLBB_API void dlbb_attn_set_concurrent(int on) { g_attn_concurrent = on ? 1 : 0; }
-DLBB_API void dlbb_attn_set_fwd_variant(int v) {
-  g_attn_fwd_variant = (v >= 0 && v <= 7) || v == 14 || v == 100 ? v : 6;
-}
-DLBB_API int dlbb_attn_get_fwd_variant() { return g_attn_fwd_variant; }
-DLBB_API void dlbb_attn_set_bwd_incr(int m) { g_attn_bwd_incr = m & 3; }
-DLBB_API int dlbb_attn_get_bwd_incr() { return g_attn_bwd_incr; }
 
-// Per-device side stream + fork/join events for the concurrent backward (created once; a fork
-// through an event recorded on the caller's stream is also how a HIP-graph capture of that
-// stream picks up the side-stream work).
-struct AttnSide {
-  hipStream_t s = nullptr;
-  hipEvent_t fork = nullptr, join = nullptr;
-};
-static AttnSide g_side[64];
-
-static int attn_side(AttnSide** out) {
-  int dev = 0;
-  hipError_t e = hipGetDevice(&dev);
-  if (e != hipSuccess) return e;
-  if (dev < 0 || dev >= 64) return hipErrorInvalidDevice;
-  AttnSide& sd = g_side[dev];
-  if (!sd.s) {
-    if ((e = hipStreamCreateWithFlags(&sd.s, hipStreamNonBlocking)) != hipSuccess) return e;
-    if ((e = hipEventCreateWithFlags(&sd.fork, hipEventDisableTiming)) != hipSuccess) return e;
-    if ((e = hipEventCreateWithFlags(&sd.join, hipEventDisableTiming)) != hipSuccess) return e;
-  }
-  *out = &sd;
-  return hipSuccess;
-}
-
-// qkv: [B, T, 3, H, 64] bf16 (token row stride ld elements, 16-B aligned rows);
-// out: [B, T, H, 64] bf16 (row stride ldo); lse: [B, H, T] fp32 (may be null). Causal only.
+// qkv: [B, T, 3, H, D] bf16, D = 64 or 128 (token row stride ld elements, 16-B aligned rows);
+// out: [B, T, H, D] bf16 (row stride ldo); lse: [B, H, T] fp32 (may be null). Causal only.
 DLBB_API int dlbb_attn_fwd(const void* qkv, int64_t ld, void* out, int64_t ldo, float* lse,
                            int B, int T, int H, int D, float scale, hipStream_t stream) {
   if (B <= 0 || T <= 0 || H <= 0) return hipSuccess;
-  if (D != kAttnD) return hipErrorInvalidValue;
+  if (D != 64 && D != 128) return hipErrorInvalidValue;
   if (ld % 8 || ldo % 4 || (reinterpret_cast<uintptr_t>(qkv) & 15) ||
       (reinterpret_cast<uintptr_t>(out) & 7))
     return hipErrorInvalidValue;
@@ -1215,27 +759,21 @@ DLBB_API int dlbb_attn_fwd(const void* qkv, int64_t ld, void* out, int64_t ldo, 
   AttnArgs a{static_cast<const uint16_t*>(qkv), static_cast<uint16_t*>(out), lse, ld, ldo,
              B, T, H, scale * 1.4426950408889634f, g_attn_xcd};
   const dim3 grid((T + kQB - 1) / kQB, H, B);
-  if (g_attn_fwd_variant == 100) {
-    hipLaunchKernelGGL(attn_fwd_pipe_kernel, grid, dim3(kAttnThreads), 2 * kRing * kTileKV, stream,
-                       a);
-    return hipGetLastError();
-  }
-  switch (g_attn_fwd_variant) {
-#define FWD_V(N)                                                                           \
-  case N:                                                                                  \
-    hipLaunchKernelGGL(attn_fwd_d64_kernel<N>, grid, dim3(kAttnThreads), 4 * kTileKV, stream, a); \
-    break;
-    FWD_V(1) FWD_V(2) FWD_V(3) FWD_V(4) FWD_V(5) FWD_V(6) FWD_V(7) FWD_V(14)
-#undef FWD_V
-    default:
-      hipLaunchKernelGGL(attn_fwd_d64_kernel<0>, grid, dim3(kAttnThreads), 4 * kTileKV, stream, a);
-  }
+  if (D == 64)
+    hipLaunchKernelGGL(attn_fwd_kernel<64>, grid, dim3(kAttnThreads), 4 * FwdGeo<64>::TILE,
+                       stream, a);
+  else
+    hipLaunchKernelGGL(attn_fwd_kernel<128>, grid, dim3(kAttnThreads), 4 * FwdGeo<128>::TILE,
+                       stream, a);
   return hipGetLastError();
 }
 
-// Backward of dlbb_attn_fwd. dout / out: [B, T, H, 64] (row stride ldo); lse: forward's;
-// delta: [2, B, H, T] fp32 workspace (-delta, -LSE sqrt(D)); dqkv: [B, T, 3, H, 64] (row stride
-// ld, written fully).
+// Backward of dlbb_attn_fwd (D = 64). dout / out: [B, T, H, 64] (row stride ldo); lse:
+// forward's; delta: [2, B, H, T] fp32 workspace (-delta, -LSE sqrt(D), produced by the dQ
+// kernel for the dK/dV kernel after it); dqkv: [B, T, 3, H, 64] (row stride ld, written fully).
+// (Round-5 A/B forms removed in round 6: the dK/dV kernel concurrently on a side stream — its
+// backward 5 % faster alone, the GPT-2 step 0.25 ms slower; a separate delta pass; per-row DMA
+// addresses in dQ / incremental ones in dK/dV — each measured slower.)
 DLBB_API int dlbb_attn_bwd(const void* qkv, int64_t ld, const void* out, const void* dout,
                            int64_t ldo, const float* lse, float* delta, void* dqkv, int B, int T,
                            int H, int D, float scale, hipStream_t stream) {
@@ -1246,50 +784,14 @@ DLBB_API int dlbb_attn_bwd(const void* qkv, int64_t ld, const void* out, const v
   if (mis16(qkv) || mis16(out) || mis16(dout) || mis16(dqkv)) return hipErrorInvalidValue;
   if (!lse || !delta || !out || !dout) return hipErrorInvalidValue;
   const int64_t rows = static_cast<int64_t>(B) * T * H;
-  // sequential (default): the dQ kernel produces delta / nls for the dK/dV kernel after it;
-  // concurrent: both read them, so the separate delta kernel runs first
-  const int fuse = g_attn_concurrent ? 0 : g_attn_fuse_delta;
-  if (!fuse)
-    hipLaunchKernelGGL(attn_bwd_delta_kernel, dim3(static_cast<unsigned>((rows + 255) / 256)),
-                       dim3(256), 0, stream, static_cast<const uint16_t*>(dout),
-                       static_cast<const uint16_t*>(out), ldo, lse, delta, delta + rows,
-                       scale, B, T, H);
   AttnBwdArgs a{static_cast<const uint16_t*>(qkv), static_cast<const uint16_t*>(dout), lse, delta,
-                delta + rows, static_cast<const uint16_t*>(out), fuse,
+                delta + rows, static_cast<const uint16_t*>(out), 1,
                 static_cast<uint16_t*>(dqkv), ld, ldo, B, T, H,
                 scale * 1.4426950408889634f, scale, g_attn_xcd};
-  // dK/dV and dQ are independent (both read Q/K/V/dO/LSE/delta, write disjoint dQKV columns):
-  // dQ runs on a side stream forked after the delta kernel and joined back, so each kernel's
-  // causal tail (its last, lightest blocks) overlaps the other's work instead of idling CUs
-  AttnSide* sd = nullptr;
-  if (g_attn_concurrent) {
-    const int e = attn_side(&sd);
-    if (e != hipSuccess) return e;
-  }
-  hipStream_t dq_stream = stream;
-  if (sd) {
-    hipError_t e;
-    if ((e = hipEventRecord(sd->fork, stream)) != hipSuccess) return e;
-    if ((e = hipStreamWaitEvent(sd->s, sd->fork, 0)) != hipSuccess) return e;
-    dq_stream = sd->s;
-  }
   const dim3 gq((T + kQB - 1) / kQB, H, B), gk((T + kBwdKeys - 1) / kBwdKeys, H, B);
-  if (g_attn_bwd_incr & 1)
-    hipLaunchKernelGGL(attn_bwd_dq_d64_kernel<true>, gq, dim3(kAttnThreads), 4 * kTileKV,
-                       dq_stream, a);
-  else
-    hipLaunchKernelGGL(attn_bwd_dq_d64_kernel<false>, gq, dim3(kAttnThreads), 4 * kTileKV,
-                       dq_stream, a);
-  if (g_attn_bwd_incr & 2)
-    hipLaunchKernelGGL(attn_bwd_dkdv_d64_kernel<true>, gk, dim3(kAttnThreads),
-                       4 * kSliceImg + 1024, stream, a);
-  else
-    hipLaunchKernelGGL(attn_bwd_dkdv_d64_kernel<false>, gk, dim3(kAttnThreads),
-                       4 * kSliceImg + 1024, stream, a);
-  if (sd) {
-    hipError_t e;
-    if ((e = hipEventRecord(sd->join, sd->s)) != hipSuccess) return e;
-    if ((e = hipStreamWaitEvent(stream, sd->join, 0)) != hipSuccess) return e;
-  }
+  hipLaunchKernelGGL(attn_bwd_dq_d64_kernel<true>, gq, dim3(kAttnThreads), 4 * kTileKV, stream,
+                     a);
+  hipLaunchKernelGGL(attn_bwd_dkdv_d64_kernel<false>, gk, dim3(kAttnThreads),
+                     4 * kSliceImg + 1024, stream, a);
   return hipGetLastError();
 }

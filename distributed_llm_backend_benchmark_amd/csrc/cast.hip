@@ -10,47 +10,28 @@
 
 namespace dlbb {
 
-template <int DTI, int DTO>
-__global__ void __launch_bounds__(256) cast_kernel(const void* __restrict__ src,
-                                                   void* __restrict__ dst, int64_t n) {
-  const int64_t nvec = n / 8;
-  const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
-  int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  for (; i + 3 * stride < nvec; i += 4 * stride) {   // 4 loads in flight before any store
-    float v[4][8];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) load8<DTI>(src, i + u * stride, v[u]);
-#pragma unroll
-    for (int u = 0; u < 4; ++u) store8<DTO>(dst, i + u * stride, v[u]);
-  }
-  for (; i < nvec; i += stride) {
-    float v[8];
-    load8<DTI>(src, i, v);
-    store8<DTO>(dst, i, v);
-  }
-  if (blockIdx.x == 0) {
-    const int64_t t = nvec * 8 + threadIdx.x;
-    if (t < n)
-      Elem<DTO>::st(static_cast<typename Elem<DTO>::T*>(dst), t,
-                    Elem<DTI>::ld(static_cast<const typename Elem<DTI>::T*>(src), t));
-  }
-}
-
-// Cast v2 (default). The kernel above measured 4.10 TB/s bf16 -> fp32 against 5.49 for torch's
-// copy (profiles/r01_initial/kernel_microbench.jsonl:14): it moves 8 elements per lane, so
-// one of its two sides is a 32-B-per-lane access split over two instructions that each touch
-// every other 16 B of a wave's span. Here a lane moves E elements with E chosen so the WIDER side
+// Cast. An 8-elements-per-lane kernel measured 4.10 TB/s bf16 -> fp32 against 5.49 for torch's
+// copy (profiles/r01_initial/kernel_microbench.jsonl:14): one of its two sides is a
+// 32-B-per-lane access split over two instructions that each touch every other 16 B of a
+// wave's span. Here a lane moves E elements with E chosen so the WIDER side
 // is exactly one 16-B access per lane (bf16 <-> fp32: 8 B in, 16 B out; 16-bit <-> 16-bit: 16 B
 // both): every wave instruction covers one contiguous 512 B / 1 KiB span. U such vectors per
 // lane are loaded before any is stored (U x 16 B in flight per lane), block-contiguous tiles of
 // 256 x U vectors, grid-stride over tiles. NT: non-temporal stores (a streaming destination is
-// not re-read by this kernel; A/B via dlbb_cast_set_variant).
+// not re-read by this kernel). Round 6 (profiles/r06_kernels/memroof_variants.jsonl, TB/s at
+// 64 MiB / 256 MiB / 1 GiB, torch copy in brackets): bf16 -> fp32 6.83 (6.89) / 6.95 (5.86) /
+// 5.57 (5.84), fp32 -> bf16 6.61 (6.70) / 6.67 (5.84) / 5.65 (5.89) with U = 8 and NT stores,
+// the best or within 2 % of the best of U 4 / 8 / 16, plain / NT stores, NT loads at every size
+// but 1 GiB, where torch's copy stays 4 % ahead; plain stores lost 20 % at 256 MiB.
 template <int DT, int E>
 struct VecIO;
 template <>
 struct VecIO<DT_F32, 4> {
+  template <bool NT = false>
   __device__ __forceinline__ static void ld(const void* p, int64_t i, float (&v)[4]) {
-    const f32x4 t = reinterpret_cast<const f32x4*>(p)[i];
+    const f32x4* q = reinterpret_cast<const f32x4*>(p) + i;
+    f32x4 t;
+    if constexpr (NT) t = __builtin_nontemporal_load(q); else t = *q;
     v[0] = t[0]; v[1] = t[1]; v[2] = t[2]; v[3] = t[3];
   }
   template <bool NT>
@@ -62,8 +43,11 @@ struct VecIO<DT_F32, 4> {
 };
 template <int DT>
 struct VecIO16_4 {
+  template <bool NT = false>
   __device__ __forceinline__ static void ld(const void* p, int64_t i, float (&v)[4]) {
-    const u16x4 t = reinterpret_cast<const u16x4*>(p)[i];
+    const u16x4* q = reinterpret_cast<const u16x4*>(p) + i;
+    u16x4 t;
+    if constexpr (NT) t = __builtin_nontemporal_load(q); else t = *q;
 #pragma unroll
     for (int j = 0; j < 4; ++j) v[j] = DT == DT_BF16 ? bf16_to_f32(t[j]) : f16_to_f32(t[j]);
   }
@@ -78,8 +62,11 @@ struct VecIO16_4 {
 };
 template <int DT>
 struct VecIO16_8 {
+  template <bool NT = false>
   __device__ __forceinline__ static void ld(const void* p, int64_t i, float (&v)[8]) {
-    const u16x8 t = reinterpret_cast<const u16x8*>(p)[i];
+    const u16x8* q = reinterpret_cast<const u16x8*>(p) + i;
+    u16x8 t;
+    if constexpr (NT) t = __builtin_nontemporal_load(q); else t = *q;
 #pragma unroll
     for (int j = 0; j < 8; ++j) v[j] = DT == DT_BF16 ? bf16_to_f32(t[j]) : f16_to_f32(t[j]);
   }
@@ -130,11 +117,14 @@ __global__ void __launch_bounds__(256) cast2_kernel(const void* __restrict__ src
   }
 }
 
-// 0: 8-element kernel above, 1: cast2, 2: cast2 + nt stores, 3: 2 with one tile per block,
-// 4: 1 with one tile per block, 5 (default): 1 while source + destination fit the 256 MiB MALL,
-// else 2 — measured (profiles/r05_kernels/memroof_pass1.jsonl, TB/s v1 / v2): bf16->fp32 64 MiB
-// 5.54 / 5.43, 256 MiB 5.15 / 6.56, 1 GiB 5.36 / 5.49; fp32->bf16 256 MiB 4.65 / 5.72
-static int g_cast_variant = 5;
+template <int DTI, int DTO>
+__global__ void __launch_bounds__(256) cast_scalar_kernel(const void* __restrict__ src,
+                                                          void* __restrict__ dst, int64_t n) {
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n;
+       i += static_cast<int64_t>(gridDim.x) * blockDim.x)
+    Elem<DTO>::st(static_cast<typename Elem<DTO>::T*>(dst), i,
+                  Elem<DTI>::ld(static_cast<const typename Elem<DTI>::T*>(src), i));
+}
 
 // One wave-row loop: rows x cols, source row stride ld_src (elements), dense-or-strided dest.
 template <int DTI, int DTO>
@@ -161,27 +151,53 @@ __global__ void __launch_bounds__(256) pack_rows_kernel(const void* __restrict__
   }
 }
 
+// Round-6 pack: a 2-D grid — x over 16-B column vectors of a row,
+// y over groups of R rows (grid-stride) — so a lane never divides a flat index by the row
+// length (the 64-bit division per vector of pack_rows_kernel), and R rows' loads are in flight
+// before the first store.
+template <int DTI, int DTO, int R, bool NT>
+__global__ void __launch_bounds__(256) pack2_kernel(const void* __restrict__ src,
+                                                    void* __restrict__ dst, int64_t rows,
+                                                    int64_t cols, int64_t ld_src, int64_t ld_dst) {
+  using TI = typename Elem<DTI>::T;
+  using TO = typename Elem<DTO>::T;
+  const int64_t c = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
+  if (c >= cols / 8) return;
+  for (int64_t r0 = static_cast<int64_t>(blockIdx.y) * R; r0 < rows;
+       r0 += static_cast<int64_t>(gridDim.y) * R) {
+    float v[R][8];
+#pragma unroll
+    for (int u = 0; u < R; ++u)
+      if (r0 + u < rows) load8<DTI>(static_cast<const TI*>(src) + (r0 + u) * ld_src, c, v[u]);
+#pragma unroll
+    for (int u = 0; u < R; ++u) {
+      if (r0 + u >= rows) continue;
+      TO* q = static_cast<TO*>(dst) + (r0 + u) * ld_dst;
+      if constexpr (NT && DTO != DT_F32) {
+        u16x8 t;
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          t[j] = DTO == DT_BF16 ? f32_to_bf16(v[u][j]) : f32_to_f16(v[u][j]);
+        __builtin_nontemporal_store(t, reinterpret_cast<u16x8*>(q) + c);
+      } else {
+        store8<DTO>(q, c, v[u]);
+      }
+    }
+  }
+}
 template <int DTI, int DTO>
 static hipError_t launch_cast(const void* s, void* d, int64_t n, hipStream_t st) {
   const int block = 256;
   constexpr int E = cast_vec<DTI, DTO>(), U = 8;
   const uintptr_t align = reinterpret_cast<uintptr_t>(s) | reinterpret_cast<uintptr_t>(d);
-  if (g_cast_variant == 0 || (align & 15)) {
-    hipLaunchKernelGGL((cast_kernel<DTI, DTO>), dim3(stream_grid((n + 7) / 8, block)),
-                       dim3(block), 0, st, s, d, n);
+  if (align & 15) {       // a view not 16-B aligned: one element per lane
+    hipLaunchKernelGGL((cast_scalar_kernel<DTI, DTO>), dim3(stream_grid(n, block)), dim3(block),
+                       0, st, s, d, n);
     return hipGetLastError();
   }
-  int v = g_cast_variant;
-  if (v == 5)
-    v = n * (Elem<DTI>::kBytes + Elem<DTO>::kBytes) > (int64_t{256} << 20) ? 2 : 1;
   int64_t g = (n / E + 256 * U - 1) / (256 * U);
-  // variants 3/4: one tile per block (no grid-stride loop), as torch's elementwise launch
-  const int64_t cap = v >= 3 ? (int64_t{1} << 30) : 4096;
-  g = g < 1 ? 1 : (g > cap ? cap : g);
-  if (v == 2 || v == 3)
-    hipLaunchKernelGGL((cast2_kernel<DTI, DTO, U, true>), dim3(g), dim3(block), 0, st, s, d, n);
-  else
-    hipLaunchKernelGGL((cast2_kernel<DTI, DTO, U, false>), dim3(g), dim3(block), 0, st, s, d, n);
+  g = g < 1 ? 1 : (g > 4096 ? 4096 : g);
+  hipLaunchKernelGGL((cast2_kernel<DTI, DTO, U, true>), dim3(g), dim3(block), 0, st, s, d, n);
   return hipGetLastError();
 }
 
@@ -194,6 +210,24 @@ static hipError_t launch_pack(const void* s, void* d, int64_t rows, int64_t cols
                       (reinterpret_cast<uintptr_t>(d) % (8 * eo) == 0);
   const int64_t work = rows * (vec_ok ? cols / 8 : cols);
   const int block = 256;
+  if (vec_ok) {
+    // round 6 (memroof_variants.jsonl): 6.49 / 5.22 / 5.24 TB/s at 64 MiB / 256 MiB / 1 GiB vs
+    // the flat kernel's 6.33 / 5.19 / 5.07; non-temporal stores for destinations past half the
+    // MALL (the cast's measured gain at 256 MiB)
+    constexpr int R = 4;
+    const int64_t gx = (cols / 8 + 255) / 256;
+    int64_t gy = (rows + R - 1) / R;
+    const int64_t gy_cap = (4096 + gx - 1) / gx;     // ~4096 workgroups in all
+    gy = gy < gy_cap ? gy : gy_cap;
+    const dim3 gd(static_cast<unsigned>(gx), static_cast<unsigned>(gy < 65535 ? gy : 65535));
+    if (rows * cols * eo >= (int64_t{128} << 20))
+      hipLaunchKernelGGL((pack2_kernel<DTI, DTO, R, true>), gd, dim3(block), 0, st, s, d, rows,
+                         cols, lds, ldd);
+    else
+      hipLaunchKernelGGL((pack2_kernel<DTI, DTO, R, false>), gd, dim3(block), 0, st, s, d, rows,
+                         cols, lds, ldd);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL((pack_rows_kernel<DTI, DTO>), dim3(stream_grid(work, block)), dim3(block),
                      0, st, s, d, rows, cols, lds, ldd, vec_ok ? 1 : 0);
   return hipGetLastError();
@@ -203,10 +237,6 @@ static hipError_t launch_pack(const void* s, void* d, int64_t rows, int64_t cols
 
 using namespace dlbb;
 
-
-// A/B switch: 0 = 8-element kernel, 1 = one 16-B wide side per lane, 2 = 1 + nt stores,
-// 3 = 2 without the grid-stride cap, 4 = 1 without it, 5 = 1 or 2 by size (default)
-DLBB_API void dlbb_cast_set_variant(int v) { g_cast_variant = v < 0 || v > 5 ? 5 : v; }
 
 DLBB_API int dlbb_cast(const void* src, int dtype_in, void* dst, int dtype_out, int64_t n,
                        hipStream_t stream) {

@@ -65,7 +65,6 @@ struct GemmArgs {
   int vec_ok;              // 16-B aligned C / residual / preact / bias rows (vector epilogue)
   int kt_split;            // NN split-K (gridDim.y > 1): K-tiles per split; split s writes fp32
                            // partials to C + s * M * ldc
-  int group_m = 0;         // tile_of's GROUP_M (0 = kGroupM; A/B only, dlbb_gemm_set_group_m)
 };
 
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
@@ -221,7 +220,7 @@ __device__ __forceinline__ Tile256 tile_of(const GemmArgs& a, int vb) {
   const int nwg = tiles_m * tiles_n;
   const int q = nwg >> 3, r = nwg & 7, x = vb & 7;
   const int wid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (vb >> 3);
-  const int gmx = a.group_m > 0 ? a.group_m : kGroupM;
+  const int gmx = kGroupM;
   const int group_size = gmx * tiles_n;
   const int group = wid / group_size;
   const int first_m = group * gmx;
@@ -481,200 +480,32 @@ __global__ void __launch_bounds__(kThreads, 2) gemm_bf16_nt_kernel(GemmArgs a) {
 }
 
 
-template <int MODE>   // 0 lock-step, 1 staggered, 2 staggered + whole next tile issued at phase 1,
-                      // 3 staggered + deep (one K-tile in flight) restaging
-__global__ void __launch_bounds__(kThreads2, 1) gemm_bf16_nt_256_kernel(GemmArgs a) {
+// 256^2 tile on the deep pipeline (deep_prologue / deep_mainloop, wave rows staggered by one
+// barrier): the general-contract fallback of the 256^2 grid (ragged N % 64 / M % 8, 64-bit
+// panel offsets) where the ping-pong's buffer-resource staging does not apply. (Round-1/2
+// lock-step / staggered / early-issue schedules and the persistent deep form were removed in
+// round 6: never faster than this or the ping-pong.)
+__global__ void __launch_bounds__(kThreads2, 1) gemm_bf16_nt_256_deep(GemmArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wr = wave >> 2, wc = wave & 3;
-  const int fr = lane & 15, fq = lane >> 4;
-
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = wave >> 2;
   const Tile256 tl = tile_of(a, static_cast<int>(blockIdx.x));
   const int64_t m0 = tl.m0, n0 = tl.n0;
-
   f32x4 acc[8][4];
 #pragma unroll
   for (int i = 0; i < 8; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
   const int64_t nk = a.K / BK;
-  // prologue: all four sections of K-tile 0 into buffer 0, wait for SA0 + SB0
-  if constexpr (MODE != 3) {
-    stage_next(a, m0, n0, 0, smem, 0, wave, lane);
-    stage_next(a, m0, n0, 0, smem, 1, wave, lane);
-    stage_next(a, m0, n0, 0, smem, 2, wave, lane);
-    stage_next(a, m0, n0, 0, smem, 3, wave, lane);
-    DLBB_WAIT_VM(4);
-    DLBB_BARRIER();
-  }
-
-  bf16x8 af[2][4], b0[2][2], b1[2][2];
-  if constexpr (MODE == 3) {
-    const bool lag = wr == 1;
-    deep_prologue(a, m0, n0, nk, smem, wave, lane);
-    if (nk > 1) DLBB_WAIT_VM(8); else DLBB_WAIT_VM(4);   // retire S0(0), S1(0)
-    __builtin_amdgcn_s_barrier();
-    if (lag) __builtin_amdgcn_s_barrier();
-    deep_mainloop(a, acc, m0, n0, nk, smem, wave, lane);
-    if (!lag) __builtin_amdgcn_s_barrier();
-  } else if constexpr (MODE >= 1) {
-    // Two barriers per phase ([stage + ds_read] | barrier | [16 MFMA] | barrier) and wave
-    // row 1 one barrier behind wave row 0: on every SIMD one wave's LDS reads overlap its
-    // partner's MFMA cluster (CDNA guide 8-phase template, T3). With the groups offset, a
-    // section read at phase q must be waited for (by every wave) before the FIRST barrier of
-    // phase q-1. MODE 1 issues section p of tile t+1 at phase p (waits: vmcnt(4) at phases
-    // 1, 2, 4); MODE 2 issues all four sections at phase 1, so each has 3-5 phases to land
-    // (waits: vmcnt(10) / vmcnt(8) / - / vmcnt(4) at phases 1-4).
-    const bool lag = wr == 1;
-    if (lag) __builtin_amdgcn_s_barrier();
-    for (int64_t t = 0; t < nk; ++t) {
-      char* cur = smem + (t & 1) * kBuf2Bytes;
-      char* nxt = smem + ((t + 1) & 1) * kBuf2Bytes;
-      const bool more = t + 1 < nk;
-      const bool more0 = t > 0;          // MODE 2: tile t's own sections were issued at t-1 P1
-      const int64_t kn = (t + 1) * BK;
-      // phase 1
-      if (more) {
-        stage_next(a, m0, n0, kn, nxt, 0, wave, lane);
-        if constexpr (MODE == 2) {
-          stage_next(a, m0, n0, kn, nxt, 1, wave, lane);
-          stage_next(a, m0, n0, kn, nxt, 2, wave, lane);
-          stage_next(a, m0, n0, kn, nxt, 3, wave, lane);
-        }
-      }
-      read_a(cur, wr, 0, fr, fq, af);
-      read_b(cur + kTile2Bytes, wc, 0, fr, fq, b0);
-      if constexpr (MODE == 2) {
-        // queue [SB1, SA1 | next 4 sections]: retire SB1 (needed at phase 2)
-        if (more) DLBB_WAIT_VM(10); else DLBB_WAIT_VM(2);
-      } else {
-        if (more) DLBB_WAIT_VM(4); else DLBB_WAIT_VM(0);
-      }
-      (void)more0;
-      DLBB_BARRIER();
-      __builtin_amdgcn_sched_barrier(0);
-      mfma_quadrant<0, 0>(acc, af, b0);
-      __builtin_amdgcn_sched_barrier(0);
-      __builtin_amdgcn_s_barrier();
-      // phase 2
-      if constexpr (MODE == 1) {
-        if (more) stage_next(a, m0, n0, kn, nxt, 1, wave, lane);
-      }
-      read_b(cur + kTile2Bytes, wc, 1, fr, fq, b1);
-      if constexpr (MODE == 2) {
-        if (more) DLBB_WAIT_VM(8); else DLBB_WAIT_VM(0);   // retire SA1 (phase 3)
-      } else {
-        if (more) DLBB_WAIT_VM(4); else DLBB_WAIT_VM(0);
-      }
-      DLBB_BARRIER();
-      __builtin_amdgcn_sched_barrier(0);
-      mfma_quadrant<0, 1>(acc, af, b1);
-      __builtin_amdgcn_sched_barrier(0);
-      __builtin_amdgcn_s_barrier();
-      // phase 3
-      if constexpr (MODE == 1) {
-        if (more) stage_next(a, m0, n0, kn, nxt, 2, wave, lane);
-      }
-      read_a(cur, wr, 1, fr, fq, af);
-      DLBB_BARRIER();
-      __builtin_amdgcn_sched_barrier(0);
-      mfma_quadrant<1, 1>(acc, af, b1);
-      __builtin_amdgcn_sched_barrier(0);
-      __builtin_amdgcn_s_barrier();
-      // phase 4
-      if constexpr (MODE == 1) {
-        if (more) stage_next(a, m0, n0, kn, nxt, 3, wave, lane);
-      }
-      if (more) DLBB_WAIT_VM(4); else DLBB_WAIT_VM(0);       // retire SA0', SB0'
-      DLBB_BARRIER();
-      __builtin_amdgcn_sched_barrier(0);
-      mfma_quadrant<1, 0>(acc, af, b0);
-      __builtin_amdgcn_sched_barrier(0);
-      __builtin_amdgcn_s_barrier();
-    }
-    if (!lag) __builtin_amdgcn_s_barrier();   // equal barrier counts for both wave rows
-  } else {
-  for (int64_t t = 0; t < nk; ++t) {
-    char* cur = smem + (t & 1) * kBuf2Bytes;
-    char* nxt = smem + ((t + 1) & 1) * kBuf2Bytes;
-    const bool more = t + 1 < nk;
-    const int64_t kn = (t + 1) * BK;
-    // phase 1
-    if (more) stage_next(a, m0, n0, kn, nxt, 0, wave, lane);
-    read_a(cur, wr, 0, fr, fq, af);
-    read_b(cur + kTile2Bytes, wc, 0, fr, fq, b0);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-    mfma_quadrant<0, 0>(acc, af, b0);
-    if (more) DLBB_WAIT_VM(4); else DLBB_WAIT_VM(0);
-    DLBB_BARRIER();
-    // phase 2
-    if (more) stage_next(a, m0, n0, kn, nxt, 1, wave, lane);
-    read_b(cur + kTile2Bytes, wc, 1, fr, fq, b1);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-    mfma_quadrant<0, 1>(acc, af, b1);
-    if (more) DLBB_WAIT_VM(4); else DLBB_WAIT_VM(0);
-    DLBB_BARRIER();
-    // phase 3
-    if (more) stage_next(a, m0, n0, kn, nxt, 2, wave, lane);
-    read_a(cur, wr, 1, fr, fq, af);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-    mfma_quadrant<1, 1>(acc, af, b1);
-    DLBB_BARRIER();
-    // phase 4
-    if (more) stage_next(a, m0, n0, kn, nxt, 3, wave, lane);
-    mfma_quadrant<1, 0>(acc, af, b0);
-    if (more) DLBB_WAIT_VM(4); else DLBB_WAIT_VM(0);
-    DLBB_BARRIER();
-  }
-  }
-
-  store_tile_256(a, acc, m0, n0, wave, lane);
-}
-
-// Persistent form of the deep schedule: gridDim.x <= #CUs workgroups walk the virtual
-// workgroup ids vb = blockIdx.x, +gridDim.x, ... (same XCD chunk, same GROUP_M order as the
-// one-tile-per-workgroup launch). After a tile's main loop the NEXT tile's six prologue
-// sections are issued before this tile's epilogue stores, so the pipeline refill overlaps the
-// stores instead of following them (matters at small K: GPT-2's K = 768 is 12 K-tiles).
-__global__ void __launch_bounds__(kThreads2, 1) gemm_bf16_nt_256_persistent(GemmArgs a) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const bool lag = (wave >> 2) == 1;
-  const int nwg = static_cast<int>(((a.M + BM2 - 1) / BM2) * ((a.N + BN2 - 1) / BN2));
-  const int64_t nk = a.K / BK;
-  int vb = blockIdx.x;
-  if (vb >= nwg) return;
-  Tile256 tl = tile_of(a, vb);
-  deep_prologue(a, tl.m0, tl.n0, nk, smem, wave, lane);
-  if (nk > 1) DLBB_WAIT_VM(8); else DLBB_WAIT_VM(4);
+  const bool lag = wr == 1;
+  deep_prologue(a, m0, n0, nk, smem, wave, lane);
+  if (nk > 1) DLBB_WAIT_VM(8); else DLBB_WAIT_VM(4);   // retire S0(0), S1(0)
   __builtin_amdgcn_s_barrier();
-  f32x4 acc[8][4];
-  for (;;) {
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    if (lag) __builtin_amdgcn_s_barrier();
-    deep_mainloop(a, acc, tl.m0, tl.n0, nk, smem, wave, lane);
-    if (!lag) __builtin_amdgcn_s_barrier();     // rows re-aligned; every LDS read retired
-    const int vn = vb + static_cast<int>(gridDim.x);
-    const bool more = vn < nwg;
-    store_tile_256(a, acc, tl.m0, tl.n0, wave, lane);
-    if (!more) break;
-    const Tile256 tn = tile_of(a, vn);
-    deep_prologue(a, tn.m0, tn.n0, nk, smem, wave, lane);
-    DLBB_WAIT_VM(0);           // stores and prologue sections (stores and loads share vmcnt)
-    __builtin_amdgcn_s_barrier();
-    vb = vn;
-    tl = tn;
-  }
+  if (lag) __builtin_amdgcn_s_barrier();
+  deep_mainloop(a, acc, m0, n0, nk, smem, wave, lane);
+  if (!lag) __builtin_amdgcn_s_barrier();
+  store_tile_256(a, acc, m0, n0, wave, lane);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1039,15 +870,9 @@ __device__ __forceinline__ void wait_vm() {
 // below is written in it (NJ = 4 gives the original literals).
 // PHASES (diagnostic only, dlbb_gemm_nt_phase_probe): thread 0 stamps start / first MFMA (after
 // the prologue waits) / end of the K-loop / end of the stores: 4 u64 per workgroup into `st`.
-// MOVEB (A/B, set_stagger(11); NT 256² only): wave row 0 issues B(u+2) between the two k-halves
-// of its MFMA phase instead of in its memory interval — the memory interval (24 ds_reads + 8
-// LDS-DMA pieces at 60-185 issue cycles each) outlasts the MFMA phase (PMC: MFMA busy 82 % on
-// the single-round long-K case, profiles/r04_gemm/SUMMARY.md). Its first counted wait then has
-// B(u+2) not yet issued: NBx fewer younger loads.
 template <bool NN, bool BAL = false, bool TN = false, bool STAMP = false, int NJ = 4,
-          bool PHASES = false, int MOVEB = 0>
+          bool PHASES = false>
 __device__ __forceinline__ void pingpong_body(GemmArgs a, char* smem, uint64_t* st = nullptr) {
-  static_assert(!MOVEB || (NJ == 4 && !NN && !TN && BAL), "MOVEB: NT 256² balanced only");
   static_assert(NJ == 4 || (NJ == 3 && !NN && !TN), "192-wide tiles: NT only");
   constexpr int NBI = 2 * NJ;                 // B DMA instructions per staging wave per K-tile
   constexpr int kTileB = NJ * 64 * BK * 2;    // bytes of one B tile buffer
@@ -1170,7 +995,7 @@ __device__ __forceinline__ void pingpong_body(GemmArgs a, char* smem, uint64_t* 
       const char* ab = abuf0 + (u & 1) * kTile2Bytes;
       read_frags(ab, bbuf0 + cb * kTileB, 0);
       const bool h1 = u + 1 < nk, b2 = u + 2 < nk;
-      if (MOVEB != 3 && h1)
+      if (h1)
         DLBB_STAGE_A(u + 1, abuf0 + ((u + 1) & 1) * kTile2Bytes, 1,
                      stage_a_half(ra, lda2, rows_a, (u + 1) * kStep,
                                   abuf0 + ((u + 1) & 1) * kTile2Bytes, 1, wc, aoff));
@@ -1181,15 +1006,10 @@ __device__ __forceinline__ void pingpong_body(GemmArgs a, char* smem, uint64_t* 
         else
           stage_bt(Z{}, F{}, u + 2, bbuf0 + cb2 * kTileB);
       };
-      if (!MOVEB && b2) stage_b2();
+      if (b2) stage_b2();
       // retire A-hi(u) (issued two intervals ago; tile 0's came from row 1)
-      constexpr int kB2 = MOVEB ? 0 : (BAL ? NBI / 2 : NBI);   // B(u+2) instructions issued
-      if constexpr (MOVEB == 3) {
-        // A-hi(u) and B0(u+1) were both issued in the previous MFMA phase (A-hi first); only
-        // B0(u+1) is younger than A-hi(u) — and nothing of this interval is issued yet
-        if (h1) wait_vm<NBI / 2>();
-        else wait_vm<0>();
-      } else if constexpr (BAL) {
+      constexpr int kB2 = BAL ? NBI / 2 : NBI;         // B(u+2) instructions issued
+      if constexpr (BAL) {
         if (b2) wait_vm<NBI / 2 + 4 + kB2>();
         else if (h1) wait_vm<NBI / 2 + 4>();
         else wait_vm<0>();
@@ -1202,83 +1022,8 @@ __device__ __forceinline__ void pingpong_body(GemmArgs a, char* smem, uint64_t* 
       __builtin_amdgcn_sched_barrier(0);
       __builtin_amdgcn_s_barrier();                   // end of interval 2u
       __builtin_amdgcn_sched_barrier(0);
-      if constexpr (MOVEB == 1) {
-#pragma unroll
-        for (int i = 0; i < 8; ++i)
-#pragma unroll
-          for (int j = 0; j < 4; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[0][j], af[0][i], acc[i][j],
-                                                                0, 0, 0);
-        __builtin_amdgcn_sched_barrier(0);
-        if (b2) stage_b2();                           // buffer (u+2)%3 free since 2u-1
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int i = 0; i < 8; ++i)
-#pragma unroll
-          for (int j = 0; j < 4; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[1][j], af[1][i], acc[i][j],
-                                                                0, 0, 0);
-      } else if constexpr (MOVEB == 3) {
-        // A-hi(u+1)'s four pieces, then B0(u+2)'s four, one piece per 8 MFMAs: the memory
-        // interval keeps only its ds_reads and one counted wait
-        const int cb2 = cb == 0 ? 2 : cb - 1;
-        char* const anext = abuf0 + ((u + 1) & 1) * kTile2Bytes;
-        auto group = [&](auto gc) {
-          constexpr int gi = decltype(gc)::value, ks = gi >> 2, i0 = 2 * (gi & 3);
-#pragma unroll
-          for (int i = i0; i < i0 + 2; ++i)
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[ks][j], af[ks][i],
-                                                                  acc[i][j], 0, 0, 0);
-          __builtin_amdgcn_sched_barrier(0);
-          if constexpr (gi < 4) {
-            if (h1) stage_a_piece<gi>(ra, lda2, rows_a, (u + 1) * kStep, anext, 1, wc, aoff);
-          } else {
-            if (b2) stage_bt(std::integral_constant<int, gi - 4>{},
-                             std::integral_constant<int, gi - 3>{}, u + 2, bbuf0 + cb2 * kTileB);
-          }
-          __builtin_amdgcn_sched_barrier(0);
-        };
-        group(std::integral_constant<int, 0>{});
-        group(std::integral_constant<int, 1>{});
-        group(std::integral_constant<int, 2>{});
-        group(std::integral_constant<int, 3>{});
-        group(std::integral_constant<int, 4>{});
-        group(std::integral_constant<int, 5>{});
-        group(std::integral_constant<int, 6>{});
-        group(std::integral_constant<int, 7>{});
-      } else if constexpr (MOVEB == 2) {
-        // B(u+2)'s four pieces spread one per 16 MFMAs (the guide: a lone LDS-DMA piece among
-        // bare MFMAs costs ~60 issue cycles, within the 8 free issue cycles x 16 MFMAs after it)
-        const int cb2 = cb == 0 ? 2 : cb - 1;
-        auto group = [&](auto ksc, auto i0c) {
-          constexpr int ks = decltype(ksc)::value, i0 = decltype(i0c)::value;
-#pragma unroll
-          for (int i = i0; i < i0 + 4; ++i)
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[ks][j], af[ks][i],
-                                                                  acc[i][j], 0, 0, 0);
-        };
-        auto piece = [&](auto pc) {
-          constexpr int pp = decltype(pc)::value;
-          __builtin_amdgcn_sched_barrier(0);
-          if (b2) stage_bt(std::integral_constant<int, pp>{}, std::integral_constant<int, pp + 1>{},
-                           u + 2, bbuf0 + cb2 * kTileB);
-          __builtin_amdgcn_sched_barrier(0);
-        };
-        group(std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{});
-        piece(std::integral_constant<int, 0>{});
-        group(std::integral_constant<int, 0>{}, std::integral_constant<int, 4>{});
-        piece(std::integral_constant<int, 1>{});
-        group(std::integral_constant<int, 1>{}, std::integral_constant<int, 0>{});
-        piece(std::integral_constant<int, 2>{});
-        group(std::integral_constant<int, 1>{}, std::integral_constant<int, 4>{});
-        piece(std::integral_constant<int, 3>{});
-      } else {
-        mfma_all();
-      }
+      mfma_all();
+
       __builtin_amdgcn_sched_barrier(0);
       if (h1) {                                       // retire B(u+1) (BAL: its first half)
         if (b2) { if (BAL) wait_vm<4 + NBI / 2>(); else wait_vm<4 + NBI>(); }
@@ -1360,22 +1105,6 @@ __global__ void __launch_bounds__(kThreads2, 1) gemm_bf16_nt_256_pingpong3_bal(G
   extern __shared__ __attribute__((aligned(16))) char smem[];
   pingpong_body<false, true>(a, smem);
 }
-// A/B variant (set_stagger(11)): BAL with wave row 0's B DMA inside its MFMA phase (MOVEB)
-__global__ void __launch_bounds__(kThreads2, 1) gemm_bf16_nt_256_pingpong3_bal_mb(GemmArgs a) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  pingpong_body<false, true, false, false, 4, false, 1>(a, smem);
-}
-// A/B variant (set_stagger(12)): BAL with row 0's B DMA pieces spread one per 16 MFMAs
-__global__ void __launch_bounds__(kThreads2, 1) gemm_bf16_nt_256_pingpong3_bal_mb2(GemmArgs a) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  pingpong_body<false, true, false, false, 4, false, 2>(a, smem);
-}
-// A/B variant (set_stagger(13)): row 0's A-hi(u+1) AND B0(u+2) pieces spread one per 8 MFMAs
-__global__ void __launch_bounds__(kThreads2, 1) gemm_bf16_nt_256_pingpong3_bal_mb3(GemmArgs a) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  pingpong_body<false, true, false, false, 4, false, 3>(a, smem);
-}
-
 // 256 x 192 tiles (N % 192 == 0): grids that end in a partial round of 256² tiles
 constexpr int kPP192Lds = 2 * kTile2Bytes + 3 * (3 * 64 * BK * 2);   // 136 KiB
 __global__ void __launch_bounds__(kThreads2, 1) gemm_bf16_nt_192_pingpong3(GemmArgs a) {
@@ -1464,7 +1193,6 @@ DLBB_PP_STAMPED(gemm_bf16_tn_256_pingpong3_bal, true, true, true)
 enum PpLean : int {
   PP_PLAIN = 0, PP_BIAS = 1, PP_BIAS_GELU_TANH = 2, PP_BIAS_GELU_ERF = 3,
   PP_DGELU_TANH = 4, PP_DGELU_ERF = 5,
-  PP_NOSTORE = 99,   // diagnostic: no C output (dlbb_gemm_set_diag_nostore)
 };
 
 // What the epilogue reads (the bias of the lane's 16 columns, or its 8 x 16 values of u) is loaded
@@ -1644,8 +1372,7 @@ __device__ __forceinline__ void pp_persist_body(GemmArgs a, char* smem) {
     __builtin_amdgcn_sched_barrier(0);                                             \
     int ln_ = lane;                                                                \
     asm volatile("" : "+v"(ln_));                                                  \
-    if (LEAN != PP_NOSTORE || a.out_f32 == 77)  /* (no-store: never; keeps the MFMAs) */ \
-      store_lean_bf16<NN, LEAN == PP_NOSTORE ? PP_PLAIN : LEAN>(                   \
+    store_lean_bf16<NN, LEAN>(                                                     \
           a, acc, (T).m0 + (wave >> 2) * 128, (T).n0 + (wave & 3) * 64, ln_, pre_);  \
     _Pragma("unroll") for (int x_ = 0; x_ < 8; ++x_)                                \
       _Pragma("unroll") for (int y_ = 0; y_ < 4; ++y_)                              \
@@ -2079,13 +1806,9 @@ __device__ __forceinline__ void wait_vmc() {   // any compile-time count
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-// EARLY_ = kNoStores (diagnostic, dlbb_gemm_set_diag_nostore(1)): no C stores at all — the
-// loop's own time for the same tile sequence.
-constexpr int kNoStores = 99;
 template <bool BAL, int EARLY_>
 __device__ __forceinline__ void pp192_spread_body(GemmArgs a, char* smem) {
-  constexpr bool kNoStore = EARLY_ == kNoStores;
-  constexpr int kEarly = kNoStore ? 12 : EARLY_;
+  constexpr int kEarly = EARLY_;
   constexpr int kSpreadIters = spread_iters(kEarly);
   constexpr int NJ = 3, NBI = 6;
   constexpr int NBx = BAL ? NBI / 2 : NBI;      // B instructions of wave row 0 per iteration
@@ -2293,7 +2016,7 @@ __device__ __forceinline__ void pp192_spread_body(GemmArgs a, char* smem) {
       using Z = integral_constant<int, 0>;
       using S = integral_constant<int, kSpi>;
       int k = 0;
-      if (i > 0 && !kNoStore) {                 // boundary + spread iterations (host: nk > them)
+      if (i > 0) {                              // boundary + spread iterations (host: nk > them)
         tp = tprev;                             // the finished tile: E early stores,
         __builtin_amdgcn_sched_barrier(0);      // the rest parked in pk (fenced: the next
         park();                                 // ds_reads must not rise above the packing)
@@ -2314,7 +2037,6 @@ __device__ __forceinline__ void pp192_spread_body(GemmArgs a, char* smem) {
   else run(integral_constant<int, 1>{});
   // the last tile: plain epilogue (nothing left to hide it under)
   DLBB_WAIT_VM(0);
-  if (kNoStore && a.out_f32 != 77) return;      // (never 77: the accumulators stay live)
   tp = tprev;
   park();
 #pragma unroll
@@ -2333,244 +2055,6 @@ __global__ void __launch_bounds__(kThreads2, 1) gemm_bf16_nt_192_pp_spread_bal(G
   pp192_spread_body<true, EARLY>(a, smem);
 }
 
-// ---------------------------------------------------------------------------------------
-// One wave per SIMD (A/B only, set_stagger(9); profiles/r03_gemm/w4_experiment.md): 256 x 256
-// tile, 256 threads = 4 waves as 2 (M) x 2 (N), each wave 128 x 128 outputs = 64 accumulators of
-// 16x16 held in AGPRs — hipBLASLt's MT256x256x64 MI16x16 structure. The MFMAs are inline asm
-// with "+a" accumulator operands, so hipcc keeps all 256 accumulators in AGPRs across the loop
-// and never moves them through VGPRs (round 2's builtin-MFMA 4-wave build did, and spilled:
-// ~500 TF/s). Correct (bitwise equal to the ping-pong) but 1300-1340 TF/s at 8192^3 against
-// 1550 for the ping-pong and 1640-1680 for hipBLASLt: MFMA busy 64 % vs 82 / 88 %. A register-
-// staged form (buffer_load -> ds_write) measured 1300-1315 and was dropped.
-// The asm MFMAs are invisible to hipcc's hazard recognizer, so (1) every loop iteration must
-// run the SAME code — a peeled copy got its own register assignment and hipcc permuted
-// accumulators with v_accvgpr_mov right behind the MFMAs that wrote them — and (2) the
-// accumulators are read out only after s_nop padding past the last MFMA's write latency.
-constexpr int kThreadsW4 = 256;
-
-#define DLBB_FENCE() asm volatile("" ::: "memory")
-
-__device__ __forceinline__ void mfma_agpr(f32x4& acc, const bf16x8& b, const bf16x8& a) {
-  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(b), "v"(a));
-}
-
-// MFMA group g of a half: output rows i = g / 2, column blocks j = (g % 2) * 4 .. + 3
-template <int G>
-__device__ __forceinline__ void w4_mfma(f32x4 (&acc)[2][8][4], const bf16x8 (&fa)[8],
-                                        const bf16x8 (&fb)[8]) {
-  constexpr int i = G >> 1, jg = G & 1;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) mfma_agpr(acc[jg][i][j], fb[jg * 4 + j], fa[i]);
-}
-
-// ---------------------------------------------------------------------------------------
-// The one-wave-per-SIMD kernel with LDS-DMA staging in half-K-tile stages (set_stagger(9)).
-// hipBLASLt's MT256x256x64 MI16x16 kernel (disassembled from the ROCm library: 4 waves, 128
-// MFMA + 32 ds_read_b128 + 16 buffer_load...lds per K-tile, the loads spread between MFMAs,
-// vmcnt(13) kept in flight across its barriers) stages by DMA, not through registers; this is
-// that structure in HIP: staging costs no VGPRs and no ds_write, and the LDS ring is deep.
-//   * A stage is one k-step of 32: A [256 rows][64 B] + B [256][64 B] = 32 KiB; 4 stages
-//     (128 KiB) in a ring. One DMA piece = 16 rows x 64 B; 8 pieces per wave per stage (4 of A
-//     rows [64w, 64w + 64), 4 of B rows [64w, 64w + 64)).
-//   * 64-B rows: 16-B slot s of row r holds k-chunk s ^ f((r >> 2) & 3), f = {0, 3, 2, 1}:
-//     every lane group of a ds_read_b128 (groups {0-3,12-15,20-27}, {4-11,16-19,28-31}, ...)
-//     then hits 16 distinct bank quads for the MFMA fragment pattern (row = lane & 15, chunk =
-//     lane >> 4) — checked exhaustively on the host (ops/gemm.py w4_swizzle_check).
-//   * Half h (k-step h): 16 groups of 4 MFMAs on F(h); groups 0-7 also read F(h+1) (2 each),
-//     groups 8-15 issue one DMA piece each of k-step h + 4 into stage (h + 4) % 4 = h % 4.
-//     End of half: vmcnt(16) (k-step h+2 landed: only h+3, h+4's 16 pieces may stay in
-//     flight), lgkmcnt(0), barrier. One barrier per k-step.
-//   RAW: F(h+1) is read in half h; its DMA (issued in half h-3) was retired by the vmcnt of half
-//   h-1 and published by that half's barrier. WAR: k-step h+4 overwrites stage h % 4, whose
-//   fragments F(h) were read in half h-1 and retired (lgkmcnt(0)) before half h-1's barrier.
-//   Past the last k-step the DMA re-reads the last one (clamped source, dead stage) so every
-//   half runs the same code and the counted waits stay exact.
-// Host contract: M % 16 == 0, N % 64 == 0, K % 64 == 0, K >= 128, 32-bit buffer offsets.
-constexpr int kW4dStage = 2 * BM2 * 32 * 2;          // 32 KiB
-constexpr int kW4dStages = 4;
-constexpr int kW4dLds = kW4dStages * kW4dStage;      // 128 KiB
-
-__device__ __forceinline__ int w4d_f(int q) { return (4 - q) & 3; }
-
-struct W4dCtx {
-  __amdgpu_buffer_rsrc_t ra, rb;
-  uint32_t voff_a, voff_b;     // per lane: row-in-piece x ld + swizzled 16-B chunk
-  uint32_t lda2, ldb2;
-  uint32_t sa[4], sb[4];       // per piece: group row x ld (SGPR)
-  uint32_t rd_off;             // per lane: fragment row fr x 64 B + swizzled slot
-  int wr, wc;
-  char* smem;
-};
-
-template <int P>   // piece P: 0..3 A, 4..7 B
-__device__ __forceinline__ void w4d_dma(const W4dCtx& c, char* stage, int ks) {
-  const uint32_t k2 = static_cast<uint32_t>(ks) * 64;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  if constexpr (P < 4)
-    bldsx4(c.ra, c.voff_a, c.sa[P] + k2, stage + (wave * 64 + P * 16) * 64);
-  else
-    bldsx4(c.rb, c.voff_b, c.sb[P - 4] + k2, stage + BM2 * 64 + (wave * 64 + (P - 4) * 16) * 64);
-}
-
-// fragment G of F(h) (order of first use: a0, b0..b7, a1..a7)
-template <int G>
-__device__ __forceinline__ void w4d_read(const W4dCtx& c, const char* stage, bf16x8 (&fa)[8],
-                                         bf16x8 (&fb)[8]) {
-  if constexpr (G == 0)
-    fa[0] = *reinterpret_cast<const bf16x8*>(stage + (c.wr * 128) * 64 + c.rd_off);
-  else if constexpr (G <= 8)
-    fb[G - 1] = *reinterpret_cast<const bf16x8*>(stage + BM2 * 64 +
-                                                 (c.wc * 128 + (G - 1) * 16) * 64 + c.rd_off);
-  else
-    fa[G - 8] = *reinterpret_cast<const bf16x8*>(stage + (c.wr * 128 + (G - 8) * 16) * 64 +
-                                                 c.rd_off);
-}
-
-// V (A/B variants, set_stagger(9 + V)): bit 0 = the 8 DMA pieces go out in groups 0-7 beside
-// the reads (else groups 8-15); bit 1 = the half's last MFMA is issued AFTER its waits, just
-// before the barrier, so the matrix pipe has work while the wave waits there.
-template <int V, int G>
-__device__ __forceinline__ void w4d_group(const W4dCtx& c, f32x4 (&acc)[2][8][4],
-                                          const bf16x8 (&ca)[8], const bf16x8 (&cb)[8],
-                                          bf16x8 (&na)[8], bf16x8 (&nb)[8], const char* rd,
-                                          char* wr_stage, int ksd) {
-  if constexpr ((V & 2) && G == 15) {
-    constexpr int i = G >> 1, jg = G & 1;
-#pragma unroll
-    for (int j = 0; j < 3; ++j) mfma_agpr(acc[jg][i][j], cb[jg * 4 + j], ca[i]);
-  } else {
-    w4_mfma<G>(acc, ca, cb);
-  }
-  DLBB_FENCE();
-  if constexpr (G < 8) {
-    w4d_read<2 * G>(c, rd, na, nb);
-    w4d_read<2 * G + 1>(c, rd, na, nb);
-    if constexpr (V & 1) w4d_dma<G>(c, wr_stage, ksd);
-  } else {
-    if constexpr (!(V & 1)) w4d_dma<G - 8>(c, wr_stage, ksd);
-  }
-  DLBB_FENCE();
-}
-
-template <int V, int... G>
-__device__ __forceinline__ void w4d_half(const W4dCtx& c, f32x4 (&acc)[2][8][4],
-                                         const bf16x8 (&ca)[8], const bf16x8 (&cb)[8],
-                                         bf16x8 (&na)[8], bf16x8 (&nb)[8], const char* rd,
-                                         char* wr_stage, int ksd,
-                                         std::integer_sequence<int, G...>) {
-  (w4d_group<V, G>(c, acc, ca, cb, na, nb, rd, wr_stage, ksd), ...);
-  DLBB_WAIT_VM(16);
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  if constexpr (V & 2) {
-    __builtin_amdgcn_sched_barrier(0);
-    mfma_agpr(acc[1][7][3], cb[7], ca[7]);
-    __builtin_amdgcn_sched_barrier(0);
-  }
-  __builtin_amdgcn_s_barrier();
-  DLBB_FENCE();
-}
-
-template <int... P>
-__device__ __forceinline__ void w4d_dma_all(const W4dCtx& c, char* stage, int ks,
-                                            std::integer_sequence<int, P...>) {
-  (w4d_dma<P>(c, stage, ks), ...);
-}
-
-template <int... G>
-__device__ __forceinline__ void w4d_read_all(const W4dCtx& c, const char* stage, bf16x8 (&fa)[8],
-                                             bf16x8 (&fb)[8], std::integer_sequence<int, G...>) {
-  (w4d_read<G>(c, stage, fa, fb), ...);
-}
-
-// epilogue quarter (column half JG, row half Q) with compile-time indices only: an array
-// indexed by a loop the unroller declines to unroll would send all 256 accumulators to scratch
-template <int JG, int Q>
-__device__ __forceinline__ void w4d_store_quarter(const GemmArgs& a, const f32x4 (&acc)[2][8][4],
-                                                  int64_t r0, int64_t c0, int lane) {
-  f32x4 part[4][4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) part[i][j] = acc[JG][4 * Q + i][j];
-  store_tile<4>(a, part, r0 + 64 * Q, c0 + 64 * JG, lane);
-}
-
-template <int V>
-__global__ void __launch_bounds__(kThreadsW4, 1) gemm_bf16_nt_w4d(GemmArgs a) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  W4dCtx c;
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  c.wr = wave >> 1;
-  c.wc = wave & 1;
-  c.smem = smem;
-  const Tile256 tl = tile_of(a, static_cast<int>(blockIdx.x));
-  const int64_t m0 = tl.m0, n0 = tl.n0;
-  const int H = static_cast<int>(a.K / 32);           // k-steps
-  c.lda2 = static_cast<uint32_t>(a.lda) * 2;
-  c.ldb2 = static_cast<uint32_t>(a.ldb) * 2;
-  const int rows_a = static_cast<int>(a.M - m0), rows_b = static_cast<int>(a.N - n0);
-  {
-    // DMA lane l -> LDS row l >> 2 of the piece, slot l & 3; it loads k-chunk slot ^ f(row)
-    const int r = lane >> 2, slot = lane & 3;
-    const int ch = slot ^ w4d_f((r >> 2) & 3);
-    c.voff_a = static_cast<uint32_t>(r) * c.lda2 + ch * 16;
-    c.voff_b = static_cast<uint32_t>(perm_brow(r)) * c.ldb2 + ch * 16;
-  }
-#pragma unroll
-  for (int p = 0; p < 4; ++p) {
-    const int trow = wave * 64 + p * 16;
-    const int ga = trow < rows_a - 16 ? trow : rows_a - 16;
-    const int gb = (trow & ~63) < rows_b ? perm_brow(trow) : (perm_brow(trow) & 63);
-    c.sa[p] = static_cast<uint32_t>(ga) * c.lda2;
-    c.sb[p] = static_cast<uint32_t>(gb) * c.ldb2;
-  }
-  {
-    const int fr = lane & 15, fq = lane >> 4;
-    c.rd_off = static_cast<uint32_t>(fr * 64 + ((fq ^ w4d_f((fr >> 2) & 3)) << 4));
-  }
-  c.ra = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(a.A + m0 * a.lda), 0, 0x7fffffff,
-                                           0x00020000);
-  c.rb = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(a.B + n0 * a.ldb), 0, 0x7fffffff,
-                                           0x00020000);
-  f32x4 acc[2][8][4];
-#pragma unroll
-  for (int h = 0; h < 2; ++h)
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[h][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  bf16x8 fa0[8], fb0[8], fa1[8], fb1[8];
-  constexpr auto seq8 = std::make_integer_sequence<int, 8>{};
-  constexpr auto seq16 = std::make_integer_sequence<int, 16>{};
-  // prologue: k-steps 0..3 in flight (stages 0..3), k-step 0 landed -> F(0)
-#pragma unroll
-  for (int d = 0; d < kW4dStages; ++d)
-    w4d_dma_all(c, smem + d * kW4dStage, d < H ? d : H - 1, seq8);
-  DLBB_WAIT_VM(24);
-  __builtin_amdgcn_s_barrier();
-  DLBB_FENCE();
-  w4d_read_all(c, smem, fa0, fb0, seq16);
-  for (int h = 0; h < H; h += 2) {
-    // even half: compute F(h) (fa0/fb0), read F(h+1) into fa1/fb1, DMA k-step h+4
-    w4d_half<V>(c, acc, fa0, fb0, fa1, fb1, smem + ((h + 1) & 3) * kW4dStage,
-                smem + (h & 3) * kW4dStage, h + 4 < H ? h + 4 : H - 1, seq16);
-    // odd half
-    w4d_half<V>(c, acc, fa1, fb1, fa0, fb0, smem + ((h + 2) & 3) * kW4dStage,
-                smem + ((h + 1) & 3) * kW4dStage, h + 5 < H ? h + 5 : H - 1, seq16);
-  }
-  DLBB_WAIT_VM(0);
-  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
-  // the epilogue in 64-row quarters: fewer accumulators live in VGPRs at once (no spill)
-  w4d_store_quarter<0, 0>(a, acc, m0 + c.wr * 128, n0 + c.wc * 128, lane);
-  w4d_store_quarter<0, 1>(a, acc, m0 + c.wr * 128, n0 + c.wc * 128, lane);
-  w4d_store_quarter<1, 0>(a, acc, m0 + c.wr * 128, n0 + c.wc * 128, lane);
-  w4d_store_quarter<1, 1>(a, acc, m0 + c.wr * 128, n0 + c.wc * 128, lane);
-}
-
-static void launch_w4d(dim3 g, const GemmArgs& a, hipStream_t stream) {
-  hipLaunchKernelGGL(gemm_bf16_nt_w4d<0>, g, dim3(kThreadsW4), kW4dLds, stream, a);
-}
 
 }  // namespace dlbb
 
@@ -2605,7 +2089,10 @@ static int num_cus() {
   return ncu[dev];
 }
 
-static int dlbb_gemm_stagger = 6;      // 256^2 schedule (set_stagger): 6 = ping-pong, 160 KiB LDS, measured fastest
+// 256^2 schedule (set_stagger): 6 = ping-pong (160 KiB LDS, measured fastest; the default),
+// 10 = its persistent form on multi-round grids (the default's upgrade, see below), 3 = the
+// deep-pipeline general-contract kernel (forced for A/B; also every ragged shape's fallback)
+static int dlbb_gemm_stagger = 6;
 // Balanced DMA issue (BAL) for the ping-pong kernels: 0 never, 1 always, 2 (default) = always
 // for NN (dgrad: +1-5 % on every measured shape, K 768 .. 50304) and for NT when the reduction
 // has >= kBalMinKTiles K-tiles (NT: +1-5 % at K >= 2048, -1.5 % at K = 768)
@@ -2618,24 +2105,11 @@ constexpr int64_t kPersistMaxKTiles = 48;
 // co-resident, and comm workgroups holding CUs push part of such a grid into a second round
 // (the same slowdown as hipBLASLt's persistent Stream-K there), so they are off meanwhile
 static int dlbb_gemm_concurrent = 0;
-// DLBB_GEMM_PERSIST=0: never upgrade the default ping-pong to the persistent form (A/B)
-static bool persist_enabled() {
-  static const int on = [] {
-    const char* e = getenv("DLBB_GEMM_PERSIST");
-    return (e && e[0] == '0') ? 0 : 1;
-  }();
-  return on != 0 && dlbb_gemm_concurrent <= 0;
-}
-// DLBB_GEMM_PERSIST_EPI=0 (or dlbb_gemm_set_persist_epi(0)): keep bias / bias-GELU epilogues on
-// the non-persistent ping-pong (A/B)
-static int dlbb_persist_epi = -1;
-static bool persist_epi_enabled() {
-  if (dlbb_persist_epi < 0) {
-    const char* e = getenv("DLBB_GEMM_PERSIST_EPI");
-    dlbb_persist_epi = (e && e[0] == '0') ? 0 : 1;
-  }
-  return dlbb_persist_epi != 0;
-}
+static bool persist_enabled() { return dlbb_gemm_concurrent <= 0; }
+// dlbb_gemm_set_persist_epi(0): keep bias / bias-GELU epilogues on the non-persistent
+// ping-pong (A/B)
+static int dlbb_persist_epi = 1;
+static bool persist_epi_enabled() { return dlbb_persist_epi != 0; }
 static bool use_bal(int64_t k_tiles, bool nn) {
   return dlbb_gemm_bal == 1 || (dlbb_gemm_bal == 2 && (nn || k_tiles >= kBalMinKTiles));
 }
@@ -2646,16 +2120,6 @@ DLBB_API int dlbb_gemm_get_stagger() { return dlbb_gemm_stagger; }
 DLBB_API void dlbb_gemm_set_persist_epi(int on) { dlbb_persist_epi = on ? 1 : 0; }
 DLBB_API void dlbb_gemm_set_concurrent(int on) { dlbb_gemm_concurrent = on; }
 DLBB_API int dlbb_gemm_get_concurrent() { return dlbb_gemm_concurrent; }
-// spread-store persistent 192 kernel (variant 2): stores issued at the tile boundary, 12 or 18
-static int dlbb_spread_early = 12;
-DLBB_API void dlbb_gemm_set_spread_early(int n) { dlbb_spread_early = n == 18 ? 18 : 12; }
-// diagnostic: the plain persistent kernels (256² mode 10, 256 x 192 variant 2) skip their C
-// stores — the K-loop's own time over the same tile sequence (C is left unwritten)
-static int dlbb_diag_nostore = 0;
-DLBB_API void dlbb_gemm_set_diag_nostore(int on) { dlbb_diag_nostore = on ? 1 : 0; }
-// tile order experiment: GROUP_M of tile_of for the NT forward launches (0 = kGroupM)
-static int dlbb_group_m = 0;
-DLBB_API void dlbb_gemm_set_group_m(int g) { dlbb_group_m = g > 0 ? g : 0; }
 DLBB_API void dlbb_gemm_set_bal(int mode) { dlbb_gemm_bal = mode >= 0 && mode <= 2 ? mode : 2; }
 
 // ---------------------------------------------------------------------------------------
@@ -2781,7 +2245,6 @@ DLBB_API int dlbb_gemm_bf16_nt_v(const void* A, int64_t lda, const void* B, int6
              static_cast<const uint16_t*>(bias), static_cast<const uint16_t*>(residual),
              static_cast<uint16_t*>(preact), M, N, K, lda, ldb, ldc, ldr, epi, out_f32,
              vec_ok, 0};
-  a.group_m = dlbb_group_m;
   const int64_t tiles256 = ((M + BM2 - 1) / BM2) * ((N + BN2 - 1) / BN2);
   // variant 2: persistent 256 x 192 with spread C stores (plain bf16 output only, >= 9 K-tiles,
   // 8-byte aligned rows; pp192_spread_body); anything else falls back to variant 1
@@ -2792,16 +2255,8 @@ DLBB_API int dlbb_gemm_bf16_nt_v(const void* A, int64_t lda, const void* B, int6
     const int64_t grid = tiles < num_cus() ? tiles : num_cus();
     const dim3 g(static_cast<unsigned>(grid)), b(kThreads2);
     const bool bal = use_bal(K / BK, false);
-    if (dlbb_diag_nostore) {                // diagnostic: no C output
-      if (bal) hipLaunchKernelGGL(gemm_bf16_nt_192_pp_spread_bal<kNoStores>, g, b, kPP192Lds, stream, a);
-      else hipLaunchKernelGGL(gemm_bf16_nt_192_pp_spread<kNoStores>, g, b, kPP192Lds, stream, a);
-    } else if (dlbb_spread_early == 18) {
-      if (bal) hipLaunchKernelGGL(gemm_bf16_nt_192_pp_spread_bal<18>, g, b, kPP192Lds, stream, a);
-      else hipLaunchKernelGGL(gemm_bf16_nt_192_pp_spread<18>, g, b, kPP192Lds, stream, a);
-    } else {
-      if (bal) hipLaunchKernelGGL(gemm_bf16_nt_192_pp_spread_bal<12>, g, b, kPP192Lds, stream, a);
-      else hipLaunchKernelGGL(gemm_bf16_nt_192_pp_spread<12>, g, b, kPP192Lds, stream, a);
-    }
+    if (bal) hipLaunchKernelGGL(gemm_bf16_nt_192_pp_spread_bal<12>, g, b, kPP192Lds, stream, a);
+    else hipLaunchKernelGGL(gemm_bf16_nt_192_pp_spread<12>, g, b, kPP192Lds, stream, a);
     return hipGetLastError();
   }
   if (variant == 2) variant = 1;
@@ -2818,11 +2273,7 @@ DLBB_API int dlbb_gemm_bf16_nt_v(const void* A, int64_t lda, const void* B, int6
   const int force = dlbb_gemm_force_tile;
   if (force == 256 || (force != 128 && tiles256 >= 192)) {
     const dim3 g(static_cast<unsigned>(tiles256)), b(kThreads2);
-    int mode = dlbb_gemm_stagger;
-    // one-wave-per-SIMD kernel (mode 9): M % 16, N % 64, at least two K-tiles
-    if (mode == 9 && !(M % 16 == 0 && N % 64 == 0 && K >= 2 * BK &&
-                       lda * 2 * 256 + K * 2 < (1LL << 31) && ldb * 2 * 256 + K * 2 < (1LL << 31)))
-      mode = 6;                       // (then held to the ping-pong contract below)
+    int mode = dlbb_gemm_stagger == 10 || dlbb_gemm_stagger == 3 ? dlbb_gemm_stagger : 6;
     // default ping-pong on a multi-round grid with a short reduction: the persistent form
     // (tools/gemm_ab.py, profiles/r03_gemm/persistent_ab.jsonl, plain bf16: +6.6 % at
     // 16384 x 3072 x 768, +10.6 % GPT-2 LM head; neutral at K = 4096 over 3 rounds; -2 % on
@@ -2844,11 +2295,11 @@ DLBB_API int dlbb_gemm_bf16_nt_v(const void* A, int64_t lda, const void* B, int6
     // epilogue
     if (mode == 10 && (K < 2 * BK || lean < 0)) mode = 6;
     // ping-pong contract: 8-row A groups and 64-row B blocks wholly in or out (uniform clamps),
-    // 32-bit buffer offsets within a 256-row panel
-    if ((mode == 6 || mode == 7 || mode == 10 || mode == 11) && !(M % 8 == 0 && N % 64 == 0 && M >= 8 && lda * 2 * 256 + K * 2 < (1LL << 31) &&
-                       ldb * 2 * 256 + K * 2 < (1LL << 31)))
+    // 32-bit buffer offsets within a 256-row panel; otherwise the deep-pipeline kernel
+    if ((mode == 6 || mode == 10) &&
+        !(M % 8 == 0 && N % 64 == 0 && M >= 8 && lda * 2 * 256 + K * 2 < (1LL << 31) &&
+          ldb * 2 * 256 + K * 2 < (1LL << 31)))
       mode = 3;
-    if (mode == 5 || mode == 8 || mode > 11) mode = 3;
     if (mode == 10) {
       const int64_t grid = tiles256 < num_cus() ? tiles256 : num_cus();
       const dim3 gp(static_cast<unsigned>(grid)), bp(kThreads2);
@@ -2858,9 +2309,7 @@ DLBB_API int dlbb_gemm_bf16_nt_v(const void* A, int64_t lda, const void* B, int6
     if (bal) hipLaunchKernelGGL(gemm_bf16_nt_256_pp_persist_bal<L>, gp, bp, kPP6Lds, stream, a); \
     else hipLaunchKernelGGL(gemm_bf16_nt_256_pp_persist<L>, gp, bp, kPP6Lds, stream, a);   \
   } while (0)
-      if (lean == PP_PLAIN && dlbb_diag_nostore) lean = PP_NOSTORE;
       switch (lean) {
-        case PP_NOSTORE: DLBB_PP_PERSIST_LAUNCH(PP_NOSTORE); break;
         case PP_BIAS: DLBB_PP_PERSIST_LAUNCH(PP_BIAS); break;
         case PP_BIAS_GELU_TANH: DLBB_PP_PERSIST_LAUNCH(PP_BIAS_GELU_TANH); break;
         case PP_BIAS_GELU_ERF: DLBB_PP_PERSIST_LAUNCH(PP_BIAS_GELU_ERF); break;
@@ -2869,41 +2318,12 @@ DLBB_API int dlbb_gemm_bf16_nt_v(const void* A, int64_t lda, const void* B, int6
 #undef DLBB_PP_PERSIST_LAUNCH
       return hipGetLastError();
     }
-    if (mode == 4) {
-      static int ncu[64] = {0};
-      int dev = 0;
-      (void)hipGetDevice(&dev);
-      if (dev < 0 || dev >= 64) dev = 0;
-      if (ncu[dev] == 0) {
-        int n = 0;
-        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-            n <= 0)
-          n = 256;
-        ncu[dev] = n;
-      }
-      const int64_t grid = tiles256 < ncu[dev] ? tiles256 : ncu[dev];
-      hipLaunchKernelGGL(gemm_bf16_nt_256_persistent, dim3(static_cast<unsigned>(grid)), b,
-                         2 * kBuf2Bytes, stream, a);
-    } else if (mode == 9)
-      launch_w4d(g, a, stream);
-    else if (mode == 11)                  // A/B: BAL + row 0's B DMA inside its MFMA phase
-      hipLaunchKernelGGL(gemm_bf16_nt_256_pingpong3_bal_mb, g, dim3(kThreads2), kPP6Lds, stream, a);
-    else if (mode == 12)                  // A/B: same, one piece per 16 MFMAs
-      hipLaunchKernelGGL(gemm_bf16_nt_256_pingpong3_bal_mb2, g, dim3(kThreads2), kPP6Lds, stream, a);
-    else if (mode == 13)                  // A/B: A-hi + B pieces, one per 8 MFMAs
-      hipLaunchKernelGGL(gemm_bf16_nt_256_pingpong3_bal_mb3, g, dim3(kThreads2), kPP6Lds, stream, a);
-    else if (mode == 7 || (mode == 6 && use_bal(K / BK, false)))
+    if (mode == 6 && use_bal(K / BK, false))
       DLBB_PP_LAUNCH(gemm_bf16_nt_256_pingpong3_bal, STAMP_GEMM_NT, g, a);
     else if (mode == 6)
       DLBB_PP_LAUNCH(gemm_bf16_nt_256_pingpong3, STAMP_GEMM_NT, g, a);
-    else if (mode == 3)
-      hipLaunchKernelGGL(gemm_bf16_nt_256_kernel<3>, g, b, 2 * kBuf2Bytes, stream, a);
-    else if (mode == 2)
-      hipLaunchKernelGGL(gemm_bf16_nt_256_kernel<2>, g, b, 2 * kBuf2Bytes, stream, a);
-    else if (mode == 1)
-      hipLaunchKernelGGL(gemm_bf16_nt_256_kernel<1>, g, b, 2 * kBuf2Bytes, stream, a);
     else
-      hipLaunchKernelGGL(gemm_bf16_nt_256_kernel<0>, g, b, 2 * kBuf2Bytes, stream, a);
+      hipLaunchKernelGGL(gemm_bf16_nt_256_deep, g, b, 2 * kBuf2Bytes, stream, a);
     return hipGetLastError();
   }
   const int64_t tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);

@@ -408,44 +408,11 @@ __global__ void __launch_bounds__(256) split_reduce_kernel(const float* __restri
 }
 
 // Round-4 form (A/B variant 0): 8 floats per thread, one slab per loop trip.
-template <int DTO>
-__global__ void __launch_bounds__(256) split_reduce8_kernel(const float* __restrict__ ws,
-                                                            void* __restrict__ out, int64_t n,
-                                                            void* __restrict__ outb, int64_t nb,
-                                                            int split, int accumulate) {
-  const int64_t nv = n / 8, nvb = nb / 8;
-  const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
-  for (int64_t v = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; v < nv + nvb;
-       v += stride) {
-    const bool is_b = v >= nv;
-    const float* src = is_b ? ws + split * n : ws;
-    const int64_t ld = is_b ? nb : n, vi = is_b ? v - nv : v;
-    void* dst = is_b ? outb : out;
-    float acc[8];
-    load8<DT_F32>(src, vi, acc);
-    for (int s = 1; s < split; ++s) {
-      float t[8];
-      load8<DT_F32>(src + static_cast<int64_t>(s) * ld, vi, t);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) acc[j] += t[j];
-    }
-    if (accumulate) {
-      float o[8];
-      load8<DTO>(dst, vi, o);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) acc[j] += o[j];
-    }
-    store8<DTO>(dst, vi, acc);
-  }
-}
 
-// split-reduce form (A/B: dlbb_split_reduce_set_variant): 0 = round-4 8-float form, 1 = all
-// slab loads in flight, non-temporal loads (default), 2 = all slab loads in flight, plain loads.
-// Isolated at the GPT-2 dW shapes all three run at 4.5-5.4 TB/s (11-18 us; v1 fastest by 2-5 %,
-// profiles/r05_kernels/split_reduce.jsonl): the 40-118 us seen inside the training step is
-// contention with the main stream's kernels, not the pass itself. The slabs are read once, so
-// v1's streaming loads also keep them from displacing the main stream's L2 lines.
-static int g_split_reduce_variant = 1;
+// split-reduce form: every slab load in flight, non-temporal loads. Round 5 measured it against
+// an 8-float form and plain loads: all three 4.5-5.4 TB/s at the GPT-2 dW shapes isolated
+// (11-18 us; this one fastest by 2-5 %, profiles/r05_kernels/split_reduce.jsonl); the slabs are
+// read once, so streaming loads also keep them from displacing the main stream's L2 lines.
 
 template <int DTO, bool NT>
 static void split_reduce_dispatch_v(const float* ws, void* out, int64_t n, void* outb, int64_t nb,
@@ -468,15 +435,7 @@ static void split_reduce_dispatch_v(const float* ws, void* out, int64_t n, void*
 template <int DTO>
 static void split_reduce_dispatch(const float* ws, void* out, int64_t n, void* outb, int64_t nb,
                                   int split, int accumulate, hipStream_t stream) {
-  if (g_split_reduce_variant == 0) {
-    const int g = stream_grid((n + nb) / 8, 256);
-    hipLaunchKernelGGL(split_reduce8_kernel<DTO>, dim3(g), dim3(256), 0, stream, ws, out, n, outb,
-                       nb, split, accumulate);
-  } else if (g_split_reduce_variant == 1) {
-    split_reduce_dispatch_v<DTO, true>(ws, out, n, outb, nb, split, accumulate, stream);
-  } else {
-    split_reduce_dispatch_v<DTO, false>(ws, out, n, outb, nb, split, accumulate, stream);
-  }
+  split_reduce_dispatch_v<DTO, true>(ws, out, n, outb, nb, split, accumulate, stream);
 }
 
 }  // namespace tn
@@ -489,14 +448,6 @@ static int g_wgrad_stages = 2;
 
 DLBB_API void dlbb_gemm_wgrad_set_stages(int nb) { g_wgrad_stages = nb >= 2 && nb <= 4 ? nb : 2; }
 
-// Minimum dynamic LDS per weight-gradient workgroup (bytes; 0 = what the tile needs). Raising it
-// caps how many of these workgroups one CU holds (48 KiB tiles: 3 per CU), so a CU keeps LDS free
-// for the compute stream's kernels that run beside this side-stream GEMM (A/B:
-// dlbb_gemm_wgrad_set_min_lds, DLBB_WGRAD_MIN_LDS_KB).
-static int g_wgrad_min_lds = 0;
-DLBB_API void dlbb_gemm_wgrad_set_min_lds(int bytes) {
-  g_wgrad_min_lds = bytes > 0 && bytes <= 160 * 1024 ? bytes : 0;
-}
 
 // dW[N][K] = A^T B with A = [M][lda] (N columns used), B = [M][ldb] (K columns used), bf16.
 // Requires M % 32 == 0, N % bn == 0, K % 128 == 0, lda/ldb % 8 == 0, 16-B aligned bases;
@@ -546,7 +497,7 @@ static int wgrad_launch(const void* A, int64_t lda, const void* B, int64_t ldb, 
   const int stages = g_wgrad_stages;
 #define WG_LAUNCH(BIASV, NBV, WMV, WJV)                                                     \
   hipLaunchKernelGGL((wgrad_kernel<BIASV, NBV, WMV, WJV>), grid, dim3(128 * (WMV)),        \
-                     std::max(NBV * ((WMV) / 2 + (WJV) / 4) * kTile, g_wgrad_min_lds), stream, a)
+                     NBV * ((WMV) / 2 + (WJV) / 4) * kTile, stream, a)
 #define WG_STAGES(BIASV, WMV, WJV)                \
   if (stages == 4) WG_LAUNCH(BIASV, 4, WMV, WJV); \
   else if (stages == 3) WG_LAUNCH(BIASV, 3, WMV, WJV); \
@@ -568,10 +519,6 @@ static int wgrad_launch(const void* A, int64_t lda, const void* B, int64_t ldb, 
   else
     split_reduce_dispatch<DT_F32>(ws, out, n, out_bias, nb, split, accumulate, stream);
   return hipGetLastError();
-}
-
-DLBB_API void dlbb_split_reduce_set_variant(int v) {
-  tn::g_split_reduce_variant = v >= 0 && v <= 2 ? v : 1;
 }
 
 // The weight-gradient split-K reduce alone (microbenchmarks): out[n] (+ outb[nb]) = sum of the

@@ -520,15 +520,11 @@ static inline int bwd_pipe_grid(int64_t rows, int wpb) {
   return static_cast<int>(g < 1 ? 1 : g);
 }
 
-static int g_ln_bwd_variant = 1;   // 0: wave-per-row-sequence kernel, 1: pipelined (A/B)
-
 template <int NV, int PDT>
 static hipError_t bwd_nv(const LnBwdArgs& a, int grid, hipStream_t s) {
-  if constexpr (NV <= 4) {
-    if (g_ln_bwd_variant != 0) {
-      hipLaunchKernelGGL((ln_bwd_pipe_kernel<NV, PDT, 8>), dim3(grid), dim3(512), 0, s, a);
-      return hipGetLastError();
-    }
+  if constexpr (NV <= 4) {        // the pipelined kernel (rows up to 1024 wide)
+    hipLaunchKernelGGL((ln_bwd_pipe_kernel<NV, PDT, 8>), dim3(grid), dim3(512), 0, s, a);
+    return hipGetLastError();
   }
   hipLaunchKernelGGL((ln_bwd_kernel<NV, PDT>), dim3(grid), dim3(256), 0, s, a);
   return hipGetLastError();
@@ -560,9 +556,6 @@ DLBB_API int dlbb_layernorm_bwd_grid(int64_t rows) {
   return static_cast<int>(g < 1 ? 1 : g);
 }
 
-// A/B switch of the backward kernel: 0 = wave-per-row-sequence, 1 = pipelined (default)
-DLBB_API void dlbb_layernorm_bwd_set_variant(int v) { g_ln_bwd_variant = v == 0 ? 0 : 1; }
-
 DLBB_API int dlbb_layernorm_bwd(const void* dy, const void* h, const void* gamma, int param_dtype,
                                 const float* mean, const float* rstd, const void* dres, void* dx,
                                 float* part_ws, void* dgamma, void* dbeta, int64_t rows,
@@ -570,7 +563,7 @@ DLBB_API int dlbb_layernorm_bwd(const void* dy, const void* h, const void* gamma
   if (rows <= 0) return hipSuccess;
   if (cols % 256 != 0) return hipErrorInvalidValue;
   // partial rows actually used (<= dlbb_layernorm_bwd_grid(rows), the caller's ws size)
-  const int grid = g_ln_bwd_variant != 0 && cols <= 1024 ? bwd_pipe_grid(rows, 8)
+  const int grid = cols <= 1024 ? bwd_pipe_grid(rows, 8)
                                                          : dlbb_layernorm_bwd_grid(rows);
   float* pg = part_ws;
   float* pb = dbeta ? part_ws + static_cast<int64_t>(grid) * cols : nullptr;

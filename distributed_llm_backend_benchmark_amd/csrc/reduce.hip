@@ -23,10 +23,12 @@ struct ReduceArgs {
   uint64_t* stamps;  // per-workgroup start/end records (diagnostic), usually null
 };
 
-// NS > 0: the source count is a template constant and every source's 16-byte vector of an item
-// is loaded before the first add (NS loads in flight per lane; A/B: dlbb_reduce_set_variant(1));
-// NS == 0: runtime count, one source per loop trip (the default).
-template <int DTI, int DTO, int NS>
+// Runtime source count, one source per loop trip. Round 5 measured a templated count with every
+// source's load in flight equal within noise (1-3 % behind), round 6 block-contiguous tiles of
+// 1-4 vectors per lane with and without non-temporal source loads: within +-10 % of this at
+// 64 MiB-1 GiB in both directions (profiles/r06_kernels/memroof_variants.jsonl) — the hardware
+// already overlaps the loop trips' loads.
+template <int DTI, int DTO>
 __global__ void __launch_bounds__(256) reduce_sum_kernel(ReduceArgs a) {
   uint64_t t0 = 0;
   if (a.stamps) t0 = stamp_now();
@@ -35,24 +37,12 @@ __global__ void __launch_bounds__(256) reduce_sum_kernel(ReduceArgs a) {
   for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < nvec;
        i += stride) {
     float acc[8];
-    if constexpr (NS > 0) {
-      float v[NS][8];
+    load8<DTI>(a.src[0], i, acc);
+    for (int s = 1; s < a.nsrc; ++s) {
+      float v[8];
+      load8<DTI>(a.src[s], i, v);
 #pragma unroll
-      for (int s = 0; s < NS; ++s) load8<DTI>(a.src[s], i, v[s]);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) acc[j] = v[0][j];
-#pragma unroll
-      for (int s = 1; s < NS; ++s)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) acc[j] += v[s][j];
-    } else {
-      load8<DTI>(a.src[0], i, acc);
-      for (int s = 1; s < a.nsrc; ++s) {
-        float v[8];
-        load8<DTI>(a.src[s], i, v);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) acc[j] += v[j];
-      }
+      for (int j = 0; j < 8; ++j) acc[j] += v[j];
     }
     if (a.scale != 1.0f) {
 #pragma unroll
@@ -106,27 +96,11 @@ uint64_t* stamp_acquire(int kind, int64_t nrec) {
   return p;
 }
 
-// 0 (default): runtime source count; 1: templated counts 2/3/4/8 with every source's load in
-// flight. Measured equal within noise, the runtime loop 1-3 % ahead at 64 MiB-1 GiB x 8 sources
-// (profiles/r05_kernels/memroof_pass2.jsonl, memroof_rocprof_kernel_stats.csv: 100.1 vs 101.7 us
-// average): the hardware already overlaps the loop trips' loads, unlike the split-K reduce's.
-static int g_reduce_variant = 0;
-
 template <int DTI, int DTO>
 static hipError_t launch_reduce(const ReduceArgs& a, int nblocks, hipStream_t s) {
   const int block = 256;
   const int grid = nblocks > 0 ? nblocks : stream_grid((a.n + 7) / 8, block);
-  const int ns = g_reduce_variant ? a.nsrc : 0;
-#define DLBB_RN(NSV)                                                                     \
-  case NSV:                                                                              \
-    hipLaunchKernelGGL((reduce_sum_kernel<DTI, DTO, NSV>), dim3(grid), dim3(block), 0, s, a); \
-    break;
-  switch (ns) {
-    DLBB_RN(2) DLBB_RN(3) DLBB_RN(4) DLBB_RN(8)
-    default:
-      hipLaunchKernelGGL((reduce_sum_kernel<DTI, DTO, 0>), dim3(grid), dim3(block), 0, s, a);
-  }
-#undef DLBB_RN
+  hipLaunchKernelGGL((reduce_sum_kernel<DTI, DTO>), dim3(grid), dim3(block), 0, s, a);
   return hipGetLastError();
 }
 
@@ -158,8 +132,6 @@ DLBB_API int dlbb_reduce_sum_grid(const void* const* srcs, int nsrc, void* dst, 
 #undef DLBB_R
   return hipErrorInvalidValue;
 }
-
-DLBB_API void dlbb_reduce_set_variant(int v) { g_reduce_variant = v ? 1 : 0; }
 
 DLBB_API int dlbb_reduce_sum(const void* const* srcs, int nsrc, void* dst, int64_t n,
                              int dtype_in, int dtype_out, float scale, hipStream_t stream) {

@@ -110,9 +110,6 @@ class GPT2(nn.Module):
         if self._fused_embedding:
             self.wpe._dlbb_single_use = True
             self.wte._dlbb_sink_uses = 2
-            # its second use (the embedding backward) adds only to the rows of the input ids:
-            # a trainer may update the other rows right after the LM-head backward
-            self.wte._dlbb_rows_from_input = True
         self.blocks = nn.ModuleList([Block(cfg, device, gen) for _ in range(cfg.n_layer)])
         self.ln_f = LN(cfg.n_embd, device)
 

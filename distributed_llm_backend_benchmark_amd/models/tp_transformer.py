@@ -12,7 +12,8 @@ reference; ``init_std`` lets callers scale them).
 MI355X-specific: all compute on-device in bf16 through the gfx950 kernels (MFMA GEMM with fused
 GELU, fused residual+LayerNorm); the residual add of each sublayer is fused into the NEXT
 LayerNorm, so the block is ``LN1 → QKV → out-proj → AR → (add+LN2) → up+GELU → down → AR →
-(add+LN1 of the next block)``. ``attention="sdpa"`` swaps the stub for real causal attention.
+(add+LN1 of the next block)``. ``attention="sdpa"`` swaps the stub for real causal attention
+(torch SDPA), ``attention="flash"`` for our causal flash kernel (``ops.causal_attention``).
 ``overlap_chunks`` > 1 interleaves micro-batches so the all-reduces run under GEMMs (forward()).
 """
 
@@ -93,6 +94,10 @@ class TransformerBlock(nn.Module):
         B, S, _ = qkv.shape
         heads = self.num_heads // self.P
         hd = hpr // heads
+        if self.attention == "flash" and self.kernels != "torch":
+            # our causal flash kernel (csrc/attention.hip, head dim 64 / 128) straight on the
+            # rank's fused [B, S, 3, heads, hd] QKV shard — no unbind / transpose copies
+            return ops.causal_attention(qkv, heads)
         q, k, v = qkv.view(B, S, 3, heads, hd).permute(2, 0, 3, 1, 4).unbind(0)
         o = F.scaled_dot_product_attention(q, k, v, is_causal=True)
         return o.transpose(1, 2).reshape(B, S, hpr)
@@ -185,8 +190,8 @@ class LLM(nn.Module):
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         """Plain: one pass, each all-reduce inline. Overlapped (``overlap_chunks`` = n > 1): the
         batch is split into n micro-batches run round-robin, each advancing to its next
-        all-reduce; the all-reduce goes to a side comm stream (normal priority — see
-        parallel/ddp.comm_stream_priority) and the micro-batch resumes only after its compute
+        all-reduce; the all-reduce goes to a side comm stream (normal priority: a high-priority one stretches
+        every compute dispatch, profiles/r03_overlap) and the micro-batch resumes only after its compute
         stream waited for it. So all-reduce k of micro-batch A runs under the GEMMs of
         micro-batch B, and every rank issues its collectives in the same order on one comm
         stream. The reference blocks on each all-reduce (models.py:95)."""

@@ -41,7 +41,6 @@ _SIGS = {
     "dlbb_stamps_entry": (c_int, [c_int64, ctypes.POINTER(c_int), ctypes.POINTER(c_int64),
                                   ctypes.POINTER(c_int64)]),
     "dlbb_cast": (c_int, [c_void_p, c_int, c_void_p, c_int, c_int64, c_void_p]),
-    "dlbb_cast_set_variant": (None, [c_int]),
     "dlbb_pack_rows": (c_int, [c_void_p, c_int, c_int64, c_void_p, c_int, c_int64, c_int64,
                                c_int64, c_void_p]),
     "dlbb_chunk_copy": (c_int, [c_void_p, c_int64, c_void_p]),
@@ -52,7 +51,6 @@ _SIGS = {
                                    c_void_p, c_void_p, c_void_p, c_int64, c_int, c_float,
                                    c_void_p]),
     "dlbb_layernorm_bwd_grid": (c_int, [c_int64]),
-    "dlbb_layernorm_bwd_set_variant": (None, [c_int]),
     "dlbb_layernorm_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p,
                                    c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64,
                                    c_int, c_int, c_void_p]),
@@ -83,20 +81,12 @@ _SIGS = {
     "dlbb_gemm_set_stagger": (None, [c_int]),
     "dlbb_gemm_get_stagger": (c_int, []),
     "dlbb_gemm_set_bal": (None, [c_int]),
-    "dlbb_gemm_set_spread_early": (None, [c_int]),
-    "dlbb_gemm_set_group_m": (None, [c_int]),
-    "dlbb_gemm_set_diag_nostore": (None, [c_int]),
     "dlbb_gemm_set_persist_epi": (None, [c_int]),
     "dlbb_gemm_set_concurrent": (None, [c_int]),
     "dlbb_gemm_get_concurrent": (c_int, []),
     "dlbb_gemm_wgrad_set_stages": (None, [c_int]),
     "dlbb_attn_set_xcd": (None, [c_int]),
-    "dlbb_attn_set_concurrent": (None, [c_int]),
     "dlbb_xent_set_variant": (None, [c_int]),
-    "dlbb_adamw_set_nt": (None, [c_int]),
-    "dlbb_adamw_rows": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p,
-                                c_int64, c_float, c_float, c_float, c_float, c_float, c_int,
-                                c_void_p, c_float, c_void_p, c_int64, c_int, c_void_p]),
     "dlbb_xent_count_inv": (c_int, [c_void_p, c_int64, c_void_p, c_void_p]),
     "dlbb_xent_loss_mean": (c_int, [c_void_p, c_int64, c_void_p, c_void_p, c_void_p]),
     "dlbb_xent_fused": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int64,
@@ -124,18 +114,8 @@ _SIGS = {
                                       c_int, c_int, c_void_p, c_int, c_void_p]),
     "dlbb_gemm_wgrad_counters": (c_int, [c_int, c_int, c_int, c_int]),
     "dlbb_gemm_wgrad_set_order": (None, [c_int]),
-    "dlbb_split_reduce_set_variant": (None, [c_int]),
-    "dlbb_reduce_set_variant": (None, [c_int]),
     "dlbb_sort_ids": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int, c_void_p]),
-    "dlbb_attn_set_fuse_delta": (None, [c_int]),
-    "dlbb_stream_create_cu_share": (c_int, [c_int, c_int, c_int, c_void_p, c_void_p]),
-    "dlbb_stream_cu_count": (c_int, [c_void_p, c_int]),
     "dlbb_stream_fork": (c_int, [c_void_p, c_void_p, c_int]),
-    "dlbb_gemm_wgrad_set_min_lds": (None, [c_int]),
-    "dlbb_attn_set_fwd_variant": (None, [c_int]),
-    "dlbb_attn_get_fwd_variant": (c_int, []),
-    "dlbb_attn_set_bwd_incr": (None, [c_int]),
-    "dlbb_attn_get_bwd_incr": (c_int, []),
     "dlbb_split_reduce": (c_int, [c_void_p, c_void_p, c_int, c_int64, c_void_p, c_int64, c_int,
                                   c_int, c_void_p]),
     "dlbb_embedding_fwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int, c_int,
@@ -213,20 +193,6 @@ def _load() -> ctypes.CDLL:
                 fn = getattr(lib, name)
                 fn.restype = res
                 fn.argtypes = args
-            # A/B kernel variants selectable per process from the environment
-            for env, setter in (("DLBB_LN_BWD_VARIANT", "dlbb_layernorm_bwd_set_variant"),
-                                ("DLBB_CAST_VARIANT", "dlbb_cast_set_variant"),
-                                ("DLBB_WGRAD_ORDER", "dlbb_gemm_wgrad_set_order"),
-                                ("DLBB_CHUNK_NT", "dlbb_chunk_copy_set_nt"),
-                                ("DLBB_SPLIT_REDUCE_VARIANT", "dlbb_split_reduce_set_variant"),
-                                ("DLBB_ATTN_FUSE_DELTA", "dlbb_attn_set_fuse_delta"),
-                                ("DLBB_ATTN_FWD_VARIANT", "dlbb_attn_set_fwd_variant"),
-                                ("DLBB_ATTN_BWD_INCR", "dlbb_attn_set_bwd_incr"),
-                                ("DLBB_ADAMW_NT", "dlbb_adamw_set_nt")):
-                if os.environ.get(env, "") != "":
-                    getattr(lib, setter)(int(os.environ[env]))
-            if os.environ.get("DLBB_WGRAD_MIN_LDS_KB", "") != "":
-                lib.dlbb_gemm_wgrad_set_min_lds(int(float(os.environ["DLBB_WGRAD_MIN_LDS_KB"]) * 1024))
             _lib = lib
             return lib
         except BaseException as e:  # remember and re-raise loudly on every use

@@ -1,12 +1,14 @@
 """Causal self-attention on the fused QKV activation (``csrc/attention.hip``).
 
-``causal_attention(qkv, n_head)`` takes GPT-2's fused ``[B, T, 3C]`` QKV GEMM output and returns
-``[B, T, C]`` (heads interleaved, ready for the projection GEMM). The forward is our gfx950
-flash kernel (head dim 64); it reads Q/K/V straight out of ``qkv`` — no unbind/transpose copies
-— and emits the per-row log-sum-exp. The backward is ours too (delta = rowsum(dO * O), then a
-key-block kernel for dK/dV and a query-block kernel for dQ, no atomics), writing the fused
-``[B, T, 3C]`` gradient directly. ``attn_bwd_library`` (the stack's flash backward on our
-forward's O / LSE — same natural-log ``[B, H, T]`` convention) is kept as the A/B baseline.
+``causal_attention(qkv, n_head)`` takes a fused ``[B, T, 3C]`` QKV GEMM output (GPT-2's, or a
+tensor-parallel rank's shard, models/tp_transformer.py) and returns ``[B, T, C]`` (heads
+interleaved, ready for the projection GEMM). The forward is our gfx950 flash kernel (head dim 64
+or 128); it reads Q/K/V straight out of ``qkv`` — no unbind/transpose copies — and emits the
+per-row log-sum-exp. The backward (head dim 64) is ours too (a query-block kernel for dQ that
+also writes the row constants, then a key-block kernel for dK/dV, no atomics), writing the fused
+``[B, T, 3C]`` gradient directly. At head dim 128 the backward is the stack's flash backward on
+our forward's O / LSE (``attn_bwd_library``: same natural-log ``[B, H, T]`` convention; no
+training path here uses it — the TP model is forward only).
 
 Other head dims, CPU tensors and ``DLBB_KERNELS=torch`` use ``F.scaled_dot_product_attention``.
 """
@@ -36,10 +38,14 @@ def _torch_attention(qkv: torch.Tensor, n_head: int) -> torch.Tensor:
     return y.transpose(1, 2).reshape(B, T, C3 // 3)
 
 
+HEAD_DIMS = (64, 128)
+
+
 def hip_supported(qkv: torch.Tensor, n_head: int) -> bool:
     if qkv.dim() != 3 or qkv.dtype != torch.bfloat16 or not qkv.is_contiguous():
         return False
-    return (qkv.shape[2] // 3) // n_head == 64 and qkv.shape[2] % 3 == 0
+    C = qkv.shape[2] // 3
+    return qkv.shape[2] % 3 == 0 and C % n_head == 0 and C // n_head in HEAD_DIMS
 
 
 def attn_fwd(qkv: torch.Tensor, n_head: int):
@@ -66,6 +72,8 @@ class _CausalAttention(torch.autograd.Function):
     @staticmethod
     def backward(ctx, gout):
         qkv, out, lse = ctx.saved_tensors
+        if (qkv.shape[2] // 3) // ctx.n_head != 64:
+            return attn_bwd_library(qkv, out, lse, gout.contiguous(), ctx.n_head), None
         return attn_bwd(qkv, out, lse, gout, ctx.n_head), None
 
 
@@ -87,7 +95,7 @@ def attn_bwd(qkv: torch.Tensor, out: torch.Tensor, lse: torch.Tensor, gout: torc
 
 def attn_bwd_library(qkv, out, lse, gout, n_head: int) -> torch.Tensor:
     """The stack's flash backward on our forward's (O, LSE), dQ/dK/dV packed into [B, T, 3C]
-    (A/B baseline for :func:`attn_bwd`)."""
+    (head dim 128, and the A/B baseline for :func:`attn_bwd`)."""
     B, T, C3 = qkv.shape
     C = C3 // 3
     D = C // n_head

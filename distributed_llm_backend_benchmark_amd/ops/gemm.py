@@ -48,10 +48,7 @@ def set_tune_agreement(fn) -> None:
 # env knobs that change which candidates exist or how they run: part of every agreed name, so
 # ranks started with different settings fail at the first tuned shape instead of "agreeing" on
 # timings of different kernels
-_AGREED_ENV = ("DLBB_GEMM", "DLBB_TUNE_TIMING", "DLBB_WGRAD256", "DLBB_PP_TAIL",
-               "DLBB_WGRAD_FUSED", "DLBB_GEMM_PERSIST", "DLBB_GEMM_PERSIST_EPI",
-               "DLBB_WGRAD_STREAM", "DLBB_WGRAD_SLOTS", "DLBB_WGRAD_IMPL",
-               "DLBB_WGRAD_MIN_LDS_KB")
+_AGREED_ENV = ("DLBB_GEMM", "DLBB_TUNE_TIMING", "DLBB_WGRAD_STREAM")
 
 
 def _agree_names(kind: str, key, names) -> list:
@@ -166,29 +163,25 @@ def set_tile(tile: int) -> None:
 
 
 def set_stagger(mode: int) -> None:
-    """256^2 kernel schedule: 0 lock-step, 1 staggered wave rows, 2 staggered + next tile
-    issued at phase 1, 3 staggered + deep restaging (one K-tile in flight), 4 = 3 as a
-    persistent kernel (next tile's prologue overlaps this tile's epilogue), 6 ping-pong (the
-    two waves of each SIMD alternate whole-K-tile MFMA clusters and fragment loads, 160 KiB of
-    LDS; M % 8 == 0 and N % 64 == 0, else 3 — the default; balanced DMA issue per
-    :func:`set_bal`), 7 ping-pong with the balanced DMA issue forced, 11 = 7 with wave row 0's B
-    DMA issued inside its MFMA phase (NT only). For A/B benchmarking; the
-    library default is the measured fastest (profiles/r02_gemm)."""
+    """256^2 NT schedule: 6 = the ping-pong (default; upgraded to its persistent form on
+    multi-round grids with a lean epilogue), 10 = the persistent ping-pong wherever its contract
+    holds, 3 = the deep-pipeline kernel (the general-contract fallback) forced. The balanced DMA
+    issue of the ping-pong is :func:`set_bal`. Other round-1..5 schedules were removed in round 6
+    (never the fastest; profiles/r0*_gemm)."""
     _lib.lib().dlbb_gemm_set_stagger(int(mode))
 
 
 def set_bal(mode: int) -> None:
     """Balanced LDS-DMA issue of the ping-pong kernels (NT forward and NN dgrad): 0 never,
-    1 always (``set_stagger(7)`` forces it for NT), 2 = always for NN and for NT when
+    1 always, 2 = always for NN and for NT when
     K >= 2048 (default, measured: profiles/r02_gemm)."""
     _lib.lib().dlbb_gemm_set_bal(int(mode))
 
 
 def set_persist_epi(on: bool) -> None:
     """Persistent forms with lean epilogues on multi-round short-K grids: NT bias / bias-GELU
-    (+ pre-activation) and NN plain / GELU backward (default on; ``DLBB_GEMM_PERSIST_EPI=0`` or
-    ``set_persist_epi(False)`` keeps them on the non-persistent ping-pong; the NT plain form
-    follows ``DLBB_GEMM_PERSIST``)."""
+    (+ pre-activation) and NN plain / GELU backward (default on; ``set_persist_epi(False)``
+    keeps them on the non-persistent ping-pong; the NT plain form is picked by the autotuner)."""
     _lib.lib().dlbb_gemm_set_persist_epi(int(bool(on)))
 
 
@@ -494,16 +487,20 @@ def wgrad_supported(dy2: torch.Tensor, x2: torch.Tensor) -> bool:
 
 
 _COUNTERS = {}   # (device index, stream handle) -> int32 tile counters, zero between launches
-_WGRAD_SLOTS_SCALE = float(os.environ.get("DLBB_WGRAD_SLOTS", "1.0"))
+# In-launch split-K combine of the weight-gradient kernel (each tile's last-arriving workgroup
+# sums the fp32 slabs). OFF: measured 1.3-2.3x SLOWER than the separate reduce pass at every
+# GPT-2 dW shape (profiles/r05_wgrad): a tile's slabs are split x 64 KiB (0.4-1.4 MB), read
+# serially by ONE workgroup at ~0.1 TB/s, far past the "few tens of KB per tile" where an
+# in-launch combine pays (CDNA guide §5). Kept as a tested form (set_wgrad_fused) for A/B.
+_WGRAD_FUSED = [False]
+
+
+def set_wgrad_fused(on: bool) -> None:
+    _WGRAD_FUSED[0] = bool(on)
 
 
 def wgrad_fused_reduce() -> bool:
-    """In-launch split-K combine of the weight-gradient kernel (each tile's last-arriving
-    workgroup sums the fp32 slabs; ``DLBB_WGRAD_FUSED=1``). OFF by default: measured 1.3-2.3x
-    SLOWER than the separate reduce pass at every GPT-2 dW shape (profiles/r05_wgrad): a tile's
-    slabs are split x 64 KiB (0.4-1.4 MB), read serially by ONE workgroup at ~0.1 TB/s, i.e.
-    far past the "few tens of KB per tile" where an in-launch combine pays (CDNA guide §5)."""
-    return os.environ.get("DLBB_WGRAD_FUSED", "0") == "1"
+    return _WGRAD_FUSED[0]
 
 
 def _tile_counters(device: torch.device, n: int) -> torch.Tensor:
@@ -529,13 +526,8 @@ def _wgrad_hip(dy2, x2, out, accumulate, split=None, bias_out=None, bn=128, bk=1
         # (profiles/r01_gpt2/wgrad_split_xcd.jsonl)
         # (two-per-CU tiles: at most the 512 resident slots — a 2nd partial round costs a
         # whole workgroup time)
-        # DLBB_WGRAD_SLOTS scales the workgroup budget (A/B: the weight gradients run on the
-        # side stream beside the main stream's kernels, where fewer, longer workgroups may
-        # leave more of the GPU to the critical path; round-5 asm reads made long K-loops
-        # 25-30 % cheaper per workgroup)
-        slots = _WGRAD_SLOTS_SCALE
-        split = max(1, min(M // 256, (-(-int(768 * slots) // tiles)) if bn == bk == 128
-                           else max(1, int(512 * slots) // tiles)))
+        split = max(1, min(M // 256, (-(-768 // tiles)) if bn == bk == 128
+                           else max(1, 512 // tiles)))
     # one split, plain store, no bias: the kernel stores dW itself (no fp32 partials, no
     # reduce pass — the LM-head dW)
     direct = split == 1 and not accumulate and bias_out is None
@@ -623,7 +615,7 @@ def _wgrad_pp(dy2, x2, out, accumulate, split=None, bias_out=None):
     M, N = dy2.shape
     K = x2.shape[1]
     head, tsplit = (N, 1)
-    if not accumulate and os.environ.get("DLBB_PP_TAIL", "1") != "0":
+    if not accumulate:
         ncu = torch.cuda.get_device_properties(dy2.device).multi_processor_count
         head, tsplit = pp_tail_plan(M, N, K, ncu)
     _pp_launch(dy2, x2, out, accumulate, 0, head, 1)
@@ -631,8 +623,8 @@ def _wgrad_pp(dy2, x2, out, accumulate, split=None, bias_out=None):
         _pp_launch(dy2, x2, out, accumulate, head, N, tsplit)
     if bias_out is not None:            # no fused bias on this kernel: one column-sum pass
         db = dy2.sum(0, dtype=torch.float32)
-        if accumulate:
-            bias_out.add_(db.to(bias_out.dtype))
+        if accumulate:                  # fp32 add, one rounding (as the fused kernels)
+            bias_out.copy_((bias_out.float() + db).to(bias_out.dtype))
         else:
             bias_out.copy_(db)
 
@@ -660,14 +652,6 @@ _WGRAD_IMPLS = {"mfma": _wgrad_hip, "mfma256": _wgrad_hip256, "mfma_wide": _wgra
 
 
 def _wgrad_choice(dy2, x2, out, bias_out=None) -> str:
-    forced = os.environ.get("DLBB_WGRAD_IMPL", "").lower()   # A/B: weight gradients only
-    if forced in _WGRAD_IMPLS:
-        if forced == "pp" and not wgrad_pp_supported(dy2, x2, out, False, bias_out):
-            return "mfma"
-        if (forced == "mfma256" and dy2.shape[1] % 256) or (forced == "mfma_wide" and
-                                                             x2.shape[1] % 256):
-            return "mfma"
-        return forced
     mode = os.environ.get("DLBB_GEMM", "auto").lower()
     if mode in _WGRAD_IMPLS:
         if mode == "pp" and not wgrad_pp_supported(dy2, x2, out, False, bias_out):
@@ -685,7 +669,7 @@ def _wgrad_choice(dy2, x2, out, bias_out=None) -> str:
     scratch_b = torch.empty_like(bias_out) if bias_out is not None else None
     cands = {}
     for name, fn in _WGRAD_IMPLS.items():
-        if name == "mfma256" and (dy2.shape[1] % 256 or os.environ.get("DLBB_WGRAD256") == "0"):
+        if name == "mfma256" and dy2.shape[1] % 256:
             continue
         if name == "mfma_wide" and x2.shape[1] % 256:
             continue

@@ -207,9 +207,6 @@ def sink_used(p: torch.Tensor) -> None:
         p._dlbb_grad_sink(p)
     else:
         p._dlbb_sink_count = n
-        partial = getattr(p, "_dlbb_partial_sink", None)   # trainer opt-in (parallel/ddp.py)
-        if partial is not None:
-            partial(p, n)
 
 
 def linear_train(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor] = None,

@@ -37,12 +37,10 @@ class FlatAdamW:
 
     @torch.no_grad()
     def step(self, grad: torch.Tensor, working_bf16: Optional[torch.Tensor] = None,
-             grad_scale: float = 1.0, ranges=None, advance: bool = True, rows=None) -> None:
+             grad_scale: float = 1.0, ranges=None, advance: bool = True) -> None:
         """One AdamW update. ``ranges``: update only these [start, end) element ranges (one
         kernel each; the rest of the step's ranges follow in later calls with
-        ``advance=False``, so the step count — and the bias correction — moves once).
-        ``rows = (mask, row_len, sel)``: each range is a [rows, row_len] table and only its rows
-        r with ``mask[r] == sel`` are updated (uint8 mask on the device; HIP path only)."""
+        ``advance=False``, so the step count — and the bias correction — moves once)."""
         if grad.numel() != self.p.numel():
             raise ValueError("grad / master size mismatch")
         if advance:
@@ -58,16 +56,7 @@ class FlatAdamW:
                 continue
             p, m, v, g = self.p[a:e], self.m[a:e], self.v[a:e], grad[a:e]
             w = working_bf16[a:e] if working_bf16 is not None else None
-            if rows is not None:
-                mask, row_len, sel = rows
-                if not use_hip(self.p, grad):
-                    raise ValueError("row-filtered AdamW runs on the HIP path only")
-                check(_lib.lib().dlbb_adamw_rows(
-                    p.data_ptr(), m.data_ptr(), v.data_ptr(), g.data_ptr(), dt(grad), _lib.ptr(w),
-                    e - a, self.lr, b1, b2, self.eps, self.wd, self.t, _lib.ptr(self.t_dev),
-                    float(grad_scale), mask.data_ptr(), int(row_len), int(sel),
-                    _lib.stream(self.p.device)), "adamw_rows")
-            elif use_hip(self.p, grad) and self.t_dev is not None:
+            if use_hip(self.p, grad) and self.t_dev is not None:
                 check(_lib.lib().dlbb_adamw_devstep(
                     p.data_ptr(), m.data_ptr(), v.data_ptr(), g.data_ptr(), dt(grad),
                     _lib.ptr(w), e - a, self.lr, b1, b2, self.eps, self.wd,

@@ -42,37 +42,18 @@ from ..ops.elementwise import ChunkTable, ScaleTable, reduce_sum, spin_ns
 from ..ops.xent import mark_unit_upstream
 from ..utils import tracing
 from .comm import Comm
-from .streams import concurrent_stream, cu_share_stream, fork, runs_concurrently
+from .streams import concurrent_stream, fork, runs_concurrently
 
-_GRAD_SINKS = os.environ.get("DLBB_GRAD_SINKS", "1") != "0"   # A/B switch for the sinks
 # sink dW GEMMs on a side stream (default on; DLBB_WGRAD_STREAM=0 for the A/B). Rounds 1-2
 # measured +4 % step time on GPT-2 with a pool stream; since the side streams are chosen by the
 # concurrency probe (parallel/streams.py: a pool stream could share the compute stream's
 # hardware queue) the weight gradients fill the CUs the 192-tile dgrad grids leave idle: 19.30 ->
 # 18.90 ms, and 19.17 -> 18.58 ms with the interleaved autotune timing
-# (profiles/r03_lean/tune_ab)
+# (profiles/r03_lean/tune_ab). Not adopted and removed in round 6: several
+# weight-gradient streams, CU-masked side streams (2.7-3x slower), side / comm stream
+# priorities (high-priority comm stretched every dispatch, profiles/r03_overlap), the early
+# AdamW of untouched embedding rows (no gain, profiles/r05_step §11).
 _WGRAD_STREAM = os.environ.get("DLBB_WGRAD_STREAM", "1") == "1"
-# number of side streams the weight gradients are dealt over, round-robin by parameter (A/B;
-# with k > 1 a weight-gradient kernel depends only on its dY and on the one k layers back)
-_WGRAD_STREAMS = max(1, int(os.environ.get("DLBB_WGRAD_STREAMS", "1")))
-# "num/den": the weight-gradient side stream(s) run on that share of every XCD's CUs (hardware CU
-# mask, parallel/streams.py cu_share_stream), leaving the rest to the critical path (A/B)
-_WGRAD_CU_SHARE = os.environ.get("DLBB_WGRAD_CU_SHARE", "")
-# HIP priority of the weight-gradient side stream(s): 0 = normal (default), 1 = low (where the
-# runtime offers it), -1 = high (A/B)
-_WGRAD_PRIORITY = int(os.environ.get("DLBB_WGRAD_STREAM_PRIORITY", "0"))
-# priority of the dedicated bucket-reduction stream: 0 = normal (default, measured), -1 = high
-# (A/B knob; see the module docstring and profiles/r02_overlap/SUMMARY.md)
-_COMM_PRIORITY = int(os.environ.get("DLBB_COMM_STREAM_PRIORITY", "0"))
-# mark the model's loss as the backward root (ops.xent.mark_unit_upstream; A/B: 0 = off)
-_UNIT_UPSTREAM = os.environ.get("DLBB_UNIT_UPSTREAM", "1") != "0"
-# world 1, overlapped optimizer: the rows of a tied embedding / LM-head table that this step's
-# input ids do not touch have their final gradient after the LM-head backward (the embedding
-# backward adds only to the input ids' rows): their AdamW runs then, during backward, and only
-# the touched rows stay behind the embedding backward. Bit-exact, but measured no faster on the
-# GPT-2 step (17.30-17.42 vs 17.29-17.32 ms, profiles/r05_step/SUMMARY.md §11): off by default
-# (DLBB_EARLY_ROWS=1 enables it)
-_EARLY_ROWS = os.environ.get("DLBB_EARLY_ROWS", "0") == "1"
 # split optimizer only: AdamW of a head bucket is issued as soon as that bucket is reduced,
 # during backward, on a stream of its own (1) or on the weight-gradient side stream (2, default),
 # instead of for all head buckets after backward (0). GPT-2 step, three interleaved reps in one
@@ -83,25 +64,6 @@ _EARLY_ROWS = os.environ.get("DLBB_EARLY_ROWS", "0") == "1"
 # bucket's all-reduce (the AdamW range waits for it on that stream), and mode 1 is unmeasured
 # across GPUs.
 _OPT_OVERLAP = os.environ.get("DLBB_OPT_OVERLAP")
-
-
-def comm_stream_priority() -> int:
-    """Priority of the bucket-reduction stream, FENCED to normal. Per-workgroup stamps of the
-    trap (profiles/r03_overlap/SUMMARY.md): with the comm stream at high priority, from the
-    first bucket reduction on every kernel launch of the step — compute and comm queue alike —
-    spreads its workgroup starts over 25-38 us instead of ~1 us (workgroup run times unchanged),
-    ~+30 us per launch, +10 ms per GPT-2 step; intermittent, absent under a profiler's kernel
-    trace. A dispatch (queue-arbitration) effect, not CU contention, so a CU mask or grid cap
-    would not fence it: high priority needs DLBB_ALLOW_HIGH_PRIO_COMM=1."""
-    p = _COMM_PRIORITY
-    if p < 0 and os.environ.get("DLBB_ALLOW_HIGH_PRIO_COMM") != "1":
-        import warnings
-
-        warnings.warn("DLBB_COMM_STREAM_PRIORITY < 0 ignored: high-priority comm streams "
-                      "stretch every kernel dispatch (profiles/r03_overlap/SUMMARY.md); set "
-                      "DLBB_ALLOW_HIGH_PRIO_COMM=1 to force it", RuntimeWarning, stacklevel=2)
-        return 0
-    return p
 _ALIGN = 64  # elements: keeps every param view 128-B aligned (16-B MFMA/glds rows)
 
 
@@ -185,19 +147,9 @@ class FlatParamTrainer:
         self._params = order
         # weight-gradient GEMMs of sink params run on this side stream (off the backward's
         # critical path); bucket reductions and the optimizer are ordered after it
-        side_ok = mode == "view" and dev.type == "cuda" and _GRAD_SINKS and _WGRAD_STREAM
-        if side_ok and _WGRAD_CU_SHARE:
-            num, den = (int(v) for v in _WGRAD_CU_SHARE.split("/"))
-            self._wgrad_streams = [cu_share_stream(dev, f"ddp_wgrad{i}", num, den)
-                                   for i in range(_WGRAD_STREAMS)]
-            self._wgrad_stream = self._wgrad_streams[0]
-        else:
-            self._wgrad_stream = (concurrent_stream(dev, "ddp_wgrad", _WGRAD_PRIORITY)
-                                  if side_ok else None)
-            self._wgrad_streams = ([self._wgrad_stream] + [
-                concurrent_stream(dev, f"ddp_wgrad{i}", _WGRAD_PRIORITY)
-                for i in range(1, _WGRAD_STREAMS)]
-                if self._wgrad_stream is not None else [])
+        side_ok = mode == "view" and dev.type == "cuda" and _WGRAD_STREAM
+        self._wgrad_stream = concurrent_stream(dev, "ddp_wgrad") if side_ok else None
+        self._wgrad_streams = [self._wgrad_stream] if self._wgrad_stream is not None else []
         n_sink = 0
         if mode == "view":
             for p, o in zip(order, offs):
@@ -207,7 +159,7 @@ class FlatParamTrainer:
                 # (a param used n > 1 times per step opts in with _dlbb_sink_uses = n, e.g. a
                 # tied embedding / LM head: ready after its last use, ops.linear_fn.sink_used)
                 if (getattr(p, "_dlbb_single_use", False)
-                        or getattr(p, "_dlbb_sink_uses", 0) > 0) and _GRAD_SINKS:
+                        or getattr(p, "_dlbb_sink_uses", 0) > 0):
                     p._dlbb_grad_sink = self._on_grad
                     if self._wgrad_stream is not None:
                         p._dlbb_grad_stream = self._wgrad_streams[n_sink % len(
@@ -224,7 +176,7 @@ class FlatParamTrainer:
             from .custom_allreduce import get_custom_allreduce
 
             self._car = get_custom_allreduce(comm)
-            self._comm_stream = concurrent_stream(dev, "ddp_comm", comm_stream_priority())
+            self._comm_stream = concurrent_stream(dev, "ddp_comm", 0)
             # buckets are fixed slices of flat_grad: IPC-map them once, then every bucket
             # all-reduce is the in-place two-shot (no staging copy, no capacity limit)
             if self._car is not None and self._car.reg_healthy:
@@ -236,7 +188,7 @@ class FlatParamTrainer:
             from .rccl_native import get_native
 
             self._native = get_native(comm)
-            self._comm_stream = concurrent_stream(dev, "ddp_comm", comm_stream_priority())
+            self._comm_stream = concurrent_stream(dev, "ddp_comm", 0)
         if allreduce == "auto" and comm is not None and comm.is_gpu and self.world > 1:
             self._setup_auto(comm, dev)
         # CU budget of the bucket reductions that run beside backward: workgroups per IPC /
@@ -257,7 +209,7 @@ class FlatParamTrainer:
         if emulate_comm:
             if self.world != 1 or dev.type != "cuda":
                 raise ValueError("emulate_comm is a single-GPU measurement (world 1, HIP device)")
-            self._comm_stream = concurrent_stream(dev, "ddp_comm", comm_stream_priority())
+            self._comm_stream = concurrent_stream(dev, "ddp_comm", 0)
             self._emu_zero = torch.zeros(max(b.end - b.start for b in self.buckets),
                                          dtype=grad_dtype, device=dev)
             if not isinstance(emulate_comm, bool):
@@ -275,18 +227,6 @@ class FlatParamTrainer:
         self._opt_issued = 0          # head-bucket AdamW ranges issued in this step's backward
         self._in_step = False         # only step() (which joins the optimizer stream) overlaps
         self.side_stream_checks = []  # warm-up concurrency re-checks (_recheck_side_streams)
-        self._rows_param = None       # table whose untouched rows update early (_EARLY_ROWS)
-        self._rows_early = False
-        self._row_mask = None
-        if (_EARLY_ROWS and mode == "view" and dev.type == "cuda" and self.world == 1
-                and len(self.buckets) > 1):
-            cands = [q for q in order if getattr(q, "_dlbb_rows_from_input", False)
-                     and getattr(q, "_dlbb_sink_uses", 1) == 2 and hasattr(q, "_dlbb_grad_sink")
-                     and q.dim() == 2 and q.shape[1] % 8 == 0]
-            if len(cands) == 1 and self._bucket_of[id(cands[0])] is self.buckets[-1]:
-                self._rows_param = cands[0]
-                self._row_mask = torch.zeros(cands[0].shape[0], dtype=torch.uint8, device=dev)
-                cands[0]._dlbb_partial_sink = self._on_partial
         self.timeline = False       # record comm events per bucket (comm_tail_report)
         self._tl = None
         self.step_count = 0
@@ -300,7 +240,7 @@ class FlatParamTrainer:
         engine cannot be created (e.g. ranks sharing one GPU). Per-bucket choice: ``bucket_paths``."""
         from .custom_allreduce import get_custom_allreduce
 
-        self._comm_stream = concurrent_stream(dev, "ddp_comm", comm_stream_priority())
+        self._comm_stream = concurrent_stream(dev, "ddp_comm", 0)
         car = get_custom_allreduce(comm)
         reg_max = int(getattr(car, "reg_max", 0) or 0) if car is not None else 0
         need_native = False
@@ -354,9 +294,9 @@ class FlatParamTrainer:
         self.master = self.flat_param.float()
         self.opt = FlatAdamW(self.master, lr=lr, betas=betas, weight_decay=weight_decay)
 
-    def _optimizer_step(self, ranges=None, advance: bool = True, rows=None) -> None:
+    def _optimizer_step(self, ranges=None, advance: bool = True) -> None:
         self.opt.step(self.flat_grad, working_bf16=self.flat_param, grad_scale=1.0 / self.world,
-                      ranges=ranges, advance=advance, rows=rows)
+                      ranges=ranges, advance=advance)
 
     # ------------------------------------------------------------------ buckets
     def _add_bucket(self, start: int, end: int, params) -> None:
@@ -370,7 +310,6 @@ class FlatParamTrainer:
             b.ready, b.launched, b.work = 0, False, None
         self._next = 0
         self._opt_issued = 0
-        self._rows_early = False
         for b in self.buckets:
             b.opt_done = False
         self._seen.clear()
@@ -420,7 +359,7 @@ class FlatParamTrainer:
         """Public form of the re-check (no-op without side streams, under CU-masked streams or
         during a capture); runners call it once after their warm-up steps."""
         if ((self._wgrad_stream is not None or self._comm_stream is not None)
-                and not _WGRAD_CU_SHARE and not torch.cuda.is_current_stream_capturing()):
+                and not torch.cuda.is_current_stream_capturing()):
             self._recheck_side_streams()
 
     def _recheck_side_streams(self) -> None:
@@ -438,13 +377,12 @@ class FlatParamTrainer:
         if self._comm_stream is not None and not runs_concurrently(cur, self._comm_stream, dev):
             # the bucket reductions' stream (IPC / native RCCL / emulated): same check
             self._comm_stream = concurrent_stream(dev, f"ddp_comm_s{self.step_count}",
-                                                  comm_stream_priority(), ref=cur)
+                                                  0, ref=cur)
             rec["comm_replaced"] = True
         if bad:
             new = list(self._wgrad_streams)
             for i in bad:
-                new[i] = concurrent_stream(dev, f"ddp_wgrad_s{self.step_count}_{i}",
-                                           _WGRAD_PRIORITY, ref=cur)
+                new[i] = concurrent_stream(dev, f"ddp_wgrad_s{self.step_count}_{i}", 0, ref=cur)
             remap = {i: new[i] for i in bad}
             for q in self._params:
                 old = getattr(q, "_dlbb_grad_stream", None)
@@ -468,24 +406,6 @@ class FlatParamTrainer:
                                 and self._wgrad_stream is not None
                                 else concurrent_stream(self.flat_grad.device, "ddp_opt"))
         return self._opt_stream
-
-    def _on_partial(self, p, n: int) -> None:
-        """First (LM-head) use of the tied table done: AdamW of the rows this step's input ids do
-        not touch (their gradient is final) on the optimizer stream, during backward. Ordered
-        after the main stream (the LM-head dgrad read the table before its gradient was
-        reported) and the weight-gradient streams (an unfused LM head computes it there)."""
-        if (p is not self._rows_param or n != 1 or not self.opt_overlap or not self._in_step
-                or not self._split_optimizer_ok()):
-            return
-        os_ = self._get_opt_stream()
-        fork(os_)
-        self._wait_wgrad(os_)
-        o = self._offsets[id(p)]
-        with torch.cuda.stream(os_):
-            self._optimizer_step(ranges=[(o, o + p.numel())], advance=self._opt_issued == 0,
-                                 rows=(self._row_mask, p.shape[1], 0))
-        self._opt_issued += 1
-        self._rows_early = True
 
     def _launch(self, b: _Bucket) -> None:
         b.launched = True
@@ -639,22 +559,15 @@ class FlatParamTrainer:
 
     def step(self, idx: torch.Tensor, targets: torch.Tensor, sync_loss: bool = True):
         """One full training step: forward, backward (+ overlapped all-reduce), AdamW."""
-        if self.step_count in (1, 2):       # early warm-up steps (a runner adds one after)
-            self.recheck_side_streams()
         self.zero_grad()
         self._reset()
         self._in_step = True
-        if self._rows_param is not None and self.opt_overlap and self._split_optimizer_ok():
-            # rows of the tied table the embedding backward will add to (= this step's ids)
-            self._row_mask.zero_()
-            self._row_mask.index_fill_(0, idx.reshape(-1), 1)
         if self.timeline and not torch.cuda.is_current_stream_capturing():
             self._tl = {"buckets": {}}
         with tracing.range("fwd"):
             loss = self.model(idx, targets)
         with tracing.range("bwd+overlapped_grad_sync"):
-            if _UNIT_UPSTREAM:              # loss.backward(): the fused loss skips its scaling
-                mark_unit_upstream(loss)
+            mark_unit_upstream(loss)        # loss.backward(): the fused loss skips its scaling
             loss.backward()
         if self._tl is not None:
             self._tl["bwd_end"] = torch.cuda.Event(enable_timing=True)
@@ -681,15 +594,7 @@ class FlatParamTrainer:
                         else [(b.start, b.end) for b in todo], advance=adv)
                     adv = False
                 self._wait_bucket(tail)
-                if self._rows_early:
-                    p = self._rows_param
-                    o = self._offsets[id(p)]
-                    e = o + p.numel()
-                    self._optimizer_step(ranges=[(tail.start, o), (e, self.numel)], advance=adv)
-                    self._optimizer_step(ranges=[(o, e)], advance=False,
-                                         rows=(self._row_mask, p.shape[1], 1))
-                else:
-                    self._optimizer_step(ranges=[(tail.start, self.numel)], advance=adv)
+                self._optimizer_step(ranges=[(tail.start, self.numel)], advance=adv)
         else:
             with tracing.range("grad_sync_tail"):
                 self.finish()
@@ -854,6 +759,6 @@ class FlatParamTrainer:
             h.remove()
         for p in self._params:
             for attr in ("_dlbb_grad_sink", "_dlbb_grad_stream", "_dlbb_sink_count",
-                         "_dlbb_grad_fresh", "_dlbb_grad_event", "_dlbb_partial_sink"):
+                         "_dlbb_grad_fresh", "_dlbb_grad_event"):
                 if hasattr(p, attr):
                     delattr(p, attr)

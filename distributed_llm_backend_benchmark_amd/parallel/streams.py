@@ -132,51 +132,13 @@ def reset() -> None:
     _GROUPS.clear()
 
 
-_SHARE_CACHE: Dict[Tuple[int, str, int, int], "torch.cuda.Stream"] = {}
-
-
-def cu_share_stream(device, role: str, num: int, den: int) -> "torch.cuda.Stream":
-    """A stream whose kernels run only on ``num / den`` of every XCD's CUs (a hardware CU mask,
-    ``csrc/streams.hip``), as a torch ``ExternalStream``; created once per (device, role, share)
-    and kept for the process lifetime. Raises if the runtime refuses the mask or the stream does
-    not run beside the current stream."""
-    from ..ops import _lib
-
-    dev = torch.device(device)
-    idx = dev.index if dev.index is not None else torch.cuda.current_device()
-    key = (idx, role, int(num), int(den))
-    if key in _SHARE_CACHE:
-        return _SHARE_CACHE[key]
-    import ctypes
-
-    ncu = torch.cuda.get_device_properties(idx).multi_processor_count
-    handle, kept = ctypes.c_void_p(), ctypes.c_int(0)
-    with torch.cuda.device(idx):
-        rc = _lib.lib().dlbb_stream_create_cu_share(ncu, int(num), int(den), ctypes.byref(handle),
-                                                    ctypes.byref(kept))
-    if rc != 0 or not handle.value:
-        raise RuntimeError(f"CU-masked stream for {role!r} refused (hip error {rc})")
-    s = torch.cuda.ExternalStream(handle.value, device=torch.device("cuda", idx))
-    got = _lib.lib().dlbb_stream_cu_count(ctypes.c_void_p(handle.value), ncu)
-    if got != kept.value:
-        raise RuntimeError(f"CU mask of {role!r}: {got} CUs active, {kept.value} requested")
-    if not runs_concurrently(torch.cuda.current_stream(dev), s, dev):
-        warnings.warn(f"CU-masked stream for {role!r} does not run beside the compute stream",
-                      RuntimeWarning, stacklevel=2)
-    s.dlbb_cus = got
-    _SHARE_CACHE[key] = s
-    return s
-
-
-# how a side stream is ordered after the compute stream: "device" (default) / "nofence" = one
-# event record + wait through csrc/streams.hip dlbb_stream_fork (a device-scope release / no
-# fence), "torch" = Stream.wait_stream (default HIP event: system-scope fence). GPT-2 step, three
-# interleaved reps (profiles/r05_step/SUMMARY.md §7): torch 17.89-17.98 ms and one 19.53 ms run
-# (compute-stream dispatch stalled ~58 us after every forked-from kernel — the same pattern
-# rocprofv3 shows for torch and nofence events, never for device-scope ones), device
-# 17.86-17.88, nofence 17.81-17.87.
-_FORK_MODE = {"nofence": 1, "device": 2, "torch": 0}[
-    __import__("os").environ.get("DLBB_FORK_EVENT", "device")]
+# A side stream is ordered after the compute stream by one event record + wait through
+# csrc/streams.hip dlbb_stream_fork with a device-scope release (mode 2). GPT-2 step, three
+# interleaved reps (profiles/r05_step/SUMMARY.md §7): torch's Stream.wait_stream (default HIP
+# event: system-scope fence) 17.89-17.98 ms and one 19.53 ms run (compute-stream dispatch stalled
+# ~58 us after every forked-from kernel — the pattern rocprofv3 shows for system-fenced events,
+# never for device-scope ones), device-scope 17.86-17.88.
+_FORK_MODE = 2
 
 
 def fork(to: "torch.cuda.Stream", frm: Optional["torch.cuda.Stream"] = None) -> None:
@@ -185,7 +147,7 @@ def fork(to: "torch.cuda.Stream", frm: Optional["torch.cuda.Stream"] = None) -> 
     streams of one device need only the device-scope ordering every kernel dispatch already
     releases (``profiles/r05_step/SUMMARY.md`` §7)."""
     frm = frm if frm is not None else torch.cuda.current_stream(to.device)
-    if _FORK_MODE == 0 or to.device.type != "cuda":
+    if to.device.type != "cuda":
         to.wait_stream(frm)
         return
     from ..ops import _lib

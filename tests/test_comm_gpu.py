@@ -550,26 +550,21 @@ def test_run_tp_shard_as_overlapped(tmp_path, graph):
     assert th["gemm_kernel_mix"]["hand_written_time_fraction"] == 1.0
 
 
-def test_ddp_comm_stream_fenced_to_normal_priority(monkeypatch):
-    """The fence in action: DLBB_COMM_STREAM_PRIORITY=-1 alone yields a NORMAL-priority comm
-    stream (the high-priority dispatch trap, profiles/r03_overlap/SUMMARY.md)."""
+def test_ddp_comm_stream_is_normal_priority():
+    """The comm stream is always normal priority: a high-priority one stretched every kernel
+    dispatch of the step (the high-priority dispatch trap, profiles/r03_overlap/SUMMARY.md), so
+    round 6 removed the option altogether."""
     import warnings
 
     from distributed_llm_backend_benchmark_amd.models.gpt2 import GPT2, GPT2Config
     from distributed_llm_backend_benchmark_amd.parallel import ddp
 
-    monkeypatch.setattr(ddp, "_COMM_PRIORITY", -1)
-    monkeypatch.delenv("DLBB_ALLOW_HIGH_PRIO_COMM", raising=False)
     cfg = GPT2Config(vocab_size=256, block_size=32, n_layer=1, n_head=2, n_embd=64)
     m = GPT2(cfg, device=torch.device("cuda"), seed=1)
     with warnings.catch_warnings(record=True):
         warnings.simplefilter("always")
         tr = ddp.FlatParamTrainer(m, None, emulate_comm=True)
     assert tr._comm_stream.priority == 0
-    tr.close()
-    monkeypatch.setenv("DLBB_ALLOW_HIGH_PRIO_COMM", "1")
-    tr = ddp.FlatParamTrainer(m, None, emulate_comm=True)
-    assert tr._comm_stream.priority < 0
     tr.close()
 
 
@@ -886,8 +881,7 @@ def test_ddp_overlapped_optimizer_is_bit_exact(mode):
         assert len(tr.buckets) > 2 and tr._split_optimizer_ok()
         losses = [tr.step(data[s, :, :-1], data[s, :, 1:]) for s in range(3)]
         if ov:
-            assert (tr._opt_issued == len(tr.buckets) - 1 + int(tr._rows_early)
-                    and tr._opt_stream is not None)
+            assert tr._opt_issued == len(tr.buckets) - 1 and tr._opt_stream is not None
         replay = tr.capture_step(data[3, :, :-1], data[3, :, 1:])
         losses += [float(replay(data[s, :, :-1], data[s, :, 1:]).item()) for s in (4, 5)]
         torch.cuda.synchronize()
@@ -896,37 +890,6 @@ def test_ddp_overlapped_optimizer_is_bit_exact(mode):
         tr.close()
     assert out[0][0] == out[1][0]
     assert torch.equal(out[0][1], out[1][1])
-
-
-def test_cu_share_stream_and_ddp_step(monkeypatch):
-    """A weight-gradient side stream confined to a share of every XCD's CUs (hardware CU mask):
-    the mask holds the requested CU count, kernels on it compute correctly, and a DDP step with
-    it trains (same buckets / optimizer path)."""
-    from distributed_llm_backend_benchmark_amd.models.gpt2 import GPT2, GPT2Config
-    from distributed_llm_backend_benchmark_amd.ops import linear
-    from distributed_llm_backend_benchmark_amd.parallel import ddp
-    from distributed_llm_backend_benchmark_amd.parallel.streams import cu_share_stream
-
-    dev = torch.device("cuda", 0)
-    ncu = torch.cuda.get_device_properties(0).multi_processor_count
-    s = cu_share_stream(dev, "test_share", 1, 4)
-    assert s.dlbb_cus == sum(1 for i in range(ncu) if (i // 8) % 4 < 1)
-    assert cu_share_stream(dev, "test_share", 1, 4) is s
-    x = torch.randn(512, 256, device=dev).to(torch.bfloat16)
-    w = torch.randn(384, 256, device=dev).to(torch.bfloat16)
-    s.wait_stream(torch.cuda.current_stream())
-    with torch.cuda.stream(s):
-        y = linear(x, w, out_dtype=torch.float32)
-    torch.cuda.current_stream().wait_stream(s)
-    torch.testing.assert_close(y, x.float() @ w.float().t(), rtol=2e-3, atol=2e-2)
-    monkeypatch.setattr(ddp, "_WGRAD_CU_SHARE", "1/2")
-    cfg = GPT2Config(vocab_size=1024, block_size=128, n_layer=2, n_head=4, n_embd=256)
-    tr = ddp.FlatParamTrainer(GPT2(cfg, device=dev, seed=3), None, lr=1e-3, bucket_mb=0.5)
-    assert tr._wgrad_stream is not None and getattr(tr._wgrad_stream, "dlbb_cus", 0) > 0
-    idx = torch.randint(0, cfg.vocab_size, (4, 129), device=dev)
-    losses = [tr.step(idx[:, :-1], idx[:, 1:]) for _ in range(6)]
-    assert all(map(lambda v: v == v, losses)) and losses[-1] < losses[0], losses
-    tr.close()
 
 
 def test_unit_upstream_mark_is_bit_exact():
@@ -951,34 +914,6 @@ def test_unit_upstream_mark_is_bit_exact():
         assert torch.equal(a, b)
     ref = GPT2(cfg, device=dev, seed=21)
     assert not mark_unit_upstream(ref(idx[:, :-1], idx[:, 1:]) * 2.0)   # not the fused output
-
-
-def test_early_rows_adamw_bit_exact(monkeypatch):
-    """The tied table's rows untouched by the step's ids are updated right after the LM-head
-    backward (row-filtered AdamW), the touched rows after the embedding backward: losses and
-    masters bit-identical to the whole-table update, eager and graph-replayed."""
-    from distributed_llm_backend_benchmark_amd.models.gpt2 import GPT2, GPT2Config
-    from distributed_llm_backend_benchmark_amd.parallel import ddp
-
-    dev = torch.device("cuda", 0)
-    cfg = GPT2Config(vocab_size=4096, block_size=64, n_layer=2, n_head=4, n_embd=256)
-    g = torch.Generator(device="cuda").manual_seed(9)
-    data = torch.randint(0, 1024, (6, 4, 65), device=dev, generator=g)   # rows >= 1024 untouched
-    out = []
-    for early in (False, True):
-        monkeypatch.setattr(ddp, "_EARLY_ROWS", early)
-        tr = ddp.FlatParamTrainer(GPT2(cfg, device=dev, seed=8), None, lr=1e-3, bucket_mb=0.3)
-        assert (tr._rows_param is not None) == early
-        losses = [tr.step(data[s, :, :-1], data[s, :, 1:]) for s in range(3)]
-        if early:
-            assert tr._rows_early
-        replay = tr.capture_step(data[3, :, :-1], data[3, :, 1:])
-        losses += [float(replay(data[s, :, :-1], data[s, :, 1:]).item()) for s in (4, 5)]
-        torch.cuda.synchronize()
-        out.append((losses, tr.master.clone(), tr.opt.m.clone()))
-        tr.close()
-    assert out[0][0] == out[1][0]
-    assert torch.equal(out[0][1], out[1][1]) and torch.equal(out[0][2], out[1][2])
 
 
 def test_side_stream_recheck_replaces_a_serialised_stream():

@@ -678,21 +678,6 @@ def test_run_tp_cli_shard_as(tmp_path):
     assert run_tp.main(["--config", path, "--backend", "gloo", "--kernels", "torch"]) == 1
 
 
-def test_high_priority_comm_stream_is_fenced(monkeypatch):
-    """a high-priority comm stream stretched every kernel dispatch of the
-    step (stamps, profiles/r03_overlap); the trainer clamps it to normal unless forced."""
-    from distributed_llm_backend_benchmark_amd.parallel import ddp
-
-    monkeypatch.setattr(ddp, "_COMM_PRIORITY", -1)
-    monkeypatch.delenv("DLBB_ALLOW_HIGH_PRIO_COMM", raising=False)
-    with pytest.warns(RuntimeWarning, match="high-priority"):
-        assert ddp.comm_stream_priority() == 0
-    monkeypatch.setenv("DLBB_ALLOW_HIGH_PRIO_COMM", "1")
-    assert ddp.comm_stream_priority() == -1
-    monkeypatch.setattr(ddp, "_COMM_PRIORITY", 0)
-    assert ddp.comm_stream_priority() == 0
-
-
 def _list_allgather_worker(rank, world):
     import torch
 

@@ -31,7 +31,7 @@ def test_asm_lds_reads_are_waited_for(src):
 
 
 # kernels that keep the builtin transposed read on purpose (measured faster, see the source)
-ALLOWED_DRAINS = ("attn_fwd_d64_kernel",)
+ALLOWED_DRAINS = ("attn_fwd_kernel",)
 
 
 def test_checker_flags_an_early_use():

@@ -25,20 +25,14 @@ def _randn(*shape, dtype=torch.bfloat16, seed=0, scale=1.0):
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16, torch.float32])
 @pytest.mark.parametrize("nsrc", [1, 2, 3, 4, 5, 8, 16])
 @pytest.mark.parametrize("n", [7, 4096, 1000003])
-@pytest.mark.parametrize("variant", [0, 1])
-def test_reduce_sum(dtype, nsrc, n, variant):
-    """Both forms (templated source counts 2/3/4/8 with every load in flight; runtime loop)."""
-    from distributed_llm_backend_benchmark_amd.ops import _lib, reduce_sum
+def test_reduce_sum(dtype, nsrc, n):
+    from distributed_llm_backend_benchmark_amd.ops import reduce_sum
 
     srcs = [_randn(n, dtype=dtype, seed=i) for i in range(nsrc)]
     ref = sum(s.float() for s in srcs) * 0.5
-    _lib.lib().dlbb_reduce_set_variant(variant)
-    try:
-        out = reduce_sum(srcs, out_dtype=torch.float32, scale=0.5)
-        torch.testing.assert_close(out, ref, rtol=1e-5, atol=1e-5)
-        out2 = reduce_sum(srcs, scale=0.5)
-    finally:
-        _lib.lib().dlbb_reduce_set_variant(0)
+    out = reduce_sum(srcs, out_dtype=torch.float32, scale=0.5)
+    torch.testing.assert_close(out, ref, rtol=1e-5, atol=1e-5)
+    out2 = reduce_sum(srcs, scale=0.5)
     tol = 1e-2 if dtype != torch.float32 else 1e-5
     torch.testing.assert_close(out2.float(), ref, rtol=tol, atol=tol * nsrc)
 
@@ -46,22 +40,17 @@ def test_reduce_sum(dtype, nsrc, n, variant):
 @pytest.mark.parametrize("src,dst", [(torch.bfloat16, torch.float32), (torch.float32, torch.bfloat16),
                                      (torch.float16, torch.float32), (torch.float32, torch.float16),
                                      (torch.bfloat16, torch.float16)])
-@pytest.mark.parametrize("n", [1, 13, 65536 + 5, 3 * 2048 * 256 + 3])
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5])
-def test_cast(src, dst, n, variant):
-    """Every cast kernel variant (8-element, one-16-B-side, + non-temporal stores) bit-exact
-    against torch's conversion, with ragged tails and multi-tile grids."""
-    from distributed_llm_backend_benchmark_amd.ops import _lib, cast
+@pytest.mark.parametrize("n", [1, 13, 65536 + 5, 3 * 2048 * 256 + 3, 9 * 2048 * 256 * 8 + 1])
+def test_cast(src, dst, n):
+    """The cast (one 16-B wide side per lane, non-temporal stores) bit-exact against torch's
+    conversion, with ragged tails, multi-tile grids past the 4096-block grid-stride cap, and an
+    unaligned view (the one-element-per-lane kernel)."""
+    from distributed_llm_backend_benchmark_amd.ops import cast
 
     x = _randn(n, dtype=src, seed=3)
-    _lib.lib().dlbb_cast_set_variant(variant)
-    try:
-        torch.testing.assert_close(cast(x, dst), x.to(dst), rtol=0, atol=0)
-        # unaligned source (16-B alignment lost): the 8-element kernel takes it
-        if n > 1:
-            torch.testing.assert_close(cast(x[1:], dst), x[1:].to(dst), rtol=0, atol=0)
-    finally:
-        _lib.lib().dlbb_cast_set_variant(5)
+    torch.testing.assert_close(cast(x, dst), x.to(dst), rtol=0, atol=0)
+    if n > 1:
+        torch.testing.assert_close(cast(x[1:], dst), x[1:].to(dst), rtol=0, atol=0)
 
 
 def test_cast_nan_inf_preserved():
@@ -114,16 +103,12 @@ def test_chunk_copy_and_scale(nt):
     _lib.lib().dlbb_chunk_copy_set_nt(2)
 
 
-@pytest.fixture(params=[("mfma", 0, 1), ("mfma", 128, 1), ("mfma", 256, 1), ("mfma", 256, 0),
-                        ("mfma", 256, 2), ("mfma", 256, 3), ("mfma", 256, 4), ("mfma", 256, 6),
-                        ("mfma", 256, 6, 0), ("mfma", 256, 7), ("mfma", 256, 9), ("mfma", 256, 10),
-                        ("mfma", 256, 11), ("mfma", 256, 12), ("mfma", 256, 13), ("blas", 0, 1)],
-                ids=["mfma_auto", "mfma_t128", "mfma_t256", "mfma_t256_lockstep",
-                     "mfma_t256_early", "mfma_t256_deep", "mfma_t256_persistent",
-                     "mfma_t256_pingpong", "mfma_t256_pingpong_nobal", "mfma_t256_pingpong_bal",
-                     "mfma_t256_w4_agpr", "mfma_t256_pp_persistent", "mfma_t256_pingpong_moveb",
-                     "mfma_t256_pingpong_moveb_spread", "mfma_t256_pingpong_moveab_spread",
-                     "blas"])
+@pytest.fixture(params=[("mfma", 0, 6), ("mfma", 128, 6), ("mfma", 256, 3), ("mfma", 256, 6),
+                        ("mfma", 256, 6, 0), ("mfma", 256, 6, 1), ("mfma", 256, 10),
+                        ("blas", 0, 6)],
+                ids=["mfma_auto", "mfma_t128", "mfma_t256_deep", "mfma_t256_pingpong",
+                     "mfma_t256_pingpong_nobal", "mfma_t256_pingpong_bal",
+                     "mfma_t256_pp_persistent", "blas"])
 def gemm_tile(request, monkeypatch):
     from distributed_llm_backend_benchmark_amd.ops.gemm import (get_stagger, set_bal, set_stagger,
                                                                 set_tile)
@@ -493,12 +478,12 @@ def test_layernorm_bwd(cols, with_res):
     assert norm_act.LN_FALLBACKS["count"] - fb0 == (0 if cols % 256 == 0 else 1)
 
 
-@pytest.mark.parametrize("rows,cols", [(16384, 768), (520, 768), (4099, 1024), (7, 256)])
+@pytest.mark.parametrize("rows,cols", [(16384, 768), (520, 768), (4099, 1024), (7, 256),
+                                       (1000, 2048)])
 @pytest.mark.parametrize("with_res", [False, True])
-def test_layernorm_bwd_pipelined_matches_sequential(rows, cols, with_res):
-    """The pipelined LN backward (8 waves / block, next row's loads in flight) against the
-    wave-per-row-sequence kernel: dx BITWISE equal (same per-row math), dgamma / dbeta equal to
-    fp32 summation-order noise, and both against the fp32 torch reference."""
+def test_layernorm_bwd_matches_fp32(rows, cols, with_res):
+    """The LN backward (pipelined kernel up to 1024 columns, the wave-per-row-sequence kernel
+    beyond) against the fp32 torch reference: dx, dgamma, dbeta (+ the residual gradient)."""
     from distributed_llm_backend_benchmark_amd.ops import _lib
     from distributed_llm_backend_benchmark_amd.ops.norm_act import _ln_bwd_reference
 
@@ -509,29 +494,19 @@ def test_layernorm_bwd_pipelined_matches_sequential(rows, cols, with_res):
     mean = h.float().mean(1)
     rstd = torch.rsqrt(h.float().var(1, unbiased=False) + 1e-5)
     grid = L.dlbb_layernorm_bwd_grid(rows)
-    outs = {}
-    for var in (0, 1):
-        L.dlbb_layernorm_bwd_set_variant(var)
-        dx = torch.empty_like(h)
-        ws = torch.full((2 * grid * cols,), float("nan"), device=DEV)
-        # dgamma / dbeta come out in the parameter dtype (bf16 here)
-        dg = torch.empty(cols, device=DEV, dtype=torch.bfloat16)
-        db = torch.empty(cols, device=DEV, dtype=torch.bfloat16)
-        _lib.check(L.dlbb_layernorm_bwd(
-            dy.data_ptr(), h.data_ptr(), gam.data_ptr(), 1, mean.data_ptr(), rstd.data_ptr(),
-            _lib.ptr(dres), dx.data_ptr(), ws.data_ptr(), dg.data_ptr(), db.data_ptr(), rows,
-            cols, 0, _lib.stream(h.device)), "ln_bwd")
-        outs[var] = (dx, dg, db)
-    L.dlbb_layernorm_bwd_set_variant(1)
-    assert torch.equal(outs[0][0], outs[1][0])
-    # fp32 sums in a different order, then one bf16 rounding: at most an ulp apart
-    torch.testing.assert_close(outs[1][1].float(), outs[0][1].float(), rtol=8e-3, atol=1e-2)
-    torch.testing.assert_close(outs[1][2].float(), outs[0][2].float(), rtol=8e-3, atol=1e-2)
+    dx = torch.empty_like(h)
+    ws = torch.full((2 * grid * cols,), float("nan"), device=DEV)
+    dg = torch.empty(cols, device=DEV, dtype=torch.bfloat16)
+    db = torch.empty(cols, device=DEV, dtype=torch.bfloat16)
+    _lib.check(L.dlbb_layernorm_bwd(
+        dy.data_ptr(), h.data_ptr(), gam.data_ptr(), 1, mean.data_ptr(), rstd.data_ptr(),
+        _lib.ptr(dres), dx.data_ptr(), ws.data_ptr(), dg.data_ptr(), db.data_ptr(), rows,
+        cols, 0, _lib.stream(h.device)), "ln_bwd")
     rdg, rdb = torch.empty(cols, device=DEV), torch.empty(cols, device=DEV)
     rdx = _ln_bwd_reference(dy, h, gam, mean, rstd, dres, rdg, rdb, False)
-    torch.testing.assert_close(outs[1][0].float(), rdx.float(), rtol=2e-2, atol=2e-2)
-    torch.testing.assert_close(outs[1][1].float(), rdg, rtol=1e-2, atol=1e-2 * rows ** 0.5)
-    torch.testing.assert_close(outs[1][2].float(), rdb, rtol=1e-2, atol=1e-2 * rows ** 0.5)
+    torch.testing.assert_close(dx.float(), rdx.float(), rtol=2e-2, atol=2e-2)
+    torch.testing.assert_close(dg.float(), rdg, rtol=1e-2, atol=1e-2 * rows ** 0.5)
+    torch.testing.assert_close(db.float(), rdb, rtol=1e-2, atol=1e-2 * rows ** 0.5)
 
 
 @pytest.mark.parametrize("approx", ["none", "tanh"])
@@ -776,11 +751,11 @@ def test_wgrad_matches_fp32(M, N, K, split):
 
 @pytest.mark.parametrize("M,N,K", [(16384, 768, 768), (4096, 2304, 768), (1024, 256, 3072)])
 def test_wgrad_forced_pp_with_bias(monkeypatch, M, N, K):
-    """DLBB_WGRAD_IMPL=pp: the unsplit 256^2 TN ping-pong for dW plus a column-sum pass for the
+    """DLBB_GEMM=pp: the unsplit 256^2 TN ping-pong for dW plus a column-sum pass for the
     bias gradient (the kernel has no fused bias): bf16 store and bf16 accumulate."""
     from distributed_llm_backend_benchmark_amd.ops import gemm as G
 
-    monkeypatch.setenv("DLBB_WGRAD_IMPL", "pp")
+    monkeypatch.setenv("DLBB_GEMM", "pp")
     dy = _randn(M, N, seed=31, scale=0.5)
     x = _randn(M, K, seed=32, scale=0.5)
     assert G._wgrad_choice(dy, x, torch.empty(N, K, dtype=torch.bfloat16, device=DEV),
@@ -848,7 +823,7 @@ def test_wgrad_fused_reduce_bitwise(monkeypatch, impl, M, N, K, order):
     try:
         outs = {}
         for fused in ("0", "1"):
-            monkeypatch.setenv("DLBB_WGRAD_FUSED", fused)
+            monkeypatch.setattr(gemm, "_WGRAD_FUSED", [fused == "1"])
             w32, b32 = torch.empty(N, K, device=DEV), torch.empty(N, device=DEV)
             fn(dy, x, w32, False, None, b32)
             wacc, bacc = torch.full((N, K), 0.25, device=DEV), torch.full((N,), 0.5, device=DEV)
@@ -876,13 +851,13 @@ def test_wgrad_fused_reduce_repeated_under_load(monkeypatch):
     M, N, K = 16384, 768, 768
     xs = [_randn(M, K, seed=70 + i, scale=0.5) for i in range(4)]
     dys = [_randn(M, N, seed=80 + i, scale=0.5) for i in range(4)]
-    monkeypatch.setenv("DLBB_WGRAD_FUSED", "0")
+    monkeypatch.setattr(gemm, "_WGRAD_FUSED", [False])
     refs = []
     for i in range(4):
         o = torch.empty(N, K, device=DEV)
         gemm._wgrad_hip(dys[i], xs[i], o, False, None, None)
         refs.append(o)
-    monkeypatch.setenv("DLBB_WGRAD_FUSED", "1")
+    monkeypatch.setattr(gemm, "_WGRAD_FUSED", [True])
     side = torch.cuda.Stream()
     big = torch.empty(256 << 20, dtype=torch.uint8, device=DEV)
     outs = [torch.empty(N, K, device=DEV) for _ in range(20)]
@@ -1093,18 +1068,17 @@ def test_gemm_autotune_offers_tile_variants(monkeypatch):
     y = linear(x, w)
     torch.testing.assert_close(y.float(), x.float() @ w.float().t(), rtol=2e-2, atol=1.5)
     kind, key, times, best = gemm.TUNE_LOG[-1]
-    assert set(times) == {"mfma", "mfma192", "mfma192p", "blas"}, times
+    assert set(times) == {"mfma", "mfma192", "mfma192p", "mfma_sk", "blas"}, times
     assert gemm.CHOICES[key] == best
 
 
 @pytest.mark.parametrize("M,N,K", [(4096, 9600, 768), (2000, 19200, 640), (1040, 1536, 1024),
                                    (16384, 3840, 384)])
-@pytest.mark.parametrize("early", [12, 18])
 @pytest.mark.parametrize("bal", [0, 1])
-def test_gemm_nt_192_spread_matches_fp32(M, N, K, early, bal):
+def test_gemm_nt_192_spread_matches_fp32(M, N, K, bal):
     """Persistent 256 x 192 NT GEMM with the C stores spread under the next tile's K-loop
     (variant 2): multi-round grids (several tiles per workgroup), ragged M, the shortest
-    reduction it accepts (6 K-tiles), both boundary-store counts and both DMA schedules — against
+    reduction it accepts (6 K-tiles) and both DMA schedules — against
     fp32, and bit-identical to the non-persistent 256 x 192 kernel (same MFMA order)."""
     from distributed_llm_backend_benchmark_amd.ops import _lib, gemm
 
@@ -1114,27 +1088,24 @@ def test_gemm_nt_192_spread_matches_fp32(M, N, K, early, bal):
     y = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
     y1 = torch.empty_like(y)
     try:
-        lib.dlbb_gemm_set_spread_early(early)
         lib.dlbb_gemm_set_bal(bal)
         y.fill_(7.0)
         gemm._mfma192p_linear(x, w, None, None, None, y, None)
         gemm._mfma192_linear(x, w, None, None, None, y1, None)
         torch.cuda.synchronize()
     finally:
-        lib.dlbb_gemm_set_spread_early(12)
         lib.dlbb_gemm_set_bal(2)
     torch.testing.assert_close(y.float(), x.float() @ w.float().t(), rtol=2e-2,
                                atol=2e-2 * K ** 0.5)
     assert torch.equal(y, y1)
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2])
 @pytest.mark.parametrize("split", [1, 3, 7, 9, 16, 19])
 @pytest.mark.parametrize("dt_out", ["bf16", "fp32"])
-def test_split_reduce_variants_match_fp32(variant, split, dt_out):
-    """The weight-gradient split-K reduce (every form: round-4 8-float loop, all slabs in flight
-    with streaming / plain loads; templated splits and the runtime-split fallback) against an
-    fp32 sum of the slabs, accumulating into an existing output, with the bias slabs."""
+def test_split_reduce_matches_fp32(split, dt_out):
+    """The weight-gradient split-K reduce (all slabs in flight, streaming loads; templated splits
+    and the runtime-split fallback) against an fp32 sum of the slabs, accumulating into an
+    existing output, with the bias slabs."""
     from distributed_llm_backend_benchmark_amd.ops import _lib
 
     N, K = 384, 256
@@ -1146,15 +1117,11 @@ def test_split_reduce_variants_match_fp32(variant, split, dt_out):
     ob = torch.randn(nb, device=DEV, generator=g).to(dt)
     ref = ws[:split * n].view(split, n).sum(0) + o.float()
     refb = ws[split * n:].view(split, nb).sum(0) + ob.float()
-    _lib.lib().dlbb_split_reduce_set_variant(variant)
-    try:
-        _lib.check(_lib.lib().dlbb_split_reduce(ws.data_ptr(), o.data_ptr(),
-                                                1 if dt_out == "bf16" else 0, n, ob.data_ptr(),
-                                                nb, split, 1, _lib.stream(ws.device)),
-                   "split_reduce")
-        torch.cuda.synchronize()
-    finally:
-        _lib.lib().dlbb_split_reduce_set_variant(1)
+    _lib.check(_lib.lib().dlbb_split_reduce(ws.data_ptr(), o.data_ptr(),
+                                            1 if dt_out == "bf16" else 0, n, ob.data_ptr(),
+                                            nb, split, 1, _lib.stream(ws.device)),
+               "split_reduce")
+    torch.cuda.synchronize()
     tol = dict(rtol=1e-2, atol=1e-2) if dt_out == "bf16" else dict(rtol=1e-5, atol=1e-4)
     torch.testing.assert_close(o.float(), ref, **tol)
     torch.testing.assert_close(ob.float(), refb, **tol)
@@ -1172,29 +1139,3 @@ def test_sort_ids_matches_stable_torch_sort(n, vocab):
     s, o = sort_ids(ids, vocab)
     rs, ro = torch.sort(ids, stable=True)
     assert torch.equal(s, rs) and torch.equal(o, ro)
-
-
-def test_adamw_nontemporal_bit_exact():
-    """The non-temporal AdamW form (DLBB_ADAMW_NT) changes only the cache policy of the fp32
-    state traffic: identical parameters, moments and bf16 working copy, incl. a row-filtered
-    call."""
-    from distributed_llm_backend_benchmark_amd.ops import _lib
-    from distributed_llm_backend_benchmark_amd.ops.optim import FlatAdamW
-
-    n = 96 * 11000
-    g = _randn(n, seed=41).float().to(torch.bfloat16)
-    outs = []
-    for nt in (0, 1):
-        _lib.lib().dlbb_adamw_set_nt(nt)
-        master = _randn(n, seed=40).float()
-        opt = FlatAdamW(master, lr=1e-3, weight_decay=0.1)
-        w = torch.empty(n, dtype=torch.bfloat16, device=DEV)
-        for _ in range(3):
-            opt.step(g, working_bf16=w)
-        mask = (torch.arange(n // 96, device=DEV) % 3 == 0).to(torch.uint8)
-        opt.step(g, working_bf16=w, rows=(mask, 96, 1))
-        torch.cuda.synchronize()
-        outs.append((master.clone(), opt.m.clone(), opt.v.clone(), w.clone()))
-    _lib.lib().dlbb_adamw_set_nt(0)
-    for a, b in zip(*outs):
-        assert torch.equal(a, b)

@@ -1,6 +1,6 @@
-"""Device time of the causal attention forward (ours vs torch SDPA) and fwd+bwd, GPT-2 shape."""
+"""Device time of the causal attention forward / backward (ours vs torch SDPA vs the library
+backward) at the GPT-2 shape and longer sequences, head dim 64 and 128."""
 import json
-import math
 import os
 import sys
 
@@ -27,31 +27,24 @@ def t_best(fn, iters=20, rounds=5):
     return best
 
 
-for B, T, H in ((16, 1024, 12), (8, 2048, 12), (4, 4096, 16)):
-    qkv = torch.randn(B, T, 3 * H * 64, device="cuda").to(torch.bfloat16)
-    fl = 4.0 * B * H * T * T * 64 / 2          # causal
+for B, T, H, D in ((16, 1024, 12, 64), (8, 2048, 12, 64), (4, 4096, 16, 64),
+                   (16, 1024, 6, 128), (4, 4096, 8, 128)):
+    qkv = torch.randn(B, T, 3 * H * D, device="cuda").to(torch.bfloat16)
+    fl = 4.0 * B * H * T * T * D / 2          # causal
     t_ours = t_best(lambda: attn_fwd(qkv, H))
     t_torch = t_best(lambda: _torch_attention(qkv, H))
     x = qkv.clone().requires_grad_(True)
-    go = torch.randn(B, T, H * 64, device="cuda").to(torch.bfloat16)
+    go = torch.randn(B, T, H * D, device="cuda").to(torch.bfloat16)
     t_fb_ours = t_best(lambda: causal_attention(x, H).backward(go), iters=5, rounds=3)
     t_fb_torch = t_best(lambda: _torch_attention(x, H).backward(go), iters=5, rounds=3)
     o, lse = attn_fwd(qkv, H)
-    from distributed_llm_backend_benchmark_amd.ops import _lib as L
-    L.lib().dlbb_attn_set_concurrent(1)
-    t_bwd_conc = t_best(lambda: attn_bwd(qkv, o, lse, go, H), iters=10, rounds=3)
-    L.lib().dlbb_attn_set_concurrent(0)
-    L.lib().dlbb_attn_set_fuse_delta(0)
-    t_bwd_unfused = t_best(lambda: attn_bwd(qkv, o, lse, go, H), iters=10, rounds=3)
-    L.lib().dlbb_attn_set_fuse_delta(1)
-    t_bwd = t_best(lambda: attn_bwd(qkv, o, lse, go, H), iters=10, rounds=3)
-    t_bwd_lib = t_best(lambda: attn_bwd_library(qkv, o, lse, go, H), iters=10, rounds=3)
-    print(json.dumps({"B": B, "T": T, "H": H, "D": 64, "fwd_us_ours": t_ours * 1e6,
-                      "fwd_us_torch": t_torch * 1e6, "fwd_tflops_ours": fl / t_ours / 1e12,
-                      "fwd_tflops_torch": fl / t_torch / 1e12,
-                      "fwd_bwd_us_ours": t_fb_ours * 1e6, "fwd_bwd_us_torch": t_fb_torch * 1e6,
-                      "bwd_us_ours": t_bwd * 1e6, "bwd_us_ours_concurrent": t_bwd_conc * 1e6,
-                      "bwd_us_ours_separate_delta": t_bwd_unfused * 1e6,
-                      "bwd_us_library": t_bwd_lib * 1e6,
-                      "bwd_tflops_ours": 2.5 * fl / t_bwd / 1e12}),
-          flush=True)
+    rec = {"B": B, "T": T, "H": H, "D": D, "fwd_us_ours": t_ours * 1e6,
+           "fwd_us_torch": t_torch * 1e6, "fwd_tflops_ours": fl / t_ours / 1e12,
+           "fwd_tflops_torch": fl / t_torch / 1e12,
+           "fwd_bwd_us_ours": t_fb_ours * 1e6, "fwd_bwd_us_torch": t_fb_torch * 1e6}
+    t_lib = t_best(lambda: attn_bwd_library(qkv, o, lse, go, H), iters=10, rounds=3)
+    rec["bwd_us_library"] = t_lib * 1e6
+    if D == 64:
+        t_bwd = t_best(lambda: attn_bwd(qkv, o, lse, go, H), iters=10, rounds=3)
+        rec.update(bwd_us_ours=t_bwd * 1e6, bwd_tflops_ours=2.5 * fl / t_bwd / 1e12)
+    print(json.dumps(rec), flush=True)

@@ -207,8 +207,8 @@ if "gelu" in which:
     out(kernel="bias_gelu_tanh", fwd_us=t_f * 1e6, fwd_TBps=a.numel() * 4 / t_f / 1e12,
         bwd_us=t_b * 1e6, bwd_db_us=t_bd * 1e6, bwd_TBps=a.numel() * 6 / t_b / 1e12)
 if "lnab" in which:
-    # LayerNorm backward, wave-per-row-sequence (variant 0) vs pipelined (1), raw launcher
-    # (kernel + dgamma/dbeta column reduce); bytes = h + dy (+ dres) read + dx written
+    # LayerNorm backward, raw launcher (kernel + dgamma/dbeta column reduce); bytes = h + dy
+    # (+ dres) read + dx written
     from distributed_llm_backend_benchmark_amd.ops import _lib as L
     for rows, cols in ((16384, 768), (16384, 1024), (4096, 768)):
         h, dy, dres = rnd(rows, cols), rnd(rows, cols), rnd(rows, cols)
@@ -221,8 +221,7 @@ if "lnab" in which:
         dg, db = torch.empty(cols, device="cuda", dtype=torch.bfloat16), \
             torch.empty(cols, device="cuda", dtype=torch.bfloat16)
         res = {}
-        for var in (0, 1):
-            L.lib().dlbb_layernorm_bwd_set_variant(var)
+        for var in (0,):
             for with_res in (False, True):
                 def run():
                     L.check(L.lib().dlbb_layernorm_bwd(
@@ -232,14 +231,14 @@ if "lnab" in which:
                         L.stream(h.device)), "ln_bwd")
                 t = t_med(run, iters=50)
                 nb = rows * cols * 2 * (4 if with_res else 3)
-                res[f"v{var}_{'res' if with_res else 'nores'}"] = {
+                res[f"{'res' if with_res else 'nores'}"] = {
                     "us": round(t * 1e6, 2), "TBps": round(nb / t / 1e12, 3)}
-        L.lib().dlbb_layernorm_bwd_set_variant(1)
-        out(kernel="layernorm_bwd_ab", rows=rows, cols=cols, res=res)
+        out(kernel="layernorm_bwd", rows=rows, cols=cols, res=res)
 if "wgradfused" in which:
     # weight gradient at the GPT-2 shapes: separate split-K reduce pass vs in-launch combine
     # (both workgroup orders), accumulate into bf16 + fused bias (the training-step call)
     from distributed_llm_backend_benchmark_amd.ops import _lib as L
+    from distributed_llm_backend_benchmark_amd.ops import gemm as G
     from distributed_llm_backend_benchmark_amd.ops.gemm import (_wgrad_hip, _wgrad_hip256,
                                                                 _wgrad_hip_wide)
     for N, K in ((2304, 768), (768, 768), (3072, 768), (768, 3072)):
@@ -252,17 +251,17 @@ if "wgradfused" in which:
             if name == "t256" and N % 256 or name == "wide" and K % 256:
                 continue
             for mode in ("sep", "fused_split_major", "fused_tile_major"):
-                os.environ["DLBB_WGRAD_FUSED"] = "0" if mode == "sep" else "1"
+                G.set_wgrad_fused(mode != "sep")
                 L.lib().dlbb_gemm_wgrad_set_order(1 if mode == "fused_tile_major" else 0)
                 res[f"{name}_{mode}"] = round(t_med(
                     lambda: fn(dy, x, w_out, True, None, b_out), iters=30) * 1e6, 1)
-        os.environ["DLBB_WGRAD_FUSED"] = "1"
+        G.set_wgrad_fused(False)
         L.lib().dlbb_gemm_wgrad_set_order(1)
         out(kernel="wgrad_fused_reduce_ab", M=M, N=N, K=K, us=res,
             tflops={k: round(2 * M * N * K / v / 1e6, 1) for k, v in res.items()})
 if "memroof" in which:
-    # collective-path memory kernels against the HBM roofline: cast (every
-    # dtype pair, 3 variants) vs torch's copy, strided pack, chunk-copy flatten / list unpack,
+    # collective-path memory kernels against the HBM roofline:
+    # cast (every dtype pair) vs torch's copy, strided pack, chunk-copy flatten / list unpack,
     # chunk-copy with scale, n-way reduce — 64 MiB .. 1 GiB of source
     from distributed_llm_backend_benchmark_amd.ops import _lib as L
     from distributed_llm_backend_benchmark_amd.ops.elementwise import ChunkTable, ScaleTable
@@ -274,11 +273,7 @@ if "memroof" in which:
             x = rnd(n, dt=dts[si])
             y = torch.empty(n, device="cuda", dtype=dts[so])
             nb = n * (dts[si].itemsize + dts[so].itemsize)
-            res = {}
-            for var in (0, 1, 2, 3, 4, 5):
-                L.lib().dlbb_cast_set_variant(var)
-                res[f"v{var}"] = t_med(lambda: ops.cast(x, dts[so], out=y), iters=20)
-            L.lib().dlbb_cast_set_variant(5)
+            res = {"ours": t_med(lambda: ops.cast(x, dts[so], out=y), iters=20)}
             tt = t_med(lambda: y.copy_(x), iters=20)
             out(kernel="cast", src=si, dst=so, src_MiB=mib,
                 TBps={k: round(nb / v / 1e12, 3) for k, v in res.items()},
@@ -315,16 +310,11 @@ if "memroof" in which:
         t = t_med(st.run, iters=20)
         out(kernel="chunk_copy_scale_bf16_fp32", src_MiB=mib, TBps=round(n * 6 / t / 1e12, 3))
         srcs = [rnd(n // 8) for _ in range(8)]
-        L.lib().dlbb_reduce_set_variant(1)
-        t1 = t_med(lambda: ops.reduce_sum(srcs), iters=20)
-        L.lib().dlbb_reduce_set_variant(0)
         t = t_med(lambda: ops.reduce_sum(srcs), iters=20)
-        out(kernel="reduce_sum_8src", src_MiB=mib, TBps=round(9 * (n // 8) * 2 / t / 1e12, 3),
-            templated_TBps=round(9 * (n // 8) * 2 / t1 / 1e12, 3))
+        out(kernel="reduce_sum_8src", src_MiB=mib, TBps=round(9 * (n // 8) * 2 / t / 1e12, 3))
 if "splitred" in which:
-    # the weight-gradient split-K reduce alone (fp32 slabs -> bf16 dW += sum, + bias slabs), by
-    # variant (0 round-4 8-float form, 1 all slabs in flight + nt loads, 2 all in flight, plain)
-    # at the GPT-2 dW shapes and the splits the step uses; bytes = slabs read + dW read + written
+    # the weight-gradient split-K reduce alone (fp32 slabs -> bf16 dW += sum, + bias slabs; all
+    # slabs in flight, non-temporal loads) at the GPT-2 dW shapes and the splits the step uses; bytes = slabs read + dW read + written
     from distributed_llm_backend_benchmark_amd.ops import _lib as L
     for N, K, splits in ((2304, 768, (8, 9)), (768, 768, (6, 16)), (3072, 768, (6, 7, 9)),
                          (768, 3072, (6, 7))):
@@ -334,14 +324,12 @@ if "splitred" in which:
             o = torch.zeros(n, device="cuda", dtype=torch.bfloat16)
             ob = torch.zeros(nb, device="cuda", dtype=torch.bfloat16)
             res = {}
-            for var in (0, 1, 2):
-                L.lib().dlbb_split_reduce_set_variant(var)
+            for var in (0,):
                 t = t_med(lambda: L.check(L.lib().dlbb_split_reduce(
                     ws.data_ptr(), o.data_ptr(), 1, n, ob.data_ptr(), nb, sp, 1,
                     L.stream(ws.device)), "split_reduce"), iters=50)
                 nbytes = sp * (n + nb) * 4 + 2 * (n + nb) * 2
-                res[f"v{var}"] = {"us": round(t * 1e6, 2), "TBps": round(nbytes / t / 1e12, 3)}
-            L.lib().dlbb_split_reduce_set_variant(1)
+                res = {"us": round(t * 1e6, 2), "TBps": round(nbytes / t / 1e12, 3)}
             out(kernel="split_reduce", N=N, K=K, split=sp, res=res)
 if "wgradpp" in which:
     # GPT-2 dW shapes on the 256^2 ping-pong TN kernel with split-K over all tokens (fp32 slabs

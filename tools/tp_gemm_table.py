@@ -7,7 +7,7 @@ interleaved rounds, uniform random operands (CDNA guide §5.4 rules 24/25). One 
 ``--modes``: comma list of our-kernel variants to time: ``auto`` = the library dispatch
 (``DLBB_GEMM=mfma``), ``t128`` / ``t256`` force the tile, ``s<N>`` = set_stagger(N), ``v192`` =
 the 256 x 192 tile variant (N % 192 == 0 shapes only), ``v192p`` / ``v192p18`` = its persistent
-spread-store form (variant 2; 12 / 18 stores at the tile boundary), ``sk`` = Stream-K on 256²
+spread-store form (variant 2), ``sk`` = Stream-K on 256²
 tiles (grids below one round of the CUs only). ``--gpt2`` adds the GPT-2 forward GEMMs.
 """
 import argparse
@@ -90,15 +90,13 @@ def main():
         out = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
         ok = {"v192": gemm.mfma192_ok(M, N),
               "v192p": gemm.mfma192p_ok(M, N, K, True),
-              "v192p18": gemm.mfma192p_ok(M, N, K, True),
               "sk": gemm.streamk_ok(x, w)}
         ms = [m for m in modes if ok.get(m, True)]
 
         def run(m):
             if m == "v192":      # 256 x 192 tiles (variant 1)
                 return gemm._mfma192_linear(x, w, None, None, None, out, None)
-            if m in ("v192p", "v192p18"):   # persistent, spread C stores (variant 2)
-                _lib.lib().dlbb_gemm_set_spread_early(18 if m == "v192p18" else 12)
+            if m == "v192p":     # persistent, spread C stores (variant 2)
                 return gemm._mfma192p_linear(x, w, None, None, None, out, None)
             if m == "sk":                 # Stream-K ping-pong, in-launch combine
                 return gemm._mfma_streamk_linear(x, w, None, None, None, out, None)
