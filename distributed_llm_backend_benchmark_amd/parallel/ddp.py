@@ -363,9 +363,8 @@ class FlatParamTrainer:
             self._recheck_side_streams()
 
     def _recheck_side_streams(self) -> None:
-        """Warm-up check (starts of steps 2 and 3, and once after a runner's warm-up) that every
-        weight-gradient stream still runs beside the
-        stream the step runs on. A run whose compute stream waited, after every forked-from
+        """Warm-up check (once after a runner's warm-up steps, never inside the timed loop) that
+        every weight-gradient stream still runs beside the stream the step runs on. A run whose compute stream waited, after every forked-from
         kernel, for exactly the side stream's weight-gradient + reduce kernels — the in-order
         execution of two streams sharing one hardware queue — took 19-19.6 ms instead of
         17.3-18 (profiles/r05_step/SUMMARY.md §12); a serialised side stream is replaced by a

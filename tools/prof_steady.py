@@ -6,6 +6,16 @@ dispatches after the N-th completion of a marker kernel (e.g. the optimizer's Ad
 GPT-2 step with the split optimizer) and prints per kernel: calls, total / mean µs, share of the
 window's GPU time, plus the share of hipBLASLt (``Cijk_*``) kernels.
 
+The side-stream probes (parallel/streams.py: 1-workgroup ``spin`` kernels that check a side
+stream still runs beside the compute stream) run during the warm-up and once after it, never in
+the timed loop; the window starts after the LAST probe dispatch as well, and
+``probes_in_window`` says whether any probe was still inside it.
+
+Queue map: rocprofv3's kernel trace records the hardware queue (``Queue_Id``) and the HIP stream
+(``Stream_Id``) of every dispatch. Two streams that were meant to overlap but show ONE queue id
+execute in order (the stream-to-queue serialisation of profiles/r05_step/SUMMARY.md §12); the
+``queues`` summary lists, per queue, the streams it served in the window and their busy time.
+
     python tools/prof_steady.py TRACE.csv --marker adamw_kernel --skip 6 [--csv OUT.csv]
 """
 
@@ -16,7 +26,20 @@ import sys
 from collections import defaultdict
 
 
-def steady(path, marker, skip):
+def _queue_map(win):
+    """Per hardware queue: the streams it served and their busy time in the window."""
+    if not win or "Queue_Id" not in win[0]:
+        return None
+    q = defaultdict(lambda: defaultdict(lambda: [0, 0]))
+    for r in win:
+        a = q[r["Queue_Id"]][r.get("Stream_Id", "?")]
+        a[0] += 1
+        a[1] += int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+    return {qid: {sid: {"dispatches": v[0], "busy_ms": round(v[1] / 1e6, 3)}
+                  for sid, v in streams.items()} for qid, streams in sorted(q.items())}
+
+
+def steady(path, marker, skip, probe="spin"):
     rows = list(csv.DictReader(open(path)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     t0 = None
@@ -29,7 +52,18 @@ def steady(path, marker, skip):
                 break
     if t0 is None:
         raise SystemExit(f"marker {marker!r} seen {seen} times, fewer than --skip {skip}")
+    probes = [r for r in rows if probe and probe in r["Kernel_Name"]]
+    skipped_markers = 0
+    if probes:
+        # start after the last probe too; a probe after t0 is the post-warm-up re-check, and the
+        # marker completions it pushes out of the window are reported
+        t_probe = max(int(r["End_Timestamp"]) for r in probes)
+        if t_probe > t0:
+            skipped_markers = sum(1 for r in rows if marker in r["Kernel_Name"]
+                                  and t0 < int(r["End_Timestamp"]) <= t_probe)
+            t0 = t_probe
     win = [r for r in rows if int(r["Start_Timestamp"]) >= t0]
+    n_probe_win = sum(1 for r in win if probe and probe in r["Kernel_Name"])    # 0 by design
     agg = defaultdict(lambda: [0, 0])
     for r in win:
         a = agg[r["Kernel_Name"]]
@@ -43,7 +77,9 @@ def steady(path, marker, skip):
     cijk = sum(d["total_us"] for d in out if "Cijk" in d["name"])
     return out, {"window_dispatches": len(win), "gpu_time_ms": total / 1e6,
                  "window_wall_ms": span / 1e6, "cijk_pct": round(100 * cijk * 1e3 / total, 2)
-                 if total else None, "marker": marker, "skip": skip}
+                 if total else None, "marker": marker, "skip": skip,
+                 "probes_in_window": n_probe_win, "markers_skipped_for_probes": skipped_markers,
+                 "queues": _queue_map(win)}
 
 
 def main():
@@ -53,8 +89,10 @@ def main():
     ap.add_argument("--skip", type=int, required=True)
     ap.add_argument("--csv", default=None)
     ap.add_argument("--top", type=int, default=25)
+    ap.add_argument("--probe", default="spin",
+                    help="name fragment of the side-stream probe kernel ('' = keep probes)")
     a = ap.parse_args()
-    out, summ = steady(a.trace, a.marker, a.skip)
+    out, summ = steady(a.trace, a.marker, a.skip, a.probe)
     print(json.dumps(summ))
     for d in out[:a.top]:
         print(f"{d['pct']:6.2f}%  {d['calls']:6d}  {d['mean_us']:9.2f} us  {d['name'][:110]}")
