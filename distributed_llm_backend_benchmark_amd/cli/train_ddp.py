@@ -97,6 +97,24 @@ def _path_counts(tr) -> dict:
     return out
 
 
+def _stream_roles(tr, comm) -> dict:
+    """hipStream_t handles of the step's streams by role, plus every probed candidate, so a
+    rocprofv3 kernel trace (Stream_Id / Queue_Id per dispatch) can be read by role."""
+    if not comm.is_gpu:
+        return {}
+    import torch
+
+    from ..parallel import streams as S
+
+    def h(s):
+        return hex(s.cuda_stream) if s is not None else None
+    return {"compute": h(torch.cuda.current_stream(comm.device)),
+            "wgrad": [h(s) for s in getattr(tr, "_wgrad_streams", []) or []],
+            "comm": h(getattr(tr, "_comm_stream", None)),
+            "opt": h(getattr(tr, "_opt_stream", None)),
+            "probed": list(S.LOG)}
+
+
 def run(args, comm, overlap: bool):
     import torch
 
@@ -187,6 +205,7 @@ def _train(args, comm, tr, model, cfg):
         # per-bucket AdamW during backward (parallel/ddp.py _OPT_OVERLAP; 0 = after backward)
         "opt_overlap": getattr(tr, "opt_overlap", 0),
         "side_stream_checks": getattr(tr, "side_stream_checks", []),
+        "streams": _stream_roles(tr, comm),
     }
     if args.comm_timeline and not args.zero:
         tr.timeline = True

@@ -18,11 +18,7 @@ namespace dlbb {
 // both): every wave instruction covers one contiguous 512 B / 1 KiB span. U such vectors per
 // lane are loaded before any is stored (U x 16 B in flight per lane), block-contiguous tiles of
 // 256 x U vectors, grid-stride over tiles. NT: non-temporal stores (a streaming destination is
-// not re-read by this kernel). Round 6 (profiles/r06_kernels/memroof_variants.jsonl, TB/s at
-// 64 MiB / 256 MiB / 1 GiB, torch copy in brackets): bf16 -> fp32 6.83 (6.89) / 6.95 (5.86) /
-// 5.57 (5.84), fp32 -> bf16 6.61 (6.70) / 6.67 (5.84) / 5.65 (5.89) with U = 8 and NT stores,
-// the best or within 2 % of the best of U 4 / 8 / 16, plain / NT stores, NT loads at every size
-// but 1 GiB, where torch's copy stays 4 % ahead; plain stores lost 20 % at 256 MiB.
+// not re-read by this kernel). U, NT and the grid cap per dtype pair and size: launch_cast.
 template <int DT, int E>
 struct VecIO;
 template <>
@@ -185,19 +181,42 @@ __global__ void __launch_bounds__(256) pack2_kernel(const void* __restrict__ src
     }
   }
 }
+// Launch policy from the grid-shape A/B of these kernels (profiles/r06_kernels/
+// memroof_grid_ab.jsonl, TB/s at 64 MiB / 1 GiB of source): past the MALL a one-tile-per-
+// workgroup grid beats the 4096-workgroup grid-stride form by 5-17 % (bf16 -> fp32 6.48 vs 5.55,
+// torch's copy 5.83); widening casts take non-temporal stores at every size (U = 2: 6.93 / 6.48),
+// narrowing ones U = 8 + NT below the MALL (6.67) and U = 2 plain above it (5.94 vs torch 5.87),
+// same-width copies U = 2 plain (6.70 / 5.84).
+template <int DTI, int DTO, int U, bool NT>
+static void launch_cast2(const void* s, void* d, int64_t n, int64_t cap, hipStream_t st) {
+  constexpr int E = cast_vec<DTI, DTO>();
+  int64_t g = (n / E + 256 * U - 1) / (256 * U);
+  g = g < 1 ? 1 : g;
+  if (cap > 0 && g > cap) g = cap;
+  if (g > (int64_t{1} << 30)) g = int64_t{1} << 30;    // grid-stride beyond
+  hipLaunchKernelGGL((cast2_kernel<DTI, DTO, U, NT>), dim3(static_cast<unsigned>(g)), dim3(256),
+                     0, st, s, d, n);
+}
+
 template <int DTI, int DTO>
 static hipError_t launch_cast(const void* s, void* d, int64_t n, hipStream_t st) {
   const int block = 256;
-  constexpr int E = cast_vec<DTI, DTO>(), U = 8;
   const uintptr_t align = reinterpret_cast<uintptr_t>(s) | reinterpret_cast<uintptr_t>(d);
   if (align & 15) {       // a view not 16-B aligned: one element per lane
     hipLaunchKernelGGL((cast_scalar_kernel<DTI, DTO>), dim3(stream_grid(n, block)), dim3(block),
                        0, st, s, d, n);
     return hipGetLastError();
   }
-  int64_t g = (n / E + 256 * U - 1) / (256 * U);
-  g = g < 1 ? 1 : (g > 4096 ? 4096 : g);
-  hipLaunchKernelGGL((cast2_kernel<DTI, DTO, U, true>), dim3(g), dim3(block), 0, st, s, d, n);
+  constexpr int ei = Elem<DTI>::kBytes, eo = Elem<DTO>::kBytes;
+  const bool big = n * ei > (int64_t{256} << 20);       // past the 256-MB MALL
+  if constexpr (eo > ei) {
+    launch_cast2<DTI, DTO, 2, true>(s, d, n, big ? 0 : 16384, st);
+  } else if constexpr (eo < ei) {
+    if (big) launch_cast2<DTI, DTO, 2, false>(s, d, n, 0, st);
+    else launch_cast2<DTI, DTO, 8, true>(s, d, n, 4096, st);
+  } else {
+    launch_cast2<DTI, DTO, 2, false>(s, d, n, big ? 0 : 4096, st);
+  }
   return hipGetLastError();
 }
 
@@ -211,20 +230,20 @@ static hipError_t launch_pack(const void* s, void* d, int64_t rows, int64_t cols
   const int64_t work = rows * (vec_ok ? cols / 8 : cols);
   const int block = 256;
   if (vec_ok) {
-    // round 6 (memroof_variants.jsonl): 6.49 / 5.22 / 5.24 TB/s at 64 MiB / 256 MiB / 1 GiB vs
-    // the flat kernel's 6.33 / 5.19 / 5.07; non-temporal stores for destinations past half the
-    // MALL (the cast's measured gain at 256 MiB)
-    constexpr int R = 4;
+    // grid-shape A/B (profiles/r06_kernels/memroof_grid_ab.jsonl, QKV column slice): one row
+    // per lane-group and one tile per workgroup below 128 MiB of destination (64 MiB: 6.84 TB/s
+    // vs torch's strided copy 6.21), 4 rows in flight + non-temporal stores past it (1 GiB:
+    // 5.68 vs 5.79 — the one size torch's copy still leads); both on the uncapped grid
     const int64_t gx = (cols / 8 + 255) / 256;
-    int64_t gy = (rows + R - 1) / R;
-    const int64_t gy_cap = (4096 + gx - 1) / gx;     // ~4096 workgroups in all
-    gy = gy < gy_cap ? gy : gy_cap;
+    const bool big = rows * cols * eo >= (int64_t{128} << 20);
+    const int R = big ? 4 : 1;
+    const int64_t gy = (rows + R - 1) / R;
     const dim3 gd(static_cast<unsigned>(gx), static_cast<unsigned>(gy < 65535 ? gy : 65535));
-    if (rows * cols * eo >= (int64_t{128} << 20))
-      hipLaunchKernelGGL((pack2_kernel<DTI, DTO, R, true>), gd, dim3(block), 0, st, s, d, rows,
+    if (big)
+      hipLaunchKernelGGL((pack2_kernel<DTI, DTO, 4, true>), gd, dim3(block), 0, st, s, d, rows,
                          cols, lds, ldd);
     else
-      hipLaunchKernelGGL((pack2_kernel<DTI, DTO, R, false>), gd, dim3(block), 0, st, s, d, rows,
+      hipLaunchKernelGGL((pack2_kernel<DTI, DTO, 1, false>), gd, dim3(block), 0, st, s, d, rows,
                          cols, lds, ldd);
     return hipGetLastError();
   }

@@ -516,6 +516,16 @@ def _tile_counters(device: torch.device, n: int) -> torch.Tensor:
     return buf
 
 
+# Cap on the default split-K of the weight gradient (None: no cap). The default fills about one
+# resident wave when the kernel has the chip; beside the main stream's backward a smaller split
+# writes and re-reads fewer fp32 partials (A/B: tools/wgrad_split_step_ab.py).
+_WGRAD_SPLIT_CAP = [None]
+
+
+def set_wgrad_split_cap(cap: Optional[int]) -> None:
+    _WGRAD_SPLIT_CAP[0] = None if cap is None else max(1, int(cap))
+
+
 def _wgrad_hip(dy2, x2, out, accumulate, split=None, bias_out=None, bn=128, bk=128):
     M, N = dy2.shape
     K = x2.shape[1]
@@ -528,6 +538,8 @@ def _wgrad_hip(dy2, x2, out, accumulate, split=None, bias_out=None, bn=128, bk=1
         # whole workgroup time)
         split = max(1, min(M // 256, (-(-768 // tiles)) if bn == bk == 128
                            else max(1, 512 // tiles)))
+        if _WGRAD_SPLIT_CAP[0] is not None:
+            split = min(split, _WGRAD_SPLIT_CAP[0])
     # one split, plain store, no bias: the kernel stores dW itself (no fp32 partials, no
     # reduce pass — the LM-head dW)
     direct = split == 1 and not accumulate and bias_out is None

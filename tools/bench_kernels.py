@@ -11,7 +11,9 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from distributed_llm_backend_benchmark_amd import ops  # noqa: E402
 
 
-def t_med(fn, iters=20, warm=3):
+def t_med(fn, iters=20, warm=3, batch=1):
+    """Median seconds per call; ``batch`` calls back to back per event pair (steady clocks for
+    short memory-bound kernels, as they run inside a collective's staging)."""
     for _ in range(warm):
         fn()
     torch.cuda.synchronize()
@@ -19,10 +21,11 @@ def t_med(fn, iters=20, warm=3):
     for _ in range(iters):
         s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         s.record()
-        fn()
+        for _ in range(batch):
+            fn()
         e.record()
         e.synchronize()
-        ts.append(s.elapsed_time(e) * 1e-3)
+        ts.append(s.elapsed_time(e) * 1e-3 / batch)
     ts.sort()
     return ts[len(ts) // 2]
 
@@ -267,14 +270,15 @@ if "memroof" in which:
     from distributed_llm_backend_benchmark_amd.ops.elementwise import ChunkTable, ScaleTable
     dts = {"bf16": torch.bfloat16, "fp16": torch.float16, "fp32": torch.float32}
     for mib in (64, 256, 1024):
+        MB = 10 if mib <= 256 else 4
         for si, so in (("bf16", "fp32"), ("fp32", "bf16"), ("fp16", "fp32"), ("fp32", "fp16"),
                        ("bf16", "fp16"), ("bf16", "bf16"), ("fp32", "fp32")):
             n = (mib << 20) // dts[si].itemsize
             x = rnd(n, dt=dts[si])
             y = torch.empty(n, device="cuda", dtype=dts[so])
             nb = n * (dts[si].itemsize + dts[so].itemsize)
-            res = {"ours": t_med(lambda: ops.cast(x, dts[so], out=y), iters=20)}
-            tt = t_med(lambda: y.copy_(x), iters=20)
+            res = {"ours": t_med(lambda: ops.cast(x, dts[so], out=y), iters=15, batch=MB)}
+            tt = t_med(lambda: y.copy_(x), iters=15, batch=MB)
             out(kernel="cast", src=si, dst=so, src_MiB=mib,
                 TBps={k: round(nb / v / 1e12, 3) for k, v in res.items()},
                 torch_copy_TBps=round(nb / tt / 1e12, 3))
@@ -283,8 +287,8 @@ if "memroof" in which:
         rows = (mib << 20) // (2 * cols)
         src = rnd(rows, 3 * cols)
         dst = torch.empty(rows, cols, device="cuda", dtype=torch.bfloat16)
-        t = t_med(lambda: ops.pack_rows(src[:, :cols], out=dst), iters=20)
-        tt = t_med(lambda: dst.copy_(src[:, :cols]), iters=20)
+        t = t_med(lambda: ops.pack_rows(src[:, :cols], out=dst), iters=15, batch=MB)
+        tt = t_med(lambda: dst.copy_(src[:, :cols]), iters=15, batch=MB)
         nb = rows * cols * 4
         out(kernel="pack_rows", src_MiB=mib, TBps=round(nb / t / 1e12, 3),
             torch_copy_TBps=round(nb / tt / 1e12, 3))
@@ -294,23 +298,23 @@ if "memroof" in which:
         outs = [torch.empty(n // 8, device="cuda", dtype=torch.bfloat16) for _ in range(8)]
         tab = ChunkTable([(flat[i * (n // 8):(i + 1) * (n // 8)], outs[i]) for i in range(8)])
         L.lib().dlbb_chunk_copy_set_nt(0)
-        t = t_med(tab.run, iters=20)
+        t = t_med(tab.run, iters=15, batch=MB)
         L.lib().dlbb_chunk_copy_set_nt(1)
-        tnt = t_med(tab.run, iters=20)
+        tnt = t_med(tab.run, iters=15, batch=MB)
         L.lib().dlbb_chunk_copy_set_nt(2)
-        tauto = t_med(tab.run, iters=20)
+        tauto = t_med(tab.run, iters=15, batch=MB)
         tt = t_med(lambda: [o.copy_(flat[i * (n // 8):(i + 1) * (n // 8)])
-                            for i, o in enumerate(outs)], iters=20)
+                            for i, o in enumerate(outs)], iters=15, batch=MB)
         out(kernel="chunk_copy", src_MiB=mib, chunks=tab.nchunks,
             TBps=round(2 * n * 2 / t / 1e12, 3), nt_TBps=round(2 * n * 2 / tnt / 1e12, 3),
             auto_TBps=round(2 * n * 2 / tauto / 1e12, 3),
             torch_8copies_TBps=round(2 * n * 2 / tt / 1e12, 3))
         g32 = torch.empty(n, device="cuda")
         st = ScaleTable([(flat, g32)], 0.125)
-        t = t_med(st.run, iters=20)
+        t = t_med(st.run, iters=15, batch=MB)
         out(kernel="chunk_copy_scale_bf16_fp32", src_MiB=mib, TBps=round(n * 6 / t / 1e12, 3))
         srcs = [rnd(n // 8) for _ in range(8)]
-        t = t_med(lambda: ops.reduce_sum(srcs), iters=20)
+        t = t_med(lambda: ops.reduce_sum(srcs), iters=15, batch=MB)
         out(kernel="reduce_sum_8src", src_MiB=mib, TBps=round(9 * (n // 8) * 2 / t / 1e12, 3))
 if "splitred" in which:
     # the weight-gradient split-K reduce alone (fp32 slabs -> bf16 dW += sum, + bias slabs; all
