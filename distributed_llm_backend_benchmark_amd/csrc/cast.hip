@@ -186,7 +186,7 @@ __global__ void __launch_bounds__(256) pack2_kernel(const void* __restrict__ src
 // workgroup grid beats the 4096-workgroup grid-stride form by 5-17 % (bf16 -> fp32 6.48 vs 5.55,
 // torch's copy 5.83); widening casts take non-temporal stores at every size (U = 2: 6.93 / 6.48),
 // narrowing ones U = 8 + NT below the MALL (6.67) and U = 2 plain above it (5.94 vs torch 5.87),
-// same-width copies U = 2 plain (6.70 / 5.84).
+// same-width copies U = 2 plain (6.70 / 5.84) except between 128 and 256 MiB (U = 8 + NT).
 template <int DTI, int DTO, int U, bool NT>
 static void launch_cast2(const void* s, void* d, int64_t n, int64_t cap, hipStream_t st) {
   constexpr int E = cast_vec<DTI, DTO>();
@@ -214,6 +214,10 @@ static hipError_t launch_cast(const void* s, void* d, int64_t n, hipStream_t st)
   } else if constexpr (eo < ei) {
     if (big) launch_cast2<DTI, DTO, 2, false>(s, d, n, 0, st);
     else launch_cast2<DTI, DTO, 8, true>(s, d, n, 4096, st);
+  } else if (n * ei > (int64_t{128} << 20) && !big) {
+    // same width, source + destination past the MALL but the source within it: NT stores
+    // (256 MiB: 6.94 TB/s vs 5.50 plain, memroof_batched_*.jsonl)
+    launch_cast2<DTI, DTO, 8, true>(s, d, n, 4096, st);
   } else {
     launch_cast2<DTI, DTO, 2, false>(s, d, n, big ? 0 : 4096, st);
   }
