@@ -113,27 +113,24 @@ __device__ __forceinline__ int vswz_d(int r) { return D == 64 ? vswz(r) : ((r & 
 // SIMD). Round 6 measured a software-pipelined body (QK^T of tile j+1 and PV of tile j-1 beside
 // the softmax of tile j in one straight block): 75.1 vs 56.5 us at the GPT-2 shape — its 212
 // VGPRs left 2 waves per SIMD, and the hardware's interleave of 4 waves beat the compiler's
-// in-wave interleave (profiles/r06_kernels/attn_fwd_pipelined_ab.jsonl); removed.
-template <int D, int NW, int NS>
-__global__ void __launch_bounds__(64 * NW, 2) attn_fwd_kernel(AttnArgs a) {
-  // NS-deep K/V ring: NS = 2 reads LDS through the builtins (the compiler then drains the
-  // in-flight DMA before the first V read); NS = 3 through inline asm with its own counted
-  // waits, so tile kt+1's DMA stays in flight across tile kt
-  constexpr bool kAsm = NS > 2;
+// in-wave interleave (profiles/r06_kernels/attn_fwd_pipelined_ab.jsonl); removed. Also measured
+// and removed (commit 62e38ff, profiles/r06_kernels/attn_fwd_shape_ab.jsonl, bit-identical
+// outputs): 8 waves / 256 queries per workgroup sharing each K/V tile (55.97 vs 50.81 us at the
+// GPT-2 shape; 84 vs 58 at D = 128) and a 3-deep K/V ring with asm LDS reads and counted waits,
+// so no DMA drain at the first V read (59.3 us): this loop is not DMA-latency bound.
+template <int D>
+__global__ void __launch_bounds__(kAttnThreads, 2) attn_fwd_kernel(AttnArgs a) {
   using G = FwdGeo<D>;
   constexpr int KB = G::KB, ROW = G::ROW, RPI = G::RPI, TILE = G::TILE;
-  constexpr int WROWS = KB / NW;                  // image rows staged per wave
-  constexpr int NI = WROWS / RPI;                 // DMA wave-instructions per image per wave
-  constexpr int QB = 32 * NW;                     // queries per workgroup
-  static_assert(NI >= 1 && WROWS % RPI == 0, "tile rows per wave");
+  constexpr int WROWS = KB / 4;                   // image rows staged per wave
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int nqb = (a.T + QB - 1) / QB;
+  const int nqb = (a.T + kQB - 1) / kQB;
   int blk, h, b;
   head_block(a.xcd, blk, h, b);
   const int qb = nqb - 1 - blk;                   // heaviest first
-  const int q0 = qb * QB;
+  const int q0 = qb * kQB;
   const int qw = q0 + wave * 32;                  // this wave's first query
   const int r = lane & 31, hi = lane >> 5;
   const uint16_t* base_bt = a.qkv + static_cast<int64_t>(b) * a.T * a.ld;
@@ -157,7 +154,7 @@ __global__ void __launch_bounds__(64 * NW, 2) attn_fwd_kernel(AttnArgs a) {
   float m = -INFINITY, l = 0.f;
   const int qme = qw + r;                          // this lane's query
   const int q_hi = qw + 31;                        // wave's last query
-  const int last_key = (q0 + QB - 1) < (a.T - 1) ? (q0 + QB - 1) : (a.T - 1);
+  const int last_key = (q0 + kQB - 1) < (a.T - 1) ? (q0 + kQB - 1) : (a.T - 1);
   const int nt = last_key / KB + 1;
 
   auto tileK = [&](int c) { return smem + c * 2 * TILE; };
@@ -166,9 +163,9 @@ __global__ void __launch_bounds__(64 * NW, 2) attn_fwd_kernel(AttnArgs a) {
   // DMA: this lane's sources of image rows wave * WROWS + i * RPI + lane / (ROW / 16) of key
   // tile 0 (K and V sections, swizzled chunk); tile kt adds kt * KB rows, uniform
   const int r_in = lane / (ROW / 16), slot = lane % (ROW / 16);
-  const uint16_t* dsrc[2 * NI];
+  const uint16_t* dsrc[4];
 #pragma unroll
-  for (int i = 0; i < NI; ++i) {
+  for (int i = 0; i < 2; ++i) {
     const int row = wave * WROWS + i * RPI + r_in;
     const uint16_t* src = base_bt + static_cast<int64_t>(row) * a.ld + hoff;
     dsrc[2 * i] = src + D * a.H + (slot ^ kswz_d<D>(row)) * 8;
@@ -178,14 +175,14 @@ __global__ void __launch_bounds__(64 * NW, 2) attn_fwd_kernel(AttnArgs a) {
     if (k0 + KB <= a.T) {                          // wave-uniform: no row past T
       const int64_t off = static_cast<int64_t>(k0) * a.ld;
 #pragma unroll
-      for (int i = 0; i < NI; ++i) {
+      for (int i = 0; i < 2; ++i) {
         attn_glds16(dsrc[2 * i] + off, tk + (wave * WROWS + i * RPI) * ROW);
         attn_glds16(dsrc[2 * i + 1] + off, tv + (wave * WROWS + i * RPI) * ROW);
       }
       return;
     }
 #pragma unroll
-    for (int i = 0; i < NI; ++i) {                 // rows past T clamped (scores masked)
+    for (int i = 0; i < 2; ++i) {                  // rows past T clamped (scores masked)
       const int row = wave * WROWS + i * RPI + r_in;
       int key = k0 + row;
       key = key < a.T ? key : a.T - 1;
@@ -196,19 +193,14 @@ __global__ void __launch_bounds__(64 * NW, 2) attn_fwd_kernel(AttnArgs a) {
                   tv + (wave * WROWS + i * RPI) * ROW);
     }
   };
-#pragma unroll
-  for (int i = 0; i < NS - 1; ++i)
-    if (i < nt) stage(i * KB, tileK(i), tileV(i));
-  int cur = 0, nxt = NS - 1;                       // ring slots of tile kt and tile kt+NS-1
+  stage(0, tileK(0), tileV(0));
   for (int kt = 0; kt < nt; ++kt) {
+    const int cur = kt & 1;
     // one barrier per tile: it both publishes tile kt (every wave's DMA retired) and frees
-    // the slot of tile kt-1 (every wave finished it), so the restage goes right after it
-    if (NS > 2 && kt + 1 < nt)
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NI) : "memory");   // tile kt+1 in flight
-    else
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // buffer cur^1 (every wave finished tile kt-1), so the restage goes right after it
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-    if (kt + NS - 1 < nt) stage((kt + NS - 1) * KB, tileK(nxt), tileV(nxt));
+    if (kt + 1 < nt) stage((kt + 1) * KB, tileK(cur ^ 1), tileV(cur ^ 1));
     const int k0 = kt * KB;
     if (k0 <= q_hi) {                               // wave-uniform: tile has keys <= a query
       const char* tk = tileK(cur);
@@ -220,25 +212,12 @@ __global__ void __launch_bounds__(64 * NW, 2) attn_fwd_kernel(AttnArgs a) {
 #pragma unroll
         for (int e = 0; e < 16; ++e) s[kk][e] = 0.f;
         const int row = kk * 32 + r;
-        if constexpr (kAsm) {
-          f32x4 kr[G::NKS];
 #pragma unroll
-          for (int ks = 0; ks < G::NKS; ++ks)
-            kr[ks] = ds_read_b128_asm(tk + row * ROW + (((2 * ks + hi) ^ kswz_d<D>(row)) << 4));
-          if constexpr (G::NKS == 4) tr_wait(kr[0], kr[1], kr[2], kr[3]);
-          else tr_wait(kr[0], kr[1], kr[2], kr[3], kr[4], kr[5], kr[6], kr[7]);
-#pragma unroll
-          for (int ks = 0; ks < G::NKS; ++ks)
-            s[kk] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, kr[ks]),
-                                                            qf[ks], s[kk], 0, 0, 0);
-        } else {
-#pragma unroll
-          for (int ks = 0; ks < G::NKS; ++ks) {
-            const int c = 2 * ks + hi;
-            const bf16x8 kf =
-                *reinterpret_cast<const bf16x8*>(tk + row * ROW + ((c ^ kswz_d<D>(row)) << 4));
-            s[kk] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[ks], s[kk], 0, 0, 0);
-          }
+        for (int ks = 0; ks < G::NKS; ++ks) {
+          const int c = 2 * ks + hi;
+          const bf16x8 kf =
+              *reinterpret_cast<const bf16x8*>(tk + row * ROW + ((c ^ kswz_d<D>(row)) << 4));
+          s[kk] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[ks], s[kk], 0, 0, 0);
         }
       }
       // ---- scale, causal mask, online softmax (lane = one query; keys in registers)
@@ -288,32 +267,6 @@ __global__ void __launch_bounds__(64 * NW, 2) attn_fwd_kernel(AttnArgs a) {
 #pragma unroll
           for (int j = 0; j < 8; ++j)
             pf[j] = __builtin_bit_cast(short, static_cast<__bf16>(s[kk][8 * st + j]));
-          if constexpr (kAsm) {
-            i16x4 vt[G::NDT][2];
-#pragma unroll
-            for (int dt = 0; dt < G::NDT; ++dt)
-#pragma unroll
-              for (int half = 0; half < 2; ++half) {
-                const int row = kk * 32 + 16 * st + 8 * half + 4 * (g >> 1) + tq;
-                const int col = dt * 32 + 16 * (g & 1) + 4 * tp;
-                vt[dt][half] = ds_read_tr16(tv + row * ROW +
-                                            (((col >> 3) ^ vswz_d<D>(row)) << 4) + (col & 7) * 2);
-              }
-            if constexpr (G::NDT == 2) tr_wait(vt[0][0], vt[0][1], vt[1][0], vt[1][1]);
-            else tr_wait(vt[0][0], vt[0][1], vt[1][0], vt[1][1], vt[2][0], vt[2][1], vt[3][0],
-                         vt[3][1]);
-#pragma unroll
-            for (int dt = 0; dt < G::NDT; ++dt) {
-              bf16x8 vf;
-#pragma unroll
-              for (int u = 0; u < 4; ++u) {
-                vf[u] = vt[dt][0][u];
-                vf[4 + u] = vt[dt][1][u];
-              }
-              o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf, o[dt], 0, 0, 0);
-            }
-            continue;
-          }
 #pragma unroll
           for (int dt = 0; dt < G::NDT; ++dt) {
             bf16x8 vf;
@@ -335,8 +288,6 @@ __global__ void __launch_bounds__(64 * NW, 2) attn_fwd_kernel(AttnArgs a) {
           }
         }
     }
-    cur = cur + 1 == NS ? 0 : cur + 1;
-    nxt = nxt + 1 == NS ? 0 : nxt + 1;
   }
 
   // ---- finalize: l over both lane halves, O / l, store O [B,T,H,D] and LSE
@@ -798,13 +749,6 @@ using namespace dlbb;
 
 static int g_attn_xcd = 1;   // A/B switch for the XCD-aware block order (dlbb_attn_set_xcd)
 DLBB_API void dlbb_attn_set_xcd(int on) { g_attn_xcd = on ? 1 : 0; }
-// forward shape A/B: waves per workgroup (4: 128 queries; 8: 256 queries sharing each K/V
-// tile) and K/V ring depth (2 or 3 tiles)
-static int g_attn_fwd_nw = 4, g_attn_fwd_ns = 2;
-DLBB_API void dlbb_attn_set_fwd_shape(int nw, int ns) {
-  g_attn_fwd_nw = nw == 8 ? 8 : 4;
-  g_attn_fwd_ns = ns == 3 ? 3 : 2;
-}
 
 // qkv: [B, T, 3, H, D] bf16, D = 64 or 128 (token row stride ld elements, 16-B aligned rows);
 // out: [B, T, H, D] bf16 (row stride ldo); lse: [B, H, T] fp32 (may be null). Causal only.
@@ -818,17 +762,13 @@ DLBB_API int dlbb_attn_fwd(const void* qkv, int64_t ld, void* out, int64_t ldo, 
   if (ld < 3 * H * D || ldo < H * D) return hipErrorInvalidValue;
   AttnArgs a{static_cast<const uint16_t*>(qkv), static_cast<uint16_t*>(out), lse, ld, ldo,
              B, T, H, scale * 1.4426950408889634f, g_attn_xcd};
-  const int nw = g_attn_fwd_nw, ns = g_attn_fwd_ns;
-  const dim3 grid((T + 32 * nw - 1) / (32 * nw), H, B);
-#define DLBB_FWD(DD, NW_, NS_)                                                                 \
-  if (D == DD && nw == NW_ && ns == NS_) {                                                    \
-    hipLaunchKernelGGL((attn_fwd_kernel<DD, NW_, NS_>), grid, dim3(64 * NW_),                 \
-                       NS_ * 2 * FwdGeo<DD>::TILE, stream, a);                                 \
-    return hipGetLastError();                                                                 \
-  }
-  DLBB_FWD(64, 4, 2) DLBB_FWD(64, 8, 2) DLBB_FWD(64, 4, 3) DLBB_FWD(64, 8, 3)
-  DLBB_FWD(128, 4, 2) DLBB_FWD(128, 8, 2) DLBB_FWD(128, 4, 3) DLBB_FWD(128, 8, 3)
-#undef DLBB_FWD
+  const dim3 grid((T + kQB - 1) / kQB, H, B);
+  if (D == 64)
+    hipLaunchKernelGGL(attn_fwd_kernel<64>, grid, dim3(kAttnThreads), 4 * FwdGeo<64>::TILE,
+                       stream, a);
+  else
+    hipLaunchKernelGGL(attn_fwd_kernel<128>, grid, dim3(kAttnThreads), 4 * FwdGeo<128>::TILE,
+                       stream, a);
   return hipGetLastError();
 }
 

@@ -518,7 +518,8 @@ def _tile_counters(device: torch.device, n: int) -> torch.Tensor:
 
 # Cap on the default split-K of the weight gradient (None: no cap). The default fills about one
 # resident wave when the kernel has the chip; beside the main stream's backward a smaller split
-# writes and re-reads fewer fp32 partials (A/B: tools/wgrad_split_step_ab.py).
+# writes and re-reads fewer fp32 partials — but measured slower in the step at every cap
+# (tools/step_ab.py split_cap=N, profiles/r06_step/wgrad_split_cap_ab.jsonl); default no cap.
 _WGRAD_SPLIT_CAP = [None]
 
 
