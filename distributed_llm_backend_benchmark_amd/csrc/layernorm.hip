@@ -352,16 +352,15 @@ __global__ void __launch_bounds__(64 * WPB) ln_bwd_pipe_kernel(LnBwdArgs a) {
   }
 }
 
-// out[c] = sum_b part[b * rstride + c]  (fp32 accumulate, out in bf16 or fp32).
+// out[c] = sum_b part[b, c]  (fp32 accumulate, out in bf16 or fp32).
 // 256 threads = 8 row groups x 32 columns: every wave reads 2 x 128 contiguous bytes per
 // partial row, and each thread keeps 8 independent loads in flight (the naive
 // one-thread-per-column loop was latency-bound: 118 us for 512 x 768 partials).
 template <int DTO>
 __global__ void __launch_bounds__(256) col_reduce_kernel(const float* __restrict__ part_g,
                                                          const float* __restrict__ part_b,
-                                                         int nparts, int cols, int64_t rstride,
-                                                         void* out_g, void* out_b,
-                                                         int accumulate) {
+                                                         int nparts, int cols, void* out_g,
+                                                         void* out_b, int accumulate) {
   // blockIdx.y: 0 = dgamma, 1 = dbeta (one launch for both)
   const float* part = blockIdx.y ? part_b : part_g;
   void* out = blockIdx.y ? out_b : out_g;
@@ -374,11 +373,11 @@ __global__ void __launch_bounds__(256) col_reduce_kernel(const float* __restrict
     for (; b + 56 < nparts; b += 64) {
       float v[8];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = part[static_cast<int64_t>(b + 8 * u) * rstride + c];
+      for (int u = 0; u < 8; ++u) v[u] = part[static_cast<int64_t>(b + 8 * u) * cols + c];
 #pragma unroll
       for (int u = 0; u < 8; ++u) s += v[u];
     }
-    for (; b < nparts; b += 8) s += part[static_cast<int64_t>(b) * rstride + c];
+    for (; b < nparts; b += 8) s += part[static_cast<int64_t>(b) * cols + c];
   }
   red[ty][tx] = s;
   __syncthreads();
@@ -389,44 +388,6 @@ __global__ void __launch_bounds__(256) col_reduce_kernel(const float* __restrict
     auto* o = static_cast<typename Elem<DTO>::T*>(out);
     if (accumulate) t += Elem<DTO>::ld(o, c);     // into an existing gradient (grad sinks)
     Elem<DTO>::st(o, c, t);
-  }
-}
-
-// First pass of the column reduce for many partial rows: the 48-workgroup single pass above
-// (768 columns) ran 8 dependent load rounds per thread — 32 us per LayerNorm backward in the
-// GPT-2 step (profiles/r06_queues/normal/gpt2_kernel_stats_steady.csv), latency-bound beside the
-// side stream's weight gradients. Here blockIdx.z takes one slice of `per` partial rows, sums it
-// with one round of loads per thread and writes the sum IN PLACE into the slice's first row
-// (only this workgroup touches those rows' 32 columns); col_reduce_kernel then adds the slices'
-// first rows (row stride per * cols).
-__global__ void __launch_bounds__(256) col_slice_kernel(float* __restrict__ part_g,
-                                                        float* __restrict__ part_b, int nparts,
-                                                        int cols, int per) {
-  float* part = blockIdx.y ? part_b : part_g;
-  __shared__ float red[8][33];
-  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
-  const int c = blockIdx.x * 32 + tx;
-  const int r0 = blockIdx.z * per;
-  const int r1 = r0 + per < nparts ? r0 + per : nparts;
-  float s = 0.f;
-  if (c < cols) {
-    float v[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int b = r0 + ty + 8 * u;
-      v[u] = b < r1 ? part[static_cast<int64_t>(b) * cols + c] : 0.f;
-    }
-#pragma unroll
-    for (int u = 0; u < 8; ++u) s += v[u];
-    for (int b = r0 + ty + 64; b < r1; b += 8) s += part[static_cast<int64_t>(b) * cols + c];
-  }
-  red[ty][tx] = s;
-  __syncthreads();
-  if (ty == 0 && c < cols) {
-    float t = 0.f;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) t += red[k][tx];
-    part[static_cast<int64_t>(r0) * cols + c] = t;
   }
 }
 
@@ -589,10 +550,6 @@ DLBB_API int dlbb_layernorm_fwd(const void* x, const void* residual, const void*
 // Supported widths for the backward: cols in {256,512,768,1024,1536,2048,3072,4096}
 // (LDS: 2 x 4 x cols floats <= 128 KiB). Returns the number of partial rows the caller
 // must provide via `max_parts` query: call with dx == nullptr to get the grid size.
-// A/B switch of the two-pass dgamma / dbeta column reduce (1, default) vs one pass (0)
-static int g_col_two_pass = 1;
-DLBB_API void dlbb_layernorm_set_col_two_pass(int on) { g_col_two_pass = on ? 1 : 0; }
-
 DLBB_API int dlbb_layernorm_bwd_grid(int64_t rows) {
   int64_t g = (rows + 3) / 4;
   if (g > 512) g = 512;
@@ -626,20 +583,11 @@ DLBB_API int dlbb_layernorm_bwd(const void* dy, const void* h, const void* gamma
 #undef LB
   if (e != hipSuccess) return e;
   const dim3 cg((cols + 31) / 32, dbeta ? 2 : 1), cb(256);
-  int nparts = grid;
-  int64_t rstride = cols;
-  if (grid >= 128 && g_col_two_pass) {   // two passes: slices of 64 partial rows, then sums
-    const int per = 64, nsl = (grid + per - 1) / per;
-    hipLaunchKernelGGL(col_slice_kernel, dim3(cg.x, cg.y, nsl), cb, 0, stream, pg, pb, grid, cols,
-                       per);
-    nparts = nsl;
-    rstride = static_cast<int64_t>(per) * cols;
-  }
   if (param_dtype == DT_F32)
-    hipLaunchKernelGGL((col_reduce_kernel<DT_F32>), cg, cb, 0, stream, pg, pb, nparts, cols,
-                       rstride, dgamma, dbeta, accumulate);
+    hipLaunchKernelGGL((col_reduce_kernel<DT_F32>), cg, cb, 0, stream, pg, pb, grid, cols, dgamma,
+                       dbeta, accumulate);
   else
-    hipLaunchKernelGGL((col_reduce_kernel<DT_BF16>), cg, cb, 0, stream, pg, pb, nparts, cols,
-                       rstride, dgamma, dbeta, accumulate);
+    hipLaunchKernelGGL((col_reduce_kernel<DT_BF16>), cg, cb, 0, stream, pg, pb, grid, cols,
+                       dgamma, dbeta, accumulate);
   return hipGetLastError();
 }

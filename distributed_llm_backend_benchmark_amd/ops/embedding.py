@@ -23,11 +23,6 @@ from . import _lib
 from ._lib import check, use_hip
 
 
-# the backward's token sort issued in the forward on a side stream (True, default) or in the
-# backward on the compute stream (False); A/B switch (tools/step_ab.py)
-PRESORT = [True]
-
-
 class _EmbeddingFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, idx, wte, wpe):
@@ -41,20 +36,6 @@ class _EmbeddingFn(torch.autograd.Function):
         ctx.save_for_backward(ids)
         ctx.params = (wte, wpe)
         ctx.T = T
-        ctx.presorted = None
-        if ctx.needs_input_grad[1] and wte.is_cuda and PRESORT[0]:
-            # the backward's token sort (one-workgroup radix sort, ~70 us in the GPT-2 step at
-            # the very end of the backward, profiles/r06_queues/normal) depends only on the ids:
-            # run it now on a side stream beside the forward, joined by an event in backward
-            from ..parallel.streams import concurrent_stream, fork
-
-            side = concurrent_stream(wte.device, "embedding_sort")
-            fork(side)
-            with torch.cuda.stream(side):
-                srt, order = sort_ids(ids, V)
-                ev = torch.cuda.Event()
-                ev.record(side)
-            ctx.presorted = (srt, order, ev)
         return out
 
     @staticmethod
@@ -84,13 +65,7 @@ class _EmbeddingFn(torch.autograd.Function):
         groups = [(ge, gp)] if (ge is None or gp is None or ge.dtype == gp.dtype) \
             else [(ge, None), (None, gp)]
         sorted_ids = order = None
-        if ge is not None and ctx.presorted is not None:
-            sorted_ids, order, ev = ctx.presorted
-            cur = torch.cuda.current_stream(d2.device)
-            cur.wait_event(ev)
-            sorted_ids.record_stream(cur)       # allocated on the side stream, read here
-            order.record_stream(cur)
-        elif ge is not None:
+        if ge is not None:
             sorted_ids, order = sort_ids(ids, wte.shape[0])
         if sink_e is not None and getattr(wte, "_dlbb_grad_event", None) is not None:
             # the tied LM head's weight gradient may still be accumulating into the same buffer

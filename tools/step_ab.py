@@ -5,12 +5,15 @@ alternate round by round on one box, so box-to-box spread does not enter the com
 One JSON line per run.
 
   base           the tree's defaults
-  no_presort     embedding backward sorts the token ids itself (ops/embedding.PRESORT)
-  col_one_pass   LayerNorm dgamma/dbeta column reduce in one 48-workgroup pass
-  old            no_presort + col_one_pass (the round-6 start)
   split_cap=N    weight-gradient split-K capped at N (ops/gemm.set_wgrad_split_cap)
+  wgrad_fused    weight-gradient split-K combined in-launch (ops/gemm.set_wgrad_fused)
+  no_wgrad_side  weight gradients on the compute stream (parallel/ddp._WGRAD_STREAM)
 
-    python tools/step_ab.py --variants base,old,no_presort,col_one_pass --reps 3
+(Round 6 also ran a two-pass LayerNorm column reduce and the embedding token sort moved into the
+forward on a side stream through this tool — profiles/r06_step/step_ab_presort_colreduce.jsonl,
+commit bc963df — both slower in the step, removed.)
+
+    python tools/step_ab.py --variants base,split_cap=4 --reps 3
 """
 import argparse
 import json
@@ -20,21 +23,20 @@ import sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
+_DEFAULT_WGRAD_STREAM = [None]
+
+
 def apply(name):
-    import importlib
+    from distributed_llm_backend_benchmark_amd.ops import gemm
+    from distributed_llm_backend_benchmark_amd.parallel import ddp
 
-    from distributed_llm_backend_benchmark_amd.ops import _lib, gemm
-
-    # (the package re-exports the embedding FUNCTION under the module's name)
-    embedding = importlib.import_module("distributed_llm_backend_benchmark_amd.ops.embedding")
-
-    embedding.PRESORT[0] = True
-    _lib.lib().dlbb_layernorm_set_col_two_pass(1)
     gemm.set_wgrad_split_cap(None)
-    if name in ("no_presort", "old"):
-        embedding.PRESORT[0] = False
-    if name in ("col_one_pass", "old"):
-        _lib.lib().dlbb_layernorm_set_col_two_pass(0)
+    gemm.set_wgrad_fused(False)
+    ddp._WGRAD_STREAM = _DEFAULT_WGRAD_STREAM[0]
+    if name == "wgrad_fused":
+        gemm.set_wgrad_fused(True)
+    if name == "no_wgrad_side":
+        ddp._WGRAD_STREAM = False
     if name.startswith("split_cap="):
         gemm.set_wgrad_split_cap(int(name.split("=")[1]))
         gemm.WGRAD_CHOICES.clear()
@@ -51,6 +53,9 @@ def main():
     from distributed_llm_backend_benchmark_amd.cli import train_ddp
     from distributed_llm_backend_benchmark_amd.parallel.comm import init_distributed
 
+    from distributed_llm_backend_benchmark_amd.parallel import ddp
+
+    _DEFAULT_WGRAD_STREAM[0] = ddp._WGRAD_STREAM
     comm = init_distributed("auto")
     args = train_ddp.parse_args(["--steps", str(a.steps), "--warmup", str(a.warmup)])
     for rep in range(a.reps):
