@@ -140,9 +140,16 @@ __device__ __forceinline__ bf16x8 frag(const char* img, int colbase, int lane) {
 // One stage = BM rows of m of the NA = WM / 2 A sub-images ([BM][128 cols of dY] each) and the B
 // image ([BM][128 cols of X]); every 4-row x 256-B wave-instruction of the stage is one slot
 // j = wave * per + q of NIMG * BM / 4, spread evenly over the workgroup's waves.
+// buffer_load ... lds with the split's operand bases in buffer resources (SGPRs): the lane's
+// row-in-group and swizzled chunk are a loop-invariant 32-bit voffset, the stage's row the
+// uniform soffset. The former global_load_lds form rebuilt a 64-bit address per load every
+// stage: 78 VALU (12 v_mul_lo_u32, 6 v_mad_u64_u32) per 34 MFMAs, 3.35 VALU instructions per
+// MFMA over the kernel (PMC, profiles/r06_kernels/pmc_wgradqkv_summary.jsonl) — issue slots the
+// 16x16x32 MFMAs' 8 free cycles cannot hold. Host contract: every offset below 2 GiB.
 template <int WM, int WJ = 4>
-__device__ __forceinline__ void stage_all(const Args& a, int m0, int n0, int k0, char* buf,
-                                          int wave, int lane) {
+__device__ __forceinline__ void stage_all(__amdgpu_buffer_rsrc_t ra, __amdgpu_buffer_rsrc_t rb,
+                                          uint32_t lda2, uint32_t ldb2, uint32_t mrel, int n0,
+                                          int k0, char* buf, int wave, int lane) {
   constexpr int NA = WM / 2, NIMG = NA + WJ / 4, RG = BM / 4, NW = 2 * WM;
   constexpr int PER = NIMG * RG / NW;
   static_assert(NIMG * RG % NW == 0, "stage slots must divide evenly over the waves");
@@ -154,12 +161,13 @@ __device__ __forceinline__ void stage_all(const Args& a, int m0, int n0, int k0,
     const int row = rg * 4 + rq;
     const int chunk = slot ^ swz(row);
     const bool is_a = img < NA;
-    const uint16_t* X = is_a ? a.A : a.B;
-    const int64_t ld = is_a ? a.lda : a.ldb;
+    const uint32_t ld2 = is_a ? lda2 : ldb2;
     const int c0 = is_a ? n0 + img * 128 : k0 + (img - NA) * 128;
-    const uint16_t* src = X + static_cast<int64_t>(m0 + row) * ld + c0 + chunk * 8;
-    __builtin_amdgcn_global_load_lds(src, (lds_vptr_t)(buf + img * kTile + rg * 4 * 256), 16, 0,
-                                     0);
+    const uint32_t voff = static_cast<uint32_t>(rq) * ld2 + static_cast<uint32_t>(c0 + chunk * 8) * 2;
+    const uint32_t soff = (mrel + static_cast<uint32_t>(rg * 4)) * ld2;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(is_a ? ra : rb,
+                                             (lds_vptr_t)(buf + img * kTile + rg * 4 * 256), 16,
+                                             voff, soff, 0, 0);
   }
 }
 
@@ -218,10 +226,17 @@ __global__ void __launch_bounds__(128 * WM, WJ == 8 ? 2 : (WM == 2 ? 3 : 2))
   const int asub = (wm * 64) / 128, acol = (wm * 64) % 128;
   // and its B image / column offset (WJ = 8: one whole 128-column image per wave)
   const int bsub = WM / 2 + (wn * 16 * WJ) / 128, bcol = (wn * 16 * WJ) % 128;
-  constexpr int kLoadsPerStage = NIMG * (BM / 4) / (2 * WM);   // global_load_lds per wave
+  constexpr int kLoadsPerStage = NIMG * (BM / 4) / (2 * WM);   // buffer_load lds per wave
+  // the split's rows [mb, me) of dY and X as buffer resources (offsets < 2 GiB: host contract)
+  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint16_t*>(a.A + static_cast<int64_t>(mb) * a.lda), 0, 0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint16_t*>(a.B + static_cast<int64_t>(mb) * a.ldb), 0, 0x7fffffff, 0x00020000);
+  const uint32_t lda2 = static_cast<uint32_t>(a.lda) * 2, ldb2 = static_cast<uint32_t>(a.ldb) * 2;
 #pragma unroll
   for (int p = 0; p < NB - 1; ++p)
-    if (p < nsteps) stage_all<WM, WJ>(a, mb + p * BM, n0, k0, stg(p), wave, lane);
+    if (p < nsteps)
+      stage_all<WM, WJ>(ra, rb, lda2, ldb2, p * BM, n0, k0, stg(p), wave, lane);
   for (int s = 0; s < nsteps; ++s) {
     const int cur = s % NB;
     // stage s landed: later stages (up to NB - 2 of them) may still be in flight
@@ -236,7 +251,8 @@ __global__ void __launch_bounds__(128 * WM, WJ == 8 ? 2 : (WM == 2 ? 3 : 2))
     // the buffer of stage s - 1 (every wave finished it), which stage s + NB - 1 now refills
     __builtin_amdgcn_s_barrier();
     if (s + NB - 1 < nsteps)
-      stage_all<WM, WJ>(a, mb + (s + NB - 1) * BM, n0, k0, stg((s + NB - 1) % NB), wave, lane);
+      stage_all<WM, WJ>(ra, rb, lda2, ldb2, (s + NB - 1) * BM, n0, k0, stg((s + NB - 1) % NB),
+                        wave, lane);
     const char* ia = stg(cur) + asub * kTile;
     const char* ib = stg(cur) + bsub * kTile;
     auto kstep = [&](auto ksc) {
@@ -480,6 +496,9 @@ static int wgrad_launch(const void* A, int64_t lda, const void* B, int64_t ldb, 
   int per = (M / split + BM - 1) / BM * BM;
   if (per <= 0) per = BM;
   split = (M + per - 1) / per;
+  // buffer offsets from a split's first row stay below 2 GiB (wgrad_kernel's resources)
+  if (static_cast<int64_t>(per) * (lda > ldb ? lda : ldb) * 2 >= (int64_t{1} << 31))
+    return hipErrorInvalidValue;
   // one split, plain store, no bias: the kernel writes dW itself (ws may be null)
   const bool direct = split == 1 && !accumulate && !out_bias;
   if (!direct && !ws) return hipErrorInvalidValue;

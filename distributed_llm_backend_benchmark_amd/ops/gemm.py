@@ -483,7 +483,9 @@ def wgrad_supported(dy2: torch.Tensor, x2: torch.Tensor) -> bool:
     return (dy2.dtype == torch.bfloat16 and x2.dtype == torch.bfloat16 and x2.shape[0] == M
             and M % 32 == 0 and N % 128 == 0 and K % 128 == 0 and dy2.stride(1) == 1
             and x2.stride(1) == 1 and dy2.stride(0) % 8 == 0 and x2.stride(0) % 8 == 0
-            and dy2.data_ptr() % 16 == 0 and x2.data_ptr() % 16 == 0)
+            and dy2.data_ptr() % 16 == 0 and x2.data_ptr() % 16 == 0
+            # the kernel's buffer offsets (from a split's first row) stay below 2 GiB
+            and M * max(dy2.stride(0), x2.stride(0)) * 2 < (1 << 31))
 
 
 _COUNTERS = {}   # (device index, stream handle) -> int32 tile counters, zero between launches

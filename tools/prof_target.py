@@ -1,6 +1,6 @@
 """Tiny driver for PMC-counter profiling: runs ONE op a few times (no timing logic).
 usage: prof_target.py longk|longkblas|attnfwd|attnbwd|lmhead|lmhead192|lmhead192p|lmheadblas|gemm256|gemm256s6|gemm256s7|gemm128|blas|nn|nnplain|tn|tnplain|wgrad128|
-blastn|reduce8|ln|xent|xentfused|embbwd"""
+blastn|wgradqkv|wgradqkv256|reduce8|ln|xent|xentfused|embbwd"""
 import os
 import sys
 
@@ -71,6 +71,16 @@ elif what in ("tn", "tnplain", "wgrad128", "blastn"):  # weight gradient dW = dY
           "tnplain": lambda: G._wgrad_pp(dy, xx, out, False),
           "wgrad128": lambda: G._wgrad_hip(dy, xx, out, False),
           "blastn": lambda: G._wgrad_blas(dy, xx, out, False)}[what]
+elif what in ("wgradqkv", "wgradqkv256"):  # GPT-2 QKV dW 16384 x 2304 x 768 as in the step
+    # (fused bias, bf16 accumulate): 128 x 256 tiles (wide, the step's choice) / 256 x 128
+    from distributed_llm_backend_benchmark_amd.ops import gemm as G
+
+    dy = torch.randn(16384, 2304, device=dev, generator=g).to(torch.bfloat16)
+    xx = torch.randn(16384, 768, device=dev, generator=g).to(torch.bfloat16)
+    out = torch.zeros(2304, 768, device=dev, dtype=torch.bfloat16)
+    bo = torch.zeros(2304, device=dev, dtype=torch.bfloat16)
+    impl = G._wgrad_hip_wide if what == "wgradqkv" else G._wgrad_hip256
+    fn = lambda: impl(dy, xx, out, True, None, bo)  # noqa: E731
 elif what == "reduce8":
     srcs = [torch.randn(1 << 25, device=dev, generator=g).to(torch.bfloat16) for _ in range(8)]
     fn = lambda: ops.reduce_sum(srcs)  # noqa: E731
