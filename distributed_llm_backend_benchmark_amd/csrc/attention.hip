@@ -129,184 +129,194 @@ __global__ void __launch_bounds__(kAttnThreads, 2) attn_fwd_kernel(AttnArgs a) {
   const int nqb = (a.T + kQB - 1) / kQB;
   int blk, h, b;
   head_block(a.xcd, blk, h, b);
-  const int qb = nqb - 1 - blk;                   // heaviest first
-  const int q0 = qb * kQB;
-  const int qw = q0 + wave * 32;                  // this wave's first query
-  const int r = lane & 31, hi = lane >> 5;
-  const uint16_t* base_bt = a.qkv + static_cast<int64_t>(b) * a.T * a.ld;
-  const int hoff = h * D;
+  // causal pairing: workgroup blk of a head runs query block nqb-1-blk (the heaviest) and then
+  // block blk (the lightest), so every workgroup does about the same 2 (nqb + 1) tiles. The
+  // heavy-first single-block grid left its second round of workgroups half the chip's slots:
+  // 1.7 of 4 waves resident per SIMD on average (PMC SQ_WAVE_CYCLES vs kernel cycles,
+  // profiles/r06_kernels/pmc_attn_summary.jsonl).
+  const int npass = nqb - 1 - blk != blk ? 2 : 1;
+  for (int pass = 0; pass < npass; ++pass) {
+    if (pass) __syncthreads();                    // every wave done with the LDS ring
+    const int qb = pass == 0 ? nqb - 1 - blk : blk;
+    const int q0 = qb * kQB;
+    const int qw = q0 + wave * 32;                  // this wave's first query
+    const int r = lane & 31, hi = lane >> 5;
+    const uint16_t* base_bt = a.qkv + static_cast<int64_t>(b) * a.T * a.ld;
+    const int hoff = h * D;
 
-  // Q fragments (B operand of S^T = K Q^T): lane holds Q[qw + r][16 ks + 8 hi + j]
-  bf16x8 qf[G::NKS];
-  {
-    int q = qw + r;
-    q = q < a.T ? q : a.T - 1;
-    const uint16_t* qp = base_bt + static_cast<int64_t>(q) * a.ld + hoff + 8 * hi;
-#pragma unroll
-    for (int ks = 0; ks < G::NKS; ++ks) qf[ks] = *reinterpret_cast<const bf16x8*>(qp + 16 * ks);
-  }
-
-  f32x16 o[G::NDT];
-#pragma unroll
-  for (int dt = 0; dt < G::NDT; ++dt)
-#pragma unroll
-    for (int e = 0; e < 16; ++e) o[dt][e] = 0.f;
-  float m = -INFINITY, l = 0.f;
-  const int qme = qw + r;                          // this lane's query
-  const int q_hi = qw + 31;                        // wave's last query
-  const int last_key = (q0 + kQB - 1) < (a.T - 1) ? (q0 + kQB - 1) : (a.T - 1);
-  const int nt = last_key / KB + 1;
-
-  auto tileK = [&](int c) { return smem + c * 2 * TILE; };
-  auto tileV = [&](int c) { return smem + c * 2 * TILE + TILE; };
-
-  // DMA: this lane's sources of image rows wave * WROWS + i * RPI + lane / (ROW / 16) of key
-  // tile 0 (K and V sections, swizzled chunk); tile kt adds kt * KB rows, uniform
-  const int r_in = lane / (ROW / 16), slot = lane % (ROW / 16);
-  const uint16_t* dsrc[4];
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int row = wave * WROWS + i * RPI + r_in;
-    const uint16_t* src = base_bt + static_cast<int64_t>(row) * a.ld + hoff;
-    dsrc[2 * i] = src + D * a.H + (slot ^ kswz_d<D>(row)) * 8;
-    dsrc[2 * i + 1] = src + 2 * D * a.H + (slot ^ vswz_d<D>(row)) * 8;
-  }
-  auto stage = [&](int k0, char* tk, char* tv) {
-    if (k0 + KB <= a.T) {                          // wave-uniform: no row past T
-      const int64_t off = static_cast<int64_t>(k0) * a.ld;
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        attn_glds16(dsrc[2 * i] + off, tk + (wave * WROWS + i * RPI) * ROW);
-        attn_glds16(dsrc[2 * i + 1] + off, tv + (wave * WROWS + i * RPI) * ROW);
-      }
-      return;
+    // Q fragments (B operand of S^T = K Q^T): lane holds Q[qw + r][16 ks + 8 hi + j]
+    bf16x8 qf[G::NKS];
+    {
+      int q = qw + r;
+      q = q < a.T ? q : a.T - 1;
+      const uint16_t* qp = base_bt + static_cast<int64_t>(q) * a.ld + hoff + 8 * hi;
+  #pragma unroll
+      for (int ks = 0; ks < G::NKS; ++ks) qf[ks] = *reinterpret_cast<const bf16x8*>(qp + 16 * ks);
     }
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {                  // rows past T clamped (scores masked)
+
+    f32x16 o[G::NDT];
+  #pragma unroll
+    for (int dt = 0; dt < G::NDT; ++dt)
+  #pragma unroll
+      for (int e = 0; e < 16; ++e) o[dt][e] = 0.f;
+    float m = -INFINITY, l = 0.f;
+    const int qme = qw + r;                          // this lane's query
+    const int q_hi = qw + 31;                        // wave's last query
+    const int last_key = (q0 + kQB - 1) < (a.T - 1) ? (q0 + kQB - 1) : (a.T - 1);
+    const int nt = last_key / KB + 1;
+
+    auto tileK = [&](int c) { return smem + c * 2 * TILE; };
+    auto tileV = [&](int c) { return smem + c * 2 * TILE + TILE; };
+
+    // DMA: this lane's sources of image rows wave * WROWS + i * RPI + lane / (ROW / 16) of key
+    // tile 0 (K and V sections, swizzled chunk); tile kt adds kt * KB rows, uniform
+    const int r_in = lane / (ROW / 16), slot = lane % (ROW / 16);
+    const uint16_t* dsrc[4];
+  #pragma unroll
+    for (int i = 0; i < 2; ++i) {
       const int row = wave * WROWS + i * RPI + r_in;
-      int key = k0 + row;
-      key = key < a.T ? key : a.T - 1;
-      const uint16_t* src = base_bt + static_cast<int64_t>(key) * a.ld + hoff;
-      attn_glds16(src + D * a.H + (slot ^ kswz_d<D>(row)) * 8,
-                  tk + (wave * WROWS + i * RPI) * ROW);
-      attn_glds16(src + 2 * D * a.H + (slot ^ vswz_d<D>(row)) * 8,
-                  tv + (wave * WROWS + i * RPI) * ROW);
+      const uint16_t* src = base_bt + static_cast<int64_t>(row) * a.ld + hoff;
+      dsrc[2 * i] = src + D * a.H + (slot ^ kswz_d<D>(row)) * 8;
+      dsrc[2 * i + 1] = src + 2 * D * a.H + (slot ^ vswz_d<D>(row)) * 8;
     }
-  };
-  stage(0, tileK(0), tileV(0));
-  for (int kt = 0; kt < nt; ++kt) {
-    const int cur = kt & 1;
-    // one barrier per tile: it both publishes tile kt (every wave's DMA retired) and frees
-    // buffer cur^1 (every wave finished tile kt-1), so the restage goes right after it
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    if (kt + 1 < nt) stage((kt + 1) * KB, tileK(cur ^ 1), tileV(cur ^ 1));
-    const int k0 = kt * KB;
-    if (k0 <= q_hi) {                               // wave-uniform: tile has keys <= a query
-      const char* tk = tileK(cur);
-      const char* tv = tileV(cur);
-      // ---- S^T for the 32-key halves
-      f32x16 s[G::NKK];
-#pragma unroll
-      for (int kk = 0; kk < G::NKK; ++kk) {
-#pragma unroll
-        for (int e = 0; e < 16; ++e) s[kk][e] = 0.f;
-        const int row = kk * 32 + r;
-#pragma unroll
-        for (int ks = 0; ks < G::NKS; ++ks) {
-          const int c = 2 * ks + hi;
-          const bf16x8 kf =
-              *reinterpret_cast<const bf16x8*>(tk + row * ROW + ((c ^ kswz_d<D>(row)) << 4));
-          s[kk] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[ks], s[kk], 0, 0, 0);
+    auto stage = [&](int k0, char* tk, char* tv) {
+      if (k0 + KB <= a.T) {                          // wave-uniform: no row past T
+        const int64_t off = static_cast<int64_t>(k0) * a.ld;
+  #pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          attn_glds16(dsrc[2 * i] + off, tk + (wave * WROWS + i * RPI) * ROW);
+          attn_glds16(dsrc[2 * i + 1] + off, tv + (wave * WROWS + i * RPI) * ROW);
         }
+        return;
       }
-      // ---- scale, causal mask, online softmax (lane = one query; keys in registers)
-      const bool diag = k0 + KB - 1 > qw;           // some key of this tile beyond some query
-      if (diag) {
-        // key(kk, e) = k0 + 4 hi + kk*32 + (e & 3) + 8 (e >> 2): one per-lane threshold
-        const int th = qme - k0 - 4 * hi;
-#pragma unroll
-        for (int kk = 0; kk < G::NKK; ++kk)
-#pragma unroll
-          for (int e = 0; e < 16; ++e)
-            if (kk * 32 + (e & 3) + 8 * (e >> 2) > th) s[kk][e] = -INFINITY;
+  #pragma unroll
+      for (int i = 0; i < 2; ++i) {                  // rows past T clamped (scores masked)
+        const int row = wave * WROWS + i * RPI + r_in;
+        int key = k0 + row;
+        key = key < a.T ? key : a.T - 1;
+        const uint16_t* src = base_bt + static_cast<int64_t>(key) * a.ld + hoff;
+        attn_glds16(src + D * a.H + (slot ^ kswz_d<D>(row)) * 8,
+                    tk + (wave * WROWS + i * RPI) * ROW);
+        attn_glds16(src + 2 * D * a.H + (slot ^ vswz_d<D>(row)) * 8,
+                    tv + (wave * WROWS + i * RPI) * ROW);
       }
-      float mx = -INFINITY;                          // max of the RAW scores (scale > 0)
-#pragma unroll
-      for (int kk = 0; kk < G::NKK; ++kk)
-#pragma unroll
-        for (int e = 0; e < 16; ++e) mx = fmaxf(mx, s[kk][e]);
-      mx = xhalf_max(mx);
-      const float mn = fmaxf(m, mx * a.scale_log2);
-      const float alpha = __builtin_amdgcn_exp2f(m - mn);   // m = -inf on the first tile -> 0
-      const bool rescale = m != mn;
-      m = mn;
-      float ls = 0.f;
-#pragma unroll
-      for (int kk = 0; kk < G::NKK; ++kk)
-#pragma unroll
-        for (int e = 0; e < 16; ++e) {
-          s[kk][e] = __builtin_amdgcn_exp2f(__builtin_fmaf(s[kk][e], a.scale_log2, -mn));
-          ls += s[kk][e];
-        }
-      l = l * alpha + ls;
-      if (__any(rescale)) {                          // wave-uniform skip when no max moved
-#pragma unroll
-        for (int dt = 0; dt < G::NDT; ++dt)
-#pragma unroll
-          for (int e = 0; e < 16; ++e) o[dt][e] *= alpha;
-      }
-      // ---- O^T += V^T P^T: k-step = 16 keys; P^T element j <-> key 16 s + 8 (j>>2) + 4 hi + (j&3)
-      const int g = lane >> 4, i16 = lane & 15;
-      const int tq = i16 >> 2, tp = i16 & 3;        // tr-read lane role: block row / col group
-#pragma unroll
-      for (int kk = 0; kk < G::NKK; ++kk)
-#pragma unroll
-        for (int st = 0; st < 2; ++st) {
-          bf16x8 pf;
-#pragma unroll
-          for (int j = 0; j < 8; ++j)
-            pf[j] = __builtin_bit_cast(short, static_cast<__bf16>(s[kk][8 * st + j]));
-#pragma unroll
-          for (int dt = 0; dt < G::NDT; ++dt) {
-            bf16x8 vf;
-#pragma unroll
-            for (int half = 0; half < 2; ++half) {
-              const int row = kk * 32 + 16 * st + 8 * half + 4 * (g >> 1) + tq;
-              const int col = dt * 32 + 16 * (g & 1) + 4 * tp;
-              const int off = row * ROW + (((col >> 3) ^ vswz_d<D>(row)) << 4) + (col & 7) * 2;
-              // builtin read, kept on purpose: the compiler drains the next tile's K/V DMA
-              // (vmcnt(0)) before the first of these, but that DMA has had the S MFMAs and the
-              // softmax to land, and the builtin lets it interleave the reads with the MFMAs
-              // under counted lgkmcnt waits (the asm form measured 3-4 % slower here,
-              // profiles/r05_attention/). tools/isa_check.py allows this kernel.
-              const i16x4 t = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4_ptr)(tv + off));
-#pragma unroll
-              for (int u = 0; u < 4; ++u) vf[4 * half + u] = t[u];
-            }
-            o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf, o[dt], 0, 0, 0);
+    };
+    stage(0, tileK(0), tileV(0));
+    for (int kt = 0; kt < nt; ++kt) {
+      const int cur = kt & 1;
+      // one barrier per tile: it both publishes tile kt (every wave's DMA retired) and frees
+      // buffer cur^1 (every wave finished tile kt-1), so the restage goes right after it
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      if (kt + 1 < nt) stage((kt + 1) * KB, tileK(cur ^ 1), tileV(cur ^ 1));
+      const int k0 = kt * KB;
+      if (k0 <= q_hi) {                               // wave-uniform: tile has keys <= a query
+        const char* tk = tileK(cur);
+        const char* tv = tileV(cur);
+        // ---- S^T for the 32-key halves
+        f32x16 s[G::NKK];
+  #pragma unroll
+        for (int kk = 0; kk < G::NKK; ++kk) {
+  #pragma unroll
+          for (int e = 0; e < 16; ++e) s[kk][e] = 0.f;
+          const int row = kk * 32 + r;
+  #pragma unroll
+          for (int ks = 0; ks < G::NKS; ++ks) {
+            const int c = 2 * ks + hi;
+            const bf16x8 kf =
+                *reinterpret_cast<const bf16x8*>(tk + row * ROW + ((c ^ kswz_d<D>(row)) << 4));
+            s[kk] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[ks], s[kk], 0, 0, 0);
           }
         }
-    }
-  }
-
-  // ---- finalize: l over both lane halves, O / l, store O [B,T,H,D] and LSE
-  const float lt = l + __shfl_xor(l, 32, 64);
-  const float inv = lt > 0.f ? 1.f / lt : 0.f;
-  if (qme < a.T) {
-    uint16_t* op = a.out + (static_cast<int64_t>(b) * a.T + qme) * a.ldo + hoff;
-#pragma unroll
-    for (int dt = 0; dt < G::NDT; ++dt)
-#pragma unroll
-      for (int gg = 0; gg < 4; ++gg) {
-        u16x4 w;
-#pragma unroll
-        for (int u = 0; u < 4; ++u) w[u] = f32_to_bf16(o[dt][4 * gg + u] * inv);
-        *reinterpret_cast<u16x4*>(op + dt * 32 + 8 * gg + 4 * hi) = w;
+        // ---- scale, causal mask, online softmax (lane = one query; keys in registers)
+        const bool diag = k0 + KB - 1 > qw;           // some key of this tile beyond some query
+        if (diag) {
+          // key(kk, e) = k0 + 4 hi + kk*32 + (e & 3) + 8 (e >> 2): one per-lane threshold
+          const int th = qme - k0 - 4 * hi;
+  #pragma unroll
+          for (int kk = 0; kk < G::NKK; ++kk)
+  #pragma unroll
+            for (int e = 0; e < 16; ++e)
+              if (kk * 32 + (e & 3) + 8 * (e >> 2) > th) s[kk][e] = -INFINITY;
+        }
+        float mx = -INFINITY;                          // max of the RAW scores (scale > 0)
+  #pragma unroll
+        for (int kk = 0; kk < G::NKK; ++kk)
+  #pragma unroll
+          for (int e = 0; e < 16; ++e) mx = fmaxf(mx, s[kk][e]);
+        mx = xhalf_max(mx);
+        const float mn = fmaxf(m, mx * a.scale_log2);
+        const float alpha = __builtin_amdgcn_exp2f(m - mn);   // m = -inf on the first tile -> 0
+        const bool rescale = m != mn;
+        m = mn;
+        float ls = 0.f;
+  #pragma unroll
+        for (int kk = 0; kk < G::NKK; ++kk)
+  #pragma unroll
+          for (int e = 0; e < 16; ++e) {
+            s[kk][e] = __builtin_amdgcn_exp2f(__builtin_fmaf(s[kk][e], a.scale_log2, -mn));
+            ls += s[kk][e];
+          }
+        l = l * alpha + ls;
+        if (__any(rescale)) {                          // wave-uniform skip when no max moved
+  #pragma unroll
+          for (int dt = 0; dt < G::NDT; ++dt)
+  #pragma unroll
+            for (int e = 0; e < 16; ++e) o[dt][e] *= alpha;
+        }
+        // ---- O^T += V^T P^T: k-step = 16 keys;
+        //      P^T element j <-> key 16 s + 8 (j>>2) + 4 hi + (j&3)
+        const int g = lane >> 4, i16 = lane & 15;
+        const int tq = i16 >> 2, tp = i16 & 3;        // tr-read lane role: block row / col group
+  #pragma unroll
+        for (int kk = 0; kk < G::NKK; ++kk)
+  #pragma unroll
+          for (int st = 0; st < 2; ++st) {
+            bf16x8 pf;
+  #pragma unroll
+            for (int j = 0; j < 8; ++j)
+              pf[j] = __builtin_bit_cast(short, static_cast<__bf16>(s[kk][8 * st + j]));
+  #pragma unroll
+            for (int dt = 0; dt < G::NDT; ++dt) {
+              bf16x8 vf;
+  #pragma unroll
+              for (int half = 0; half < 2; ++half) {
+                const int row = kk * 32 + 16 * st + 8 * half + 4 * (g >> 1) + tq;
+                const int col = dt * 32 + 16 * (g & 1) + 4 * tp;
+                const int off = row * ROW + (((col >> 3) ^ vswz_d<D>(row)) << 4) + (col & 7) * 2;
+                // builtin read, kept on purpose: the compiler drains the next tile's K/V DMA
+                // (vmcnt(0)) before the first of these, but that DMA has had the S MFMAs and the
+                // softmax to land, and the builtin lets it interleave the reads with the MFMAs
+                // under counted lgkmcnt waits (the asm form measured 3-4 % slower here,
+                // profiles/r05_attention/). tools/isa_check.py allows this kernel.
+                const i16x4 t = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4_ptr)(tv + off));
+  #pragma unroll
+                for (int u = 0; u < 4; ++u) vf[4 * half + u] = t[u];
+              }
+              o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf, o[dt], 0, 0, 0);
+            }
+          }
       }
-    if (hi == 0 && a.lse)
-      a.lse[(static_cast<int64_t>(b) * a.H + h) * a.T + qme] =
-          (m + __builtin_amdgcn_logf(lt)) * 0.69314718055994531f;
+    }
+
+    // ---- finalize: l over both lane halves, O / l, store O [B,T,H,D] and LSE
+    const float lt = l + __shfl_xor(l, 32, 64);
+    const float inv = lt > 0.f ? 1.f / lt : 0.f;
+    if (qme < a.T) {
+      uint16_t* op = a.out + (static_cast<int64_t>(b) * a.T + qme) * a.ldo + hoff;
+  #pragma unroll
+      for (int dt = 0; dt < G::NDT; ++dt)
+  #pragma unroll
+        for (int gg = 0; gg < 4; ++gg) {
+          u16x4 w;
+  #pragma unroll
+          for (int u = 0; u < 4; ++u) w[u] = f32_to_bf16(o[dt][4 * gg + u] * inv);
+          *reinterpret_cast<u16x4*>(op + dt * 32 + 8 * gg + 4 * hi) = w;
+        }
+      if (hi == 0 && a.lse)
+        a.lse[(static_cast<int64_t>(b) * a.H + h) * a.T + qme] =
+            (m + __builtin_amdgcn_logf(lt)) * 0.69314718055994531f;
+    }
   }
 }
 
@@ -409,169 +419,176 @@ __global__ void __launch_bounds__(kAttnThreads, 2) attn_bwd_dkdv_d64_kernel(Attn
   const int r = lane & 31, hi = lane >> 5;
   int blk, h, b;
   head_block(a.xcd, blk, h, b);
-  const int kb0 = blk * kBwdKeys;                   // block 0 = most query slices: first
-  const int kw = kb0 + wave * 32;
-  const int mykey = kw + r;
-  const uint16_t* base_bt = a.qkv + static_cast<int64_t>(b) * a.T * a.ld;
-  const uint16_t* dout_bt = a.dout + static_cast<int64_t>(b) * a.T * a.ldo;
-  const int hoff = h * kAttnD;
-  const int64_t bh = static_cast<int64_t>(b) * a.H + h;
-  const float* lrow = a.nls + bh * a.T;            // -LSE * sqrt(D)
-  const float* drow = a.delta + bh * a.T;          // -delta
+  // causal pairing: key blocks blk (more query slices) and nkb-1-blk, equal work per workgroup
+  const int nkb = (a.T + kBwdKeys - 1) / kBwdKeys;
+  const int npass = nkb - 1 - blk != blk ? 2 : 1;
+  for (int pass = 0; pass < npass; ++pass) {
+    if (pass) __syncthreads();                    // every wave done with the LDS ring
+    const int kb0 = (pass == 0 ? blk : nkb - 1 - blk) * kBwdKeys;   // heaviest (block 0) first
+    const int kw = kb0 + wave * 32;
+    const int mykey = kw + r;
+    const uint16_t* base_bt = a.qkv + static_cast<int64_t>(b) * a.T * a.ld;
+    const uint16_t* dout_bt = a.dout + static_cast<int64_t>(b) * a.T * a.ldo;
+    const int hoff = h * kAttnD;
+    const int64_t bh = static_cast<int64_t>(b) * a.H + h;
+    const float* lrow = a.nls + bh * a.T;            // -LSE * sqrt(D)
+    const float* drow = a.delta + bh * a.T;          // -delta
 
-  bf16x8 kf[4], vf[4];
-  {
-    const int kk = mykey < a.T ? mykey : a.T - 1;
-    const uint16_t* kp = base_bt + static_cast<int64_t>(kk) * a.ld + kAttnD * a.H + hoff + 8 * hi;
-    const uint16_t* vp = kp + kAttnD * a.H;
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
-      kf[ks] = *reinterpret_cast<const bf16x8*>(kp + 16 * ks);
-      vf[ks] = *reinterpret_cast<const bf16x8*>(vp + 16 * ks);
-    }
-  }
-  f32x16 dv[2], dk[2];
-#pragma unroll
-  for (int dt = 0; dt < 2; ++dt)
-#pragma unroll
-    for (int e = 0; e < 16; ++e) { dv[dt][e] = 0.f; dk[dt][e] = 0.f; }
-
-  const int ns = (a.T - kb0 + kSlice - 1) / kSlice;
-  auto imgQ = [&](int c) { return smem + c * 2 * kSliceImg; };
-  auto imgG = [&](int c) { return smem + c * 2 * kSliceImg + kSliceImg; };
-  // per-slice row constants (LSE, delta of the slice's 64 queries) ride the same LDS-DMA
-  // double buffer as the Q / dO images instead of being loaded from global memory right
-  // before use: waves 0 / 1 stage one 256-B row each (rows past T clamped, as for Q / dO)
-  auto rowv = [&](int c) { return reinterpret_cast<float*>(smem + 4 * kSliceImg + c * 512); };
-  auto stage_rows = [&](int q0, int c) {
-    if (wave < 2) {
-      int t = q0 + lane;
-      t = t < a.T ? t : a.T - 1;
-      __builtin_amdgcn_global_load_lds((wave == 0 ? lrow : drow) + t,
-                                       (lds_vptr_t)(rowv(c) + 64 * wave), 4, 0, 0);
-    }
-  };
-  // INC: this lane's Q / dO sources for image rows wave * 16 + i * 8 + lane / 8 of slice 0
-  const uint16_t* qsrc[2];
-  const uint16_t* gsrc[2];
-  if constexpr (INC) {
-    const int r_in = lane >> 3, slot = lane & 7;
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int row = wave * 16 + i * 8 + r_in;
-      qsrc[i] = base_bt + hoff + static_cast<int64_t>(kb0 + row) * a.ld + (slot ^ bswz(row)) * 8;
-      gsrc[i] = dout_bt + hoff + static_cast<int64_t>(kb0 + row) * a.ldo + (slot ^ bswz(row)) * 8;
-    }
-  }
-  auto stage_slice = [&](int q0, int c) {
-    if constexpr (INC) {
-      if (q0 + kSlice <= a.T) {                     // wave-uniform: no row past T
-        const int d = q0 - kb0;
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-          attn_glds16(qsrc[i] + static_cast<int64_t>(d) * a.ld, imgQ(c) + (wave * 16 + i * 8) * 128);
-          attn_glds16(gsrc[i] + static_cast<int64_t>(d) * a.ldo,
-                      imgG(c) + (wave * 16 + i * 8) * 128);
-        }
-        return;
-      }
-    }
-    stage64(base_bt + hoff, a.ld, q0, a.T, imgQ(c), wave, lane);
-    stage64(dout_bt + hoff, a.ldo, q0, a.T, imgG(c), wave, lane);
-  };
-  stage_slice(kb0, 0);
-  stage_rows(kb0, 0);
-  for (int i = 0; i < ns; ++i) {
-    const int cur = i & 1;
-    const int qs = kb0 + i * kSlice;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();                   // publishes slice i, frees buffer cur^1
-    if (i + 1 < ns) {
-      stage_slice(qs + kSlice, cur ^ 1);
-      stage_rows(qs + kSlice, cur ^ 1);
-    }
-    const char* iq = imgQ(cur);
-    const char* ig = imgG(cur);
-    const float* rv = rowv(cur);
-#pragma unroll
-    for (int sub = 0; sub < 2; ++sub) {
-      const int qsub = qs + 32 * sub;
-      if (qsub + 31 < kw) continue;                 // wave-uniform: every query < every key
-      const int rb = 32 * sub;                      // image row base of this 32-query block
-      // per-row constants for rows q = qsub + 8 g + 4 hi + u (register e = 4 g + u) as the
-      // accumulators' starting values: S' = Q K^T - LSE sqrt(D), dP' = dO V^T - delta
-      // (asm reads: rowv is filled by LDS-DMA, and a compiler-visible read of it drained every
-      // DMA in flight — the next slice's Q / dO included; common.h ds_read_b128_asm)
-      f32x16 s, dp;
-      f32x4 lv[4], dv4[4];
-#pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4) {
-        lv[g4] = ds_read_b128_asm(rv + rb + 8 * g4 + 4 * hi);
-        dv4[g4] = ds_read_b128_asm(rv + 64 + rb + 8 * g4 + 4 * hi);
-      }
-      tr_wait(lv[0], lv[1], lv[2], lv[3], dv4[0], dv4[1], dv4[2], dv4[3]);
-#pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4)
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          s[4 * g4 + u] = lv[g4][u];
-          dp[4 * g4 + u] = dv4[g4][u];
-        }
-#pragma unroll
+    bf16x8 kf[4], vf[4];
+    {
+      const int kk = mykey < a.T ? mykey : a.T - 1;
+      const uint16_t* kp = base_bt + static_cast<int64_t>(kk) * a.ld + kAttnD * a.H + hoff + 8 * hi;
+      const uint16_t* vp = kp + kAttnD * a.H;
+  #pragma unroll
       for (int ks = 0; ks < 4; ++ks) {
-        s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_operand(iq, rb + r, 2 * ks + hi), kf[ks],
-                                                    s, 0, 0, 0);
-        dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_operand(ig, rb + r, 2 * ks + hi), vf[ks],
-                                                     dp, 0, 0, 0);
+        kf[ks] = *reinterpret_cast<const bf16x8*>(kp + 16 * ks);
+        vf[ks] = *reinterpret_cast<const bf16x8*>(vp + 16 * ks);
       }
-      // mask the raw scores (exp2(-inf) = 0) only where a query of the block can precede a key
-      // of the wave (the diagonal) or lies past T: a wave-uniform branch, so interior blocks run
-      // no per-element index compares
-      const bool diag = qsub < kw + 31;
-      if (diag || qsub + 31 >= a.T) {
-#pragma unroll
-        for (int e = 0; e < 16; ++e) {
-          const int q = qsub + (e & 3) + 8 * (e >> 2) + 4 * hi;
-          if ((diag && mykey > q) || q >= a.T) s[e] = -INFINITY;
+    }
+    f32x16 dv[2], dk[2];
+  #pragma unroll
+    for (int dt = 0; dt < 2; ++dt)
+  #pragma unroll
+      for (int e = 0; e < 16; ++e) { dv[dt][e] = 0.f; dk[dt][e] = 0.f; }
+
+    const int ns = (a.T - kb0 + kSlice - 1) / kSlice;
+    auto imgQ = [&](int c) { return smem + c * 2 * kSliceImg; };
+    auto imgG = [&](int c) { return smem + c * 2 * kSliceImg + kSliceImg; };
+    // per-slice row constants (LSE, delta of the slice's 64 queries) ride the same LDS-DMA
+    // double buffer as the Q / dO images instead of being loaded from global memory right
+    // before use: waves 0 / 1 stage one 256-B row each (rows past T clamped, as for Q / dO)
+    auto rowv = [&](int c) { return reinterpret_cast<float*>(smem + 4 * kSliceImg + c * 512); };
+    auto stage_rows = [&](int q0, int c) {
+      if (wave < 2) {
+        int t = q0 + lane;
+        t = t < a.T ? t : a.T - 1;
+        __builtin_amdgcn_global_load_lds((wave == 0 ? lrow : drow) + t,
+                                         (lds_vptr_t)(rowv(c) + 64 * wave), 4, 0, 0);
+      }
+    };
+    // INC: this lane's Q / dO sources for image rows wave * 16 + i * 8 + lane / 8 of slice 0
+    const uint16_t* qsrc[2];
+    const uint16_t* gsrc[2];
+    if constexpr (INC) {
+      const int r_in = lane >> 3, slot = lane & 7;
+  #pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int row = wave * 16 + i * 8 + r_in;
+        qsrc[i] = base_bt + hoff + static_cast<int64_t>(kb0 + row) * a.ld + (slot ^ bswz(row)) * 8;
+        gsrc[i] = dout_bt + hoff + static_cast<int64_t>(kb0 + row) * a.ldo + (slot ^ bswz(row)) * 8;
+      }
+    }
+    auto stage_slice = [&](int q0, int c) {
+      if constexpr (INC) {
+        if (q0 + kSlice <= a.T) {                     // wave-uniform: no row past T
+          const int d = q0 - kb0;
+  #pragma unroll
+          for (int i = 0; i < 2; ++i) {
+            attn_glds16(qsrc[i] + static_cast<int64_t>(d) * a.ld,
+                        imgQ(c) + (wave * 16 + i * 8) * 128);
+            attn_glds16(gsrc[i] + static_cast<int64_t>(d) * a.ldo,
+                        imgG(c) + (wave * 16 + i * 8) * 128);
+          }
+          return;
         }
       }
-#pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        const float p = __builtin_amdgcn_exp2f(s[e] * a.scale_log2);
-        s[e] = p;
-        dp[e] = p * dp[e];
+      stage64(base_bt + hoff, a.ld, q0, a.T, imgQ(c), wave, lane);
+      stage64(dout_bt + hoff, a.ldo, q0, a.T, imgG(c), wave, lane);
+    };
+    stage_slice(kb0, 0);
+    stage_rows(kb0, 0);
+    for (int i = 0; i < ns; ++i) {
+      const int cur = i & 1;
+      const int qs = kb0 + i * kSlice;
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();                   // publishes slice i, frees buffer cur^1
+      if (i + 1 < ns) {
+        stage_slice(qs + kSlice, cur ^ 1);
+        stage_rows(qs + kSlice, cur ^ 1);
       }
-#pragma unroll
-      for (int st = 0; st < 2; ++st) {
-        const bf16x8 pb = acc_to_bf16(s, st);
-        const bf16x8 db = acc_to_bf16(dp, st);
-#pragma unroll
-        for (int dt = 0; dt < 2; ++dt) {
-          bf16x8 gt = tr_operand(ig, rb + 16 * st, 32 * dt, lane);   // dO^T, Q^T (asm reads)
-          bf16x8 qt = tr_operand(iq, rb + 16 * st, 32 * dt, lane);
-          tr_wait(gt, qt);
-          dv[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(gt, pb, dv[dt], 0, 0, 0);
-          dk[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qt, db, dk[dt], 0, 0, 0);
+      const char* iq = imgQ(cur);
+      const char* ig = imgG(cur);
+      const float* rv = rowv(cur);
+  #pragma unroll
+      for (int sub = 0; sub < 2; ++sub) {
+        const int qsub = qs + 32 * sub;
+        if (qsub + 31 < kw) continue;                 // wave-uniform: every query < every key
+        const int rb = 32 * sub;                      // image row base of this 32-query block
+        // per-row constants for rows q = qsub + 8 g + 4 hi + u (register e = 4 g + u) as the
+        // accumulators' starting values: S' = Q K^T - LSE sqrt(D), dP' = dO V^T - delta
+        // (asm reads: rowv is filled by LDS-DMA, and a compiler-visible read of it drained every
+        // DMA in flight — the next slice's Q / dO included; common.h ds_read_b128_asm)
+        f32x16 s, dp;
+        f32x4 lv[4], dv4[4];
+  #pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+          lv[g4] = ds_read_b128_asm(rv + rb + 8 * g4 + 4 * hi);
+          dv4[g4] = ds_read_b128_asm(rv + 64 + rb + 8 * g4 + 4 * hi);
+        }
+        tr_wait(lv[0], lv[1], lv[2], lv[3], dv4[0], dv4[1], dv4[2], dv4[3]);
+  #pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4)
+  #pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            s[4 * g4 + u] = lv[g4][u];
+            dp[4 * g4 + u] = dv4[g4][u];
+          }
+  #pragma unroll
+        for (int ks = 0; ks < 4; ++ks) {
+          s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_operand(iq, rb + r, 2 * ks + hi), kf[ks],
+                                                      s, 0, 0, 0);
+          dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_operand(ig, rb + r, 2 * ks + hi), vf[ks],
+                                                       dp, 0, 0, 0);
+        }
+        // mask the raw scores (exp2(-inf) = 0) only where a query of the block can precede a key
+        // of the wave (the diagonal) or lies past T: a wave-uniform branch, so interior blocks run
+        // no per-element index compares
+        const bool diag = qsub < kw + 31;
+        if (diag || qsub + 31 >= a.T) {
+  #pragma unroll
+          for (int e = 0; e < 16; ++e) {
+            const int q = qsub + (e & 3) + 8 * (e >> 2) + 4 * hi;
+            if ((diag && mykey > q) || q >= a.T) s[e] = -INFINITY;
+          }
+        }
+  #pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const float p = __builtin_amdgcn_exp2f(s[e] * a.scale_log2);
+          s[e] = p;
+          dp[e] = p * dp[e];
+        }
+  #pragma unroll
+        for (int st = 0; st < 2; ++st) {
+          const bf16x8 pb = acc_to_bf16(s, st);
+          const bf16x8 db = acc_to_bf16(dp, st);
+  #pragma unroll
+          for (int dt = 0; dt < 2; ++dt) {
+            bf16x8 gt = tr_operand(ig, rb + 16 * st, 32 * dt, lane);   // dO^T, Q^T (asm reads)
+            bf16x8 qt = tr_operand(iq, rb + 16 * st, 32 * dt, lane);
+            tr_wait(gt, qt);
+            dv[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(gt, pb, dv[dt], 0, 0, 0);
+            dk[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qt, db, dk[dt], 0, 0, 0);
+          }
         }
       }
     }
-  }
-  if (mykey < a.T) {
-    uint16_t* dkp = a.dqkv + (static_cast<int64_t>(b) * a.T + mykey) * a.ld + kAttnD * a.H + hoff;
-    uint16_t* dvp = dkp + kAttnD * a.H;
-#pragma unroll
-    for (int dt = 0; dt < 2; ++dt)
-#pragma unroll
-      for (int gg = 0; gg < 4; ++gg) {
-        u16x4 wk, wv;
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          wk[u] = f32_to_bf16(dk[dt][4 * gg + u] * a.scale);
-          wv[u] = f32_to_bf16(dv[dt][4 * gg + u]);
+    if (mykey < a.T) {
+      uint16_t* dkp = a.dqkv + (static_cast<int64_t>(b) * a.T + mykey) * a.ld + kAttnD * a.H + hoff;
+      uint16_t* dvp = dkp + kAttnD * a.H;
+  #pragma unroll
+      for (int dt = 0; dt < 2; ++dt)
+  #pragma unroll
+        for (int gg = 0; gg < 4; ++gg) {
+          u16x4 wk, wv;
+  #pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            wk[u] = f32_to_bf16(dk[dt][4 * gg + u] * a.scale);
+            wv[u] = f32_to_bf16(dv[dt][4 * gg + u]);
+          }
+          *reinterpret_cast<u16x4*>(dkp + dt * 32 + 8 * gg + 4 * hi) = wk;
+          *reinterpret_cast<u16x4*>(dvp + dt * 32 + 8 * gg + 4 * hi) = wv;
         }
-        *reinterpret_cast<u16x4*>(dkp + dt * 32 + 8 * gg + 4 * hi) = wk;
-        *reinterpret_cast<u16x4*>(dvp + dt * 32 + 8 * gg + 4 * hi) = wv;
-      }
+    }
   }
 }
 
@@ -584,7 +601,8 @@ __device__ __forceinline__ void stage_kv64(const AttnBwdArgs& a, const uint16_t*
     const int row = wave * 16 + i * 8 + r_in;
     int key = k0 + row;
     key = key < a.T ? key : a.T - 1;
-    const uint16_t* src = base_bt + static_cast<int64_t>(key) * a.ld + hoff + (slot ^ bswz(row)) * 8;
+    const uint16_t* src =
+        base_bt + static_cast<int64_t>(key) * a.ld + hoff + (slot ^ bswz(row)) * 8;
     attn_glds16(src + kAttnD * a.H, tk + (wave * 16 + i * 8) * 128);
     attn_glds16(src + 2 * kAttnD * a.H, tv + (wave * 16 + i * 8) * 128);
   }
@@ -598,148 +616,154 @@ __global__ void __launch_bounds__(kAttnThreads, 2) attn_bwd_dq_d64_kernel(AttnBw
   const int nqb = (a.T + kQB - 1) / kQB;
   int blk, h, b;
   head_block(a.xcd, blk, h, b);
-  const int qb = nqb - 1 - blk;
-  const int q0 = qb * kQB;
-  const int qw = q0 + wave * 32;
-  const int r = lane & 31, hi = lane >> 5;
-  const uint16_t* base_bt = a.qkv + static_cast<int64_t>(b) * a.T * a.ld;
-  const int hoff = h * kAttnD;
-  const int64_t bh = static_cast<int64_t>(b) * a.H + h;
-  const int qme = qw + r;
-  const int qc = qme < a.T ? qme : a.T - 1;
+  // causal pairing as the forward: query blocks nqb-1-blk then blk, equal work per workgroup
+  const int npass = nqb - 1 - blk != blk ? 2 : 1;
+  for (int pass = 0; pass < npass; ++pass) {
+    if (pass) __syncthreads();                    // every wave done with the LDS ring
+    const int qb = pass == 0 ? nqb - 1 - blk : blk;
+    const int q0 = qb * kQB;
+    const int qw = q0 + wave * 32;
+    const int r = lane & 31, hi = lane >> 5;
+    const uint16_t* base_bt = a.qkv + static_cast<int64_t>(b) * a.T * a.ld;
+    const int hoff = h * kAttnD;
+    const int64_t bh = static_cast<int64_t>(b) * a.H + h;
+    const int qme = qw + r;
+    const int qc = qme < a.T ? qme : a.T - 1;
 
-  bf16x8 qf[4], gf[4];
-  {
-    const uint16_t* qp = base_bt + static_cast<int64_t>(qc) * a.ld + hoff + 8 * hi;
-    const uint16_t* gp = a.dout + (static_cast<int64_t>(b) * a.T + qc) * a.ldo + hoff + 8 * hi;
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
-      qf[ks] = *reinterpret_cast<const bf16x8*>(qp + 16 * ks);
-      gf[ks] = *reinterpret_cast<const bf16x8*>(gp + 16 * ks);
-    }
-  }
-  float nl2, nd;                                   // -LSE * log2(e), -delta
-  if (a.fuse_delta) {
-    // the row constants of this lane's query, here instead of a separate pass over dO and O:
-    // delta = dO . O over the 64 dims (8 per (ks, hi) fragment, halves joined by lane ^ 32)
-    const uint16_t* op = a.out + (static_cast<int64_t>(b) * a.T + qc) * a.ldo + hoff + 8 * hi;
-    float acc = 0.f;
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
-      const bf16x8 of = *reinterpret_cast<const bf16x8*>(op + 16 * ks);
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-        acc += bf16_to_f32(static_cast<uint16_t>(gf[ks][j])) *
-               bf16_to_f32(static_cast<uint16_t>(of[j]));
-    }
-    const float other = __shfl_xor(acc, 32, 64);
-    nd = -(hi == 0 ? acc + other : other + acc);   // (even chunks) + (odd chunks), as the kernel
-    const float nls = -a.lse[bh * a.T + qc] / a.scale;   // -LSE * sqrt(D)
-    nl2 = nls * a.scale_log2;
-    if (hi == 0 && qme < a.T) {
-      a.delta[bh * a.T + qme] = nd;
-      a.nls[bh * a.T + qme] = nls;
-    }
-  } else {
-    nl2 = a.nls[bh * a.T + qc] * a.scale_log2;
-    nd = a.delta[bh * a.T + qc];
-  }
-  f32x16 dq[2];
-#pragma unroll
-  for (int dt = 0; dt < 2; ++dt)
-#pragma unroll
-    for (int e = 0; e < 16; ++e) dq[dt][e] = 0.f;
-  const int q_hi = qw + 31;
-  const int last_key = (q0 + kQB - 1) < (a.T - 1) ? (q0 + kQB - 1) : (a.T - 1);
-  const int nt = last_key / kKB + 1;
-  auto tileK = [&](int c) { return smem + c * 2 * kTileKV; };
-  auto tileV = [&](int c) { return smem + c * 2 * kTileKV + kTileKV; };
-  const uint16_t* ksrc[2];
-  if constexpr (INC) {
-    const int r_in = lane >> 3, slot = lane & 7;
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int row = wave * 16 + i * 8 + r_in;
-      ksrc[i] = base_bt + static_cast<int64_t>(row) * a.ld + hoff + (slot ^ bswz(row)) * 8 +
-                kAttnD * a.H;
-    }
-  }
-  auto stage = [&](int k0, char* tk, char* tv) {
-    if constexpr (INC) {
-      if (k0 + kKB <= a.T) {                        // wave-uniform: no row past T
-        const int64_t off = static_cast<int64_t>(k0) * a.ld;
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-          attn_glds16(ksrc[i] + off, tk + (wave * 16 + i * 8) * 128);
-          attn_glds16(ksrc[i] + off + kAttnD * a.H, tv + (wave * 16 + i * 8) * 128);
-        }
-        return;
+    bf16x8 qf[4], gf[4];
+    {
+      const uint16_t* qp = base_bt + static_cast<int64_t>(qc) * a.ld + hoff + 8 * hi;
+      const uint16_t* gp = a.dout + (static_cast<int64_t>(b) * a.T + qc) * a.ldo + hoff + 8 * hi;
+  #pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        qf[ks] = *reinterpret_cast<const bf16x8*>(qp + 16 * ks);
+        gf[ks] = *reinterpret_cast<const bf16x8*>(gp + 16 * ks);
       }
     }
-    stage_kv64(a, base_bt, k0, hoff, tk, tv, wave, lane);
-  };
-  stage(0, tileK(0), tileV(0));
-  for (int kt = 0; kt < nt; ++kt) {
-    const int cur = kt & 1;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();                   // publishes tile kt, frees buffer cur^1
-    if (kt + 1 < nt) stage((kt + 1) * kKB, tileK(cur ^ 1), tileV(cur ^ 1));
-    const int k0 = kt * kKB;
-    if (k0 <= q_hi) {
-      const char* tk = tileK(cur);
-      const char* tv = tileV(cur);
-      const bool diag = k0 + kKB - 1 > qw;           // wave-uniform: a key beyond a query
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
-        f32x16 s, dp;
-#pragma unroll
-        for (int e = 0; e < 16; ++e) { s[e] = 0.f; dp[e] = 0.f; }
-#pragma unroll
-        for (int ks = 0; ks < 4; ++ks) {
-          s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_operand(tk, kk * 32 + r, 2 * ks + hi),
-                                                      qf[ks], s, 0, 0, 0);
-          dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_operand(tv, kk * 32 + r, 2 * ks + hi),
-                                                       gf[ks], dp, 0, 0, 0);
+    float nl2, nd;                                   // -LSE * log2(e), -delta
+    if (a.fuse_delta) {
+      // the row constants of this lane's query, here instead of a separate pass over dO and O:
+      // delta = dO . O over the 64 dims (8 per (ks, hi) fragment, halves joined by lane ^ 32)
+      const uint16_t* op = a.out + (static_cast<int64_t>(b) * a.T + qc) * a.ldo + hoff + 8 * hi;
+      float acc = 0.f;
+  #pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        const bf16x8 of = *reinterpret_cast<const bf16x8*>(op + 16 * ks);
+  #pragma unroll
+        for (int j = 0; j < 8; ++j)
+          acc += bf16_to_f32(static_cast<uint16_t>(gf[ks][j])) *
+                 bf16_to_f32(static_cast<uint16_t>(of[j]));
+      }
+      const float other = __shfl_xor(acc, 32, 64);
+      nd = -(hi == 0 ? acc + other : other + acc);   // (even chunks) + (odd chunks), as the kernel
+      const float nls = -a.lse[bh * a.T + qc] / a.scale;   // -LSE * sqrt(D)
+      nl2 = nls * a.scale_log2;
+      if (hi == 0 && qme < a.T) {
+        a.delta[bh * a.T + qme] = nd;
+        a.nls[bh * a.T + qme] = nls;
+      }
+    } else {
+      nl2 = a.nls[bh * a.T + qc] * a.scale_log2;
+      nd = a.delta[bh * a.T + qc];
+    }
+    f32x16 dq[2];
+  #pragma unroll
+    for (int dt = 0; dt < 2; ++dt)
+  #pragma unroll
+      for (int e = 0; e < 16; ++e) dq[dt][e] = 0.f;
+    const int q_hi = qw + 31;
+    const int last_key = (q0 + kQB - 1) < (a.T - 1) ? (q0 + kQB - 1) : (a.T - 1);
+    const int nt = last_key / kKB + 1;
+    auto tileK = [&](int c) { return smem + c * 2 * kTileKV; };
+    auto tileV = [&](int c) { return smem + c * 2 * kTileKV + kTileKV; };
+    const uint16_t* ksrc[2];
+    if constexpr (INC) {
+      const int r_in = lane >> 3, slot = lane & 7;
+  #pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int row = wave * 16 + i * 8 + r_in;
+        ksrc[i] = base_bt + static_cast<int64_t>(row) * a.ld + hoff + (slot ^ bswz(row)) * 8 +
+                  kAttnD * a.H;
+      }
+    }
+    auto stage = [&](int k0, char* tk, char* tv) {
+      if constexpr (INC) {
+        if (k0 + kKB <= a.T) {                        // wave-uniform: no row past T
+          const int64_t off = static_cast<int64_t>(k0) * a.ld;
+  #pragma unroll
+          for (int i = 0; i < 2; ++i) {
+            attn_glds16(ksrc[i] + off, tk + (wave * 16 + i * 8) * 128);
+            attn_glds16(ksrc[i] + off + kAttnD * a.H, tv + (wave * 16 + i * 8) * 128);
+          }
+          return;
         }
-        // causal mask on the raw scores of diagonal tiles only (a branch, as in the forward:
-        // exp2 of -inf is the zero probability); interior tiles run no per-element compares
-        if (diag) {
-#pragma unroll
+      }
+      stage_kv64(a, base_bt, k0, hoff, tk, tv, wave, lane);
+    };
+    stage(0, tileK(0), tileV(0));
+    for (int kt = 0; kt < nt; ++kt) {
+      const int cur = kt & 1;
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();                   // publishes tile kt, frees buffer cur^1
+      if (kt + 1 < nt) stage((kt + 1) * kKB, tileK(cur ^ 1), tileV(cur ^ 1));
+      const int k0 = kt * kKB;
+      if (k0 <= q_hi) {
+        const char* tk = tileK(cur);
+        const char* tv = tileV(cur);
+        const bool diag = k0 + kKB - 1 > qw;           // wave-uniform: a key beyond a query
+  #pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+          f32x16 s, dp;
+  #pragma unroll
+          for (int e = 0; e < 16; ++e) { s[e] = 0.f; dp[e] = 0.f; }
+  #pragma unroll
+          for (int ks = 0; ks < 4; ++ks) {
+            s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_operand(tk, kk * 32 + r, 2 * ks + hi),
+                                                        qf[ks], s, 0, 0, 0);
+            dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_operand(tv, kk * 32 + r, 2 * ks + hi),
+                                                         gf[ks], dp, 0, 0, 0);
+          }
+          // causal mask on the raw scores of diagonal tiles only (a branch, as in the forward:
+          // exp2 of -inf is the zero probability); interior tiles run no per-element compares
+          if (diag) {
+  #pragma unroll
+            for (int e = 0; e < 16; ++e) {
+              const int key = k0 + kk * 32 + (e & 3) + 8 * (e >> 2) + 4 * hi;
+              if (key > qme) s[e] = -INFINITY;
+            }
+          }
+  #pragma unroll
           for (int e = 0; e < 16; ++e) {
-            const int key = k0 + kk * 32 + (e & 3) + 8 * (e >> 2) + 4 * hi;
-            if (key > qme) s[e] = -INFINITY;
+            const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(s[e], a.scale_log2, nl2));
+            dp[e] = p * (dp[e] + nd);
+          }
+  #pragma unroll
+          for (int st = 0; st < 2; ++st) {
+            bf16x8 kt2[2];                            // K^T operands (asm reads)
+  #pragma unroll
+            for (int dt = 0; dt < 2; ++dt)
+              kt2[dt] = tr_operand(tk, kk * 32 + 16 * st, 32 * dt, lane);
+            const bf16x8 db = acc_to_bf16(dp, st);
+            tr_wait(kt2[0], kt2[1]);
+  #pragma unroll
+            for (int dt = 0; dt < 2; ++dt)
+              dq[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kt2[dt], db, dq[dt], 0, 0, 0);
           }
         }
-#pragma unroll
-        for (int e = 0; e < 16; ++e) {
-          const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(s[e], a.scale_log2, nl2));
-          dp[e] = p * (dp[e] + nd);
-        }
-#pragma unroll
-        for (int st = 0; st < 2; ++st) {
-          bf16x8 kt2[2];                            // K^T operands (asm reads)
-#pragma unroll
-          for (int dt = 0; dt < 2; ++dt) kt2[dt] = tr_operand(tk, kk * 32 + 16 * st, 32 * dt, lane);
-          const bf16x8 db = acc_to_bf16(dp, st);
-          tr_wait(kt2[0], kt2[1]);
-#pragma unroll
-          for (int dt = 0; dt < 2; ++dt)
-            dq[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kt2[dt], db, dq[dt], 0, 0, 0);
-        }
       }
     }
-  }
-  if (qme < a.T) {
-    uint16_t* dqp = a.dqkv + (static_cast<int64_t>(b) * a.T + qme) * a.ld + hoff;
-#pragma unroll
-    for (int dt = 0; dt < 2; ++dt)
-#pragma unroll
-      for (int gg = 0; gg < 4; ++gg) {
-        u16x4 w;
-#pragma unroll
-        for (int u = 0; u < 4; ++u) w[u] = f32_to_bf16(dq[dt][4 * gg + u] * a.scale);
-        *reinterpret_cast<u16x4*>(dqp + dt * 32 + 8 * gg + 4 * hi) = w;
-      }
+    if (qme < a.T) {
+      uint16_t* dqp = a.dqkv + (static_cast<int64_t>(b) * a.T + qme) * a.ld + hoff;
+  #pragma unroll
+      for (int dt = 0; dt < 2; ++dt)
+  #pragma unroll
+        for (int gg = 0; gg < 4; ++gg) {
+          u16x4 w;
+  #pragma unroll
+          for (int u = 0; u < 4; ++u) w[u] = f32_to_bf16(dq[dt][4 * gg + u] * a.scale);
+          *reinterpret_cast<u16x4*>(dqp + dt * 32 + 8 * gg + 4 * hi) = w;
+        }
+    }
   }
 }
 
@@ -762,7 +786,7 @@ DLBB_API int dlbb_attn_fwd(const void* qkv, int64_t ld, void* out, int64_t ldo, 
   if (ld < 3 * H * D || ldo < H * D) return hipErrorInvalidValue;
   AttnArgs a{static_cast<const uint16_t*>(qkv), static_cast<uint16_t*>(out), lse, ld, ldo,
              B, T, H, scale * 1.4426950408889634f, g_attn_xcd};
-  const dim3 grid((T + kQB - 1) / kQB, H, B);
+  const dim3 grid(((T + kQB - 1) / kQB + 1) / 2, H, B);   // query blocks paired (causal)
   if (D == 64)
     hipLaunchKernelGGL(attn_fwd_kernel<64>, grid, dim3(kAttnThreads), 4 * FwdGeo<64>::TILE,
                        stream, a);
@@ -792,7 +816,9 @@ DLBB_API int dlbb_attn_bwd(const void* qkv, int64_t ld, const void* out, const v
                 delta + rows, static_cast<const uint16_t*>(out), 1,
                 static_cast<uint16_t*>(dqkv), ld, ldo, B, T, H,
                 scale * 1.4426950408889634f, scale, g_attn_xcd};
-  const dim3 gq((T + kQB - 1) / kQB, H, B), gk((T + kBwdKeys - 1) / kBwdKeys, H, B);
+  // both kernels pair a heavy and a light causal block per workgroup (see the forward)
+  const dim3 gq(((T + kQB - 1) / kQB + 1) / 2, H, B),
+      gk(((T + kBwdKeys - 1) / kBwdKeys + 1) / 2, H, B);
   hipLaunchKernelGGL(attn_bwd_dq_d64_kernel<true>, gq, dim3(kAttnThreads), 4 * kTileKV, stream,
                      a);
   hipLaunchKernelGGL(attn_bwd_dkdv_d64_kernel<false>, gk, dim3(kAttnThreads),
