@@ -150,14 +150,14 @@ __global__ void __launch_bounds__(kAttnThreads, 2) attn_fwd_kernel(AttnArgs a) {
       int q = qw + r;
       q = q < a.T ? q : a.T - 1;
       const uint16_t* qp = base_bt + static_cast<int64_t>(q) * a.ld + hoff + 8 * hi;
-  #pragma unroll
+#pragma unroll
       for (int ks = 0; ks < G::NKS; ++ks) qf[ks] = *reinterpret_cast<const bf16x8*>(qp + 16 * ks);
     }
 
     f32x16 o[G::NDT];
-  #pragma unroll
+#pragma unroll
     for (int dt = 0; dt < G::NDT; ++dt)
-  #pragma unroll
+#pragma unroll
       for (int e = 0; e < 16; ++e) o[dt][e] = 0.f;
     float m = -INFINITY, l = 0.f;
     const int qme = qw + r;                          // this lane's query
@@ -172,7 +172,7 @@ __global__ void __launch_bounds__(kAttnThreads, 2) attn_fwd_kernel(AttnArgs a) {
     // tile 0 (K and V sections, swizzled chunk); tile kt adds kt * KB rows, uniform
     const int r_in = lane / (ROW / 16), slot = lane % (ROW / 16);
     const uint16_t* dsrc[4];
-  #pragma unroll
+#pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int row = wave * WROWS + i * RPI + r_in;
       const uint16_t* src = base_bt + static_cast<int64_t>(row) * a.ld + hoff;
@@ -182,14 +182,14 @@ __global__ void __launch_bounds__(kAttnThreads, 2) attn_fwd_kernel(AttnArgs a) {
     auto stage = [&](int k0, char* tk, char* tv) {
       if (k0 + KB <= a.T) {                          // wave-uniform: no row past T
         const int64_t off = static_cast<int64_t>(k0) * a.ld;
-  #pragma unroll
+#pragma unroll
         for (int i = 0; i < 2; ++i) {
           attn_glds16(dsrc[2 * i] + off, tk + (wave * WROWS + i * RPI) * ROW);
           attn_glds16(dsrc[2 * i + 1] + off, tv + (wave * WROWS + i * RPI) * ROW);
         }
         return;
       }
-  #pragma unroll
+#pragma unroll
       for (int i = 0; i < 2; ++i) {                  // rows past T clamped (scores masked)
         const int row = wave * WROWS + i * RPI + r_in;
         int key = k0 + row;
@@ -215,12 +215,12 @@ __global__ void __launch_bounds__(kAttnThreads, 2) attn_fwd_kernel(AttnArgs a) {
         const char* tv = tileV(cur);
         // ---- S^T for the 32-key halves
         f32x16 s[G::NKK];
-  #pragma unroll
+#pragma unroll
         for (int kk = 0; kk < G::NKK; ++kk) {
-  #pragma unroll
+#pragma unroll
           for (int e = 0; e < 16; ++e) s[kk][e] = 0.f;
           const int row = kk * 32 + r;
-  #pragma unroll
+#pragma unroll
           for (int ks = 0; ks < G::NKS; ++ks) {
             const int c = 2 * ks + hi;
             const bf16x8 kf =
@@ -233,16 +233,16 @@ __global__ void __launch_bounds__(kAttnThreads, 2) attn_fwd_kernel(AttnArgs a) {
         if (diag) {
           // key(kk, e) = k0 + 4 hi + kk*32 + (e & 3) + 8 (e >> 2): one per-lane threshold
           const int th = qme - k0 - 4 * hi;
-  #pragma unroll
+#pragma unroll
           for (int kk = 0; kk < G::NKK; ++kk)
-  #pragma unroll
+#pragma unroll
             for (int e = 0; e < 16; ++e)
               if (kk * 32 + (e & 3) + 8 * (e >> 2) > th) s[kk][e] = -INFINITY;
         }
         float mx = -INFINITY;                          // max of the RAW scores (scale > 0)
-  #pragma unroll
+#pragma unroll
         for (int kk = 0; kk < G::NKK; ++kk)
-  #pragma unroll
+#pragma unroll
           for (int e = 0; e < 16; ++e) mx = fmaxf(mx, s[kk][e]);
         mx = xhalf_max(mx);
         const float mn = fmaxf(m, mx * a.scale_log2);
@@ -250,36 +250,36 @@ __global__ void __launch_bounds__(kAttnThreads, 2) attn_fwd_kernel(AttnArgs a) {
         const bool rescale = m != mn;
         m = mn;
         float ls = 0.f;
-  #pragma unroll
+#pragma unroll
         for (int kk = 0; kk < G::NKK; ++kk)
-  #pragma unroll
+#pragma unroll
           for (int e = 0; e < 16; ++e) {
             s[kk][e] = __builtin_amdgcn_exp2f(__builtin_fmaf(s[kk][e], a.scale_log2, -mn));
             ls += s[kk][e];
           }
         l = l * alpha + ls;
         if (__any(rescale)) {                          // wave-uniform skip when no max moved
-  #pragma unroll
+#pragma unroll
           for (int dt = 0; dt < G::NDT; ++dt)
-  #pragma unroll
+#pragma unroll
             for (int e = 0; e < 16; ++e) o[dt][e] *= alpha;
         }
         // ---- O^T += V^T P^T: k-step = 16 keys;
         //      P^T element j <-> key 16 s + 8 (j>>2) + 4 hi + (j&3)
         const int g = lane >> 4, i16 = lane & 15;
         const int tq = i16 >> 2, tp = i16 & 3;        // tr-read lane role: block row / col group
-  #pragma unroll
+#pragma unroll
         for (int kk = 0; kk < G::NKK; ++kk)
-  #pragma unroll
+#pragma unroll
           for (int st = 0; st < 2; ++st) {
             bf16x8 pf;
-  #pragma unroll
+#pragma unroll
             for (int j = 0; j < 8; ++j)
               pf[j] = __builtin_bit_cast(short, static_cast<__bf16>(s[kk][8 * st + j]));
-  #pragma unroll
+#pragma unroll
             for (int dt = 0; dt < G::NDT; ++dt) {
               bf16x8 vf;
-  #pragma unroll
+#pragma unroll
               for (int half = 0; half < 2; ++half) {
                 const int row = kk * 32 + 16 * st + 8 * half + 4 * (g >> 1) + tq;
                 const int col = dt * 32 + 16 * (g & 1) + 4 * tp;
@@ -290,7 +290,7 @@ __global__ void __launch_bounds__(kAttnThreads, 2) attn_fwd_kernel(AttnArgs a) {
                 // under counted lgkmcnt waits (the asm form measured 3-4 % slower here,
                 // profiles/r05_attention/). tools/isa_check.py allows this kernel.
                 const i16x4 t = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4_ptr)(tv + off));
-  #pragma unroll
+#pragma unroll
                 for (int u = 0; u < 4; ++u) vf[4 * half + u] = t[u];
               }
               o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf, o[dt], 0, 0, 0);
@@ -304,12 +304,12 @@ __global__ void __launch_bounds__(kAttnThreads, 2) attn_fwd_kernel(AttnArgs a) {
     const float inv = lt > 0.f ? 1.f / lt : 0.f;
     if (qme < a.T) {
       uint16_t* op = a.out + (static_cast<int64_t>(b) * a.T + qme) * a.ldo + hoff;
-  #pragma unroll
+#pragma unroll
       for (int dt = 0; dt < G::NDT; ++dt)
-  #pragma unroll
+#pragma unroll
         for (int gg = 0; gg < 4; ++gg) {
           u16x4 w;
-  #pragma unroll
+#pragma unroll
           for (int u = 0; u < 4; ++u) w[u] = f32_to_bf16(o[dt][4 * gg + u] * inv);
           *reinterpret_cast<u16x4*>(op + dt * 32 + 8 * gg + 4 * hi) = w;
         }
@@ -439,16 +439,16 @@ __global__ void __launch_bounds__(kAttnThreads, 2) attn_bwd_dkdv_d64_kernel(Attn
       const int kk = mykey < a.T ? mykey : a.T - 1;
       const uint16_t* kp = base_bt + static_cast<int64_t>(kk) * a.ld + kAttnD * a.H + hoff + 8 * hi;
       const uint16_t* vp = kp + kAttnD * a.H;
-  #pragma unroll
+#pragma unroll
       for (int ks = 0; ks < 4; ++ks) {
         kf[ks] = *reinterpret_cast<const bf16x8*>(kp + 16 * ks);
         vf[ks] = *reinterpret_cast<const bf16x8*>(vp + 16 * ks);
       }
     }
     f32x16 dv[2], dk[2];
-  #pragma unroll
+#pragma unroll
     for (int dt = 0; dt < 2; ++dt)
-  #pragma unroll
+#pragma unroll
       for (int e = 0; e < 16; ++e) { dv[dt][e] = 0.f; dk[dt][e] = 0.f; }
 
     const int ns = (a.T - kb0 + kSlice - 1) / kSlice;
@@ -471,7 +471,7 @@ __global__ void __launch_bounds__(kAttnThreads, 2) attn_bwd_dkdv_d64_kernel(Attn
     const uint16_t* gsrc[2];
     if constexpr (INC) {
       const int r_in = lane >> 3, slot = lane & 7;
-  #pragma unroll
+#pragma unroll
       for (int i = 0; i < 2; ++i) {
         const int row = wave * 16 + i * 8 + r_in;
         qsrc[i] = base_bt + hoff + static_cast<int64_t>(kb0 + row) * a.ld + (slot ^ bswz(row)) * 8;
@@ -482,7 +482,7 @@ __global__ void __launch_bounds__(kAttnThreads, 2) attn_bwd_dkdv_d64_kernel(Attn
       if constexpr (INC) {
         if (q0 + kSlice <= a.T) {                     // wave-uniform: no row past T
           const int d = q0 - kb0;
-  #pragma unroll
+#pragma unroll
           for (int i = 0; i < 2; ++i) {
             attn_glds16(qsrc[i] + static_cast<int64_t>(d) * a.ld,
                         imgQ(c) + (wave * 16 + i * 8) * 128);
@@ -509,7 +509,7 @@ __global__ void __launch_bounds__(kAttnThreads, 2) attn_bwd_dkdv_d64_kernel(Attn
       const char* iq = imgQ(cur);
       const char* ig = imgG(cur);
       const float* rv = rowv(cur);
-  #pragma unroll
+#pragma unroll
       for (int sub = 0; sub < 2; ++sub) {
         const int qsub = qs + 32 * sub;
         if (qsub + 31 < kw) continue;                 // wave-uniform: every query < every key
@@ -520,20 +520,20 @@ __global__ void __launch_bounds__(kAttnThreads, 2) attn_bwd_dkdv_d64_kernel(Attn
         // DMA in flight — the next slice's Q / dO included; common.h ds_read_b128_asm)
         f32x16 s, dp;
         f32x4 lv[4], dv4[4];
-  #pragma unroll
+#pragma unroll
         for (int g4 = 0; g4 < 4; ++g4) {
           lv[g4] = ds_read_b128_asm(rv + rb + 8 * g4 + 4 * hi);
           dv4[g4] = ds_read_b128_asm(rv + 64 + rb + 8 * g4 + 4 * hi);
         }
         tr_wait(lv[0], lv[1], lv[2], lv[3], dv4[0], dv4[1], dv4[2], dv4[3]);
-  #pragma unroll
+#pragma unroll
         for (int g4 = 0; g4 < 4; ++g4)
-  #pragma unroll
+#pragma unroll
           for (int u = 0; u < 4; ++u) {
             s[4 * g4 + u] = lv[g4][u];
             dp[4 * g4 + u] = dv4[g4][u];
           }
-  #pragma unroll
+#pragma unroll
         for (int ks = 0; ks < 4; ++ks) {
           s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_operand(iq, rb + r, 2 * ks + hi), kf[ks],
                                                       s, 0, 0, 0);
@@ -545,23 +545,23 @@ __global__ void __launch_bounds__(kAttnThreads, 2) attn_bwd_dkdv_d64_kernel(Attn
         // no per-element index compares
         const bool diag = qsub < kw + 31;
         if (diag || qsub + 31 >= a.T) {
-  #pragma unroll
+#pragma unroll
           for (int e = 0; e < 16; ++e) {
             const int q = qsub + (e & 3) + 8 * (e >> 2) + 4 * hi;
             if ((diag && mykey > q) || q >= a.T) s[e] = -INFINITY;
           }
         }
-  #pragma unroll
+#pragma unroll
         for (int e = 0; e < 16; ++e) {
           const float p = __builtin_amdgcn_exp2f(s[e] * a.scale_log2);
           s[e] = p;
           dp[e] = p * dp[e];
         }
-  #pragma unroll
+#pragma unroll
         for (int st = 0; st < 2; ++st) {
           const bf16x8 pb = acc_to_bf16(s, st);
           const bf16x8 db = acc_to_bf16(dp, st);
-  #pragma unroll
+#pragma unroll
           for (int dt = 0; dt < 2; ++dt) {
             bf16x8 gt = tr_operand(ig, rb + 16 * st, 32 * dt, lane);   // dO^T, Q^T (asm reads)
             bf16x8 qt = tr_operand(iq, rb + 16 * st, 32 * dt, lane);
@@ -575,12 +575,12 @@ __global__ void __launch_bounds__(kAttnThreads, 2) attn_bwd_dkdv_d64_kernel(Attn
     if (mykey < a.T) {
       uint16_t* dkp = a.dqkv + (static_cast<int64_t>(b) * a.T + mykey) * a.ld + kAttnD * a.H + hoff;
       uint16_t* dvp = dkp + kAttnD * a.H;
-  #pragma unroll
+#pragma unroll
       for (int dt = 0; dt < 2; ++dt)
-  #pragma unroll
+#pragma unroll
         for (int gg = 0; gg < 4; ++gg) {
           u16x4 wk, wv;
-  #pragma unroll
+#pragma unroll
           for (int u = 0; u < 4; ++u) {
             wk[u] = f32_to_bf16(dk[dt][4 * gg + u] * a.scale);
             wv[u] = f32_to_bf16(dv[dt][4 * gg + u]);
@@ -634,7 +634,7 @@ __global__ void __launch_bounds__(kAttnThreads, 2) attn_bwd_dq_d64_kernel(AttnBw
     {
       const uint16_t* qp = base_bt + static_cast<int64_t>(qc) * a.ld + hoff + 8 * hi;
       const uint16_t* gp = a.dout + (static_cast<int64_t>(b) * a.T + qc) * a.ldo + hoff + 8 * hi;
-  #pragma unroll
+#pragma unroll
       for (int ks = 0; ks < 4; ++ks) {
         qf[ks] = *reinterpret_cast<const bf16x8*>(qp + 16 * ks);
         gf[ks] = *reinterpret_cast<const bf16x8*>(gp + 16 * ks);
@@ -646,10 +646,10 @@ __global__ void __launch_bounds__(kAttnThreads, 2) attn_bwd_dq_d64_kernel(AttnBw
       // delta = dO . O over the 64 dims (8 per (ks, hi) fragment, halves joined by lane ^ 32)
       const uint16_t* op = a.out + (static_cast<int64_t>(b) * a.T + qc) * a.ldo + hoff + 8 * hi;
       float acc = 0.f;
-  #pragma unroll
+#pragma unroll
       for (int ks = 0; ks < 4; ++ks) {
         const bf16x8 of = *reinterpret_cast<const bf16x8*>(op + 16 * ks);
-  #pragma unroll
+#pragma unroll
         for (int j = 0; j < 8; ++j)
           acc += bf16_to_f32(static_cast<uint16_t>(gf[ks][j])) *
                  bf16_to_f32(static_cast<uint16_t>(of[j]));
@@ -667,9 +667,9 @@ __global__ void __launch_bounds__(kAttnThreads, 2) attn_bwd_dq_d64_kernel(AttnBw
       nd = a.delta[bh * a.T + qc];
     }
     f32x16 dq[2];
-  #pragma unroll
+#pragma unroll
     for (int dt = 0; dt < 2; ++dt)
-  #pragma unroll
+#pragma unroll
       for (int e = 0; e < 16; ++e) dq[dt][e] = 0.f;
     const int q_hi = qw + 31;
     const int last_key = (q0 + kQB - 1) < (a.T - 1) ? (q0 + kQB - 1) : (a.T - 1);
@@ -679,7 +679,7 @@ __global__ void __launch_bounds__(kAttnThreads, 2) attn_bwd_dq_d64_kernel(AttnBw
     const uint16_t* ksrc[2];
     if constexpr (INC) {
       const int r_in = lane >> 3, slot = lane & 7;
-  #pragma unroll
+#pragma unroll
       for (int i = 0; i < 2; ++i) {
         const int row = wave * 16 + i * 8 + r_in;
         ksrc[i] = base_bt + static_cast<int64_t>(row) * a.ld + hoff + (slot ^ bswz(row)) * 8 +
@@ -690,7 +690,7 @@ __global__ void __launch_bounds__(kAttnThreads, 2) attn_bwd_dq_d64_kernel(AttnBw
       if constexpr (INC) {
         if (k0 + kKB <= a.T) {                        // wave-uniform: no row past T
           const int64_t off = static_cast<int64_t>(k0) * a.ld;
-  #pragma unroll
+#pragma unroll
           for (int i = 0; i < 2; ++i) {
             attn_glds16(ksrc[i] + off, tk + (wave * 16 + i * 8) * 128);
             attn_glds16(ksrc[i] + off + kAttnD * a.H, tv + (wave * 16 + i * 8) * 128);
@@ -711,12 +711,12 @@ __global__ void __launch_bounds__(kAttnThreads, 2) attn_bwd_dq_d64_kernel(AttnBw
         const char* tk = tileK(cur);
         const char* tv = tileV(cur);
         const bool diag = k0 + kKB - 1 > qw;           // wave-uniform: a key beyond a query
-  #pragma unroll
+#pragma unroll
         for (int kk = 0; kk < 2; ++kk) {
           f32x16 s, dp;
-  #pragma unroll
+#pragma unroll
           for (int e = 0; e < 16; ++e) { s[e] = 0.f; dp[e] = 0.f; }
-  #pragma unroll
+#pragma unroll
           for (int ks = 0; ks < 4; ++ks) {
             s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_operand(tk, kk * 32 + r, 2 * ks + hi),
                                                         qf[ks], s, 0, 0, 0);
@@ -726,26 +726,26 @@ __global__ void __launch_bounds__(kAttnThreads, 2) attn_bwd_dq_d64_kernel(AttnBw
           // causal mask on the raw scores of diagonal tiles only (a branch, as in the forward:
           // exp2 of -inf is the zero probability); interior tiles run no per-element compares
           if (diag) {
-  #pragma unroll
+#pragma unroll
             for (int e = 0; e < 16; ++e) {
               const int key = k0 + kk * 32 + (e & 3) + 8 * (e >> 2) + 4 * hi;
               if (key > qme) s[e] = -INFINITY;
             }
           }
-  #pragma unroll
+#pragma unroll
           for (int e = 0; e < 16; ++e) {
             const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(s[e], a.scale_log2, nl2));
             dp[e] = p * (dp[e] + nd);
           }
-  #pragma unroll
+#pragma unroll
           for (int st = 0; st < 2; ++st) {
             bf16x8 kt2[2];                            // K^T operands (asm reads)
-  #pragma unroll
+#pragma unroll
             for (int dt = 0; dt < 2; ++dt)
               kt2[dt] = tr_operand(tk, kk * 32 + 16 * st, 32 * dt, lane);
             const bf16x8 db = acc_to_bf16(dp, st);
             tr_wait(kt2[0], kt2[1]);
-  #pragma unroll
+#pragma unroll
             for (int dt = 0; dt < 2; ++dt)
               dq[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kt2[dt], db, dq[dt], 0, 0, 0);
           }
@@ -754,12 +754,12 @@ __global__ void __launch_bounds__(kAttnThreads, 2) attn_bwd_dq_d64_kernel(AttnBw
     }
     if (qme < a.T) {
       uint16_t* dqp = a.dqkv + (static_cast<int64_t>(b) * a.T + qme) * a.ld + hoff;
-  #pragma unroll
+#pragma unroll
       for (int dt = 0; dt < 2; ++dt)
-  #pragma unroll
+#pragma unroll
         for (int gg = 0; gg < 4; ++gg) {
           u16x4 w;
-  #pragma unroll
+#pragma unroll
           for (int u = 0; u < 4; ++u) w[u] = f32_to_bf16(dq[dt][4 * gg + u] * a.scale);
           *reinterpret_cast<u16x4*>(dqp + dt * 32 + 8 * gg + 4 * hi) = w;
         }
