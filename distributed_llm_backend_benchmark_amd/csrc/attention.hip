@@ -245,7 +245,12 @@ __global__ void __launch_bounds__(kAttnThreads, 2) attn_fwd_kernel(AttnArgs a) {
 #pragma unroll
           for (int e = 0; e < 16; ++e) mx = fmaxf(mx, s[kk][e]);
         mx = xhalf_max(mx);
-        const float mn = fmaxf(m, mx * a.scale_log2);
+        // deferred max (CDNA guide §B "defer-max RESCALE_THRESHOLD"): the running max moves only
+        // when some lane's tile max exceeds it by more than 2^8 in probability, so after the
+        // first tiles p = exp2(s - m) stays <= 256 (bf16 / fp32 safe) and the O rescale and its
+        // exp are skipped; the normaliser l and LSE use the same m, so the result is unchanged
+        const float mc = mx * a.scale_log2;
+        const float mn = __any(mc > m + 8.f) ? fmaxf(m, mc) : m;   // m = -inf first: moves
         const float alpha = __builtin_amdgcn_exp2f(m - mn);   // m = -inf on the first tile -> 0
         const bool rescale = m != mn;
         m = mn;
