@@ -24,6 +24,7 @@
 #include "common.h"
 
 #include <cstdlib>
+#include <type_traits>
 
 namespace dlbb {
 
@@ -383,6 +384,32 @@ __device__ __forceinline__ bf16x8 tr_operand(const char* img, int rowbase, int c
   return f;
 }
 
+// tr_operand with the row offset as the reads' immediate: rows rowbase + 8 half + 4 (g>>1) + tq
+// of column block dt. For rowbase % 16 == 0 the bswz chunk is (lane bits) | ((dt ^ half ^
+// lane bit) << 2), so the address is one of two per-lane values (tr_lane_off(P), P = dt ^
+// half) plus (rowbase + 8 half) * 128 — `same` = image + tr_lane_off(dt), `flip` = image +
+// tr_lane_off(dt ^ 1). Equal to tr_operand for every lane / rowbase / dt (checked offline
+// over all combinations when written); asm reads: the caller waits (tr_wait).
+__device__ __forceinline__ uint32_t tr_lane_off(int lane, int P) {
+  const int g = lane >> 4, i16 = lane & 15, tq = i16 >> 2, tp = i16 & 3;
+  const int L = 2 * (g >> 1) + (tq >> 1);
+  const int chunk = (((2 * (g & 1) + (tp >> 1)) ^ L) & 3) | (((P ^ (L & 1)) & 1) << 2);
+  return static_cast<uint32_t>((4 * (g >> 1) + tq) * 128 + chunk * 16 + ((4 * tp) & 7) * 2);
+}
+template <int ROWBASE>
+__device__ __forceinline__ bf16x8 tr_operand_at(const char* same, const char* flip) {
+  static_assert(ROWBASE % 16 == 0, "row base");
+  const i16x4 t0 = ds_read_tr16<ROWBASE * 128>(same);
+  const i16x4 t1 = ds_read_tr16<(ROWBASE + 8) * 128>(flip);
+  bf16x8 f;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    f[u] = t0[u];
+    f[4 + u] = t1[u];
+  }
+  return f;
+}
+
 __device__ __forceinline__ bf16x8 row_operand(const char* img, int row, int chunk) {
   return *reinterpret_cast<const bf16x8*>(img + row * 128 + ((chunk ^ bswz(row)) << 4));
 }
@@ -514,11 +541,16 @@ __global__ void __launch_bounds__(kAttnThreads, 2) attn_bwd_dkdv_d64_kernel(Attn
       const char* iq = imgQ(cur);
       const char* ig = imgG(cur);
       const float* rv = rowv(cur);
-#pragma unroll
-      for (int sub = 0; sub < 2; ++sub) {
+      // transposed-read lane addresses of this slice's images (parity 0 / 1, tr_operand_at)
+      const char* gq0 = iq + tr_lane_off(lane, 0);
+      const char* gq1 = iq + tr_lane_off(lane, 1);
+      const char* gg0 = ig + tr_lane_off(lane, 0);
+      const char* gg1 = ig + tr_lane_off(lane, 1);
+      auto sub_body = [&](auto subc) __attribute__((always_inline)) {
+        constexpr int sub = decltype(subc)::value;
         const int qsub = qs + 32 * sub;
-        if (qsub + 31 < kw) continue;                 // wave-uniform: every query < every key
-        const int rb = 32 * sub;                      // image row base of this 32-query block
+        if (qsub + 31 < kw) return;                   // wave-uniform: every query < every key
+        constexpr int rb = 32 * sub;                  // image row base of this 32-query block
         // per-row constants for rows q = qsub + 8 g + 4 hi + u (register e = 4 g + u) as the
         // accumulators' starting values: S' = Q K^T - LSE sqrt(D), dP' = dO V^T - delta
         // (asm reads: rowv is filled by LDS-DMA, and a compiler-visible read of it drained every
@@ -562,20 +594,25 @@ __global__ void __launch_bounds__(kAttnThreads, 2) attn_bwd_dkdv_d64_kernel(Attn
           s[e] = p;
           dp[e] = p * dp[e];
         }
-#pragma unroll
-        for (int st = 0; st < 2; ++st) {
+        auto st_body = [&](auto stc) __attribute__((always_inline)) {
+          constexpr int st = decltype(stc)::value;
           const bf16x8 pb = acc_to_bf16(s, st);
           const bf16x8 db = acc_to_bf16(dp, st);
 #pragma unroll
           for (int dt = 0; dt < 2; ++dt) {
-            bf16x8 gt = tr_operand(ig, rb + 16 * st, 32 * dt, lane);   // dO^T, Q^T (asm reads)
-            bf16x8 qt = tr_operand(iq, rb + 16 * st, 32 * dt, lane);
+            // dO^T, Q^T (asm reads; row offset in the immediate)
+            bf16x8 gt = tr_operand_at<rb + 16 * st>(dt ? gg1 : gg0, dt ? gg0 : gg1);
+            bf16x8 qt = tr_operand_at<rb + 16 * st>(dt ? gq1 : gq0, dt ? gq0 : gq1);
             tr_wait(gt, qt);
             dv[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(gt, pb, dv[dt], 0, 0, 0);
             dk[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qt, db, dk[dt], 0, 0, 0);
           }
-        }
-      }
+        };
+        st_body(std::integral_constant<int, 0>{});
+        st_body(std::integral_constant<int, 1>{});
+      };
+      sub_body(std::integral_constant<int, 0>{});
+      sub_body(std::integral_constant<int, 1>{});
     }
     if (mykey < a.T) {
       uint16_t* dkp = a.dqkv + (static_cast<int64_t>(b) * a.T + mykey) * a.ld + kAttnD * a.H + hoff;
@@ -714,6 +751,17 @@ __global__ void __launch_bounds__(kAttnThreads, 2) attn_bwd_dq_d64_kernel(AttnBw
       const int k0 = kt * kKB;
       if (k0 <= q_hi) {
         const char* tk = tileK(cur);
+        // K^T transposed-read lane addresses (parity 0 / 1) and the row offset as the immediate
+        const char* tk0 = tk + tr_lane_off(lane, 0);
+        const char* tk1 = tk + tr_lane_off(lane, 1);
+        auto trk = [&](int sel, const char* same, const char* flip) __attribute__((always_inline)) {
+          switch (sel) {                              // (compile-time after unrolling)
+            case 0: return tr_operand_at<0>(same, flip);
+            case 1: return tr_operand_at<16>(same, flip);
+            case 2: return tr_operand_at<32>(same, flip);
+            default: return tr_operand_at<48>(same, flip);
+          }
+        };
         const char* tv = tileV(cur);
         const bool diag = k0 + kKB - 1 > qw;           // wave-uniform: a key beyond a query
 #pragma unroll
@@ -747,7 +795,7 @@ __global__ void __launch_bounds__(kAttnThreads, 2) attn_bwd_dq_d64_kernel(AttnBw
             bf16x8 kt2[2];                            // K^T operands (asm reads)
 #pragma unroll
             for (int dt = 0; dt < 2; ++dt)
-              kt2[dt] = tr_operand(tk, kk * 32 + 16 * st, 32 * dt, lane);
+              kt2[dt] = trk(kk * 2 + st, dt ? tk1 : tk0, dt ? tk0 : tk1);
             const bf16x8 db = acc_to_bf16(dp, st);
             tr_wait(kt2[0], kt2[1]);
 #pragma unroll
