@@ -396,11 +396,11 @@ __device__ __forceinline__ uint32_t tr_lane_off(int lane, int P) {
   const int chunk = (((2 * (g & 1) + (tp >> 1)) ^ L) & 3) | (((P ^ (L & 1)) & 1) << 2);
   return static_cast<uint32_t>((4 * (g >> 1) + tq) * 128 + chunk * 16 + ((4 * tp) & 7) * 2);
 }
-template <int ROWBASE>
+template <int ROWBASE, int IMG = 0>   // IMG: byte offset of the image from `same` / `flip`'s one
 __device__ __forceinline__ bf16x8 tr_operand_at(const char* same, const char* flip) {
   static_assert(ROWBASE % 16 == 0, "row base");
-  const i16x4 t0 = ds_read_tr16<ROWBASE * 128>(same);
-  const i16x4 t1 = ds_read_tr16<(ROWBASE + 8) * 128>(flip);
+  const i16x4 t0 = ds_read_tr16<IMG + ROWBASE * 128>(same);
+  const i16x4 t1 = ds_read_tr16<IMG + (ROWBASE + 8) * 128>(flip);
   bf16x8 f;
 #pragma unroll
   for (int u = 0; u < 4; ++u) {
@@ -444,7 +444,7 @@ constexpr int kSliceImg = kSlice * 128;      // 8 KiB
 // per slice (the clamped per-row 64-bit address arithmetic only on a slice that crosses T); the
 // forward's variant bit 4, measured 3 % there (A/B: dlbb_attn_set_bwd_incr)
 template <bool INC>
-__global__ void __launch_bounds__(kAttnThreads, 2) attn_bwd_dkdv_d64_kernel(AttnBwdArgs a) {
+__global__ void __launch_bounds__(kAttnThreads, 3) attn_bwd_dkdv_d64_kernel(AttnBwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -563,13 +563,13 @@ __global__ void __launch_bounds__(kAttnThreads, 2) attn_bwd_dkdv_d64_kernel(Attn
           dv4[g4] = ds_read_b128_asm(rv + 64 + rb + 8 * g4 + 4 * hi);
         }
         tr_wait(lv[0], lv[1], lv[2], lv[3], dv4[0], dv4[1], dv4[2], dv4[3]);
-#pragma unroll
-        for (int g4 = 0; g4 < 4; ++g4)
-#pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            s[4 * g4 + u] = lv[g4][u];
-            dp[4 * g4 + u] = dv4[g4][u];
-          }
+        s = __builtin_shufflevector(__builtin_shufflevector(lv[0], lv[1], 0, 1, 2, 3, 4, 5, 6, 7),
+                                    __builtin_shufflevector(lv[2], lv[3], 0, 1, 2, 3, 4, 5, 6, 7),
+                                    0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15);
+        dp = __builtin_shufflevector(
+            __builtin_shufflevector(dv4[0], dv4[1], 0, 1, 2, 3, 4, 5, 6, 7),
+            __builtin_shufflevector(dv4[2], dv4[3], 0, 1, 2, 3, 4, 5, 6, 7),
+            0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15);
 #pragma unroll
         for (int ks = 0; ks < 4; ++ks) {
           s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_operand(iq, rb + r, 2 * ks + hi), kf[ks],

@@ -14,7 +14,11 @@ import pytest
 
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
 
-ALLOWED_SCRATCH: dict = {}
+# Measured exceptions. The dK/dV attention kernel at 3 workgroups per CU spills 4 VGPRs (20 B of
+# scratch per lane). Its 768-workgroup causal-paired grid then fits one round instead of 1.5.
+# At the GPT-2 shape the whole backward runs 142-146 us against 156-158 us without the spill
+# (profiles/r06_kernels/attn_bwd_dkdv_3wg_ab.jsonl).
+ALLOWED_SCRATCH: dict = {"_ZN4dlbb24attn_bwd_dkdv_d64_kernelILb0EEEvNS_11AttnBwdArgsE": 20}
 
 
 @pytest.mark.skipif(shutil.which("hipcc") is None and not os.path.exists("/opt/rocm/bin/hipcc"),
