@@ -86,6 +86,7 @@ _SIGS = {
     "dlbb_gemm_get_concurrent": (c_int, []),
     "dlbb_gemm_wgrad_set_stages": (None, [c_int]),
     "dlbb_attn_set_xcd": (None, [c_int]),
+    "dlbb_attn_set_stamps": (None, [c_void_p, c_void_p, c_void_p]),
     "dlbb_xent_set_variant": (None, [c_int]),
     "dlbb_xent_count_inv": (c_int, [c_void_p, c_int64, c_void_p, c_void_p]),
     "dlbb_xent_loss_mean": (c_int, [c_void_p, c_int64, c_void_p, c_void_p, c_void_p]),
