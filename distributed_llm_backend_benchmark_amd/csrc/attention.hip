@@ -24,7 +24,6 @@
 #include "common.h"
 
 #include <cstdlib>
-#include <mutex>
 #include <type_traits>
 
 namespace dlbb {
@@ -54,103 +53,29 @@ struct AttnArgs {
   float scale_log2;      // log2(e) / sqrt(D)
   int xcd;               // 1: XCD-aware head-contiguous block order (head_block)
   uint64_t* stamps;      // diagnostic, normally null: wg_stamp per workgroup
-  int* tickets;          // WorkQ tickets (8 ints, zero between launches)
 };
 
-// Causal work queue. A job is one (block, head) unit: nblk blocks per head, the heads of all
-// batches. A 1-D persistent grid (at most one round of resident workgroups) pulls jobs from
-// queue x = blockIdx % nq (xcd = 1 and at least 8 heads and workgroups: nq = 8, the blocks that
-// share an XCD's L2 — guide T1 — so a head's K/V (forward, dQ) or Q/dO (dK/dV) tiles stay in one
-// L2; otherwise one queue). Queue x
-// owns the heads [x HB / nq, (x + 1) HB / nq), its jobs ordered heaviest block first across
-// those heads (longest-processing-time first). Workgroup rank r of the queue starts with job r;
-// every later job comes from an atomic ticket, so a workgroup that runs faster takes more jobs.
-// Why: the SIMD's arbiter favours the oldest wave, so of the 3 workgroups a CU holds the first
-// dispatched finished the statically paired grid at 27 us and the last at 40 us, the CU running
-// its tail with 1-2 resident waves per SIMD (tools/attn_timeline.py,
-// profiles/r06_kernels/attn_timeline_*.jsonl).
-// Ticket reset without a memset: every workgroup that started a job fetches exactly once past
-// the end, so a queue's fetches number exactly its job count and the fetch that returns
-// njobs - 1 is the launch's last — that workgroup stores 0 for the next launch (also under
-// HIP-graph replay). Launches sharing one ticket set must not run concurrently (one stream).
-// Job boundary: LDS traffic retired (the slot write, every wave's reads of the ring; no LDS-DMA is
-// in flight after a job's last tile) and a barrier — without __syncthreads' vmcnt(0), which
-// would also drain the job's output stores and the next ticket (tools/isa_check.py flags it).
-__device__ __forceinline__ void job_barrier() {
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-}
-struct WorkQ {
-  int* ctr;     // this queue's ticket
-  int hs, hx;   // first head, head count
-  int njobs;    // hx * nblk
-  int base;     // jobs handed out statically (= active workgroups of the queue)
-  int job;      // this workgroup's current job (>= njobs: none)
-};
-__device__ __forceinline__ WorkQ workq_init(int* tickets, int xcd, int nblk, int HB) {
-  const int L = blockIdx.x, nwg = gridDim.x;
-  // 8 queues only when each gets at least one head and one workgroup
-  const int nq = xcd && HB >= 8 && nwg >= 8 ? 8 : 1;
-  const int x = L % nq;
-  const int nwg_x = nwg / nq + (x < nwg % nq ? 1 : 0);
-  WorkQ q;
-  q.ctr = tickets + x;
-  q.hs = x * HB / nq;
-  q.hx = (x + 1) * HB / nq - q.hs;
-  q.njobs = q.hx * nblk;
-  q.base = nwg_x < q.njobs ? nwg_x : q.njobs;
-  q.job = L / nq;
-  if (xcd & 2) {            // first jobs interleaved: rank r -> block r % P of head r / P
-    const int P = q.hx ? q.base / q.hx : 0;
-    if (q.job < P * q.hx) q.job = (q.job % P) * q.hx + q.job / P;
+// Block -> (block-in-head, h, b) for a (blocks-per-head, H, B) grid. xcd = 1: XCD-aware
+// bijective remap (guide T1; blockIdx % 8 labels the blocks that share an L2) so each XCD's
+// eighth of the grid is a contiguous run of WHOLE heads — a head's K/V (forward, dQ) or Q/dO
+// (dK/dV) tiles are then fetched into one L2 instead of into all eight (the default dispatch
+// sends the consecutive blocks of one head to eight different XCDs). Order inside a head kept.
+__device__ __forceinline__ void head_block(int xcd_on, int& blk, int& h, int& b) {
+  const int nb = gridDim.x, H = gridDim.y;
+  if (!xcd_on) {
+    blk = blockIdx.x;
+    h = blockIdx.y;
+    b = blockIdx.z;
+    return;
   }
-  return q;
-}
-// job -> (block rank jb, 0 = heaviest; h; b)
-__device__ __forceinline__ void workq_job(const WorkQ& q, int H, int& jb, int& h, int& b) {
-  jb = q.job / q.hx;
-  const int head = q.hs + q.job % q.hx;
-  h = head % H;
-  b = head / H;
-}
-// thread 0: ticket for the job after this one (issued in the job's last tile, consumed at its
-// end: a job-start fetch stalled the first tile's vmcnt wait by the atomic's latency)
-__device__ __forceinline__ int workq_fetch(const WorkQ& q) {
-  return threadIdx.x == 0 ? atomicAdd(q.ctr, 1) : 0;
-}
-// end of a job: publish the next one through LDS (slot), reset the ticket after the last fetch
-__device__ __forceinline__ void workq_next(WorkQ& q, int got, int* slot) {
-  if (threadIdx.x == 0) {
-    *slot = q.base + got;
-    if (got == q.njobs - 1) atomicExch(q.ctr, 0);
-  }
-  job_barrier();
-  q.job = __builtin_amdgcn_readfirstlane(*slot);
-}
-// Static causal pairing in the same job interface (the head-dim-64 forward, where it measured
-// faster than the queue at the GPT-2 shape: 46.8 vs 50.3-51.1 us, interleaved two-tree A/B,
-// profiles/r06_kernels/attn_workq_ab.jsonl): a grid of ceil(nblk / 2) workgroups per head,
-// workgroup blk runs block blk (heavy) and then nblk-1-blk (light) of one head; xcd = 1 lays each
-// XCD's eighth of the grid over whole heads (blockIdx % 8 = XCD). No tickets.
-__device__ __forceinline__ WorkQ workq_init_paired(int xcd, int nblk, int HB) {
-  const int nb = (nblk + 1) / 2, nwg = gridDim.x, L = blockIdx.x;
-  int wid = L;
-  if (xcd) {
-    const int x = L % 8, q = nwg / 8, r = nwg % 8;
-    wid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + L / 8;
-  }
-  WorkQ w;
-  w.ctr = nullptr;
-  w.hs = wid / nb;           // the head; hx = 1 so job = block rank
-  w.hx = 1;
-  w.njobs = wid < nb * HB ? nblk : 0;
-  w.job = wid % nb;          // heavy block first
-  w.base = nblk - 1 - w.job; // then the light one
-  return w;
-}
-__device__ __forceinline__ void workq_next_paired(WorkQ& q) {
-  q.job = q.job < q.base ? q.base : q.njobs;
-  job_barrier();
+  const int nwg = nb * H * gridDim.z;
+  const int L = blockIdx.x + nb * (blockIdx.y + H * blockIdx.z);
+  const int x = L % 8, q = nwg / 8, r = nwg % 8;
+  const int wid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + L / 8;
+  blk = wid % nb;
+  const int hh = wid / nb;
+  h = hh % H;
+  b = hh / H;
 }
 
 // lane ^ 32 half exchange of a per-lane value by v_permlane32_swap (a VALU op) instead of a
@@ -164,7 +89,8 @@ __device__ __forceinline__ float xhalf_max(float x) {
 // Diagnostic workgroup timeline (dlbb_attn_set_stamps; null in production): slot k of the
 // launch-order workgroup's 4 words gets the 100 MHz wall clock (k = 0 start, 1 end of the first
 // causal pass, 2 end) and, with k = 0, word 3 = XCC id << 16 | HW_ID's SE / SH / CU fields —
-// the residency and balance of the grid on the chip, without PMC. A vector store from lane 0.
+// the residency and balance of the grid on the chip, without PMC (tools/attn_timeline.py).
+// A vector store from thread 0.
 __device__ __forceinline__ void wg_stamp(uint64_t* st, int k) {
   if (!st) return;
   __syncthreads();
@@ -223,19 +149,19 @@ __global__ void __launch_bounds__(kAttnThreads, 2) attn_fwd_kernel(AttnArgs a) {
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int nqb = (a.T + kQB - 1) / kQB;
-  int* const next_job = reinterpret_cast<int*>(smem + 4 * TILE);   // after the ring
-  // causal work queue (WorkQ): query blocks heaviest first. It replaced a static pairing of
-  // blocks nqb-1-blk and blk per workgroup (equal work, but unequal speed: see WorkQ).
-  constexpr bool PAIRED = D == 64;
-  WorkQ wq = PAIRED ? workq_init_paired(a.xcd, nqb, a.H * a.B)
-                    : workq_init(a.tickets, a.xcd, nqb, a.H * a.B);
+  int blk, h, b;
+  head_block(a.xcd, blk, h, b);
+  // causal pairing: workgroup blk of a head runs query block nqb-1-blk (the heaviest) and then
+  // block blk (the lightest), so every workgroup does about the same 2 (nqb + 1) tiles. The
+  // heavy-first single-block grid left its second round of workgroups half the chip's slots:
+  // 1.7 of 4 waves resident per SIMD on average (PMC SQ_WAVE_CYCLES vs kernel cycles,
+  // profiles/r06_kernels/pmc_attn_summary.jsonl).
+  const int npass = nqb - 1 - blk != blk ? 2 : 1;
   wg_stamp(a.stamps, 0);
-  for (int it = 0; wq.job < wq.njobs; ++it) {
-    if (it == 1) wg_stamp(a.stamps, 1);
-    int got = 0;                                  // next ticket, fetched in the last tile
-    int jb, h, b;
-    workq_job(wq, a.H, jb, h, b);
-    const int qb = nqb - 1 - jb;
+  for (int pass = 0; pass < npass; ++pass) {
+    if (pass) wg_stamp(a.stamps, 1);
+    if (pass) __syncthreads();                    // every wave done with the LDS ring
+    const int qb = pass == 0 ? nqb - 1 - blk : blk;
     const int q0 = qb * kQB;
     const int qw = q0 + wave * 32;                  // this wave's first query
     const int r = lane & 31, hi = lane >> 5;
@@ -307,9 +233,6 @@ __global__ void __launch_bounds__(kAttnThreads, 2) attn_fwd_kernel(AttnArgs a) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
       if (kt + 1 < nt) stage((kt + 1) * KB, tileK(cur ^ 1), tileV(cur ^ 1));
-      else if (!PAIRED)
-        got = workq_fetch(wq);   // the ticket's latency (device-scope atomic) hides under the
-                                 // last tile instead of stalling a job's first vmcnt wait
       const int k0 = kt * KB;
       if (k0 <= q_hi) {                               // wave-uniform: tile has keys <= a query
         const char* tk = tileK(cur);
@@ -423,10 +346,6 @@ __global__ void __launch_bounds__(kAttnThreads, 2) attn_fwd_kernel(AttnArgs a) {
         a.lse[(static_cast<int64_t>(b) * a.H + h) * a.T + qme] =
             (m + __builtin_amdgcn_logf(lt)) * 0.69314718055994531f;
     }
-    if constexpr (PAIRED)
-      workq_next_paired(wq);
-    else
-      workq_next(wq, got, next_job);
   }
   wg_stamp(a.stamps, 2);
 }
@@ -469,7 +388,6 @@ struct AttnBwdArgs {
   float scale;             // 1 / sqrt(D)
   int xcd;                 // see head_block
   uint64_t* stamps;        // diagnostic, normally null: wg_stamp per workgroup
-  int* tickets;            // WorkQ tickets (8 ints, zero between launches)
 };
 
 // transposed operand read of a [rows][64] bf16 image (bswz): A operand of a 32x32x16 MFMA whose
@@ -556,17 +474,16 @@ __global__ void __launch_bounds__(kAttnThreads, 3) attn_bwd_dkdv_d64_kernel(Attn
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int r = lane & 31, hi = lane >> 5;
-  // key block 0 (the most query slices) is the heaviest
+  int blk, h, b;
+  head_block(a.xcd, blk, h, b);
+  // causal pairing: key blocks blk (more query slices) and nkb-1-blk, equal work per workgroup
   const int nkb = (a.T + kBwdKeys - 1) / kBwdKeys;
-  WorkQ wq = workq_init_paired(a.xcd, nkb, a.H * a.B);   // static pairing: the queue's job
-  // loop state spilled into the slice loop here (a vmcnt(0) drain per slice) at no gain at the
-  // GPT-2 shape (tools/attn_timeline.py: dK/dV span 79-80 us queued vs 77-78 paired)
+  const int npass = nkb - 1 - blk != blk ? 2 : 1;
   wg_stamp(a.stamps, 0);
-  for (int it = 0; wq.job < wq.njobs; ++it) {
-    if (it == 1) wg_stamp(a.stamps, 1);
-    int jb, h, b;
-    workq_job(wq, a.H, jb, h, b);
-    const int kb0 = jb * kBwdKeys;
+  for (int pass = 0; pass < npass; ++pass) {
+    if (pass) wg_stamp(a.stamps, 1);
+    if (pass) __syncthreads();                    // every wave done with the LDS ring
+    const int kb0 = (pass == 0 ? blk : nkb - 1 - blk) * kBwdKeys;   // heaviest (block 0) first
     const int kw = kb0 + wave * 32;
     const int mykey = kw + r;
     const uint16_t* base_bt = a.qkv + static_cast<int64_t>(b) * a.T * a.ld;
@@ -741,7 +658,6 @@ __global__ void __launch_bounds__(kAttnThreads, 3) attn_bwd_dkdv_d64_kernel(Attn
           *reinterpret_cast<u16x4*>(dvp + dt * 32 + 8 * gg + 4 * hi) = wv;
         }
     }
-    workq_next_paired(wq);
   }
   wg_stamp(a.stamps, 2);
 }
@@ -768,16 +684,15 @@ __global__ void __launch_bounds__(kAttnThreads, 2) attn_bwd_dq_d64_kernel(AttnBw
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int nqb = (a.T + kQB - 1) / kQB;
-  // causal work queue (WorkQ) as the forward: query blocks heaviest first
-  int* const next_job = reinterpret_cast<int*>(smem + 4 * kTileKV);
-  WorkQ wq = workq_init(a.tickets, a.xcd, nqb, a.H * a.B);
+  int blk, h, b;
+  head_block(a.xcd, blk, h, b);
+  // causal pairing as the forward: query blocks nqb-1-blk then blk, equal work per workgroup
+  const int npass = nqb - 1 - blk != blk ? 2 : 1;
   wg_stamp(a.stamps, 0);
-  for (int it = 0; wq.job < wq.njobs; ++it) {
-    if (it == 1) wg_stamp(a.stamps, 1);
-    int got = 0;                                  // next ticket, fetched in the last tile
-    int jb, h, b;
-    workq_job(wq, a.H, jb, h, b);
-    const int qb = nqb - 1 - jb;
+  for (int pass = 0; pass < npass; ++pass) {
+    if (pass) wg_stamp(a.stamps, 1);
+    if (pass) __syncthreads();                    // every wave done with the LDS ring
+    const int qb = pass == 0 ? nqb - 1 - blk : blk;
     const int q0 = qb * kQB;
     const int qw = q0 + wave * 32;
     const int r = lane & 31, hi = lane >> 5;
@@ -863,7 +778,6 @@ __global__ void __launch_bounds__(kAttnThreads, 2) attn_bwd_dq_d64_kernel(AttnBw
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();                   // publishes tile kt, frees buffer cur^1
       if (kt + 1 < nt) stage((kt + 1) * kKB, tileK(cur ^ 1), tileV(cur ^ 1));
-      else got = workq_fetch(wq);                     // as the forward: under the last tile
       const int k0 = kt * kKB;
       if (k0 <= q_hi) {
         const char* tk = tileK(cur);
@@ -933,7 +847,6 @@ __global__ void __launch_bounds__(kAttnThreads, 2) attn_bwd_dq_d64_kernel(AttnBw
           *reinterpret_cast<u16x4*>(dqp + dt * 32 + 8 * gg + 4 * hi) = w;
         }
     }
-    workq_next(wq, got, next_job);
   }
   wg_stamp(a.stamps, 2);
 }
@@ -942,59 +855,8 @@ __global__ void __launch_bounds__(kAttnThreads, 2) attn_bwd_dq_d64_kernel(AttnBw
 
 using namespace dlbb;
 
-static int g_attn_xcd = 1;   // A/B switch: 8 per-XCD work queues (1) or one (0), see WorkQ
-DLBB_API void dlbb_attn_set_xcd(int on) { g_attn_xcd = on; }
-
-// Per-device WorkQ tickets (set k = kernel: 0 forward D64, 1 forward D128, 2 dQ, 3 dK/dV; 8 ints
-// each, zeroed once here and left zero by every launch) and the CU count for the grid size.
-// Allocated at the first launch on a device (outside graph capture: the runners warm up first).
-namespace {
-struct AttnDev {
-  int* tickets = nullptr;
-  int cus = 0;
-  int occ[4] = {0, 0, 0, 0};   // resident workgroups per CU, per kernel
-};
-AttnDev g_attn_dev[64];
-std::mutex g_attn_mu;
-
-hipError_t attn_dev(AttnDev** out) {
-  int d = 0;
-  hipError_t e = hipGetDevice(&d);
-  if (e != hipSuccess) return e;
-  if (d < 0 || d >= 64) return hipErrorInvalidDevice;
-  AttnDev& v = g_attn_dev[d];
-  if (!v.tickets) {
-    std::lock_guard<std::mutex> lk(g_attn_mu);
-    if (!v.tickets) {
-      int* p = nullptr;
-      if ((e = hipMalloc(&p, 32 * sizeof(int))) != hipSuccess) return e;
-      if ((e = hipMemset(p, 0, 32 * sizeof(int))) != hipSuccess) return e;
-      if ((e = hipDeviceSynchronize()) != hipSuccess) return e;
-      if ((e = hipDeviceGetAttribute(&v.cus, hipDeviceAttributeMultiprocessorCount, d)) !=
-          hipSuccess)
-        return e;
-      v.tickets = p;
-    }
-  }
-  *out = &v;
-  return hipSuccess;
-}
-
-// 1-D grid: every job's workgroup resident at once if possible, never more than one round
-template <typename K>
-int attn_grid(AttnDev* v, int k, K kernel, size_t lds, int njobs) {
-  if (!v->occ[k]) {
-    int n = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, kernel, kAttnThreads, lds) !=
-            hipSuccess || n < 1)
-      n = 1;
-    v->occ[k] = n;
-  }
-  const int64_t cap = static_cast<int64_t>(v->occ[k]) * v->cus;
-  return static_cast<int>(njobs < cap ? njobs : cap);
-}
-}  // namespace
-
+static int g_attn_xcd = 1;   // A/B switch for the XCD-aware block order (dlbb_attn_set_xcd)
+DLBB_API void dlbb_attn_set_xcd(int on) { g_attn_xcd = on ? 1 : 0; }
 // diagnostic workgroup timeline buffers (wg_stamp; 4 uint64 per workgroup), null = off
 static uint64_t* g_stamps_fwd = nullptr;
 static uint64_t* g_stamps_dq = nullptr;
@@ -1015,23 +877,15 @@ DLBB_API int dlbb_attn_fwd(const void* qkv, int64_t ld, void* out, int64_t ldo, 
       (reinterpret_cast<uintptr_t>(out) & 7))
     return hipErrorInvalidValue;
   if (ld < 3 * H * D || ldo < H * D) return hipErrorInvalidValue;
-  AttnDev* dev = nullptr;
-  const hipError_t de = attn_dev(&dev);
-  if (de != hipSuccess) return de;
-  const int k = D == 64 ? 0 : 1;
   AttnArgs a{static_cast<const uint16_t*>(qkv), static_cast<uint16_t*>(out), lse, ld, ldo,
-             B, T, H, scale * 1.4426950408889634f, g_attn_xcd, g_stamps_fwd,
-             dev->tickets + 8 * k};
-  const int njobs = (T + kQB - 1) / kQB * H * B;
-  if (D == 64) {   // static causal pairing (workq_init_paired)
-    const size_t lds = 4 * FwdGeo<64>::TILE + 16;
-    const int g = ((T + kQB - 1) / kQB + 1) / 2 * H * B;
-    hipLaunchKernelGGL(attn_fwd_kernel<64>, dim3(g), dim3(kAttnThreads), lds, stream, a);
-  } else {
-    const size_t lds = 4 * FwdGeo<128>::TILE + 16;
-    const int g = attn_grid(dev, k, attn_fwd_kernel<128>, lds, njobs);
-    hipLaunchKernelGGL(attn_fwd_kernel<128>, dim3(g), dim3(kAttnThreads), lds, stream, a);
-  }
+             B, T, H, scale * 1.4426950408889634f, g_attn_xcd, g_stamps_fwd};
+  const dim3 grid(((T + kQB - 1) / kQB + 1) / 2, H, B);   // query blocks paired (causal)
+  if (D == 64)
+    hipLaunchKernelGGL(attn_fwd_kernel<64>, grid, dim3(kAttnThreads), 4 * FwdGeo<64>::TILE,
+                       stream, a);
+  else
+    hipLaunchKernelGGL(attn_fwd_kernel<128>, grid, dim3(kAttnThreads), 4 * FwdGeo<128>::TILE,
+                       stream, a);
   return hipGetLastError();
 }
 
@@ -1050,22 +904,18 @@ DLBB_API int dlbb_attn_bwd(const void* qkv, int64_t ld, const void* out, const v
   auto mis16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) != 0; };
   if (mis16(qkv) || mis16(out) || mis16(dout) || mis16(dqkv)) return hipErrorInvalidValue;
   if (!lse || !delta || !out || !dout) return hipErrorInvalidValue;
-  AttnDev* dev = nullptr;
-  const hipError_t de = attn_dev(&dev);
-  if (de != hipSuccess) return de;
   const int64_t rows = static_cast<int64_t>(B) * T * H;
   AttnBwdArgs a{static_cast<const uint16_t*>(qkv), static_cast<const uint16_t*>(dout), lse, delta,
                 delta + rows, static_cast<const uint16_t*>(out), 1,
                 static_cast<uint16_t*>(dqkv), ld, ldo, B, T, H,
-                scale * 1.4426950408889634f, scale, g_attn_xcd, g_stamps_dq, dev->tickets + 16};
-  // dQ: causal work queue (WorkQ), heaviest block first; dK/dV: static causal pairing
-  const size_t lq = 4 * kTileKV + 16, lk = 4 * kSliceImg + 1024;   // + WorkQ slot (dQ)
-  const int gq = attn_grid(dev, 2, attn_bwd_dq_d64_kernel<true>, lq,
-                           (T + kQB - 1) / kQB * H * B);
-  const int gk = ((T + kBwdKeys - 1) / kBwdKeys + 1) / 2 * H * B;   // static causal pairing
-  hipLaunchKernelGGL(attn_bwd_dq_d64_kernel<true>, dim3(gq), dim3(kAttnThreads), lq, stream, a);
-  a.stamps = g_stamps_dkdv;
-  hipLaunchKernelGGL(attn_bwd_dkdv_d64_kernel<false>, dim3(gk), dim3(kAttnThreads), lk, stream,
+                scale * 1.4426950408889634f, scale, g_attn_xcd, g_stamps_dq};
+  // both kernels pair a heavy and a light causal block per workgroup (see the forward)
+  const dim3 gq(((T + kQB - 1) / kQB + 1) / 2, H, B),
+      gk(((T + kBwdKeys - 1) / kBwdKeys + 1) / 2, H, B);
+  hipLaunchKernelGGL(attn_bwd_dq_d64_kernel<true>, gq, dim3(kAttnThreads), 4 * kTileKV, stream,
                      a);
+  a.stamps = g_stamps_dkdv;
+  hipLaunchKernelGGL(attn_bwd_dkdv_d64_kernel<false>, gk, dim3(kAttnThreads),
+                     4 * kSliceImg + 1024, stream, a);
   return hipGetLastError();
 }
