@@ -131,8 +131,9 @@ template <int D>
 __device__ __forceinline__ int vswz_d(int r) { return D == 64 ? vswz(r) : ((r & 3) << 2); }
 
 // Causal forward, head dim D (64 or 128). Round-5 schedule (variant 6 of its A/B: row-max
-// exchange by v_permlane32_swap, incremental DMA sources; 128 VGPRs at D = 64 = 4 waves per
-// SIMD). Round 6 measured a software-pipelined body (QK^T of tile j+1 and PV of tile j-1 beside
+// exchange by v_permlane32_swap, incremental DMA sources; 128 VGPRs at D = 64 then, 139 since
+// the round-6 pairing and deferred max = 3 waves per SIMD: the paired GPT-2 grid of 768
+// workgroups is exactly one round of 3 per CU). Round 6 measured a software-pipelined body (QK^T of tile j+1 and PV of tile j-1 beside
 // the softmax of tile j in one straight block): 75.1 vs 56.5 us at the GPT-2 shape — its 212
 // VGPRs left 2 waves per SIMD, and the hardware's interleave of 4 waves beat the compiler's
 // in-wave interleave (profiles/r06_kernels/attn_fwd_pipelined_ab.jsonl); removed. Also measured
