@@ -123,3 +123,38 @@ def test_attn_bwd_matches_fp32_reference(B, T, H):
         err = float((got - want).abs().max())
         scale = float(want.abs().max())
         assert err <= 0.03 * scale + 0.02, (name, err, scale)
+
+
+def test_workgroup_timeline_stamps():
+    """The diagnostic timeline (wg_stamp, tools/attn_timeline.py): with stamp buffers set, every
+    workgroup of the three kernels records start <= mid <= end and a CU id, and the outputs are
+    bit-identical to an unstamped run; with the buffers cleared nothing is written."""
+    from distributed_llm_backend_benchmark_amd.ops import _lib
+    from distributed_llm_backend_benchmark_amd.ops.attention import attn_bwd, attn_fwd
+
+    B, T, H = 2, 1024, 4
+    g = torch.Generator(device="cuda").manual_seed(3)
+    qkv = torch.randn(B, T, 3 * H * 64, device="cuda", generator=g).to(torch.bfloat16)
+    gout = torch.randn(B, T, H * 64, device="cuda", generator=g).to(torch.bfloat16)
+    o0, l0 = attn_fwd(qkv, H)
+    d0 = attn_bwd(qkv, o0, l0, gout, H)
+    nq = ((T + 127) // 128 + 1) // 2 * H * B
+    st = [torch.zeros(nq, 4, dtype=torch.int64, device="cuda") for _ in range(3)]
+    L = _lib.lib()
+    L.dlbb_attn_set_stamps(st[0].data_ptr(), st[1].data_ptr(), st[2].data_ptr())
+    try:
+        o1, l1 = attn_fwd(qkv, H)
+        d1 = attn_bwd(qkv, o1, l1, gout, H)
+        torch.cuda.synchronize()
+    finally:
+        L.dlbb_attn_set_stamps(None, None, None)
+    assert torch.equal(o0, o1) and torch.equal(l0, l1) and torch.equal(d0, d1)
+    for t in st:
+        a = t.cpu()
+        assert bool((a[:, 0] > 0).all()) and bool((a[:, 2] >= a[:, 0]).all())
+        mid = a[:, 1]
+        assert bool(((mid == 0) | ((mid >= a[:, 0]) & (mid <= a[:, 2]))).all())
+    before = [t.clone() for t in st]
+    attn_fwd(qkv, H)
+    torch.cuda.synchronize()
+    assert all(torch.equal(a, b) for a, b in zip(st, before))
