@@ -2415,6 +2415,49 @@ DLBB_API int dlbb_gemm_bf16_nn(const void* A, int64_t lda, const void* B, int64_
   return hipGetLastError();
 }
 
+// Split-K NT GEMM, plain product to bf16 (C = A · B^T, ldc == N): the ping-pong on
+// (tiles, split) with fp32 partials [split][M][N] in ws, then one reduce + cast pass
+// (dlbb_split_reduce_launch). For grids below one round of the CUs — the TP-7B shard
+// projections (4096 x 1536 x 4096 at P = 8: 128 tiles of 256 x 192 -> 256 workgroups at
+// split 2) — where a whole-K tile per workgroup leaves half the chip idle and the in-launch
+// Stream-K combine measured slower (profiles/r06_kernels/tp_gemm_table_streamk.jsonl).
+// tile192: 256 x 192 tiles (N % 192 == 0), else 256^2. ws: >= split * M * N fp32, 16-B aligned.
+DLBB_API int dlbb_gemm_bf16_nt_split(const void* A, int64_t lda, const void* B, int64_t ldb,
+                                     void* C, int64_t ldc, int64_t M, int64_t N, int64_t K,
+                                     int split, int tile192, float* ws, int64_t ws_bytes,
+                                     hipStream_t stream) {
+  if (M <= 0 || N <= 0) return hipSuccess;
+  if (K <= 0 || K % BK != 0 || split < 2 || ldc != N) return hipErrorInvalidValue;
+  if (lda % 8 || ldb % 8 || M % 8 || M < 8 || N % 64) return hipErrorInvalidValue;
+  if (tile192 && N % 192) return hipErrorInvalidValue;
+  if ((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(B) |
+       reinterpret_cast<uintptr_t>(ws)) & 15)
+    return hipErrorInvalidValue;
+  const int bn = tile192 ? 192 : BN2;
+  if (lda * 2 * 256 + K * 2 >= (1LL << 31) || ldb * 2 * bn + K * 2 >= (1LL << 31))
+    return hipErrorInvalidValue;
+  const int nkt = static_cast<int>(K / BK);
+  if (split > nkt) return hipErrorInvalidValue;
+  GemmArgs a{static_cast<const uint16_t*>(A), static_cast<const uint16_t*>(B), ws, nullptr,
+             nullptr, nullptr, M, N, K, lda, ldb, N, 0, 0, 1, N % 8 == 0 ? 1 : 0, 0};
+  a.kt_split = (nkt + split - 1) / split;
+  split = (nkt + a.kt_split - 1) / a.kt_split;   // every slice starts inside the reduction
+  if (!ws || ws_bytes < static_cast<int64_t>(split) * M * N * 4) return hipErrorInvalidValue;
+  const int64_t tiles = ((M + BM2 - 1) / BM2) * ((N + bn - 1) / bn);
+  const dim3 g(static_cast<unsigned>(tiles), static_cast<unsigned>(split)), b(kThreads2);
+  const bool bal = use_bal(a.kt_split, false);
+  if (tile192) {
+    if (bal) hipLaunchKernelGGL(gemm_bf16_nt_192_pingpong3_bal, g, b, kPP192Lds, stream, a);
+    else hipLaunchKernelGGL(gemm_bf16_nt_192_pingpong3, g, b, kPP192Lds, stream, a);
+  } else {
+    if (bal) DLBB_PP_LAUNCH(gemm_bf16_nt_256_pingpong3_bal, STAMP_GEMM_NT, g, a);
+    else DLBB_PP_LAUNCH(gemm_bf16_nt_256_pingpong3, STAMP_GEMM_NT, g, a);
+  }
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  return dlbb_split_reduce_launch(ws, C, 0, M * N, split, stream);
+}
+
 // weight-gradient GEMM on the 256^2 ping-pong: C[M, N] = epilogue(A[K, M]^T · B[K, N]) with
 // A = dY [tokens][lda] and B = X [tokens][ldb], both read as transposed LDS images (no transpose
 // pass). epi: 0 or EPI_RESIDUAL (accumulate: residual = the bf16 output itself). One workgroup

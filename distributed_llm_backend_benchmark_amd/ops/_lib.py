@@ -65,6 +65,9 @@ _SIGS = {
                                     c_int64, c_int64, c_int64, c_void_p, c_void_p, c_int64,
                                     c_void_p, c_int, c_int, c_int, c_void_p]),
     "dlbb_gemm_streamk_plan": (c_int, [c_int64, c_int64, c_int64, c_int, c_void_p]),
+    "dlbb_gemm_bf16_nt_split": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64,
+                                        c_int64, c_int64, c_int64, c_int, c_int, c_void_p,
+                                        c_int64, c_void_p]),
     "dlbb_gemm_bf16_nt_streamk": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_void_p,
                                           c_int64, c_int64, c_int64, c_int64, c_void_p,
                                           c_void_p, c_int64, c_void_p, c_int, c_int, c_int,

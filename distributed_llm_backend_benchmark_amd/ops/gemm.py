@@ -320,6 +320,52 @@ def _mfma_streamk_linear(x2, w, bias, act, r2, out, preact):
     return out
 
 
+def split_plan(M: int, N: int, K: int, ncu: int):
+    """(split, tile192) of the split-K NT GEMM (``dlbb_gemm_bf16_nt_split``) or None: grids
+    below one round of the CUs, the smallest split (2-4) that fills a round with >= 8 K-tiles
+    per slice (else the deepest such split). 256 x 192 tiles when N % 192 == 0."""
+    if M % 8 or M < 8 or N % 64 or K % 64:
+        return None
+    t192 = N % 192 == 0
+    tiles = -(-M // 256) * (N // 192 if t192 else -(-N // 256))
+    if tiles >= ncu:
+        return None
+    nkt = K // 64
+    for split in (2, 3, 4):
+        if tiles * split >= ncu and nkt // split >= 8:
+            return split, int(t192)
+    split = min(4, nkt // 8)             # no split fills a round: the deepest allowed
+    return (split, int(t192)) if split >= 2 else None
+
+
+_SPLIT_WS = {}   # (device index, stream handle) -> fp32 partial workspace (stream-private)
+
+
+def _mfma_split_linear(x2, w, bias, act, r2, out, preact):
+    """Split-K NT ping-pong + one reduce / cast pass (``csrc/gemm.hip``
+    ``dlbb_gemm_bf16_nt_split``): plain bf16 products on grids below one round of the CUs (the
+    TP-7B shard projections). The fp32 partial workspace is private to the current stream."""
+    M, K = x2.shape
+    N = w.shape[0]
+    plan = split_plan(M, N, K, _num_cus(x2.device))
+    if plan is None or bias is not None or act is not None or r2 is not None or \
+            preact is not None or out.dtype != torch.bfloat16:
+        raise RuntimeError("split-K linear outside its contract")
+    split, t192 = plan
+    idx = x2.device.index if x2.device.index is not None else torch.cuda.current_device()
+    key = (idx, _lib.stream(x2.device))
+    ws = _SPLIT_WS.get(key)
+    need = split * M * N
+    if ws is None or ws.numel() < need:
+        ws = torch.empty(need, dtype=torch.float32, device=x2.device)
+        _SPLIT_WS[key] = ws
+    check(_lib.lib().dlbb_gemm_bf16_nt_split(
+        x2.data_ptr(), x2.stride(0), w.data_ptr(), w.stride(0), out.data_ptr(), N, M, N, K,
+        split, t192, ws.data_ptr(), ws.numel() * 4, _lib.stream(x2.device)),
+        "gemm_bf16_nt_split")
+    return out
+
+
 def streamk_ok(x2: torch.Tensor, w: torch.Tensor) -> bool:
     """Host contract of the Stream-K candidate (checked again in C) and a valid plan."""
     M, K = x2.shape
@@ -368,7 +414,8 @@ def _blas_linear(x2, w, bias, act, r2, out, preact):
 CHOICES = {}          # (M, N, K, epi-signature) -> "mfma" | "mfma192" | "mfma_sk" | ... | "blas"
 CALLS = {}            # ("linear" | "wgrad", key) -> calls since import (kernel-mix accounting)
 _IMPLS = {"mfma": _mfma_linear, "mfma192": _mfma192_linear, "mfma192p": _mfma192p_linear,
-          "mfma_sk": _mfma_streamk_linear, "blas": _blas_linear}
+          "mfma_sk": _mfma_streamk_linear, "mfma_split": _mfma_split_linear,
+          "blas": _blas_linear}
 
 
 # > 0 while GEMMs share the chip with communication kernels on another stream (the overlapped
@@ -420,6 +467,9 @@ def _autotune(key, args) -> str:
     # every CU is free, like the persistent forms)
     if key[-1] == "concurrent" or not streamk_ok(args[0], args[1]):
         del impls["mfma_sk"]
+    # split-K (plain bf16 products below one round of the CUs; off beside comm kernels)
+    if not plain or split_plan(key[0], key[1], key[2], _num_cus(args[0].device)) is None:
+        del impls["mfma_split"]
     times = _time_interleaved({n: (lambda f=f: f(*args)) for n, f in impls.items()})
     best, times = _choose(times, "linear", key)
     CHOICES[key] = best

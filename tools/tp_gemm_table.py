@@ -8,7 +8,8 @@ interleaved rounds, uniform random operands (CDNA guide §5.4 rules 24/25). One 
 (``DLBB_GEMM=mfma``), ``t128`` / ``t256`` force the tile, ``s<N>`` = set_stagger(N), ``v192`` =
 the 256 x 192 tile variant (N % 192 == 0 shapes only), ``v192p`` / ``v192p18`` = its persistent
 spread-store form (variant 2), ``sk`` = Stream-K on 256²
-tiles (grids below one round of the CUs only). ``--gpt2`` adds the GPT-2 forward GEMMs.
+tiles (grids below one round of the CUs only), ``split`` = split-K ping-pong + reduce pass (same
+grids). ``--gpt2`` adds the GPT-2 forward GEMMs.
 """
 import argparse
 import json
@@ -90,7 +91,8 @@ def main():
         out = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
         ok = {"v192": gemm.mfma192_ok(M, N),
               "v192p": gemm.mfma192p_ok(M, N, K, True),
-              "sk": gemm.streamk_ok(x, w)}
+              "sk": gemm.streamk_ok(x, w),
+              "split": gemm.split_plan(M, N, K, gemm._num_cus(x.device)) is not None}
         ms = [m for m in modes if ok.get(m, True)]
 
         def run(m):
@@ -100,6 +102,8 @@ def main():
                 return gemm._mfma192p_linear(x, w, None, None, None, out, None)
             if m == "sk":                 # Stream-K ping-pong, in-launch combine
                 return gemm._mfma_streamk_linear(x, w, None, None, None, out, None)
+            if m == "split":              # split-K ping-pong + reduce / cast pass
+                return gemm._mfma_split_linear(x, w, None, None, None, out, None)
             return ops.linear(x, w)
         for m in ms:
             set_mode(m)
