@@ -344,13 +344,14 @@ _SPLIT_WS = {}   # (device index, stream handle) -> fp32 partial workspace (stre
 def _mfma_split_linear(x2, w, bias, act, r2, out, preact):
     """Split-K NT ping-pong + one reduce / cast pass (``csrc/gemm.hip``
     ``dlbb_gemm_bf16_nt_split``): plain bf16 products on grids below one round of the CUs (the
-    TP-7B shard projections). The fp32 partial workspace is private to the current stream."""
+    TP-7B shard projections). The fp32 partial workspace is private to the current stream.
+    Outside its contract: the default ping-pong."""
     M, K = x2.shape
     N = w.shape[0]
     plan = split_plan(M, N, K, _num_cus(x2.device))
     if plan is None or bias is not None or act is not None or r2 is not None or \
-            preact is not None or out.dtype != torch.bfloat16:
-        raise RuntimeError("split-K linear outside its contract")
+            preact is not None or out.dtype != torch.bfloat16:   # outside: the default ping-pong
+        return _mfma_linear(x2, w, bias, act, r2, out, preact)
     split, t192 = plan
     idx = x2.device.index if x2.device.index is not None else torch.cuda.current_device()
     key = (idx, _lib.stream(x2.device))
