@@ -1058,8 +1058,8 @@ def test_gemm_nt_streamk_repeatable():
 
 
 def test_gemm_autotune_offers_tile_variants(monkeypatch):
-    """The linear autotuner times the 256 x 192 candidate where its contract holds, and records
-    whichever it picks."""
+    """The linear autotuner times the 256 x 192, Stream-K and split-K candidates where their
+    contracts hold, and records whichever it picks."""
     from distributed_llm_backend_benchmark_amd.ops import gemm, linear
 
     monkeypatch.setenv("DLBB_GEMM", "auto")
@@ -1068,7 +1068,7 @@ def test_gemm_autotune_offers_tile_variants(monkeypatch):
     y = linear(x, w)
     torch.testing.assert_close(y.float(), x.float() @ w.float().t(), rtol=2e-2, atol=1.5)
     kind, key, times, best = gemm.TUNE_LOG[-1]
-    assert set(times) == {"mfma", "mfma192", "mfma192p", "mfma_sk", "blas"}, times
+    assert set(times) == {"mfma", "mfma192", "mfma192p", "mfma_sk", "mfma_split", "blas"}, times
     assert gemm.CHOICES[key] == best
 
 
