@@ -51,12 +51,25 @@ struct Args {
   int tile_major;      // workgroup order: 0 = split-major, 1 = a tile's splits adjacent
 };
 
+// SB16 (bf16 dW outputs): the dW partial slabs are bf16, slab s = the first half of the bytes of
+// fp32 slab s of ws — half the split-K round trip's traffic; the db partials stay fp32. fp32
+// outputs keep fp32 slabs (their contract is fp32 accuracy).
+template <bool SB16>
+__device__ __forceinline__ f32x4 slab_ld4(const float* slab, int64_t off) {
+  if constexpr (SB16) {
+    const u16x4 v = *reinterpret_cast<const u16x4*>(reinterpret_cast<const uint16_t*>(slab) + off);
+    return f32x4{bf16_to_f32(v[0]), bf16_to_f32(v[1]), bf16_to_f32(v[2]), bf16_to_f32(v[3])};
+  } else {
+    return *reinterpret_cast<const f32x4*>(slab + off);
+  }
+}
+
 // The last-arriving workgroup of a tile sums the `nsplit` fp32 slabs of that tile (+ the fused
 // bias partials of column block 0) and writes the final bf16 / fp32 dW — replaces the separate
 // split_reduce_kernel pass (profiles/r04_final/gpt2_kernel_stats_steady.csv:5: 40 us x 50 calls
 // per GPT-2 step). Slab reads are 16-B, coalesced along K, 8 independent loads per thread per
 // slab; NT threads cover the BNxTBK tile in TBK / 8 float4 per thread, 8 at a time.
-template <int NT, int BN, int TBK>
+template <int NT, int BN, int TBK, bool SB16>
 __device__ __forceinline__ void wgrad_tile_reduce(const Args& a, int n0, int k0, bool bias) {
   constexpr int C4 = TBK / 4;                      // float4 per tile row
   constexpr int PER = BN * C4 / NT;                // float4 per thread
@@ -70,13 +83,13 @@ __device__ __forceinline__ void wgrad_tile_reduce(const Args& a, int n0, int k0,
     for (int u = 0; u < 8; ++u) {
       const int f = (ch * 8 + u) * NT + static_cast<int>(threadIdx.x);
       off[u] = static_cast<int64_t>(n0 + f / C4) * a.K + k0 + (f % C4) * 4;
-      acc[u] = *reinterpret_cast<const f32x4*>(a.ws + off[u]);
+      acc[u] = slab_ld4<SB16>(a.ws, off[u]);
     }
 #pragma unroll 2
     for (int s = 1; s < a.nsplit; ++s) {
       f32x4 t[8];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) t[u] = *reinterpret_cast<const f32x4*>(a.ws + s * slab + off[u]);
+      for (int u = 0; u < 8; ++u) t[u] = slab_ld4<SB16>(a.ws + s * slab, off[u]);
 #pragma unroll
       for (int u = 0; u < 8; ++u) acc[u] += t[u];
     }
@@ -179,7 +192,7 @@ __device__ __forceinline__ void stage_all(__amdgpu_buffer_rsrc_t ra, __amdgpu_bu
 // WJ: 16-column B fragments per wave — 4: 64 x 64 per wave (128 output columns per tile), 8:
 // 64 x 128 per wave (256 columns per tile): 25 % fewer LDS fragment bytes per MFMA and 2/3 of the
 // DMA per output of the 128 x 128 tile; the 128-column kernels are LDS-bound (GPT-2 dW shapes).
-template <bool BIAS, int NB, int WM, int WJ = 4>
+template <bool BIAS, int NB, int WM, int WJ = 4, bool SB16 = false>
 __global__ void __launch_bounds__(128 * WM, WJ == 8 ? 2 : (WM == 2 ? 3 : 2))
     wgrad_kernel(Args a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -315,7 +328,11 @@ __global__ void __launch_bounds__(128 * WM, WJ == 8 ? 2 : (WM == 2 ? 3 : 2))
       for (int r = 0; r < 4; ++r) {
         const int n = n0 + wm * 64 + i * 16 + fq * 4 + r;
         const int k = k0 + wn * 16 * WJ + j * 16 + fr;
-        w[static_cast<int64_t>(n) * a.K + k] = acc[i][j][r];
+        if constexpr (SB16)
+          reinterpret_cast<uint16_t*>(w)[static_cast<int64_t>(n) * a.K + k] =
+              f32_to_bf16(acc[i][j][r]);
+        else
+          w[static_cast<int64_t>(n) * a.K + k] = acc[i][j][r];
       }
   if (do_bias && fr == 0) {   // every D column holds the same sum; lanes 0/16/32/48 write
     float* wb = a.ws + static_cast<int64_t>(a.nsplit) * a.N * a.K +
@@ -349,7 +366,7 @@ __global__ void __launch_bounds__(128 * WM, WJ == 8 ? 2 : (WM == 2 ? 3 : 2))
   }
   __syncthreads();
   if (!last[0]) return;
-  wgrad_tile_reduce<128 * WM, 64 * WM, TBK>(a, n0, k0, BIAS && tk == 0);
+  wgrad_tile_reduce<128 * WM, 64 * WM, TBK, SB16>(a, n0, k0, BIAS && tk == 0);
 }
 
 // out[i] = sum_s ws[s][i] (+ out[i] if accumulate), bf16 or fp32 output; 8 elements / thread.
@@ -391,7 +408,30 @@ __device__ __forceinline__ f32x4 sum_slabs(const float* __restrict__ src, int64_
   }
 }
 
-template <int DTO, int S, bool NT>
+// sum_slabs over bf16 slabs (SB16 layout above)
+template <int S, bool NT>
+__device__ __forceinline__ f32x4 sum_slabs_b16(const float* __restrict__ src, int64_t ld,
+                                               int64_t vi, int split) {
+  auto ld16 = [&](int s) {
+    const u16x4* p = reinterpret_cast<const u16x4*>(src + static_cast<int64_t>(s) * ld) + vi;
+    const u16x4 v = NT ? __builtin_nontemporal_load(p) : *p;
+    return f32x4{bf16_to_f32(v[0]), bf16_to_f32(v[1]), bf16_to_f32(v[2]), bf16_to_f32(v[3])};
+  };
+  if constexpr (S > 0) {
+    f32x4 t[S];
+#pragma unroll
+    for (int s = 0; s < S; ++s) t[s] = ld16(s);
+#pragma unroll
+    for (int s = 1; s < S; ++s) t[0] += t[s];
+    return t[0];
+  } else {
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (int s = 0; s < split; ++s) acc += ld16(s);
+    return acc;
+  }
+}
+
+template <int DTO, int S, bool NT, bool SB = false>
 __global__ void __launch_bounds__(256) split_reduce_kernel(const float* __restrict__ ws,
                                                            void* __restrict__ out, int64_t n,
                                                            void* __restrict__ outb, int64_t nb,
@@ -404,7 +444,8 @@ __global__ void __launch_bounds__(256) split_reduce_kernel(const float* __restri
     const float* src = is_b ? ws + split * n : ws;
     const int64_t ld = is_b ? nb : n, vi = is_b ? v - nv : v;
     void* dst = is_b ? outb : out;
-    f32x4 acc = sum_slabs<S, NT>(src, ld, vi, split);
+    f32x4 acc = SB && !is_b ? sum_slabs_b16<S, NT>(src, ld, vi, split)
+                            : sum_slabs<S, NT>(src, ld, vi, split);
     if constexpr (DTO == DT_F32) {
       f32x4* o = static_cast<f32x4*>(dst) + vi;
       *o = accumulate ? *o + acc : acc;
@@ -430,28 +471,28 @@ __global__ void __launch_bounds__(256) split_reduce_kernel(const float* __restri
 // (11-18 us; this one fastest by 2-5 %, profiles/r05_kernels/split_reduce.jsonl); the slabs are
 // read once, so streaming loads also keep them from displacing the main stream's L2 lines.
 
-template <int DTO, bool NT>
+template <int DTO, bool NT, bool SB>
 static void split_reduce_dispatch_v(const float* ws, void* out, int64_t n, void* outb, int64_t nb,
                                     int split, int accumulate, hipStream_t stream) {
   const int g = stream_grid((n + nb) / 4, 256);
 #define SR(SV)                                                                                   \
   case SV:                                                                                       \
-    hipLaunchKernelGGL((split_reduce_kernel<DTO, SV, NT>), dim3(g), dim3(256), 0, stream, ws, out, \
-                       n, outb, nb, split, accumulate);                                          \
+    hipLaunchKernelGGL((split_reduce_kernel<DTO, SV, NT, SB>), dim3(g), dim3(256), 0, stream, ws, \
+                       out, n, outb, nb, split, accumulate);                                     \
     return;
   switch (split) {
     SR(1) SR(2) SR(3) SR(4) SR(5) SR(6) SR(7) SR(8) SR(9) SR(10) SR(11) SR(12) SR(16)
     default:
-      hipLaunchKernelGGL((split_reduce_kernel<DTO, 0, NT>), dim3(g), dim3(256), 0, stream, ws, out,
-                         n, outb, nb, split, accumulate);
+      hipLaunchKernelGGL((split_reduce_kernel<DTO, 0, NT, SB>), dim3(g), dim3(256), 0, stream, ws,
+                         out, n, outb, nb, split, accumulate);
   }
 #undef SR
 }
 
-template <int DTO>
+template <int DTO, bool SB = false>
 static void split_reduce_dispatch(const float* ws, void* out, int64_t n, void* outb, int64_t nb,
                                   int split, int accumulate, hipStream_t stream) {
-  split_reduce_dispatch_v<DTO, true>(ws, out, n, outb, nb, split, accumulate, stream);
+  split_reduce_dispatch_v<DTO, true, SB>(ws, out, n, outb, nb, split, accumulate, stream);
 }
 
 }  // namespace tn
@@ -514,9 +555,16 @@ static int wgrad_launch(const void* A, int64_t lda, const void* B, int64_t ldb, 
          fused ? g_wgrad_tile_major : 0};
   const dim3 grid((N / bn) * (K / bk) * split);
   const int stages = g_wgrad_stages;
+  const bool sb16 = dt_out == DT_BF16;   // bf16 partial slabs for bf16 dW (SB16)
 #define WG_LAUNCH(BIASV, NBV, WMV, WJV)                                                     \
-  hipLaunchKernelGGL((wgrad_kernel<BIASV, NBV, WMV, WJV>), grid, dim3(128 * (WMV)),        \
-                     NBV * ((WMV) / 2 + (WJV) / 4) * kTile, stream, a)
+  do {                                                                                      \
+    if (sb16)                                                                               \
+      hipLaunchKernelGGL((wgrad_kernel<BIASV, NBV, WMV, WJV, true>), grid,                  \
+                         dim3(128 * (WMV)), NBV * ((WMV) / 2 + (WJV) / 4) * kTile, stream, a); \
+    else                                                                                    \
+      hipLaunchKernelGGL((wgrad_kernel<BIASV, NBV, WMV, WJV, false>), grid,                 \
+                         dim3(128 * (WMV)), NBV * ((WMV) / 2 + (WJV) / 4) * kTile, stream, a); \
+  } while (0)
 #define WG_STAGES(BIASV, WMV, WJV)                \
   if (stages == 4) WG_LAUNCH(BIASV, 4, WMV, WJV); \
   else if (stages == 3) WG_LAUNCH(BIASV, 3, WMV, WJV); \
@@ -534,7 +582,7 @@ static int wgrad_launch(const void* A, int64_t lda, const void* B, int64_t ldb, 
   const int64_t n = static_cast<int64_t>(N) * K;
   const int64_t nb = out_bias ? N : 0;
   if (dt_out == DT_BF16)
-    split_reduce_dispatch<DT_BF16>(ws, out, n, out_bias, nb, split, accumulate, stream);
+    split_reduce_dispatch<DT_BF16, true>(ws, out, n, out_bias, nb, split, accumulate, stream);
   else
     split_reduce_dispatch<DT_F32>(ws, out, n, out_bias, nb, split, accumulate, stream);
   return hipGetLastError();
